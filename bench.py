@@ -1,0 +1,207 @@
+"""Benchmark: Mpoints/s deskewed + % of HBM roofline on synthetic Mid-70 100k-point frames.
+
+One step = one pass of the hot path over one batch: the per-step pose prep (pose selection /
+segment tables) + the deskew kernel over every point of the rank's 600 frames x 100k points
+(BASELINE config 2: urban_complex, figure_eight).  Inputs are generated on the device and are
+resident in HBM before the timed region.  Weak scaling: each rank owns 600 frames of a
+600*N-frame urban_complex run (frames shard by index, no collective on the data path); the
+RCCL gather of the merged cloud to rank 0 is timed separately after the steps.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode pose_slerp|frame|imu]
+    torchrun --nproc-per-node N ... bench.py --gpus N   (one process per GPU, RCCL over xGMI)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import mcamd as mc  # noqa: E402
+
+URBAN = {"duration": 120.0, "trajectory_type": "figure_eight", "environment_complexity": "complex",
+         "max_speed": 12.0, "lidar_fps": 10}   # LMC:1183-1189
+BYTES_PER_POINT = {"pose_slerp": 36, "imu": 36, "frame": 32}   # SURVEY §8d algorithmic bytes
+HBM_PEAK_GBS = 8000.0                                          # MI355X_MICROARCH.md chip table
+
+
+def workload(rank, world, frames, points):
+    cfg = dict(URBAN, duration=max(URBAN["duration"], frames * world / URBAN["lidar_fps"]))
+    sim = mc.LiDARMotionSimulator(cfg)
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()
+    lo = rank * frames
+    return cfg, tr, times[lo:lo + frames], lo
+
+
+def cpu_baseline(mode, tr, times, counts, frame_lo, budget_s):
+    """The oracle (numpy restatement, 1 thread) on a bounded sample of the same frames."""
+    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+    from oracle import restatement as R
+    from oracle import synth
+    done = 0
+    t_total = 0.0
+    f = 0
+    ts_imu = gyro = None
+    if mode == "imu":
+        ts_imu, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    while f < len(counts) and t_total < budget_s:
+        x, y, z, i, t = synth.synth_frame(int(counts[f]), 0, 1000 + frame_lo + f)
+        pts = np.column_stack([x, y, z, i]).astype(np.float64)
+        t0 = time.perf_counter()
+        if mode == "frame":
+            k = int(R.select_pose_index(tr["time"], times[f]))
+            R.transform_pointcloud(pts, {"translation": tr["position_gps"][k], "rotation": tr["orientation_imu"][k]})
+        elif mode == "pose_slerp":
+            out = R.deskew_pose_slerp(pts[:, :3], t, times[f], tr)
+            np.column_stack([out, pts[:, 3]])
+        else:
+            st = int(times[f] * 1e9)
+            out = R.compensate_arrays(pts[:, :3], st + t.astype(np.int64), st, ts_imu, gyro)
+            np.column_stack([out, pts[:, 3]])
+        t_total += time.perf_counter() - t0
+        done += int(counts[f])
+        f += 1
+    return {"value": done / t_total / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
+            "sample": f"{f} of {len(counts)} frames x {int(counts[0])} pts (oracle numpy restatement, "
+                      f"same synthetic frames, generation excluded, {t_total:.1f} s)"}
+
+
+def load_traffic(mode, frames, points):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    e = d.get(f"{mode}:{frames}x{points}")
+    return None if e is None else e.get("hbm_bytes_per_launch")
+
+
+def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup):
+    for _ in range(warmup):
+        ctx.deskew(b_in, b_out, mode=mode)
+    ctx.sync()
+    rdv.barrier()
+    ctx.read_timing()          # drop warmup events
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.deskew(b_in, b_out, mode=mode)
+    ctx.sync()
+    t1 = time.perf_counter()
+    ctx.timing(False)
+    rdv.barrier()
+    tm = ctx.read_timing()
+    return t1 - t0, tm
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mode", default="pose_slerp", choices=list(BYTES_PER_POINT))
+    ap.add_argument("--frames", type=int, default=600)
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra-modes", action="store_true")
+    args = ap.parse_args()
+
+    rank, local_rank, world = mc.dist.env_rank()
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    rdv = mc.dist.Rendezvous(rank, world)
+    ctx = mc.Context(local_rank)
+
+    cfg, tr, times, lo = workload(rank, world, args.frames, args.points)
+    counts = np.full(args.frames, args.points, dtype=np.int64)
+    b_in = ctx.batch(counts, with_time=True)
+    b_out = ctx.batch(counts)
+    b_in.synth(seed=0, frame_id_base=1000 + lo)
+    b_in.set_frame_times(times)
+    b_in.set_frame_starts((times * 1e9).astype(np.int64))
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    ts_imu, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    ctx.set_imu(ts_imu, gyro)
+    n_rank = int(counts.sum())
+
+    modes = [args.mode] + ([] if args.no_extra_modes else [m for m in BYTES_PER_POINT if m != args.mode])
+    results = {}
+    for mode in modes:
+        steps = args.steps if mode == args.mode else max(10, args.steps // 4)
+        wall, tm = run_mode(ctx, rdv, mode, b_in, b_out, steps, args.warmup)
+        wall_max = rdv.max(wall)
+        main_avg_s = tm["main_ms"] / max(tm["main_launches"], 1) / 1e3
+        prep_avg_s = tm["prep_ms"] / max(tm["prep_launches"], 1) / 1e3
+        achieved = BYTES_PER_POINT[mode] * n_rank / main_avg_s / 1e9
+        results[mode] = {"wall_s": wall_max, "steps": steps, "main_avg_us": main_avg_s * 1e6,
+                         "prep_avg_us": prep_avg_s * 1e6, "achieved_GBs": achieved,
+                         "value": n_rank * world * steps / wall_max / 1e6}
+
+    gather = None
+    if world > 1:
+        try:
+            comm = mc.dist.RcclComm(ctx, rdv)
+            ctx.deskew(b_in, b_out, mode=args.mode)
+            ctx.sync()
+            rdv.barrier()
+            t0 = time.perf_counter()
+            merged = mc.dist.gather_merged(ctx, comm, rdv, b_out, root=0)
+            dt = rdv.max(time.perf_counter() - t0)
+            moved = 16 * n_rank * (world - 1)
+            gather = {"seconds": dt, "bytes_into_root": moved, "GBs": moved / dt / 1e9,
+                      "merged_points": int(n_rank * world)}
+            if merged is not None:
+                merged.close()
+            comm.close()
+        except Exception as e:  # report, never fail the throughput line
+            gather = {"error": str(e)}
+
+    if rank == 0:
+        r = results[args.mode]
+        traffic = load_traffic(args.mode, args.frames, args.points)
+        line = {
+            "metric": "Mpoints/s deskewed (100k-pt Mid-70 frames) + % HBM roofline",
+            "value": r["value"],
+            "unit": "Mpoints/s",
+            "n_gpus": world,
+            "steps": r["steps"],
+            "warmup": args.warmup,
+            "ms_per_step": r["wall_s"] / r["steps"] * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (f64 pose/angle setup)",
+            "data": "synthetic Mid-70 frames (counter-hash generator, on device); reference urban_complex "
+                    "pose table, seed 42",
+            "config": {"workload": f"urban_complex figure_eight, {args.frames} frames x {args.points} pts per GPU "
+                                   f"(BASELINE config 2; weak scaling over {world} GPU)",
+                       "mode": args.mode, "frames_per_gpu": args.frames, "points_per_frame": args.points,
+                       "global_frames": args.frames * world, "parallelism": f"frame-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": r["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": r["achieved_GBs"] / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel": {"pose_slerp": "k_deskew_points<1>", "imu": "k_deskew_points<2>",
+                                    "frame": "k_deskew_frame"}[args.mode],
+                         "kernel_avg_us": r["main_avg_us"], "bytes_per_point": BYTES_PER_POINT[args.mode]},
+            "prep_avg_us": r["prep_avg_us"],
+            "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
+                          "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"]}
+                      for m, v in results.items()},
+            "gather": gather,
+        }
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(args.mode, tr, times, counts, lo, args.cpu_budget)
+            line["cpu_baseline"]["cores_available"] = len(os.sched_getaffinity(0))
+        print(json.dumps(line), flush=True)
+    rdv.close()
+
+
+if __name__ == "__main__":
+    main()

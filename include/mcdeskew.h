@@ -1,0 +1,155 @@
+/*
+ * mcdeskew.h — C-ABI of the MI355X (gfx950) LiDAR motion-compensation library.
+ *
+ * This is the drop-in boundary for the reference's hot path.
+ * The reference is pure Python, so the "FFI" a maintainer binds is ctypes:
+ * every entry point takes plain pointers, sizes and ints, never a torch or
+ * numpy type.  The Python host layer (livox-motion-compensation-sim_amd/)
+ * mirrors the reference's own methods on top of these calls:
+ *
+ *   reference (file:line)                                      replaced by
+ *   ---------------------------------------------------------  -----------------------------
+ *   LiDARMotionSimulator.transform_pointcloud  LMC:772-776     mc_batch_upload_aos_f64 +
+ *                                                              mc_deskew(MC_MODE_FRAME,
+ *                                                              MC_POSE_DIRECT) +
+ *                                                              mc_batch_download_aos_f64
+ *   run_simulation pose selection + hot loop   LMC:802-832     mc_set_trajectory +
+ *                                                              mc_batch_set_frame_times +
+ *                                                              mc_deskew(MC_MODE_FRAME,
+ *                                                              MC_POSE_SEARCHSORTED)
+ *   save_results merge (np.vstack)             LMC:887-889     padded-CSR batch layout;
+ *                                                              mc_comm_gather_batch (multi-GPU)
+ *   MotionCompensator.compensate_point_cloud   CSIM:1435-1480  mc_set_imu + mc_deskew(MC_MODE_IMU)
+ *     _interpolate_imu_data                    CSIM:1482-1516    (per-point gyro LERP in-kernel)
+ *     _create_rotation_matrix                  CSIM:1518-1536    (R_xyz(theta)^T in-kernel)
+ *   (build-added)                          mc_deskew(MC_MODE_POSE_SLERP)
+ *
+ * LMC = lidar_motion_compensation.py, CSIM = livox_mid70_complete_simulator.py.
+ *
+ * Conventions
+ *  - Every function returns int: 0 = MC_OK, < 0 = error code; the message of the
+ *    last failure on the calling thread is returned by mc_last_error().
+ *  - The caller owns host buffers; a context owns device buffers; no host
+ *    pointer is retained after a call returns.
+ *  - All device work of a context is ordered on the context's own HIP stream.
+ *    Calls that return host data synchronise that stream before returning;
+ *    mc_deskew is asynchronous (mc_sync() waits for it).
+ *  - One context per thread and device.
+ *
+ * Device layout of a batch ("padded CSR"): n_frames ragged
+ * frames; frame f holds count[f] points stored at [poff[f], poff[f]+count[f])
+ * of five columns x, y, z, intensity (float32) and t_ns (int32, nanoseconds
+ * since the frame start); poff[f] is a multiple of 4 so every frame starts
+ * 16-byte aligned.
+ */
+#ifndef MCDESKEW_H_
+#define MCDESKEW_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MC_ABI_VERSION 1
+
+/* status codes */
+#define MC_OK 0
+#define MC_ERR_INVALID -1   /* bad argument / shape: Python maps to ValueError   */
+#define MC_ERR_HIP -2       /* HIP runtime failure                                */
+#define MC_ERR_NOMEM -3     /* device allocation failed                           */
+#define MC_ERR_STATE -4     /* missing prerequisite (e.g. no trajectory uploaded) */
+#define MC_ERR_INDEX -5     /* column count < 4: Python maps to IndexError (LMC:776) */
+#define MC_ERR_COMM -6      /* RCCL failure                                       */
+
+/* deskew modes */
+#define MC_MODE_FRAME 0      /* Path A: one SE(3) pose per frame, p' = R(rpy) p + t   (LMC:772-776)    */
+#define MC_MODE_POSE_SLERP 1 /* per point: quaternion SLERP + position LERP of the pose table at
+                                t_frame + t_ns*1e-9, then p' = R(q) p + pos       */
+#define MC_MODE_IMU 2        /* Path B: per point gyro LERP, theta = w*dt, p' = R_xyz(theta)^T p
+                                                                                 (CSIM:1435-1536) */
+
+/* pose selection for MC_MODE_FRAME */
+#define MC_POSE_SEARCHSORTED 0 /* idx = clamp(searchsorted(time, t_frame, 'left'), 0, T-1)  LMC:804-806 */
+#define MC_POSE_DIRECT 1       /* frame f uses trajectory row f (explicit per-frame transformation)   */
+
+/* batch creation flags */
+#define MC_BATCH_WITH_TIME 1u  /* allocate the t_ns column (needed by SLERP / IMU modes) */
+
+typedef struct mc_ctx mc_ctx;
+typedef struct mc_batch mc_batch;
+typedef struct mc_comm mc_comm;
+
+/* ---- library / context ------------------------------------------------- */
+int mc_abi_version(void);
+const char* mc_last_error(void);
+int mc_device_count(int* count);
+int mc_create(int device, mc_ctx** out);
+int mc_destroy(mc_ctx* ctx);
+int mc_sync(mc_ctx* ctx);
+
+/* ---- pose sources (copied to device; replace any previous table) ------- */
+/* trajectory table of LMC:361-428: time (T,), position_gps (T,3), orientation_imu (T,3) rad,
+ * all float64 C-contiguous.  time must be non-decreasing. */
+int mc_set_trajectory(mc_ctx* ctx, int64_t n_poses, const double* time, const double* position,
+                      const double* rpy);
+/* IMU samples of CSIM:1191-1240: timestamp (M,) int64 ns, gyro (M,3) rad/s float64.
+ * timestamps must be non-decreasing (duplicates allowed). */
+int mc_set_imu(mc_ctx* ctx, int64_t n_samples, const int64_t* timestamp_ns, const double* gyro);
+
+/* ---- batches ------------------------------------------------------------ */
+int mc_batch_create(mc_ctx* ctx, int32_t n_frames, const int64_t* counts, uint32_t flags,
+                    mc_batch** out);
+int mc_batch_destroy(mc_batch* b);
+int mc_batch_info(const mc_batch* b, int64_t* n_points, int64_t* padded_points, int32_t* n_frames,
+                  int32_t* n_tiles);
+/* padded frame offsets (n_frames+1 entries) as laid out on the device */
+int mc_batch_padded_offsets(const mc_batch* b, int64_t* poff_out);
+/* per-frame reference time in seconds (LMC:792-793 lidar_times) for SEARCHSORTED / SLERP */
+int mc_batch_set_frame_times(mc_batch* b, const double* t_frame);
+/* per-frame start timestamp in ns (CSIM:2049 frame['timestamp']) for MC_MODE_IMU */
+int mc_batch_set_frame_start_ns(mc_batch* b, const int64_t* start_ns);
+
+/* host dense AoS (N, ld) float64, columns 0..3 = x,y,z,intensity  ->  device SoA float32.
+ * ld < 4 -> MC_ERR_INDEX (mirrors points[:, 3] in LMC:776). */
+int mc_batch_upload_aos_f64(mc_batch* b, const double* aos, int64_t ld);
+/* host dense columns (float32, N each); any pointer may be NULL to leave that column */
+int mc_batch_upload_columns_f32(mc_batch* b, const float* x, const float* y, const float* z,
+                                const float* intensity);
+int mc_batch_upload_time_ns(mc_batch* b, const int32_t* t_ns);
+/* device SoA float32 -> host dense AoS (N,4) float64 (the (N,4) f64 layout LMC:776 returns) */
+int mc_batch_download_aos_f64(mc_batch* b, double* aos_out);
+int mc_batch_download_columns_f32(mc_batch* b, float* x, float* y, float* z, float* intensity);
+int mc_batch_download_time_ns(mc_batch* b, int32_t* t_ns);
+
+/* Synthetic Mid-70 frames generated on the device (counter-hash RNG, bit-identical to
+ * oracle/synth.py): frame f uses seed  seed + frame_id_base + f. */
+int mc_batch_synth(mc_batch* b, uint64_t seed, int64_t frame_id_base);
+/* float64 sums of x, y, z, intensity, t_ns over the valid points (deterministic order) */
+int mc_batch_checksum(mc_batch* b, double* sums5);
+
+/* ---- the hot path --------------------------------------------------------- */
+/* out must have the same frame counts as in (it may be the same batch: in-place). */
+int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select);
+
+/* HIP-event timing of the hot kernels (main deskew kernel and the pose-prep kernel) */
+int mc_timing_enable(mc_ctx* ctx, int enable);
+int mc_timing_read(mc_ctx* ctx, double* main_ms_total, int64_t* main_launches,
+                   double* prep_ms_total, int64_t* prep_launches);
+/* kernel tuning knobs: 0 keeps the default */
+int mc_set_launch(mc_ctx* ctx, int32_t max_grid);
+
+/* ---- multi-GPU merged-cloud gather over RCCL/xGMI (LMC:887-889 vstack) ---- */
+int mc_comm_unique_id(char id_out[128]);
+int mc_comm_init(mc_ctx* ctx, int nranks, int rank, const char id[128], mc_comm** out);
+int mc_comm_destroy(mc_comm* comm);
+/* ragged gather of every rank's batch columns (x,y,z,intensity, padded layout) into `merged`
+ * on `root`, in rank order (== np.vstack of the frame-ordered shards).  `merged` is ignored on
+ * non-root ranks and on root must have been created with the concatenated frame counts. */
+int mc_comm_gather_batch(mc_comm* comm, const mc_batch* local, int root, mc_batch* merged);
+int mc_comm_allreduce_max_f64(mc_comm* comm, double* values, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCDESKEW_H_ */

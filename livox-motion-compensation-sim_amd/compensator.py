@@ -1,0 +1,173 @@
+"""Drop-in ``MotionCompensator`` (CSIM:1426-1536) and the per-frame driver (CSIM:2086-2105).
+
+``compensate_point_cloud`` keeps the reference signature and record types; the per-point work
+(bracketing IMU samples, gyro LERP, theta = w*dt, p' = R_xyz(theta)^T p) runs in the gfx950
+kernel ``k_deskew_points<2>``.  ``compensate_arrays`` is the array fast path and
+``apply_motion_compensation`` batches every frame of a run into one launch.
+
+Contract differences from the reference, all raised as ValueError rather than computed:
+  * IMU timestamps must be non-decreasing (the reference's list scan, CSIM:1489-1494, assumes it);
+  * a point's time relative to its frame start must fit in int32 nanoseconds (+-2.147 s;
+    frames are 0.1 s, CSIM:2069).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List
+
+import numpy as np
+
+from .runtime import Context, default_context
+
+
+@dataclass
+class IMUData:
+    """CSIM:97-106 (200 Hz IMU record)."""
+    timestamp: int
+    gyro_x: float
+    gyro_y: float
+    gyro_z: float
+    accel_x: float
+    accel_y: float
+    accel_z: float
+
+
+@dataclass
+class LiDARPoint:
+    """CSIM:120-129 (one return)."""
+    x: float
+    y: float
+    z: float
+    intensity: int
+    timestamp: int
+    ring: int
+    tag: int
+
+
+def imu_to_arrays(imu_data) -> tuple:
+    ts = np.fromiter((s.timestamp for s in imu_data), dtype=np.int64, count=len(imu_data))
+    g = np.array([(s.gyro_x, s.gyro_y, s.gyro_z) for s in imu_data], dtype=np.float64).reshape(-1, 3)
+    return ts, g
+
+
+class MotionCompensator:
+    """GPU-backed drop-in for livox_mid70_complete_simulator.MotionCompensator."""
+
+    def __init__(self, config: Dict, *, context: Context | None = None):
+        self.config = config
+        self.enable_compensation = config.get("enable_motion_compensation", True)
+        self._context = context
+        self._imu_key = None
+
+    @property
+    def context(self) -> Context:
+        if self._context is None:
+            self._context = default_context()
+        return self._context
+
+    def _upload_imu(self, ts: np.ndarray, gyro: np.ndarray, key=None):
+        if key is not None and key == self._imu_key:
+            return
+        if len(ts) > 1 and np.any(np.diff(ts) < 0):
+            raise ValueError("IMU timestamps must be non-decreasing")
+        self.context.set_imu(ts, gyro)
+        self._imu_key = key
+
+    # ---- reference signature (CSIM:1435) ---------------------------------------------------
+    def compensate_point_cloud(self, points: List[LiDARPoint], imu_data: List[IMUData],
+                               frame_start_time: int, frame_duration_ns: int) -> List[LiDARPoint]:
+        """CSIM:1435-1480.  Returns ``points`` itself when disabled or without IMU data."""
+        if not self.enable_compensation or not imu_data:
+            return points
+        if not points:
+            return []
+        ts, g = self._imu_cached(imu_data)
+        xyz = np.array([(p.x, p.y, p.z) for p in points], dtype=np.float64).reshape(-1, 3)
+        t = np.fromiter((p.timestamp for p in points), dtype=np.int64, count=len(points))
+        out = self.compensate_arrays(xyz, t, frame_start_time, ts, g, _imu_key=self._imu_key)
+        cls = type(points[0])
+        return [cls(x=float(o[0]), y=float(o[1]), z=float(o[2]), intensity=p.intensity,
+                    timestamp=p.timestamp, ring=p.ring, tag=p.tag) for o, p in zip(out, points)]
+
+    def _imu_cached(self, imu_data):
+        key = (id(imu_data), len(imu_data), imu_data[0].timestamp, imu_data[-1].timestamp)
+        if key != getattr(self, "_imu_arrays_key", None):
+            self._imu_arrays = imu_to_arrays(imu_data)
+            self._imu_arrays_key = key
+            self._imu_key = None
+        ts, g = self._imu_arrays
+        self._upload_imu(ts, g, key)
+        return ts, g
+
+    # ---- array fast path ------------------------------------------------------------------
+    def compensate_arrays(self, xyz, timestamp_ns, frame_start_ns: int, imu_ts, gyro, *,
+                          intensity=None, _imu_key=None) -> np.ndarray:
+        """(N,3) points with absolute int64 ns timestamps -> compensated (N,3) float64."""
+        xyz = np.asarray(xyz, dtype=np.float64).reshape(-1, 3)
+        if not self.enable_compensation or len(imu_ts) == 0:
+            return xyz.copy()
+        n = xyz.shape[0]
+        if n == 0:
+            return np.zeros((0, 3))
+        imu_ts = np.ascontiguousarray(imu_ts, dtype=np.int64)
+        self._upload_imu(imu_ts, np.ascontiguousarray(gyro, dtype=np.float64).reshape(-1, 3), _imu_key)
+        t_rel = np.asarray(timestamp_ns, dtype=np.int64) - int(frame_start_ns)
+        ctx = self.context
+        b = ctx.batch([n], with_time=True)
+        try:
+            aos = np.zeros((n, 4))
+            aos[:, :3] = xyz
+            if intensity is not None:
+                aos[:, 3] = intensity
+            b.upload_aos(aos)
+            b.upload_time(t_rel)
+            b.set_frame_starts([int(frame_start_ns)])
+            ctx.deskew(b, b, mode="imu")
+            return b.download_aos()[:, :3]
+        finally:
+            b.close()
+
+    # ---- per-frame driver (CSIM:2086-2105), one launch for all frames --------------------------
+    def apply_motion_compensation(self, frames_data: List[dict], imu_data: List[IMUData]) -> List[dict]:
+        out = []
+        if not self.enable_compensation or not imu_data:
+            for fr in frames_data:
+                c = fr.copy()
+                c["motion_compensated"] = True
+                out.append(c)
+            return out
+        ts, g = self._imu_cached(imu_data)
+        counts = np.array([len(fr["points"]) for fr in frames_data], np.int64)
+        ctx = self.context
+        pts_all = [p for fr in frames_data for p in fr["points"]]
+        if pts_all:
+            b = ctx.batch(counts, with_time=True)
+            try:
+                aos = np.zeros((len(pts_all), 4))
+                aos[:, 0] = [p.x for p in pts_all]
+                aos[:, 1] = [p.y for p in pts_all]
+                aos[:, 2] = [p.z for p in pts_all]
+                starts = np.repeat(np.array([int(fr["timestamp"]) for fr in frames_data], np.int64), counts)
+                t_rel = np.fromiter((p.timestamp for p in pts_all), np.int64, len(pts_all)) - starts
+                b.upload_aos(aos)
+                b.upload_time(t_rel)
+                b.set_frame_starts([int(fr["timestamp"]) for fr in frames_data])
+                ctx.deskew(b, b, mode="imu")
+                res = b.download_aos()
+            finally:
+                b.close()
+        k = 0
+        for fr in frames_data:
+            c = fr.copy()
+            pts = fr["points"]
+            if pts:
+                cls = type(pts[0])
+                c["points"] = [cls(x=float(res[k + i, 0]), y=float(res[k + i, 1]), z=float(res[k + i, 2]),
+                                   intensity=p.intensity, timestamp=p.timestamp, ring=p.ring, tag=p.tag)
+                               for i, p in enumerate(pts)]
+                k += len(pts)
+            else:
+                c["points"] = []
+            c["motion_compensated"] = True
+            out.append(c)
+        return out

@@ -1,0 +1,736 @@
+// kernels.hpp — gfx950 (CDNA4, wave64) device code of the motion-compensation hot path.
+//
+// Kernels (DESIGN.md §4 has the roofline of each):
+//   k_prep            per step, tiny: pose selection + Euler->R per frame (LMC:804-812, 774),
+//                     quaternion segment table (SLERP), IMU segment table (CSIM:1482-1516),
+//                     per-frame segment hints.
+//   k_deskew_frame    Path A, LMC:772-776: p' = R p + t, one pose per frame (SGPR-resident).
+//   k_deskew_slerp    build-added per-point mode: quaternion SLERP + position LERP
+//                     of the pose table at each point's time, fused rotate-then-translate.
+//   k_deskew_imu      Path B, CSIM:1435-1536: gyro LERP at the point timestamp,
+//                     theta = w*dt, p' = Rx(-tx) Ry(-ty) Rz(-tz) p.
+//   k_synth / k_checksum / layout converters: input generation and staging (not the hot path).
+//
+// Work decomposition: the batch is a "padded CSR" of frames (every frame starts at a multiple of
+// 4 points), cut into frame-aligned tiles of up to kTileGroups float4 groups.  A workgroup owns
+// one tile at a time, so the frame (and its pose) is uniform over the workgroup; every column
+// access is a 16-byte-per-lane coalesced load/store (global_load_dwordx4).  Per-point modes stage
+// the tile's pose/IMU window into LDS once per tile.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <limits.h>
+#include <type_traits>
+
+namespace mc {
+
+constexpr int kBlock = 256;                    // 4 waves of 64
+constexpr int kIters = 2;                      // float4 groups per thread per tile
+constexpr int kTileGroups = kBlock * kIters;   // 512 groups = 2048 points per tile
+constexpr int kWinMax = 64;                    // LDS window capacity (segments per tile)
+
+struct Tile {
+  int64_t pstart;   // padded point index of the first group (multiple of 4)
+  int32_t frame;    // frame id (uniform over the tile)
+  int32_t ngroups;  // float4 groups in this tile (<= kTileGroups)
+};
+
+// One segment [k, k+1] of the pose table (trajectory), built per step by k_prep.
+struct PoseSeg {
+  float4 q0;     // unit quaternion (x,y,z,w) of orientation_imu[k]
+  float4 q1;     // of orientation_imu[k+1], sign-flipped onto q0's hemisphere (shortest arc)
+  float4 p0c;    // position[k].xyz, cos(Theta)
+  float4 dpt;    // position[k+1]-position[k], Theta = acos(q0.q1)
+  float4 misc;   // 1/sin(Theta), small-angle flag (1: LERP), 0, 0
+  double t0;     // time[k]
+  double inv_dt; // 1/(time[k+1]-time[k]), 0 for a degenerate segment
+};
+
+// PoseSeg specialised to one frame: alpha = clamp(t_ns * scale + off, 0, 1).
+struct PoseWin {
+  float4 q0, q1, p0c, dpt;
+  float inv_sin, small, off, scale;
+};
+
+// One IMU record k (CSIM:1482-1516 semantics): gyro(t) = g + alpha*dg,
+// alpha = max(0, (t - ts) * inv_dt); the last record has dg = 0, inv_dt = 0.
+struct ImuSeg {
+  double g[3];
+  double dg[3];
+  double inv_dt;
+  int64_t ts;    // absolute ns in the global table; frame-relative ns in an LDS window
+};
+
+struct DeskewArgs {
+  const float* __restrict__ in;    // 4 columns x|y|z|i, stride in_cap
+  int64_t in_cap;
+  const int32_t* __restrict__ tns; // t_ns column of `in` (per-point modes)
+  float* __restrict__ out;         // 4 columns, stride out_cap
+  int64_t out_cap;
+  const Tile* __restrict__ tiles;
+  int32_t n_tiles;
+  // frame mode
+  const float4* __restrict__ frame_tbl;   // 3 float4 per frame: (R row i, t_i)
+  // per-point modes
+  const double* __restrict__ frame_time;  // seconds (SLERP)
+  const int64_t* __restrict__ frame_start;// ns (IMU)
+  const int32_t* __restrict__ frame_hint; // segment index at the frame reference time
+  const double* __restrict__ pose_time;   // T
+  const PoseSeg* __restrict__ pose_seg;   // nseg
+  const int64_t* __restrict__ imu_ts;     // M
+  const ImuSeg* __restrict__ imu_seg;     // M
+  int64_t nseg;                           // segments (SLERP: max(T-1,1); IMU: M)
+  int64_t ntab;                           // T or M (length of the time table)
+};
+
+// 16-byte non-temporal store (output is written once and never re-read by this kernel)
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_nt(float* p, const float4& v) {
+  v4f t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
+}
+
+// ---------------------------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// number of entries of the non-decreasing table a[0..n) that are <= x, searched by galloping
+// from `hint` (an index whose entry is usually close to x).  == numpy searchsorted(a, x, 'right').
+template <typename T>
+__device__ __forceinline__ int64_t upper_bound_from(const T* a, int64_t n, T x, int64_t hint) {
+  int64_t lo, hi;  // invariant: a[lo-1] <= x (or lo == 0), a[hi] > x (or hi == n)
+  if (hint < 0) hint = 0;
+  if (hint >= n) hint = n - 1;
+  if (a[hint] <= x) {
+    lo = hint + 1;
+    int64_t step = 1;
+    hi = lo;
+    while (hi < n && a[hi] <= x) { lo = hi + 1; hi = lo + step; step <<= 1; }
+    if (hi > n) hi = n;
+  } else {
+    hi = hint;
+    int64_t step = 1;
+    lo = hi - 1;
+    while (lo >= 0 && a[lo] > x) { hi = lo; lo = hi - 1 - step; step <<= 1; }
+    lo = lo < 0 ? 0 : lo + 1;
+  }
+  while (lo < hi) {
+    int64_t mid = lo + ((hi - lo) >> 1);
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// numpy searchsorted(a, x, 'left'): first index with a[i] >= x  (LMC:804)
+__device__ __forceinline__ int64_t lower_bound_f64(const double* a, int64_t n, double x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = lo + ((hi - lo) >> 1);
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// R = Rz(yaw) Ry(pitch) Rx(roll) == scipy Rotation.from_euler('xyz', rpy).as_matrix() (LMC:774)
+__device__ __forceinline__ void euler_xyz_matrix(double r, double p, double y, double R[9]) {
+  double sr, cr, sp, cp, sy, cy;
+  sincos(r, &sr, &cr);
+  sincos(p, &sp, &cp);
+  sincos(y, &sy, &cy);
+  R[0] = cy * cp; R[1] = cy * sp * sr - sy * cr; R[2] = cy * sp * cr + sy * sr;
+  R[3] = sy * cp; R[4] = sy * sp * sr + cy * cr; R[5] = sy * sp * cr - cy * sr;
+  R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
+}
+
+// unit quaternion (x,y,z,w) of the same rotation (q = qz * qy * qx)
+__device__ __forceinline__ void euler_xyz_quat(double r, double p, double y, double q[4]) {
+  double sr, cr, sp, cp, sy, cy;
+  sincos(0.5 * r, &sr, &cr);
+  sincos(0.5 * p, &sp, &cp);
+  sincos(0.5 * y, &sy, &cy);
+  q[0] = sr * cp * cy - cr * sp * sy;
+  q[1] = cr * sp * cy + sr * cp * sy;
+  q[2] = cr * cp * sy - sr * sp * cy;
+  q[3] = cr * cp * cy + sr * sp * sy;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_prep: everything per step that is per frame or per pose/IMU sample (a few thousand threads)
+// ---------------------------------------------------------------------------------------------
+struct PrepArgs {
+  int mode;
+  int pose_select;
+  int32_t n_frames;
+  // trajectory
+  const double* time; const double* pos; const double* rpy; int64_t T;
+  // imu
+  const int64_t* imu_ts; const double* gyro; int64_t M;
+  // frames
+  const double* frame_time; const int64_t* frame_start;
+  // outputs
+  float4* frame_tbl; PoseSeg* pose_seg; ImuSeg* imu_seg; int32_t* frame_hint;
+  int64_t nseg;
+};
+
+__global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
+  const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a.mode == 0) {
+    // Path A pose selection (LMC:804-812) + Euler->R (LMC:774)
+    if (gid >= a.n_frames) return;
+    int64_t idx;
+    if (a.pose_select == 1) {
+      idx = gid;  // explicit per-frame transformation (host checks T == n_frames)
+    } else {
+      idx = lower_bound_f64(a.time, a.T, a.frame_time[gid]);
+      if (idx > a.T - 1) idx = a.T - 1;
+      if (idx < 0) idx = 0;
+    }
+    double R[9];
+    euler_xyz_matrix(a.rpy[3 * idx], a.rpy[3 * idx + 1], a.rpy[3 * idx + 2], R);
+    const double* t = a.pos + 3 * idx;
+    a.frame_tbl[3 * gid + 0] = make_float4((float)R[0], (float)R[1], (float)R[2], (float)t[0]);
+    a.frame_tbl[3 * gid + 1] = make_float4((float)R[3], (float)R[4], (float)R[5], (float)t[1]);
+    a.frame_tbl[3 * gid + 2] = make_float4((float)R[6], (float)R[7], (float)R[8], (float)t[2]);
+    return;
+  }
+  if (a.mode == 1) {
+    if (gid < a.nseg) {
+      const int64_t k = gid, k1 = (k + 1 < a.T) ? k + 1 : k;
+      double q0[4], q1[4];
+      euler_xyz_quat(a.rpy[3 * k], a.rpy[3 * k + 1], a.rpy[3 * k + 2], q0);
+      euler_xyz_quat(a.rpy[3 * k1], a.rpy[3 * k1 + 1], a.rpy[3 * k1 + 2], q1);
+      double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
+      if (d < 0.0) { d = -d; q1[0] = -q1[0]; q1[1] = -q1[1]; q1[2] = -q1[2]; q1[3] = -q1[3]; }
+      if (d > 1.0) d = 1.0;
+      const double th = acos(d);
+      const bool small = th < 1e-6;
+      const double inv_sin = small ? 0.0 : 1.0 / sin(th);
+      PoseSeg s;
+      s.q0 = make_float4((float)q0[0], (float)q0[1], (float)q0[2], (float)q0[3]);
+      s.q1 = make_float4((float)q1[0], (float)q1[1], (float)q1[2], (float)q1[3]);
+      const double* p0 = a.pos + 3 * k;
+      const double* p1 = a.pos + 3 * k1;
+      s.p0c = make_float4((float)p0[0], (float)p0[1], (float)p0[2], (float)d);
+      s.dpt = make_float4((float)(p1[0] - p0[0]), (float)(p1[1] - p0[1]), (float)(p1[2] - p0[2]), (float)th);
+      s.misc = make_float4((float)inv_sin, small ? 1.f : 0.f, 0.f, 0.f);
+      s.t0 = a.time[k];
+      const double dt = a.time[k1] - a.time[k];
+      s.inv_dt = dt > 0.0 ? 1.0 / dt : 0.0;
+      a.pose_seg[k] = s;
+    }
+    if (gid < a.n_frames) {
+      int64_t k = upper_bound_from(a.time, a.T, a.frame_time[gid], (int64_t)0) - 1;
+      if (k > a.nseg - 1) k = a.nseg - 1;
+      if (k < 0) k = 0;
+      a.frame_hint[gid] = (int32_t)k;
+    }
+    return;
+  }
+  // mode 2: IMU records (CSIM:1482-1516)
+  if (gid < a.M) {
+    const int64_t k = gid;
+    ImuSeg s;
+    const double* g = a.gyro + 3 * k;
+    s.g[0] = g[0]; s.g[1] = g[1]; s.g[2] = g[2];
+    if (k + 1 < a.M) {
+      const double* g1 = a.gyro + 3 * (k + 1);
+      s.dg[0] = g1[0] - g[0]; s.dg[1] = g1[1] - g[1]; s.dg[2] = g1[2] - g[2];
+      const int64_t dtn = a.imu_ts[k + 1] - a.imu_ts[k];
+      s.inv_dt = dtn > 0 ? 1.0 / (double)dtn : 0.0;
+    } else {
+      s.dg[0] = s.dg[1] = s.dg[2] = 0.0;
+      s.inv_dt = 0.0;
+    }
+    s.ts = a.imu_ts[k];
+    a.imu_seg[k] = s;
+  }
+  if (gid < a.n_frames) {
+    int64_t k = upper_bound_from(a.imu_ts, a.M, a.frame_start[gid], (int64_t)0) - 1;
+    if (k < 0) k = 0;
+    a.frame_hint[gid] = (int32_t)k;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Path A: frame mode (LMC:772-776).  One pose per tile -> uniform (SGPR) operands.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = a.tiles[tile];
+    const float4 r0 = a.frame_tbl[3 * tl.frame + 0];
+    const float4 r1 = a.frame_tbl[3 * tl.frame + 1];
+    const float4 r2 = a.frame_tbl[3 * tl.frame + 2];
+    const float* ix = a.in + tl.pstart;
+    float* ox = a.out + tl.pstart;
+    float4 vx[kIters], vy[kIters], vz[kIters], vi[kIters];
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int g = it * kBlock + threadIdx.x;
+      if (g < tl.ngroups) {
+        vx[it] = *reinterpret_cast<const float4*>(ix + 4 * g);
+        vy[it] = *reinterpret_cast<const float4*>(ix + a.in_cap + 4 * g);
+        vz[it] = *reinterpret_cast<const float4*>(ix + 2 * a.in_cap + 4 * g);
+        vi[it] = *reinterpret_cast<const float4*>(ix + 3 * a.in_cap + 4 * g);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int g = it * kBlock + threadIdx.x;
+      if (g < tl.ngroups) {
+        float4 X = vx[it], Y = vy[it], Z = vz[it];
+        float4 ox4, oy4, oz4;
+#define MC_XF(c)                                                         \
+  ox4.c = fmaf(r0.x, X.c, fmaf(r0.y, Y.c, fmaf(r0.z, Z.c, r0.w)));       \
+  oy4.c = fmaf(r1.x, X.c, fmaf(r1.y, Y.c, fmaf(r1.z, Z.c, r1.w)));       \
+  oz4.c = fmaf(r2.x, X.c, fmaf(r2.y, Y.c, fmaf(r2.z, Z.c, r2.w)));
+        MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
+#undef MC_XF
+        st_nt(ox + 4 * g, ox4);
+        st_nt(ox + a.out_cap + 4 * g, oy4);
+        st_nt(ox + 2 * a.out_cap + 4 * g, oz4);
+        st_nt(ox + 3 * a.out_cap + 4 * g, vi[it]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bounded-argument sin/cos.  ocml's sincosf carries a Payne-Hanek branch for huge arguments that
+// costs ~40 VGPRs per inlined copy; every angle here is first reduced to [-pi/4, pi/4] plus a
+// quadrant (in f64 for the IMU angles, Cody-Waite in f32 for the SLERP angle alpha*Theta, which is
+// bounded by pi/2), then evaluated with the minimax polynomials of Cephes sinf/cosf (<= 2 ulp).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void sincos_quadrant(float r, int q, float& s, float& c) {
+  const float z = r * r;
+  float ps = fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
+  ps = fmaf(z, ps, -1.6666654611e-1f);
+  const float sr = fmaf(z * r, ps, r);
+  float pc = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = fmaf(z, pc, 4.166664568298827e-2f);
+  const float cr = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
+  // quadrant q: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s)
+  const bool swap = (q & 1) != 0;
+  const float s0 = swap ? cr : sr;
+  const float c0 = swap ? sr : cr;
+  s = (q & 2) ? -s0 : s0;
+  c = ((q + 1) & 2) ? -c0 : c0;
+}
+// any double angle (IMU: theta = w*dt can reach tens of rad at yaw-wrap gyro spikes)
+__device__ __forceinline__ void sincos_f64arg(double x, float& s, float& c) {
+  const double k = rint(x * 0.63661977236758134);          // 2/pi
+  const float r = (float)fma(-k, 1.5707963267948966, x);    // |r| <= pi/4 (+ulps)
+  sincos_quadrant(r, (int)(int64_t)k, s, c);
+}
+// f32 angle of moderate size (|x| < 1e4): three-term Cody-Waite pi/2 reduction
+__device__ __forceinline__ void sincos_f32arg(float x, float& s, float& c) {
+  const float k = rintf(x * 0.636619772f);
+  float r = fmaf(-k, 1.5703125f, x);
+  r = fmaf(-k, 4.837512969970703125e-4f, r);
+  r = fmaf(-k, 7.54978995489188216e-8f, r);
+  sincos_quadrant(r, (int)k, s, c);
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-point compute bodies
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ PoseWin make_pose_win(const PoseSeg& s, double tf) {
+  PoseWin w;
+  w.q0 = s.q0; w.q1 = s.q1; w.p0c = s.p0c; w.dpt = s.dpt;
+  w.inv_sin = s.misc.x;
+  w.small = s.misc.y;
+  // alpha = (tf + t_ns*1e-9 - t0) * inv_dt = t_ns * (1e-9*inv_dt) + (tf - t0)*inv_dt
+  w.off = (float)((tf - s.t0) * s.inv_dt);
+  w.scale = (float)(1e-9 * s.inv_dt);
+  return w;
+}
+
+// smallest integer n with tf + n*1e-9 >= t_abs (boundary of a segment in frame-relative ns)
+__device__ __forceinline__ int64_t rel_ns_ceil(double t_abs, double tf) {
+  double v = ceil((t_abs - tf) * 1e9);
+  if (v > 4.0e18) v = 4.0e18;
+  if (v < -4.0e18) v = -4.0e18;
+  return (int64_t)v;
+}
+
+// quaternion SLERP + position LERP at alpha, then p' = R(q) p + pos  
+__device__ __forceinline__ void slerp_point(const PoseWin& w, int t, float& x, float& y, float& z) {
+  float al = fmaf((float)t, w.scale, w.off);
+  al = fminf(fmaxf(al, 0.f), 1.f);
+  float s0, s1;
+  if (w.small != 0.f) {
+    s1 = al; s0 = 1.f - al;
+  } else {
+    float sa, ca;
+    sincos_f32arg(al * w.dpt.w, sa, ca);
+    s1 = sa * w.inv_sin;
+    s0 = fmaf(-w.p0c.w, s1, ca);
+  }
+  const float qx = fmaf(s0, w.q0.x, s1 * w.q1.x);
+  const float qy = fmaf(s0, w.q0.y, s1 * w.q1.y);
+  const float qz = fmaf(s0, w.q0.z, s1 * w.q1.z);
+  const float qw = fmaf(s0, w.q0.w, s1 * w.q1.w);
+  // v' = v + qw*t + u x t,  t = 2 u x v
+  const float tx = 2.f * fmaf(qy, z, -qz * y);
+  const float ty = 2.f * fmaf(qz, x, -qx * z);
+  const float tz = 2.f * fmaf(qx, y, -qy * x);
+  const float rx = x + fmaf(qw, tx, fmaf(qy, tz, -qz * ty));
+  const float ry = y + fmaf(qw, ty, fmaf(qz, tx, -qx * tz));
+  const float rz = z + fmaf(qw, tz, fmaf(qx, ty, -qy * tx));
+  x = rx + fmaf(al, w.dpt.x, w.p0c.x);
+  y = ry + fmaf(al, w.dpt.y, w.p0c.y);
+  z = rz + fmaf(al, w.dpt.z, w.p0c.z);
+}
+
+// Path B body (CSIM:1447-1465): w = g + alpha*dg (alpha from the bracketing IMU samples),
+// theta = w * dt, p' = Rx(-theta_x) Ry(-theta_y) Rz(-theta_z) p.  The angle is formed in f64
+// (gyro spikes at yaw wraps reach ~1e3 rad/s) and range-reduced before the f32 sincos.
+__device__ __forceinline__ void imu_point(const ImuSeg& w, int t, float& x, float& y, float& z) {
+  double al = (double)((int64_t)t - w.ts) * w.inv_dt;
+  al = al > 0.0 ? al : 0.0;
+  const double dt = (double)t * 1e-9;
+  float sa, ca, sb, cb, sc, cc;
+  sincos_f64arg(fma(al, w.dg[0], w.g[0]) * dt, sa, ca);
+  sincos_f64arg(fma(al, w.dg[1], w.g[1]) * dt, sb, cb);
+  sincos_f64arg(fma(al, w.dg[2], w.g[2]) * dt, sc, cc);
+  // Rz(-c)
+  const float x1 = fmaf(cc, x, sc * y);
+  const float y1 = fmaf(-sc, x, cc * y);
+  // Ry(-b)
+  const float x2 = fmaf(cb, x1, -sb * z);
+  const float z2 = fmaf(sb, x1, cb * z);
+  // Rx(-a)
+  const float y3 = fmaf(ca, y1, sa * z2);
+  const float z3 = fmaf(-sa, y1, ca * z2);
+  x = x2; y = y3; z = z3;
+}
+
+__device__ __forceinline__ float& f4c(float4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ int i4c(const int4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+
+// window search: index of the window segment of frame-relative time t (bnd sorted, bnd[0] unused)
+__device__ __forceinline__ int win_index(const int64_t* bnd, int W, int64_t t) {
+  if (W <= 8) {
+    int k = 0;
+    for (int j = 1; j < W; ++j) k += (bnd[j] <= t) ? 1 : 0;
+    return k;
+  }
+  int lo = 1, hi = W;   // count entries bnd[1..W) <= t
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (bnd[mid] <= t) lo = mid + 1; else hi = mid;
+  }
+  return lo - 1;
+}
+
+// out-of-line per-point path for tiles whose time span covers more than kWinMax segments
+template <int MODE>
+__device__ __forceinline__ void deskew_tile_slow(const DeskewArgs& a, const Tile tl, int g0, int64_t klo) {
+  const int f = tl.frame;
+  const int e_end = 4 * min(tl.ngroups, g0 + kBlock);
+  for (int e = 4 * g0 + threadIdx.x; e < e_end; e += kBlock) {
+    const int64_t p = tl.pstart + e;
+    float x = a.in[p], y = a.in[a.in_cap + p], z = a.in[2 * a.in_cap + p];
+    const float in = a.in[3 * a.in_cap + p];
+    const int t = a.tns[p];
+    if constexpr (MODE == 1) {
+      const double tf = a.frame_time[f];
+      int64_t k = upper_bound_from(a.pose_time, a.ntab, tf + (double)t * 1e-9, klo) - 1;
+      if (k > a.nseg - 1) k = a.nseg - 1;
+      if (k < 0) k = 0;
+      slerp_point(make_pose_win(a.pose_seg[k], tf), t, x, y, z);
+    } else {
+      int64_t k = upper_bound_from(a.imu_ts, a.ntab, a.frame_start[f] + (int64_t)t, klo) - 1;
+      if (k < 0) k = 0;
+      ImuSeg w = a.imu_seg[k];
+      w.ts -= a.frame_start[f];
+      imu_point(w, t, x, y, z);
+    }
+    a.out[p] = x; a.out[a.out_cap + p] = y; a.out[2 * a.out_cap + p] = z; a.out[3 * a.out_cap + p] = in;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-point modes: one kernel template, MODE 1 = SLERP, MODE 2 = IMU
+// ---------------------------------------------------------------------------------------------
+// wave-uniform copy of an LDS value into SGPRs (the W == 1 fast path: one segment per sub-tile)
+__device__ __forceinline__ float sgpr(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double sgpr(double v) {
+  const int64_t u = __builtin_bit_cast(int64_t, v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(u & 0xffffffff));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(u >> 32));
+  return __builtin_bit_cast(double, ((int64_t)hi << 32) | (int64_t)(uint32_t)lo);
+}
+__device__ __forceinline__ int64_t sgpr(int64_t v) {
+  return __builtin_bit_cast(int64_t, sgpr(__builtin_bit_cast(double, v)));
+}
+__device__ __forceinline__ float4 sgpr(float4 v) { return make_float4(sgpr(v.x), sgpr(v.y), sgpr(v.z), sgpr(v.w)); }
+__device__ __forceinline__ PoseWin sgpr(const PoseWin& w) {
+  PoseWin r;
+  r.q0 = sgpr(w.q0); r.q1 = sgpr(w.q1); r.p0c = sgpr(w.p0c); r.dpt = sgpr(w.dpt);
+  r.inv_sin = sgpr(w.inv_sin); r.small = sgpr(w.small); r.off = sgpr(w.off); r.scale = sgpr(w.scale);
+  return r;
+}
+__device__ __forceinline__ ImuSeg sgpr(const ImuSeg& w) {
+  ImuSeg r;
+  for (int j = 0; j < 3; ++j) { r.g[j] = sgpr(w.g[j]); r.dg[j] = sgpr(w.dg[j]); }
+  r.inv_dt = sgpr(w.inv_dt);
+  r.ts = sgpr(w.ts);
+  return r;
+}
+
+// Per-point modes: MODE 1 = SLERP, MODE 2 = IMU.  A workgroup works on a sub-tile of
+// kBlock float4 groups (1024 points; a batch tile holds kSub of them): every thread loads one
+// float4 of each column + one int4 of t_ns, the workgroup reduces the sub-tile's time span,
+// stages the pose/IMU segments covering it into LDS, and every point then picks its segment.
+constexpr int kSub = kTileGroups / kBlock;
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
+  using Win = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
+  __shared__ Win s_win[kWinMax];
+  __shared__ int64_t s_bnd[kWinMax];
+  __shared__ int s_red[2][kBlock / 64];
+  __shared__ int64_t s_hdr[2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t n_sub = (int64_t)a.n_tiles * kSub;
+
+  for (int64_t st = blockIdx.x; st < n_sub; st += gridDim.x) {
+    const Tile tl = a.tiles[st / kSub];
+    const int g0 = (int)(st % kSub) * kBlock;
+    if (g0 >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
+    const int f = tl.frame;
+    const int g = g0 + tid;
+    const bool act = g < tl.ngroups;
+    const int64_t p = tl.pstart + 4 * (int64_t)g;
+
+    float4 X, Y, Z, I;
+    int4 Tq;
+    int tmin = INT_MAX, tmax = INT_MIN;
+    if (act) {
+      Tq = *reinterpret_cast<const int4*>(a.tns + p);
+      X = *reinterpret_cast<const float4*>(a.in + p);
+      Y = *reinterpret_cast<const float4*>(a.in + a.in_cap + p);
+      Z = *reinterpret_cast<const float4*>(a.in + 2 * a.in_cap + p);
+      I = *reinterpret_cast<const float4*>(a.in + 3 * a.in_cap + p);
+      tmin = min(min(Tq.x, Tq.y), min(Tq.z, Tq.w));
+      tmax = max(max(Tq.x, Tq.y), max(Tq.z, Tq.w));
+    }
+    tmin = wave_min(tmin);
+    tmax = wave_max(tmax);
+    if (lane == 0) { s_red[0][wid] = tmin; s_red[1][wid] = tmax; }
+    __syncthreads();
+    if (wid == 0 && lane < 2) {
+      int tv = s_red[lane][0];
+      for (int w = 1; w < kBlock / 64; ++w)
+        tv = lane == 0 ? min(tv, s_red[0][w]) : max(tv, s_red[1][w]);
+      // lanes 0/1 search the two window ends concurrently, galloping from the frame's hint
+      int64_t k;
+      if constexpr (MODE == 1) {
+        const double tq = a.frame_time[f] + (double)tv * 1e-9;
+        k = upper_bound_from(a.pose_time, a.ntab, tq, (int64_t)a.frame_hint[f]) - 1;
+        if (k > a.nseg - 1) k = a.nseg - 1;
+      } else {
+        const int64_t tq = a.frame_start[f] + (int64_t)tv;
+        k = upper_bound_from(a.imu_ts, a.ntab, tq, (int64_t)a.frame_hint[f]) - 1;
+      }
+      if (k < 0) k = 0;
+      s_hdr[lane] = k;
+    }
+    __syncthreads();
+    const int64_t klo = s_hdr[0];
+    const int64_t W64 = s_hdr[1] - klo + 1;
+    const int W = W64 > kWinMax ? kWinMax + 1 : (int)W64;
+    if (W > kWinMax) {
+      // pathological time span (more than kWinMax segments in 1024 points): out-of-line path
+      deskew_tile_slow<MODE>(a, tl, g0, klo);
+      __syncthreads();
+      continue;
+    }
+    if (tid < W) {
+      const int64_t k = klo + tid;
+      if constexpr (MODE == 1) {
+        const double tf = a.frame_time[f];
+        s_win[tid] = make_pose_win(a.pose_seg[k], tf);
+        s_bnd[tid] = rel_ns_ceil(a.pose_time[k], tf);
+      } else {
+        ImuSeg sg = a.imu_seg[k];
+        sg.ts -= a.frame_start[f];
+        s_win[tid] = sg;
+        s_bnd[tid] = sg.ts;
+      }
+    }
+    __syncthreads();
+
+    if (act) {
+      if (W == 1) {
+        const Win w = sgpr(s_win[0]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if constexpr (MODE == 1) slerp_point(w, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
+          else imu_point(w, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int t = i4c(Tq, c);
+          const int k = win_index(s_bnd, W, (int64_t)t);
+          if constexpr (MODE == 1) slerp_point(s_win[k], t, f4c(X, c), f4c(Y, c), f4c(Z, c));
+          else imu_point(s_win[k], t, f4c(X, c), f4c(Y, c), f4c(Z, c));
+        }
+      }
+      st_nt(a.out + p, X);
+      st_nt(a.out + a.out_cap + p, Y);
+      st_nt(a.out + 2 * a.out_cap + p, Z);
+      st_nt(a.out + 3 * a.out_cap + p, I);
+    }
+    __syncthreads();  // the LDS window is rewritten by the next sub-tile
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// layout / staging kernels (not the hot path; PCIe-bound when fed from the host)
+// ---------------------------------------------------------------------------------------------
+struct LayoutArgs {
+  const Tile* tiles; int32_t n_tiles;
+  const int64_t* poff; const int64_t* doff; const int64_t* counts;
+  float* cols; int64_t cap; int32_t* tns;
+};
+
+// per element of the padded layout: its frame-local index, or -1 for a padding slot
+__device__ __forceinline__ int64_t local_index(const LayoutArgs& a, const Tile& tl, int64_t p) {
+  const int64_t i = p - a.poff[tl.frame];
+  return i < a.counts[tl.frame] ? i : -1;
+}
+
+// host AoS (N, ld) f64 staged on the device -> padded SoA f32  (LMC:770 layout in)
+__global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const double* __restrict__ aos, int64_t ld) {
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = a.tiles[tile];
+    const int64_t d0 = a.doff[tl.frame];
+    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
+      const int64_t p = tl.pstart + e;
+      const int64_t i = local_index(a, tl, p);
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (i >= 0) {
+        const double* r = aos + (d0 + i) * ld;
+        v[0] = (float)r[0]; v[1] = (float)r[1]; v[2] = (float)r[2]; v[3] = (float)r[3];
+      }
+      for (int c = 0; c < 4; ++c) a.cols[c * a.cap + p] = v[c];
+    }
+  }
+}
+
+// padded SoA f32 -> dense AoS (N,4) f64 on the device  (LMC:776 layout out)
+__global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, double* __restrict__ aos) {
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = a.tiles[tile];
+    const int64_t d0 = a.doff[tl.frame];
+    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
+      const int64_t p = tl.pstart + e;
+      const int64_t i = local_index(a, tl, p);
+      if (i >= 0) {
+        double* r = aos + (d0 + i) * 4;
+        r[0] = a.cols[p]; r[1] = a.cols[a.cap + p]; r[2] = a.cols[2 * a.cap + p]; r[3] = a.cols[3 * a.cap + p];
+      }
+    }
+  }
+}
+
+// dense column (N) <-> padded column; DIR 0: dense->padded (padding zeroed), 1: padded->dense
+template <typename T, int DIR>
+__global__ __launch_bounds__(kBlock) void k_column(const LayoutArgs a, const T* __restrict__ src, T* __restrict__ dst) {
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = a.tiles[tile];
+    const int64_t d0 = a.doff[tl.frame];
+    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
+      const int64_t p = tl.pstart + e;
+      const int64_t i = local_index(a, tl, p);
+      if (DIR == 0) dst[p] = i >= 0 ? src[d0 + i] : T(0);
+      else if (i >= 0) dst[d0 + i] = src[p];
+    }
+  }
+}
+
+// ---- synthetic Mid-70 frames (bit-identical to oracle/synth.py) ------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
+
+__device__ __forceinline__ float u24(uint64_t h) { return (float)(uint32_t)(h >> 40) * 0x1.0p-24f; }
+
+__global__ __launch_bounds__(kBlock) void k_synth(const LayoutArgs a, uint64_t seed, int64_t fid_base) {
+#pragma clang fp contract(off)
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = a.tiles[tile];
+    const int64_t n = a.counts[tl.frame];
+    const uint64_t key = mix64((seed + (uint64_t)fid_base + (uint64_t)tl.frame) * kGamma);
+    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
+      const int64_t p = tl.pstart + e;
+      const int64_t i = local_index(a, tl, p);
+      float x = 0.f, y = 0.f, z = 0.f, in = 0.f;
+      int32_t t = 0;
+      if (i >= 0) {
+        const uint64_t c = 4ull * (uint64_t)i;
+        const float u0 = u24(mix64(key + (c + 1) * kGamma));
+        const float u1 = u24(mix64(key + (c + 2) * kGamma));
+        const float u2 = u24(mix64(key + (c + 3) * kGamma));
+        const float u3 = u24(mix64(key + (c + 4) * kGamma));
+        x = u0 * 0x1.67cccc0p+6f + 0x1.99999a0p-5f;           // depth 0.05 .. 90 m
+        const float ah = (u1 * 2.0f - 1.0f) * 0x1.692d20p-1f;  // tan(35.2 deg) half FOV (CSIM:66)
+        const float av = (u2 * 2.0f - 1.0f) * 0x1.98b968p-1f;  // tan(38.6 deg) half FOV (CSIM:67)
+        y = x * ah;
+        z = x * av;
+        in = u3;
+        t = (int32_t)((i * 100000000ll) / n);                  // spread over the 0.1 s frame
+      }
+      a.cols[p] = x; a.cols[a.cap + p] = y; a.cols[2 * a.cap + p] = z; a.cols[3 * a.cap + p] = in;
+      if (a.tns) a.tns[p] = t;
+    }
+  }
+}
+
+// per-tile f64 partial sums of x,y,z,i,t over valid points (deterministic tree; host sums tiles)
+__global__ __launch_bounds__(kBlock) void k_checksum(const LayoutArgs a, double* __restrict__ partial) {
+  __shared__ double s[5][kBlock];
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = a.tiles[tile];
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
+      const int64_t p = tl.pstart + e;
+      if (local_index(a, tl, p) >= 0) {
+        for (int c = 0; c < 4; ++c) acc[c] += (double)a.cols[c * a.cap + p];
+        if (a.tns) acc[4] += (double)a.tns[p];
+      }
+    }
+    for (int c = 0; c < 5; ++c) s[c][threadIdx.x] = acc[c];
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+      if (threadIdx.x < w)
+        for (int c = 0; c < 5; ++c) s[c][threadIdx.x] += s[c][threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x < 5) partial[tile * 5 + threadIdx.x] = s[threadIdx.x][0];
+    __syncthreads();
+  }
+}
+
+}  // namespace mc

@@ -1,0 +1,578 @@
+// mcdeskew.hip — host side of the C-ABI declared in include/mcdeskew.h.
+//
+// Owns the per-context HIP stream, the device copies of the pose sources (trajectory / IMU),
+// the padded-CSR batches and the launch of the kernels in kernels.hpp.  No torch, no numpy:
+// plain pointers and sizes in, status codes out (thread-local message in mc_last_error()).
+#include "../../include/mcdeskew.h"
+#include "kernels.hpp"
+#include "internal.hpp"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace mc;
+
+namespace mcimpl {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+}  // namespace mcimpl
+using mcimpl::fail;
+
+#define HIPCHK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(e_ == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP, "%s failed: %s", \
+                  #expr, hipGetErrorString(e_));                                            \
+  } while (0)
+
+#define CHECK_ARG(cond, ...) \
+  do {                       \
+    if (!(cond)) return fail(MC_ERR_INVALID, __VA_ARGS__); \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// small device-buffer helpers
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+static int dev_alloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)));
+  return MC_OK;
+}
+template <typename T>
+static void dev_free(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+static int ctx_stage(mc_ctx* c, size_t bytes, void** out) {
+  if (bytes > c->stage_bytes) {
+    if (c->d_stage) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->d_stage); c->d_stage = nullptr; }
+    c->stage_bytes = 0;
+    HIPCHK(hipMalloc(&c->d_stage, bytes));
+    c->stage_bytes = bytes;
+  }
+  *out = c->d_stage;
+  return MC_OK;
+}
+
+static int launch_grid(const mc_ctx* c, int32_t n_tiles) {
+  int g = n_tiles;
+  if (c->max_grid > 0 && g > c->max_grid) g = c->max_grid;
+  return g < 1 ? 1 : g;
+}
+
+static LayoutArgs layout_of(const mc_batch* b) {
+  LayoutArgs a;
+  a.tiles = b->d_tiles; a.n_tiles = b->n_tiles;
+  a.poff = b->d_poff; a.doff = b->d_doff; a.counts = b->d_counts;
+  a.cols = b->d_cols; a.cap = b->cap; a.tns = b->d_t;
+  return a;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+};
+
+// event timing around the hot kernels
+static hipEvent_t ev_take(mc_ctx* c) {
+  if (!c->ev_pool.empty()) { hipEvent_t e = c->ev_pool.back(); c->ev_pool.pop_back(); return e; }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+struct TimedRegion {
+  mc_ctx* c; std::vector<std::pair<hipEvent_t, hipEvent_t>>* v; hipEvent_t e0 = nullptr;
+  TimedRegion(mc_ctx* c_, std::vector<std::pair<hipEvent_t, hipEvent_t>>* v_) : c(c_), v(v_) {
+    if (c->timing) { e0 = ev_take(c); if (e0) (void)hipEventRecord(e0, c->stream); }
+  }
+  ~TimedRegion() {
+    if (c->timing && e0) {
+      hipEvent_t e1 = ev_take(c);
+      if (e1) { (void)hipEventRecord(e1, c->stream); v->emplace_back(e0, e1); }
+      else c->ev_pool.push_back(e0);
+    }
+  }
+};
+
+template <typename T>
+static int upload_column(mc_batch* b, const T* src, T* dst_col) {
+  mc_ctx* c = b->ctx;
+  void* st = nullptr;
+  if (int r = ctx_stage(c, (size_t)b->N * sizeof(T), &st)) return r;
+  HIPCHK(hipMemcpyAsync(st, src, (size_t)b->N * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL((k_column<T, 0>), dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
+                     layout_of(b), static_cast<const T*>(st), dst_col);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+template <typename T>
+static int download_column(mc_batch* b, const T* src_col, T* dst) {
+  mc_ctx* c = b->ctx;
+  void* st = nullptr;
+  if (int r = ctx_stage(c, (size_t)b->N * sizeof(T), &st)) return r;
+  hipLaunchKernelGGL((k_column<T, 1>), dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
+                     layout_of(b), src_col, static_cast<T*>(st));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(dst, st, (size_t)b->N * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+int mc_abi_version(void) { return MC_ABI_VERSION; }
+
+const char* mc_last_error(void) { return mcimpl::g_err.c_str(); }
+
+int mc_device_count(int* count) {
+  CHECK_ARG(count, "count is NULL");
+  *count = 0;
+  HIPCHK(hipGetDeviceCount(count));
+  return MC_OK;
+}
+
+int mc_create(int device, mc_ctx** out) {
+  CHECK_ARG(out, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  CHECK_ARG(device >= 0 && device < n, "device %d out of range (%d visible)", device, n);
+  HIPCHK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MC_ERR_STATE, "device %d is %s; this library is built for gfx950 (MI355X) only",
+                device, prop.gcnArchName);
+  mc_ctx* c = new mc_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) { delete c; return fail(MC_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+  *out = c;
+  return MC_OK;
+}
+
+int mc_destroy(mc_ctx* c) {
+  if (!c) return MC_OK;
+  DeviceGuard g(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
+  dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
+  if (c->d_stage) (void)hipFree(c->d_stage);
+  for (auto& p : c->main_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
+  for (auto& p : c->prep_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return MC_OK;
+}
+
+int mc_sync(mc_ctx* c) {
+  CHECK_ARG(c, "ctx is NULL");
+  DeviceGuard g(c->device);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_set_launch(mc_ctx* c, int32_t max_grid) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(max_grid >= 0, "max_grid must be >= 0");
+  c->max_grid = max_grid;
+  return MC_OK;
+}
+
+// ---- pose sources -------------------------------------------------------------------------
+int mc_set_trajectory(mc_ctx* c, int64_t T, const double* time, const double* pos, const double* rpy) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(T >= 1, "trajectory needs at least one pose (got %lld)", (long long)T);
+  CHECK_ARG(time && pos && rpy, "trajectory arrays must not be NULL");
+  for (int64_t i = 1; i < T; ++i)
+    CHECK_ARG(time[i] >= time[i - 1], "trajectory time must be non-decreasing (index %lld)", (long long)i);
+  DeviceGuard g(c->device);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (T > c->T_cap) {
+    dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
+    c->T_cap = 0;
+    if (int r = dev_alloc(&c->d_time, T)) return r;
+    if (int r = dev_alloc(&c->d_pos, 3 * T)) return r;
+    if (int r = dev_alloc(&c->d_rpy, 3 * T)) return r;
+    if (int r = dev_alloc(&c->d_pose_seg, T)) return r;
+    c->T_cap = T;
+  }
+  HIPCHK(hipMemcpyAsync(c->d_time, time, T * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_pos, pos, 3 * T * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_rpy, rpy, 3 * T * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->T = T;
+  return MC_OK;
+}
+
+int mc_set_imu(mc_ctx* c, int64_t M, const int64_t* ts, const double* gyro) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(M >= 1, "IMU table needs at least one sample (got %lld)", (long long)M);
+  CHECK_ARG(ts && gyro, "IMU arrays must not be NULL");
+  for (int64_t i = 1; i < M; ++i)
+    CHECK_ARG(ts[i] >= ts[i - 1], "IMU timestamps must be non-decreasing (index %lld)", (long long)i);
+  DeviceGuard g(c->device);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (M > c->M_cap) {
+    dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
+    c->M_cap = 0;
+    if (int r = dev_alloc(&c->d_imu_ts, M)) return r;
+    if (int r = dev_alloc(&c->d_gyro, 3 * M)) return r;
+    if (int r = dev_alloc(&c->d_imu_seg, M)) return r;
+    c->M_cap = M;
+  }
+  HIPCHK(hipMemcpyAsync(c->d_imu_ts, ts, M * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_gyro, gyro, 3 * M * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->M = M;
+  return MC_OK;
+}
+
+// ---- batches ------------------------------------------------------------------------------
+int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags, mc_batch** out) {
+  CHECK_ARG(c && out, "NULL argument");
+  *out = nullptr;
+  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(F == 0 || counts, "counts is NULL");
+  mc_batch* b = new mc_batch();
+  b->ctx = c;
+  b->F = F;
+  b->counts.assign(counts, counts + F);
+  b->poff.resize(F + 1);
+  b->doff.resize(F + 1);
+  b->poff[0] = b->doff[0] = 0;
+  std::vector<Tile> tiles;
+  for (int32_t f = 0; f < F; ++f) {
+    if (b->counts[f] < 0) { delete b; return fail(MC_ERR_INVALID, "frame %d has a negative count", f); }
+    const int64_t groups = (b->counts[f] + 3) / 4;
+    b->doff[f + 1] = b->doff[f] + b->counts[f];
+    b->poff[f + 1] = b->poff[f] + 4 * groups;
+    for (int64_t g0 = 0; g0 < groups; g0 += kTileGroups) {
+      Tile t;
+      t.pstart = b->poff[f] + 4 * g0;
+      t.frame = f;
+      t.ngroups = (int32_t)std::min<int64_t>(kTileGroups, groups - g0);
+      tiles.push_back(t);
+    }
+  }
+  if (tiles.size() > (size_t)INT32_MAX) { delete b; return fail(MC_ERR_INVALID, "too many tiles"); }
+  b->N = b->doff[F];
+  b->P = b->poff[F];
+  b->cap = ((b->P + 63) / 64) * 64;
+  b->n_tiles = (int32_t)tiles.size();
+  DeviceGuard g(c->device);
+  int r = MC_OK;
+  auto bail = [&](int code) { mc_batch_destroy(b); return code; };
+  if ((r = dev_alloc(&b->d_cols, 4 * (size_t)std::max<int64_t>(b->cap, 64)))) return bail(r);
+  if (flags & MC_BATCH_WITH_TIME)
+    if ((r = dev_alloc(&b->d_t, (size_t)std::max<int64_t>(b->cap, 64)))) return bail(r);
+  if ((r = dev_alloc(&b->d_counts, F + 1))) return bail(r);
+  if ((r = dev_alloc(&b->d_poff, F + 1))) return bail(r);
+  if ((r = dev_alloc(&b->d_doff, F + 1))) return bail(r);
+  if ((r = dev_alloc(&b->d_tiles, tiles.size()))) return bail(r);
+  if ((r = dev_alloc(&b->d_frame_time, F))) return bail(r);
+  if ((r = dev_alloc(&b->d_frame_start, F))) return bail(r);
+  if ((r = dev_alloc(&b->d_frame_tbl, 3 * (size_t)F))) return bail(r);
+  if ((r = dev_alloc(&b->d_frame_hint, F))) return bail(r);
+  if ((r = dev_alloc(&b->d_partial, 5 * (size_t)b->n_tiles))) return bail(r);
+  hipStream_t s = c->stream;
+  auto cpy = [&](void* d, const void* h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s); };
+  if (F > 0) {
+    if (cpy(b->d_counts, b->counts.data(), F * sizeof(int64_t)) != hipSuccess ||
+        cpy(b->d_poff, b->poff.data(), (F + 1) * sizeof(int64_t)) != hipSuccess ||
+        cpy(b->d_doff, b->doff.data(), (F + 1) * sizeof(int64_t)) != hipSuccess)
+      return bail(fail(MC_ERR_HIP, "batch metadata upload failed"));
+    if (!tiles.empty() && cpy(b->d_tiles, tiles.data(), tiles.size() * sizeof(Tile)) != hipSuccess)
+      return bail(fail(MC_ERR_HIP, "tile table upload failed"));
+  }
+  // zero the columns so padding slots are defined even before the first upload
+  if (hipMemsetAsync(b->d_cols, 0, 4 * (size_t)std::max<int64_t>(b->cap, 64) * sizeof(float), s) != hipSuccess)
+    return bail(fail(MC_ERR_HIP, "memset failed"));
+  if (b->d_t && hipMemsetAsync(b->d_t, 0, (size_t)std::max<int64_t>(b->cap, 64) * sizeof(int32_t), s) != hipSuccess)
+    return bail(fail(MC_ERR_HIP, "memset failed"));
+  if (hipStreamSynchronize(s) != hipSuccess) return bail(fail(MC_ERR_HIP, "sync failed"));
+  *out = b;
+  return MC_OK;
+}
+
+int mc_batch_destroy(mc_batch* b) {
+  if (!b) return MC_OK;
+  DeviceGuard g(b->ctx->device);
+  (void)hipStreamSynchronize(b->ctx->stream);
+  dev_free(b->d_cols); dev_free(b->d_t); dev_free(b->d_counts); dev_free(b->d_poff); dev_free(b->d_doff);
+  dev_free(b->d_tiles); dev_free(b->d_frame_time); dev_free(b->d_frame_start); dev_free(b->d_frame_tbl);
+  dev_free(b->d_frame_hint); dev_free(b->d_partial);
+  delete b;
+  return MC_OK;
+}
+
+int mc_batch_info(const mc_batch* b, int64_t* n, int64_t* padded, int32_t* F, int32_t* n_tiles) {
+  CHECK_ARG(b, "batch is NULL");
+  if (n) *n = b->N;
+  if (padded) *padded = b->P;
+  if (F) *F = b->F;
+  if (n_tiles) *n_tiles = b->n_tiles;
+  return MC_OK;
+}
+
+int mc_batch_padded_offsets(const mc_batch* b, int64_t* poff) {
+  CHECK_ARG(b && poff, "NULL argument");
+  std::memcpy(poff, b->poff.data(), (b->F + 1) * sizeof(int64_t));
+  return MC_OK;
+}
+
+int mc_batch_set_frame_times(mc_batch* b, const double* t) {
+  CHECK_ARG(b, "batch is NULL");
+  CHECK_ARG(b->F == 0 || t, "frame times are NULL");
+  DeviceGuard g(b->ctx->device);
+  if (b->F) {
+    HIPCHK(hipMemcpyAsync(b->d_frame_time, t, b->F * sizeof(double), hipMemcpyHostToDevice, b->ctx->stream));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+  }
+  b->has_times = true;
+  return MC_OK;
+}
+
+int mc_batch_set_frame_start_ns(mc_batch* b, const int64_t* s) {
+  CHECK_ARG(b, "batch is NULL");
+  CHECK_ARG(b->F == 0 || s, "frame starts are NULL");
+  DeviceGuard g(b->ctx->device);
+  if (b->F) {
+    HIPCHK(hipMemcpyAsync(b->d_frame_start, s, b->F * sizeof(int64_t), hipMemcpyHostToDevice, b->ctx->stream));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+  }
+  b->has_starts = true;
+  return MC_OK;
+}
+
+int mc_batch_upload_aos_f64(mc_batch* b, const double* aos, int64_t ld) {
+  CHECK_ARG(b, "batch is NULL");
+  if (ld < 4) return fail(MC_ERR_INDEX, "points need at least 4 columns (x,y,z,intensity); got %lld", (long long)ld);
+  if (b->N == 0) return MC_OK;
+  CHECK_ARG(aos, "points pointer is NULL");
+  mc_ctx* c = b->ctx;
+  DeviceGuard g(c->device);
+  void* st = nullptr;
+  if (int r = ctx_stage(c, (size_t)b->N * ld * sizeof(double), &st)) return r;
+  HIPCHK(hipMemcpyAsync(st, aos, (size_t)b->N * ld * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_aos_to_soa, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
+                     layout_of(b), static_cast<const double*>(st), ld);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_batch_upload_columns_f32(mc_batch* b, const float* x, const float* y, const float* z, const float* in) {
+  CHECK_ARG(b, "batch is NULL");
+  if (b->N == 0) return MC_OK;
+  DeviceGuard g(b->ctx->device);
+  const float* src[4] = {x, y, z, in};
+  for (int k = 0; k < 4; ++k)
+    if (src[k])
+      if (int r = upload_column<float>(b, src[k], b->d_cols + k * b->cap)) return r;
+  return MC_OK;
+}
+
+int mc_batch_upload_time_ns(mc_batch* b, const int32_t* t) {
+  CHECK_ARG(b, "batch is NULL");
+  if (!b->d_t) return fail(MC_ERR_STATE, "batch was created without MC_BATCH_WITH_TIME");
+  if (b->N == 0) return MC_OK;
+  CHECK_ARG(t, "t_ns is NULL");
+  DeviceGuard g(b->ctx->device);
+  return upload_column<int32_t>(b, t, b->d_t);
+}
+
+int mc_batch_download_aos_f64(mc_batch* b, double* aos) {
+  CHECK_ARG(b, "batch is NULL");
+  if (b->N == 0) return MC_OK;
+  CHECK_ARG(aos, "output pointer is NULL");
+  mc_ctx* c = b->ctx;
+  DeviceGuard g(c->device);
+  void* st = nullptr;
+  if (int r = ctx_stage(c, (size_t)b->N * 4 * sizeof(double), &st)) return r;
+  hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
+                     layout_of(b), static_cast<double*>(st));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(aos, st, (size_t)b->N * 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_batch_download_columns_f32(mc_batch* b, float* x, float* y, float* z, float* in) {
+  CHECK_ARG(b, "batch is NULL");
+  if (b->N == 0) return MC_OK;
+  DeviceGuard g(b->ctx->device);
+  float* dst[4] = {x, y, z, in};
+  for (int k = 0; k < 4; ++k)
+    if (dst[k])
+      if (int r = download_column<float>(b, b->d_cols + k * b->cap, dst[k])) return r;
+  return MC_OK;
+}
+
+int mc_batch_download_time_ns(mc_batch* b, int32_t* t) {
+  CHECK_ARG(b, "batch is NULL");
+  if (!b->d_t) return fail(MC_ERR_STATE, "batch was created without MC_BATCH_WITH_TIME");
+  if (b->N == 0) return MC_OK;
+  CHECK_ARG(t, "t_ns is NULL");
+  DeviceGuard g(b->ctx->device);
+  return download_column<int32_t>(b, b->d_t, t);
+}
+
+int mc_batch_synth(mc_batch* b, uint64_t seed, int64_t frame_id_base) {
+  CHECK_ARG(b, "batch is NULL");
+  if (b->n_tiles == 0) return MC_OK;
+  mc_ctx* c = b->ctx;
+  DeviceGuard g(c->device);
+  hipLaunchKernelGGL(k_synth, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b), seed,
+                     frame_id_base);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_batch_checksum(mc_batch* b, double* sums) {
+  CHECK_ARG(b && sums, "NULL argument");
+  for (int k = 0; k < 5; ++k) sums[k] = 0.0;
+  if (b->n_tiles == 0) return MC_OK;
+  mc_ctx* c = b->ctx;
+  DeviceGuard g(c->device);
+  hipLaunchKernelGGL(k_checksum, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
+                     b->d_partial);
+  HIPCHK(hipGetLastError());
+  std::vector<double> part(5 * (size_t)b->n_tiles);
+  HIPCHK(hipMemcpyAsync(part.data(), b->d_partial, part.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int32_t t = 0; t < b->n_tiles; ++t)
+    for (int k = 0; k < 5; ++k) sums[k] += part[5 * (size_t)t + k];
+  return MC_OK;
+}
+
+// ---- the hot path ---------------------------------------------------------------------------
+int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select) {
+  CHECK_ARG(c && in && out, "NULL argument");
+  CHECK_ARG(in->ctx == c && out->ctx == c, "batches belong to another context");
+  CHECK_ARG(mode >= MC_MODE_FRAME && mode <= MC_MODE_IMU, "unknown mode %d", mode);
+  CHECK_ARG(in->counts == out->counts, "input and output batches have different frame counts");
+  if (mode == MC_MODE_FRAME) {
+    CHECK_ARG(pose_select == MC_POSE_SEARCHSORTED || pose_select == MC_POSE_DIRECT, "unknown pose_select %d",
+              pose_select);
+    if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
+    if (pose_select == MC_POSE_DIRECT && c->T != in->F)
+      return fail(MC_ERR_INVALID, "MC_POSE_DIRECT needs one pose per frame (T=%lld, frames=%d)", (long long)c->T,
+                  in->F);
+    if (pose_select == MC_POSE_SEARCHSORTED && !in->has_times)
+      return fail(MC_ERR_STATE, "frame times not set (mc_batch_set_frame_times)");
+  } else if (mode == MC_MODE_POSE_SLERP) {
+    if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
+    if (!in->has_times) return fail(MC_ERR_STATE, "frame times not set (mc_batch_set_frame_times)");
+    if (!in->d_t) return fail(MC_ERR_STATE, "input batch has no t_ns column");
+  } else {
+    if (c->M < 1) return fail(MC_ERR_STATE, "no IMU samples uploaded (mc_set_imu)");
+    if (!in->has_starts) return fail(MC_ERR_STATE, "frame start times not set (mc_batch_set_frame_start_ns)");
+    if (!in->d_t) return fail(MC_ERR_STATE, "input batch has no t_ns column");
+  }
+  if (in->F == 0) return MC_OK;
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  const mc_batch* pb = in;  // per-frame tables live with the input batch
+
+  PrepArgs pa;
+  std::memset(&pa, 0, sizeof(pa));
+  pa.mode = mode;
+  pa.pose_select = pose_select;
+  pa.n_frames = in->F;
+  pa.time = c->d_time; pa.pos = c->d_pos; pa.rpy = c->d_rpy; pa.T = c->T;
+  pa.imu_ts = c->d_imu_ts; pa.gyro = c->d_gyro; pa.M = c->M;
+  pa.frame_time = pb->d_frame_time; pa.frame_start = pb->d_frame_start;
+  pa.frame_tbl = pb->d_frame_tbl; pa.pose_seg = c->d_pose_seg; pa.imu_seg = c->d_imu_seg;
+  pa.frame_hint = pb->d_frame_hint;
+  int64_t prep_n = in->F;
+  if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); prep_n = std::max<int64_t>(prep_n, pa.nseg); }
+  if (mode == MC_MODE_IMU) { pa.nseg = c->M; prep_n = std::max<int64_t>(prep_n, c->M); }
+  {
+    TimedRegion tr(c, &c->prep_ev);
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((prep_n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, pa);
+  }
+  HIPCHK(hipGetLastError());
+  if (in->n_tiles == 0) return MC_OK;
+
+  DeskewArgs da;
+  std::memset(&da, 0, sizeof(da));
+  da.in = in->d_cols; da.in_cap = in->cap; da.tns = in->d_t;
+  da.out = out->d_cols; da.out_cap = out->cap;
+  da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
+  da.frame_tbl = pb->d_frame_tbl;
+  da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start; da.frame_hint = pb->d_frame_hint;
+  da.pose_time = c->d_time; da.pose_seg = c->d_pose_seg;
+  da.imu_ts = c->d_imu_ts; da.imu_seg = c->d_imu_seg;
+  if (mode == MC_MODE_POSE_SLERP) { da.nseg = pa.nseg; da.ntab = c->T; }
+  if (mode == MC_MODE_IMU) { da.nseg = c->M; da.ntab = c->M; }
+  // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
+  // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
+  const int32_t units = mode == MC_MODE_FRAME ? in->n_tiles : in->n_tiles * kSub;
+  const dim3 grid(launch_grid(c, units)), block(kBlock);
+  {
+    TimedRegion tr(c, &c->main_ev);
+    if (mode == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, da);
+    else if (mode == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, da);
+    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, da);
+  }
+  HIPCHK(hipGetLastError());
+  // per-point modes pass the timestamps through (CSIM:1472): copy the column when out != in
+  if (mode != MC_MODE_FRAME && out != in && out->d_t)
+    HIPCHK(hipMemcpyAsync(out->d_t, in->d_t, in->P * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  return MC_OK;
+}
+
+int mc_timing_enable(mc_ctx* c, int enable) {
+  CHECK_ARG(c, "ctx is NULL");
+  c->timing = enable != 0;
+  return MC_OK;
+}
+
+static int sum_events(mc_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int64_t* n) {
+  double tot = 0.0;
+  for (auto& p : v) {
+    float m = 0.f;
+    HIPCHK(hipEventElapsedTime(&m, p.first, p.second));
+    tot += m;
+  }
+  if (ms) *ms = tot;
+  if (n) *n = (int64_t)v.size();
+  for (auto& p : v) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
+  v.clear();
+  return MC_OK;
+}
+
+int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms, int64_t* prep_n) {
+  CHECK_ARG(c, "ctx is NULL");
+  DeviceGuard g(c->device);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (int r = sum_events(c, c->main_ev, main_ms, main_n)) return r;
+  return sum_events(c, c->prep_ev, prep_ms, prep_n);
+}
+
+}  // extern "C"

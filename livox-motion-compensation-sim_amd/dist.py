@@ -1,0 +1,203 @@
+"""Multi-GPU sharding of the frame batch and the merged-cloud gather.
+
+Frames are independent (LMC:802-832 carries no state across frames), so a run shards as
+contiguous, point-balanced frame ranges — one process per GPU, no collective on the data path.
+The one exchange step is the reference's merge (np.vstack, LMC:887-889): concatenating the
+ranks' shards in rank order reproduces it, done as one ragged RCCL gather over xGMI
+(``mc_comm_gather_batch``).
+
+Control plane (rank/world from torchrun's env; barrier, max-over-ranks, RCCL unique-id
+broadcast) is a small TCP star on MASTER_ADDR:MASTER_PORT+1 (stdlib sockets — the GPU
+processes load no torch).  ``Rendezvous`` works on CPU, which the world-size-2 tests use.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import socket
+import struct
+import time
+from ctypes import c_char, c_double, c_void_p
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def plan_shards(counts, world_size: int) -> np.ndarray:
+    """Contiguous frame ranges balanced by point count: rank r owns frames [b[r], b[r+1]).
+
+    b[r] = first frame whose preceding-points prefix reaches r * total / world_size, so the
+    rank-ordered concatenation of the shards is the frame-ordered merge.
+    """
+    counts = np.asarray(counts, dtype=np.int64)
+    if world_size < 1:
+        raise ValueError("world_size must be >= 1")
+    prefix = np.concatenate([[0], np.cumsum(counts)])
+    total = prefix[-1]
+    F = len(counts)
+    bounds = [0]
+    for r in range(1, world_size):
+        target = (total * r) // world_size
+        b = int(np.searchsorted(prefix, target, side="left"))
+        if total == 0:
+            b = (F * r) // world_size
+        bounds.append(min(max(b, bounds[-1]), F))
+    bounds.append(F)
+    return np.asarray(bounds, dtype=np.int64)
+
+
+def env_rank() -> tuple:
+    """(rank, local_rank, world_size) from the torchrun environment (defaults 0, 0, 1)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+# ---------------------------------------------------------------------------------------------
+# control plane
+# ---------------------------------------------------------------------------------------------
+def _send(sock, payload: bytes):
+    sock.sendall(struct.pack("!Q", len(payload)) + payload)
+
+
+def _recv(sock) -> bytes:
+    head = b""
+    while len(head) < 8:
+        chunk = sock.recv(8 - len(head))
+        if not chunk:
+            raise ConnectionError("peer closed")
+        head += chunk
+    n = struct.unpack("!Q", head)[0]
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = sock.recv(min(n - len(buf), 1 << 20))
+        if not chunk:
+            raise ConnectionError("peer closed")
+        buf += chunk
+    return bytes(buf)
+
+
+class Rendezvous:
+    """Star-topology control channel: rank 0 accepts world_size-1 connections."""
+
+    def __init__(self, rank: int, world_size: int, addr: str | None = None, port: int | None = None,
+                 timeout: float = 300.0):
+        self.rank, self.world_size = rank, world_size
+        self.peers = {}
+        self.sock = None
+        if world_size == 1:
+            return
+        addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = port if port is not None else int(os.environ.get("MASTER_PORT", "29500")) + 1
+        deadline = time.time() + timeout
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(world_size)
+            srv.settimeout(timeout)
+            while len(self.peers) < world_size - 1:
+                conn, _ = srv.accept()
+                conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                r = struct.unpack("!I", _recv(conn))[0]
+                self.peers[r] = conn
+            srv.close()
+        else:
+            while True:
+                try:
+                    s = socket.create_connection((addr, port), timeout=5.0)
+                    break
+                except OSError:
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.05)
+            s.settimeout(timeout)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            _send(s, struct.pack("!I", rank))
+            self.sock = s
+
+    def allgather(self, obj):
+        """Every rank gets the rank-ordered list of every rank's JSON-serialisable obj."""
+        if self.world_size == 1:
+            return [obj]
+        if self.rank == 0:
+            vals = [obj] + [None] * (self.world_size - 1)
+            for r, c in self.peers.items():
+                vals[r] = json.loads(_recv(c))
+            blob = json.dumps(vals).encode()
+            for c in self.peers.values():
+                _send(c, blob)
+            return vals
+        _send(self.sock, json.dumps(obj).encode())
+        return json.loads(_recv(self.sock))
+
+    def broadcast_bytes(self, data: bytes | None) -> bytes:
+        if self.world_size == 1:
+            return data
+        if self.rank == 0:
+            for c in self.peers.values():
+                _send(c, data)
+            return data
+        return _recv(self.sock)
+
+    def barrier(self):
+        self.allgather(0)
+
+    def max(self, value: float) -> float:
+        return max(self.allgather(float(value)))
+
+    def close(self):
+        for c in self.peers.values():
+            c.close()
+        if self.sock is not None:
+            self.sock.close()
+        self.peers = {}
+        self.sock = None
+
+
+# ---------------------------------------------------------------------------------------------
+# RCCL data plane
+# ---------------------------------------------------------------------------------------------
+class RcclComm:
+    """RCCL communicator over the ranks of ``rdv`` (unique id broadcast through it)."""
+
+    def __init__(self, ctx, rdv: Rendezvous):
+        self.lib = ctx.lib
+        self.ctx = ctx
+        self.rank, self.world_size = rdv.rank, rdv.world_size
+        uid = (c_char * 128)()
+        if rdv.rank == 0:
+            check(self.lib.mc_comm_unique_id(uid), "comm_unique_id")
+        data = rdv.broadcast_bytes(bytes(uid) if rdv.rank == 0 else None)
+        uid = (c_char * 128).from_buffer_copy(data)
+        h = c_void_p()
+        check(self.lib.mc_comm_init(ctx.handle, rdv.world_size, rdv.rank, uid, ctypes.byref(h)), "comm_init")
+        self.handle = h
+
+    def gather_batch(self, local, merged=None, root: int = 0):
+        """Ragged gather of every rank's batch columns into ``merged`` on ``root`` (rank order)."""
+        check(self.lib.mc_comm_gather_batch(self.handle, local.handle, root,
+                                            merged.handle if merged is not None else None), "gather_batch")
+        return merged
+
+    def allreduce_max(self, values) -> np.ndarray:
+        v = np.ascontiguousarray(np.atleast_1d(values), dtype=np.float64).copy()
+        check(self.lib.mc_comm_allreduce_max_f64(self.handle, ptr(v, c_double), len(v)), "allreduce_max")
+        return v
+
+    def close(self):
+        if self.handle:
+            self.lib.mc_comm_destroy(self.handle)
+            self.handle = None
+
+
+def gather_merged(ctx, comm: RcclComm, rdv: Rendezvous, local, root: int = 0):
+    """Merged aligned cloud of all ranks on ``root`` (None elsewhere) — the LMC:888 vstack."""
+    all_counts = rdv.allgather([int(c) for c in local.counts])
+    merged = None
+    if rdv.rank == root:
+        merged = ctx.batch(np.concatenate([np.asarray(c, np.int64) for c in all_counts]))
+    comm.gather_batch(local, merged, root)
+    return merged

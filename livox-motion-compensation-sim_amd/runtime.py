@@ -1,0 +1,211 @@
+"""Device context and padded-CSR frame batches — thin Python objects over the C-ABI handles.
+
+A ``Context`` is one HIP device + stream (one per process/rank, like the C-ABI's mc_ctx).  A
+``Batch`` is a device-resident ragged batch of frames laid out as float32 columns
+x|y|z|intensity (+ int32 t_ns) in HBM; it is what one launch of the hot kernel consumes
+(DESIGN.md §3).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import weakref
+from ctypes import c_double, c_float, c_int, c_int32, c_int64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _f64(a, shape_tail=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if shape_tail is not None and a.shape[1:] != shape_tail:
+        raise ValueError(f"expected shape (n,{','.join(map(str, shape_tail))}), got {a.shape}")
+    return a
+
+
+class Context:
+    """One device + stream.  ``device`` defaults to $LOCAL_RANK (or 0)."""
+
+    def __init__(self, device: int | None = None):
+        self.lib = _lib.load()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        h = c_void_p()
+        check(self.lib.mc_create(int(device), ctypes.byref(h)), "mc_create")
+        self.handle = h
+        self.device = device
+        self._fin = weakref.finalize(self, self.lib.mc_destroy, h)
+
+    @staticmethod
+    def device_count() -> int:
+        lib = _lib.load()
+        n = c_int(0)
+        check(lib.mc_device_count(ctypes.byref(n)), "mc_device_count")
+        return n.value
+
+    def close(self):
+        self._fin()
+
+    def sync(self):
+        check(self.lib.mc_sync(self.handle), "mc_sync")
+
+    # ---- pose sources -------------------------------------------------------------------
+    def set_trajectory(self, time, position, rpy):
+        """Pose table (LMC:361-428): time (T,), position_gps (T,3), orientation_imu (T,3) rad."""
+        t = _f64(np.atleast_1d(time))
+        p = _f64(np.atleast_2d(position), (3,))
+        r = _f64(np.atleast_2d(rpy), (3,))
+        if not (len(t) == len(p) == len(r)):
+            raise ValueError("time / position / rpy lengths differ")
+        check(self.lib.mc_set_trajectory(self.handle, len(t), ptr(t, c_double), ptr(p, c_double),
+                                         ptr(r, c_double)), "set_trajectory")
+
+    def set_imu(self, timestamp_ns, gyro):
+        """IMU samples (CSIM:98-106): int64 ns timestamps (sorted), gyro (M,3) rad/s."""
+        ts = np.ascontiguousarray(timestamp_ns, dtype=np.int64)
+        g = _f64(np.atleast_2d(gyro), (3,))
+        if len(ts) != len(g):
+            raise ValueError("timestamp / gyro lengths differ")
+        check(self.lib.mc_set_imu(self.handle, len(ts), ptr(ts, c_int64), ptr(g, c_double)), "set_imu")
+
+    # ---- batches -------------------------------------------------------------------------
+    def batch(self, counts, with_time: bool = False) -> "Batch":
+        return Batch(self, counts, with_time)
+
+    def deskew(self, inp: "Batch", out: "Batch | None" = None, mode: str = "frame",
+               pose_select: str = "searchsorted") -> "Batch":
+        """Launch the hot path on the context stream (asynchronous); returns ``out``."""
+        if out is None:
+            out = Batch(self, inp.counts, with_time=inp.with_time)
+        check(self.lib.mc_deskew(self.handle, inp.handle, out.handle, _lib.MODES[mode],
+                                 _lib.POSE_SELECT[pose_select]), f"deskew[{mode}]")
+        return out
+
+    def set_max_grid(self, max_grid: int):
+        check(self.lib.mc_set_launch(self.handle, int(max_grid)), "set_launch")
+
+    def timing(self, enable: bool = True):
+        check(self.lib.mc_timing_enable(self.handle, int(bool(enable))), "timing_enable")
+
+    def read_timing(self) -> dict:
+        mm, pm = c_double(), c_double()
+        mn, pn = c_int64(), c_int64()
+        check(self.lib.mc_timing_read(self.handle, ctypes.byref(mm), ctypes.byref(mn), ctypes.byref(pm),
+                                      ctypes.byref(pn)), "timing_read")
+        return {"main_ms": mm.value, "main_launches": mn.value, "prep_ms": pm.value, "prep_launches": pn.value}
+
+
+class Batch:
+    """Device-resident ragged frame batch (padded CSR, float32 SoA columns in HBM)."""
+
+    def __init__(self, ctx: Context, counts, with_time: bool = False):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        self.counts = np.ascontiguousarray(np.atleast_1d(counts), dtype=np.int64)
+        if self.counts.ndim != 1 or (self.counts < 0).any():
+            raise ValueError("counts must be a 1-D array of non-negative frame sizes")
+        self.with_time = bool(with_time)
+        h = c_void_p()
+        flags = _lib.MC_BATCH_WITH_TIME if with_time else 0
+        check(self.lib.mc_batch_create(ctx.handle, len(self.counts), ptr(self.counts, c_int64), flags,
+                                       ctypes.byref(h)), "batch_create")
+        self.handle = h
+        self._fin = weakref.finalize(self, self.lib.mc_batch_destroy, h)
+        n, p = c_int64(), c_int64()
+        f, t = c_int32(), c_int32()
+        check(self.lib.mc_batch_info(h, ctypes.byref(n), ctypes.byref(p), ctypes.byref(f), ctypes.byref(t)))
+        self.n_points, self.padded_points, self.n_frames, self.n_tiles = n.value, p.value, f.value, t.value
+        self.offsets = np.concatenate([[0], np.cumsum(self.counts)]).astype(np.int64)
+
+    def close(self):
+        self._fin()
+
+    def padded_offsets(self) -> np.ndarray:
+        o = np.zeros(self.n_frames + 1, np.int64)
+        check(self.lib.mc_batch_padded_offsets(self.handle, ptr(o, c_int64)))
+        return o
+
+    def set_frame_times(self, t_frame):
+        t = _f64(np.atleast_1d(t_frame))
+        if len(t) != self.n_frames:
+            raise ValueError("one frame time per frame expected")
+        check(self.lib.mc_batch_set_frame_times(self.handle, ptr(t, c_double)), "set_frame_times")
+
+    def set_frame_starts(self, start_ns):
+        s = np.ascontiguousarray(np.atleast_1d(start_ns), dtype=np.int64)
+        if len(s) != self.n_frames:
+            raise ValueError("one frame start per frame expected")
+        check(self.lib.mc_batch_set_frame_start_ns(self.handle, ptr(s, c_int64)), "set_frame_starts")
+
+    # ---- host <-> device ----------------------------------------------------------------
+    def upload_aos(self, points):
+        """Dense (N, ld>=4) float64 AoS — the reference's (N,4) [x,y,z,intensity] layout (LMC:770)."""
+        a = np.ascontiguousarray(points, dtype=np.float64)
+        if a.ndim != 2:
+            raise IndexError("too many indices for array: points must be 2-D (N, 4)")
+        if a.shape[0] != self.n_points:
+            raise ValueError(f"batch holds {self.n_points} points, got {a.shape[0]}")
+        check(self.lib.mc_batch_upload_aos_f64(self.handle, ptr(a, c_double), a.shape[1]), "upload_aos")
+
+    def upload_columns(self, x=None, y=None, z=None, intensity=None):
+        cols = []
+        for c in (x, y, z, intensity):
+            if c is None:
+                cols.append(None)
+                continue
+            c = np.ascontiguousarray(c, dtype=np.float32)
+            if c.shape != (self.n_points,):
+                raise ValueError(f"column of {self.n_points} points expected, got {c.shape}")
+            cols.append(c)
+        check(self.lib.mc_batch_upload_columns_f32(self.handle, *[ptr(c, c_float) for c in cols]), "upload_columns")
+
+    def upload_time(self, t_ns):
+        t = np.asarray(t_ns)
+        if t.shape != (self.n_points,):
+            raise ValueError(f"t_ns of {self.n_points} points expected, got {t.shape}")
+        if t.size and (t.min() < -2**31 or t.max() > 2**31 - 1):
+            raise ValueError("t_ns (time since frame start) must fit in int32 nanoseconds (+-2.147 s)")
+        t = np.ascontiguousarray(t, dtype=np.int32)
+        check(self.lib.mc_batch_upload_time_ns(self.handle, ptr(t, c_int32)), "upload_time")
+
+    def download_aos(self) -> np.ndarray:
+        out = np.empty((self.n_points, 4), np.float64)
+        check(self.lib.mc_batch_download_aos_f64(self.handle, ptr(out, c_double)), "download_aos")
+        return out
+
+    def download_columns(self):
+        cols = [np.empty(self.n_points, np.float32) for _ in range(4)]
+        check(self.lib.mc_batch_download_columns_f32(self.handle, *[ptr(c, c_float) for c in cols]),
+              "download_columns")
+        return tuple(cols)
+
+    def download_time(self) -> np.ndarray:
+        t = np.empty(self.n_points, np.int32)
+        check(self.lib.mc_batch_download_time_ns(self.handle, ptr(t, c_int32)), "download_time")
+        return t
+
+    def synth(self, seed: int = 0, frame_id_base: int = 1000):
+        """Fill with synthetic Mid-70 frames on the device (bit-identical to oracle/synth.py)."""
+        check(self.lib.mc_batch_synth(self.handle, int(seed) % 2**64, int(frame_id_base)), "synth")
+
+    def checksum(self) -> np.ndarray:
+        s = np.zeros(5, np.float64)
+        check(self.lib.mc_batch_checksum(self.handle, ptr(s, c_double)), "checksum")
+        return s
+
+    def split(self, aos: np.ndarray) -> list:
+        """Split a dense (N,4) array into per-frame arrays (frame order)."""
+        return [aos[self.offsets[f]:self.offsets[f + 1]] for f in range(self.n_frames)]
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    """Process-wide context used by the drop-in reference-compatible functions."""
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context()
+    return _default_ctx

@@ -1,0 +1,238 @@
+"""Generate the golden vectors in tests/golden/ by running the reference itself.
+
+Run in the build container only (the reference does not exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference (/root/reference, read-only) is imported with a stub ``laspy`` module: LMC:12
+imports laspy unconditionally but uses it only in ``save_las`` (LMC:950-963), off the path.
+Only inputs and outputs are written (npz / json data); no reference source is copied.
+
+Fixtures:
+  lmc_frames.npz      Path A: selected frames of the three LMC scenarios — local scan, selected
+                      pose index / position / rpy, frame time, reference aligned output.
+  lmc_traj_<cfg>.npz  trajectory tables (LMC:361-428) with the reference's seed-42 noise.
+  lmc_kat.npz         transform_pointcloud known-answer cases (zero rotation, yaw=pi/2, ...).
+  lmc_config.json     LiDARMotionSimulator config defaults and validation errors (LMC:297-359).
+  csim_pathb.npz      Path B: CSIM IMU stream + points + compensate_point_cloud output, with the
+                      before-first / after-last / duplicate-timestamp edge cases.
+  slerp.npz           build-added SLERP mode: scipy Slerp + LERP over a parking interval that
+                      straddles the yaw wrap (not a reference function: anchored on scipy).
+  synth.npz           first 4096 points and f64 column sums of a synthetic 100k frame.
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+sys.path.insert(0, REPO)
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("laspy", types.ModuleType("laspy"))
+    sys.path.insert(0, REF)
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        import lidar_motion_compensation as lmc  # noqa: E402
+        import livox_mid70_complete_simulator as csim  # noqa: E402
+    return lmc, csim
+
+
+SCENARIOS = {  # LMC:1182-1204
+    "urban_complex": {"duration": 120.0, "trajectory_type": "figure_eight",
+                      "environment_complexity": "complex", "max_speed": 12.0, "lidar_fps": 10},
+    "highway_simple": {"duration": 60.0, "trajectory_type": "linear",
+                       "environment_complexity": "simple", "max_speed": 25.0, "lidar_fps": 15},
+    "parking_detailed": {"duration": 30.0, "trajectory_type": "circular",
+                         "environment_complexity": "medium", "max_speed": 5.0, "lidar_fps": 20},
+}
+FRAMES = {"urban_complex": [0, 1, 2, 599, 1199], "parking_detailed": [0, 300], "highway_simple": [0, 1]}
+
+
+def make_lmc(lmc):
+    out = {}
+    for name, cfg in SCENARIOS.items():
+        sim = lmc.LiDARMotionSimulator(dict(cfg))
+        with contextlib.redirect_stdout(io.StringIO()):
+            res = sim.run_simulation()
+        tr = res["trajectory"]
+        np.savez_compressed(os.path.join(HERE, f"lmc_traj_{name}.npz"), time=tr["time"],
+                            position=tr["position"], velocity=tr["velocity"],
+                            orientation=tr["orientation"], position_gps=tr["position_gps"],
+                            orientation_imu=tr["orientation_imu"], acceleration=tr["acceleration"])
+        frames = list(FRAMES[name])
+        if name == "highway_simple":  # add one empty frame (845 of 900 are empty)
+            empty = [s["frame_id"] for s in res["raw_scans"] if len(s["points_local"]) == 0]
+            frames.append(empty[0])
+        for fid in frames:
+            scan = res["raw_scans"][fid]
+            pos = scan["sensor_pose"]["position"]
+            idx = int(np.flatnonzero(np.all(tr["position_gps"] == pos, axis=1))[0])
+            key = f"{name}/{fid}"
+            out[key + "/points_local"] = np.asarray(scan["points_local"], dtype=np.float64).reshape(-1, 4)
+            out[key + "/aligned"] = np.asarray(res["aligned_pointclouds"][fid], dtype=np.float64).reshape(-1, 4)
+            out[key + "/pose_idx"] = np.int64(idx)
+            out[key + "/position"] = np.asarray(pos)
+            out[key + "/rpy"] = np.asarray(scan["sensor_pose"]["orientation"])
+            out[key + "/t_frame"] = np.float64(scan["timestamp"])
+        out[name + "/n_frames"] = np.int64(len(res["raw_scans"]))
+        out[name + "/frame_counts"] = np.array([len(s["points_local"]) for s in res["raw_scans"]], np.int64)
+        print(f"{name}: {len(res['raw_scans'])} frames, fixtures for {frames}")
+    np.savez_compressed(os.path.join(HERE, "lmc_frames.npz"), **out)
+
+
+def make_kat(lmc):
+    rng = np.random.default_rng(7)
+    sim = lmc.LiDARMotionSimulator()
+    pts = np.column_stack([rng.uniform(-80, 80, (64, 3)), rng.uniform(0, 1, 64)])
+    cases = [
+        ([0.0, 0.0, 0.0], [0.0, 0.0, 0.0]),
+        ([12.5, -3.0, 1.5], [0.0, 0.0, 0.0]),           # zero rotation => pure translation
+        ([0.0, 0.0, 0.0], [0.0, 0.0, np.pi / 2]),       # yaw = pi/2 permutes x/y
+        ([1500.0, 4.9, 0.0], [0.05, -0.02, 3.1]),       # highway-scale translation, near yaw wrap
+        ([-30.0, 29.0, 1.5], [-0.08, 0.01, -3.13]),
+        ([5.0, 5.0, 5.0], [0.7, -0.4, 2.0]),
+    ]
+    out = {"points": pts}
+    for i, (t, r) in enumerate(cases):
+        out[f"t{i}"] = np.array(t)
+        out[f"r{i}"] = np.array(r)
+        out[f"out{i}"] = sim.transform_pointcloud(pts, {"translation": np.array(t), "rotation": np.array(r)})
+    out["empty_out"] = sim.transform_pointcloud(np.zeros((0, 4)), {"translation": np.zeros(3), "rotation": np.zeros(3)})
+    out["n_cases"] = np.int64(len(cases))
+    np.savez_compressed(os.path.join(HERE, "lmc_kat.npz"), **out)
+
+
+def make_config(lmc):
+    sim = lmc.LiDARMotionSimulator()
+    bad = [
+        {"duration": "60"}, {"lidar_fps": 0}, {"lidar_fps": -5}, {"duration": 0.0},
+        {"max_speed": -1.0}, {"range_max": 1.0, "range_min": 2.0}, {"range_max": 2.0, "range_min": 2.0},
+        {"points_per_frame": None}, {"range_min": 5.0},
+    ]
+    errors = []
+    for cfg in bad:
+        try:
+            lmc.LiDARMotionSimulator(cfg)
+            errors.append({"config": cfg, "error": None, "message": None})
+        except Exception as e:  # noqa: BLE001
+            errors.append({"config": cfg, "error": type(e).__name__, "message": str(e)})
+    sim2 = lmc.LiDARMotionSimulator({"trajectory_type": "spiral"})
+    try:
+        sim2.generate_trajectory()
+        unk = {"error": None}
+    except Exception as e:  # noqa: BLE001
+        unk = {"error": type(e).__name__, "message": str(e)}
+    with open(os.path.join(HERE, "lmc_config.json"), "w") as f:
+        json.dump({"defaults": sim.default_config(), "errors": errors, "unknown_trajectory": unk}, f, indent=1)
+
+
+def make_pathb(csim):
+    cfg = dict(csim.DEFAULT_CONFIG)
+    with contextlib.redirect_stderr(io.StringIO()):
+        traj = csim.TrajectoryGenerator("figure_eight", 42).generate_trajectory(duration=10.0, max_speed=12.0)
+        imu = csim.IMUSimulator(cfg).simulate_imu_data(traj, 10.0)
+        comp = csim.MotionCompensator(cfg)
+    rng = np.random.default_rng(11)
+
+    def imu_arr(lst):
+        return (np.array([s.timestamp for s in lst], np.int64),
+                np.array([[s.gyro_x, s.gyro_y, s.gyro_z, s.accel_x, s.accel_y, s.accel_z] for s in lst]).reshape(-1, 6))
+
+    def run(case, imu_list, frame_start, ts):
+        n = len(ts)
+        xyz = np.column_stack([rng.uniform(0.05, 90, n), rng.uniform(-60, 60, n), rng.uniform(-70, 70, n)])
+        inten = rng.integers(0, 256, n)
+        pts = [csim.LiDARPoint(x=float(xyz[i, 0]), y=float(xyz[i, 1]), z=float(xyz[i, 2]), intensity=int(inten[i]),
+                               timestamp=int(ts[i]), ring=i % 16, tag=i % 2) for i in range(n)]
+        out = comp.compensate_point_cloud(pts, imu_list, int(frame_start), 100_000_000)
+        its, ig = imu_arr(imu_list)
+        return {f"{case}/imu_ts": its, f"{case}/imu_gyro": ig[:, :3], f"{case}/imu_accel": ig[:, 3:],
+                f"{case}/frame_start": np.int64(frame_start), f"{case}/xyz": xyz,
+                f"{case}/intensity": inten.astype(np.int64), f"{case}/ts": np.asarray(ts, np.int64),
+                f"{case}/ring": np.arange(n) % 16, f"{case}/tag": np.arange(n) % 2,
+                f"{case}/out_xyz": np.array([[p.x, p.y, p.z] for p in out]),
+                f"{case}/out_meta": np.array([[p.intensity, p.timestamp, p.ring, p.tag] for p in out], np.int64)}
+
+    out = {}
+    # 1000 returns spread over a frame at 1.2 s (CSIM:1048 spacing), some on IMU sample times
+    fs = 1_200_000_000
+    out.update(run("mid", imu, fs, fs + np.arange(1000) * 1000 * 100))
+    # frame starting before the first IMU sample (negative timestamps -> first sample used)
+    fs = -3_000_000
+    out.update(run("before", imu, fs, fs + np.arange(400) * 25_000))
+    # frame running past the last IMU sample (9.995 s)
+    fs = 9_950_000_000
+    out.update(run("after", imu, fs, fs + np.arange(400) * 250_000))
+    # duplicate timestamp pair: sample 300 repeated with different gyro values
+    dup = list(imu[:301]) + [csim.IMUData(imu[300].timestamp, imu[300].gyro_x + 0.5, imu[300].gyro_y - 0.25,
+                                          imu[300].gyro_z + 1.0, 0.0, 0.0, 9.81)] + list(imu[301:])
+    t300 = imu[300].timestamp
+    fs = t300 - 40_000_000
+    ts = np.sort(np.concatenate([fs + np.arange(200) * 400_000, [t300, t300, t300 - 1, t300 + 1]]))
+    out.update(run("dup", dup, fs, ts))
+    # yaw-wrap gyro spike region: the Euler-difference gyro of CSIM:1214-1217 jumps at +-pi
+    ts_all, g_all = imu_arr(imu)
+    spike = int(np.argmax(np.abs(g_all[:, 2])))
+    fs = int(ts_all[max(spike - 10, 0)])
+    out.update(run("spike", imu, fs, fs + np.arange(500) * 200_000))
+    out["spike/max_gyro"] = np.float64(np.abs(g_all[:, 2]).max())
+    # empty IMU list -> points unchanged (CSIM:1439-1440)
+    out.update(run("noimu", [], 0, np.arange(50) * 1000))
+    np.savez_compressed(os.path.join(HERE, "csim_pathb.npz"), **out)
+    print("path B: IMU samples", len(imu), "max |gyro_z|", out["spike/max_gyro"])
+
+
+def make_slerp(lmc):
+    from scipy.spatial.transform import Rotation, Slerp
+    sim = lmc.LiDARMotionSimulator(dict(SCENARIOS["parking_detailed"]))
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    yaw = tr["orientation_imu"][:, 2]
+    wrap = int(np.flatnonzero(np.abs(np.diff(yaw)) > np.pi)[0])   # yaw jumps +-pi between wrap, wrap+1
+    t_lo, t_hi = tr["time"][wrap - 1], tr["time"][wrap + 2]
+    rng = np.random.default_rng(5)
+    n = 1000
+    tq = np.sort(rng.uniform(t_lo, t_hi, n))
+    tq[:3] = tr["time"][wrap - 1:wrap + 2]                         # exact sample times
+    rots = Rotation.from_euler("xyz", tr["orientation_imu"])
+    R = Slerp(tr["time"], rots)(tq)
+    pos = np.stack([np.interp(tq, tr["time"], tr["position_gps"][:, j]) for j in range(3)], axis=1)
+    xyz = np.column_stack([rng.uniform(0.05, 90, n), rng.uniform(-60, 60, n), rng.uniform(-70, 70, n)])
+    out = R.apply(xyz) + pos
+    np.savez_compressed(os.path.join(HERE, "slerp.npz"), time=tr["time"], position_gps=tr["position_gps"],
+                        orientation_imu=tr["orientation_imu"], tq=tq, xyz=xyz, out=out, wrap=np.int64(wrap))
+
+
+def make_synth():
+    from oracle import synth
+    x, y, z, i, t = synth.synth_frame(100_000, 0, 1000)
+    np.savez_compressed(os.path.join(HERE, "synth.npz"), x=x[:4096], y=y[:4096], z=z[:4096], i=i[:4096],
+                        t=t[:4096], sums=np.array([x.astype(np.float64).sum(), y.astype(np.float64).sum(),
+                                                   z.astype(np.float64).sum(), i.astype(np.float64).sum(),
+                                                   t.astype(np.float64).sum()]))
+
+
+def main():
+    lmc, csim = import_reference()
+    make_lmc(lmc)
+    make_kat(lmc)
+    make_config(lmc)
+    make_pathb(csim)
+    make_slerp(lmc)
+    make_synth()
+    for f in sorted(os.listdir(HERE)):
+        print(f"{f:24s} {os.path.getsize(os.path.join(HERE, f)):>9d} B")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,118 @@
+"""Multi-rank path on CPU: shard planning, the socket control plane, and a world-size-2
+``gloo`` run whose rank-ordered gather equals the reference's frame-ordered np.vstack
+(LMC:887-889).  The per-rank compute here is the oracle (test-only); on GPUs it is the HIP
+kernel and the gather is RCCL (tests/test_gpu_parity.py covers the single-rank RCCL path)."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, pkg
+
+
+def test_plan_shards_properties():
+    d = pkg().dist
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        F = int(rng.integers(0, 40))
+        counts = rng.integers(0, 5000, F)
+        for W in (1, 2, 3, 4, 8):
+            b = d.plan_shards(counts, W)
+            assert len(b) == W + 1 and b[0] == 0 and b[-1] == F
+            assert np.all(np.diff(b) >= 0)
+            if counts.sum() > 0 and F >= W:
+                per = [counts[b[r]:b[r + 1]].sum() for r in range(W)]
+                assert max(per) <= counts.sum() / W + counts.max() + 1
+    assert d.plan_shards([100] * 8, 8).tolist() == list(range(9))
+    with pytest.raises(ValueError):
+        d.plan_shards([1], 0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rdv_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import importlib
+    d = importlib.import_module("livox-motion-compensation-sim_amd").dist
+    r = d.Rendezvous(rank, world, "127.0.0.1", port, timeout=60)
+    got = r.allgather({"rank": rank, "n": rank * 10})
+    mx = r.max(float(rank) * 1.5)
+    r.barrier()
+    blob = r.broadcast_bytes(b"uid-" + bytes(range(124)) if rank == 0 else None)
+    r.close()
+    q.put((rank, got, mx, blob))
+
+
+def test_rendezvous_two_processes():
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rdv_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got, mx, blob in res:
+        assert got == [{"rank": r, "n": r * 10} for r in range(3)]
+        assert mx == 3.0
+        assert blob == b"uid-" + bytes(range(124))
+
+
+def _gloo_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import importlib
+    import torch.distributed as dist
+    from oracle import restatement as R
+    from oracle import synth
+    m = importlib.import_module("livox-motion-compensation-sim_amd")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sim = m.LiDARMotionSimulator({"duration": 12.0, "trajectory_type": "figure_eight", "max_speed": 12.0})
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()
+    counts = np.array([(997 * (f + 3)) % 4000 for f in range(len(times))], np.int64)
+    b = m.dist.plan_shards(counts, world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    x, y, z, i, t = synth.synth_batch(counts[lo:hi], seed=5, frame_id_base=lo)
+    pts = np.column_stack([x, y, z, i]).astype(np.float64)
+    offs = np.concatenate([[0], np.cumsum(counts[lo:hi])])
+    shard = [pts[offs[k]:offs[k + 1]] for k in range(hi - lo)]
+    aligned = R.align_frames(shard, tr, times[lo:hi])
+    local = R.merge_aligned(aligned) if aligned else np.zeros((0, 4))
+    parts = [None] * world
+    dist.all_gather_object(parts, local)
+    dist.destroy_process_group()
+    if rank == 0:
+        x, y, z, i, t = synth.synth_batch(counts, seed=5, frame_id_base=0)
+        allp = np.column_stack([x, y, z, i]).astype(np.float64)
+        offs = np.concatenate([[0], np.cumsum(counts)])
+        full = R.merge_aligned(R.align_frames([allp[offs[k]:offs[k + 1]] for k in range(len(counts))], tr, times))
+        q.put(bool(np.array_equal(np.vstack(parts), full)))
+    else:
+        q.put(True)
+
+
+def test_gloo_world2_shard_and_gather_equals_vstack():
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res)

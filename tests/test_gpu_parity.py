@@ -1,0 +1,318 @@
+"""GPU parity: the HIP path through the C-ABI vs the oracle and the reference's golden vectors.
+
+Tolerance (north_star: <= 1e-5 relative per coordinate): per coordinate
+|gpu - ref| <= 1e-5 * (|p| + |t|), p the input point, t the translation applied.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_scaled_close, golden, scale_of
+from oracle import restatement as R
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+CFGS = {
+    "urban_complex": {"duration": 120.0, "trajectory_type": "figure_eight",
+                      "environment_complexity": "complex", "max_speed": 12.0, "lidar_fps": 10},
+    "highway_simple": {"duration": 60.0, "trajectory_type": "linear",
+                       "environment_complexity": "simple", "max_speed": 25.0, "lidar_fps": 15},
+    "parking_detailed": {"duration": 30.0, "trajectory_type": "circular",
+                         "environment_complexity": "medium", "max_speed": 5.0, "lidar_fps": 20},
+}
+SCEN = {"urban_complex": [0, 1, 2, 599, 1199], "parking_detailed": [0, 300], "highway_simple": [0, 1, 55]}
+
+
+def traj_of(name):
+    g = golden(f"lmc_traj_{name}.npz")
+    return {k: g[k] for k in g.files}
+
+
+# ---------------------------------------------------------------------------------------------
+# Path A
+# ---------------------------------------------------------------------------------------------
+def test_transform_pointcloud_known_answers(mc, gpu_ctx):
+    g = golden("lmc_kat.npz")
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    pts = g["points"]
+    for i in range(int(g["n_cases"])):
+        before = pts.copy()
+        out = sim.transform_pointcloud(pts, {"translation": g[f"t{i}"], "rotation": g[f"r{i}"]})
+        assert out.dtype == np.float64 and out.shape == (len(pts), 4)
+        assert np.array_equal(pts, before)   # input untouched
+        assert_scaled_close(out[:, :3], g[f"out{i}"][:, :3], scale_of(pts[:, :3], g[f"t{i}"]), what=f"kat{i}")
+        np.testing.assert_allclose(out[:, 3], pts[:, 3], rtol=1e-7)
+    assert sim.transform_pointcloud(np.zeros((0, 4)), {"translation": np.zeros(3), "rotation": np.zeros(3)}).shape == (0, 4)
+    with pytest.raises(IndexError):
+        sim.transform_pointcloud(np.zeros((5, 3)), {"translation": np.zeros(3), "rotation": np.zeros(3)})
+    with pytest.raises(IndexError):
+        sim.transform_pointcloud(np.zeros(4), {"translation": np.zeros(3), "rotation": np.zeros(3)})
+
+
+@pytest.mark.parametrize("name", list(SCEN))
+def test_run_alignment_matches_reference_frames(mc, gpu_ctx, name):
+    g = golden("lmc_frames.npz")
+    tr = traj_of(name)
+    sim = mc.LiDARMotionSimulator(dict(CFGS[name]), context=gpu_ctx)
+    times = sim.lidar_times()
+    fids = SCEN[name]
+    scans = [g[f"{name}/{f}/points_local"] for f in fids]
+    out = sim.run_alignment(scans, tr, times[fids])
+    for f, o in zip(fids, out):
+        ref = g[f"{name}/{f}/aligned"]
+        assert o.shape == ref.shape
+        assert_scaled_close(o[:, :3], ref[:, :3], scale_of(g[f"{name}/{f}/points_local"][:, :3],
+                                                           g[f"{name}/{f}/position"]), what=f"{name}/{f}")
+        np.testing.assert_allclose(o[:, 3], ref[:, 3], rtol=1e-7)
+    merged = sim.merge_aligned(out)
+    assert merged.shape == (sum(len(s) for s in scans), 4)
+
+
+def test_align_frames_ragged_batch(mc, gpu_ctx):
+    rng = np.random.default_rng(1)
+    counts = [0, 1, 2, 3, 4, 5, 7, 4096, 0, 2049, 2047, 1023, 100_003]
+    frames = [np.column_stack([rng.uniform(-90, 90, (n, 3)), rng.uniform(0, 1, n)]) for n in counts]
+    tfs = [{"translation": rng.normal(0, 500, 3), "rotation": rng.uniform(-np.pi, np.pi, 3)} for _ in counts]
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    out = sim.align_frames(frames, tfs)
+    for f, t, o in zip(frames, tfs, out):
+        ref = R.transform_pointcloud(f, t)
+        assert o.shape == ref.shape
+        assert_scaled_close(o[:, :3], ref[:, :3], scale_of(f[:, :3], t["translation"]))
+
+
+def test_frame_mode_grid_stride_and_inplace(mc, gpu_ctx):
+    counts = np.array([30_000, 77_777, 1, 50_000])
+    tr = traj_of("urban_complex")
+    b = gpu_ctx.batch(counts, with_time=False)
+    b.synth(seed=3, frame_id_base=0)
+    b.set_frame_times([0.0, 0.35, 7.3, 119.99])
+    gpu_ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    out1 = gpu_ctx.deskew(b, mode="frame").download_aos()
+    gpu_ctx.set_max_grid(37)
+    try:
+        out2 = gpu_ctx.deskew(b, mode="frame").download_aos()
+    finally:
+        gpu_ctx.set_max_grid(0)
+    assert np.array_equal(out1, out2)
+    gpu_ctx.deskew(b, b, mode="frame")   # in place
+    assert np.array_equal(b.download_aos(), out1)
+
+
+# ---------------------------------------------------------------------------------------------
+# synthetic generator + full-size properties
+# ---------------------------------------------------------------------------------------------
+def test_device_generator_bit_identical(mc, gpu_ctx):
+    counts = np.array([100_000, 3, 0, 20_001])
+    b = gpu_ctx.batch(counts, with_time=True)
+    b.synth(seed=0, frame_id_base=1000)
+    x, y, z, i = b.download_columns()
+    t = b.download_time()
+    hx, hy, hz, hi, ht = synth.synth_batch(counts, seed=0, frame_id_base=1000)
+    for a, h in zip((x, y, z, i, t), (hx, hy, hz, hi, ht)):
+        assert np.array_equal(a, h)
+    g = golden("synth.npz")
+    assert np.array_equal(x[:4096], g["x"]) and np.array_equal(t[:4096], g["t"])
+    np.testing.assert_allclose(b.checksum(), [c.astype(np.float64).sum() for c in (hx, hy, hz, hi, ht)], rtol=1e-12)
+
+
+def _c2_batch(mc, ctx, frames=600, n=100_000, with_time=True):
+    sim = mc.LiDARMotionSimulator(dict(CFGS["urban_complex"]), context=ctx)
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:frames]
+    b = ctx.batch(np.full(frames, n), with_time=with_time)
+    b.synth(seed=0, frame_id_base=1000)
+    b.set_frame_times(times)
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    return b, tr, times
+
+
+def test_full_size_c2_frame_mode_all_points(mc, gpu_ctx):
+    """BASELINE config 2 (600 x 100k) in frame mode, every point checked against the oracle."""
+    b, tr, times = _c2_batch(mc, gpu_ctx, with_time=False)
+    out = gpu_ctx.deskew(b, mode="frame")
+    ox, oy, oz, oi = out.download_columns()
+    hx, hy, hz, hi, _ = synth.synth_batch(b.counts, seed=0, frame_id_base=1000)
+    idx = R.select_pose_index(tr["time"], times)
+    Rm = R.euler_xyz_matrix(tr["orientation_imu"][idx])
+    T = tr["position_gps"][idx]
+    n = 100_000
+    worst = 0.0
+    for f in range(0, 600, 1):
+        s = slice(f * n, (f + 1) * n)
+        p = np.stack([hx[s], hy[s], hz[s]], axis=1).astype(np.float64)
+        ref = p @ Rm[f].T + T[f]
+        got = np.stack([ox[s], oy[s], oz[s]], axis=1)
+        worst = max(worst, assert_scaled_close(got, ref, scale_of(p, T[f]), what=f"frame {f}"))
+    assert np.array_equal(oi, hi)
+
+
+@pytest.mark.parametrize("mode", ["pose_slerp", "imu"])
+def test_full_size_c2_per_point_modes_sampled(mc, gpu_ctx, mode):
+    b, tr, times = _c2_batch(mc, gpu_ctx)
+    if mode == "imu":
+        ts, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
+        gpu_ctx.set_imu(ts, gyro)
+        starts = (times * 1e9).astype(np.int64)
+        b.set_frame_starts(starts)
+    out = gpu_ctx.deskew(b, mode=mode)
+    ox, oy, oz, oi = out.download_columns()
+    hx, hy, hz, hi, ht = synth.synth_batch(b.counts, seed=0, frame_id_base=1000)
+    assert np.array_equal(oi, hi)
+    n = 100_000
+    for f in [0, 1, 2, 57, 123, 299, 300, 451, 598, 599]:
+        s = slice(f * n, (f + 1) * n)
+        p = np.stack([hx[s], hy[s], hz[s]], axis=1).astype(np.float64)
+        got = np.stack([ox[s], oy[s], oz[s]], axis=1)
+        if mode == "pose_slerp":
+            ref = R.deskew_pose_slerp(p, ht[s], times[f], tr)
+            _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[f] + ht[s] * 1e-9)
+            sc = scale_of(p, pos)
+        else:
+            ref = R.compensate_arrays(p, starts[f] + ht[s].astype(np.int64), starts[f], ts, gyro)
+            sc = scale_of(p)
+        assert_scaled_close(got, ref, sc, what=f"{mode} frame {f}")
+    # rigid motion: norms preserved (imu: rotation only) over the full 60M points
+    if mode == "imu":
+        nin = np.sqrt(hx.astype(np.float64) ** 2 + hy.astype(np.float64) ** 2 + hz.astype(np.float64) ** 2)
+        nout = np.sqrt(ox.astype(np.float64) ** 2 + oy.astype(np.float64) ** 2 + oz.astype(np.float64) ** 2)
+        assert np.max(np.abs(nout - nin) / nin) < 1e-5
+
+
+# ---------------------------------------------------------------------------------------------
+# per-point SLERP mode
+# ---------------------------------------------------------------------------------------------
+def test_slerp_matches_scipy_golden_across_yaw_wrap(mc, gpu_ctx):
+    g = golden("slerp.npz")
+    tr = {"time": g["time"], "position_gps": g["position_gps"], "orientation_imu": g["orientation_imu"]}
+    t_frame = float(g["tq"][0])
+    t_ns = np.round((g["tq"] - t_frame) * 1e9).astype(np.int64)
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    pts = np.column_stack([g["xyz"], np.linspace(0, 1, len(g["xyz"]))])
+    out = sim.deskew_frames([pts], [t_ns], tr, times=[t_frame])[0]
+    tq = t_frame + t_ns * 1e-9
+    ref = R.deskew_pose_slerp(g["xyz"], t_ns, t_frame, tr)
+    _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], tq)
+    assert_scaled_close(out[:, :3], ref, scale_of(g["xyz"], pos), what="slerp vs oracle")
+    assert_scaled_close(out[:, :3], g["out"], scale_of(g["xyz"], pos), tol=2e-5, what="slerp vs scipy golden")
+
+
+def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
+    """Unsorted times, negative offsets, times beyond both ends of the pose table (clamp), a
+    dense pose table so that one 1024-point sub-tile spans > 64 segments (out-of-line path)."""
+    rng = np.random.default_rng(9)
+    T = 4000
+    time = np.linspace(0, 40, T)                      # 100 Hz pose table
+    rpy = np.cumsum(rng.normal(0, 0.05, (T, 3)), axis=0)
+    pos = np.cumsum(rng.normal(0, 0.2, (T, 3)), axis=0)
+    tr = {"time": time, "position_gps": pos, "orientation_imu": rpy}
+    counts = [5000, 3, 1024, 2500]
+    frames = [np.column_stack([rng.uniform(-90, 90, (n, 3)), rng.uniform(0, 1, n)]) for n in counts]
+    t_ns = [rng.integers(-2_000_000_000, 2_000_000_000, counts[0]),          # spans 4 s: slow path
+            np.array([-10**9, 0, 10**9]),
+            np.sort(rng.integers(0, 100_000_000, 1024)),
+            rng.integers(0, 100_000_000, 2500)]                                # unsorted
+    times = np.array([1.0, 0.2, 20.0, 39.95])                                 # frame 3 runs off the end
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    out = sim.deskew_frames(frames, t_ns, tr, times)
+    for f in range(len(counts)):
+        ref = R.deskew_pose_slerp(frames[f][:, :3], t_ns[f], times[f], tr)
+        _, p = R.slerp_pose(time, pos, rpy, times[f] + np.asarray(t_ns[f]) * 1e-9)
+        assert_scaled_close(out[f][:, :3], ref, scale_of(frames[f][:, :3], p), what=f"frame {f}")
+
+
+def test_slerp_single_pose_table(mc, gpu_ctx):
+    tr = {"time": np.array([3.0]), "position_gps": np.array([[1.0, 2.0, 3.0]]),
+          "orientation_imu": np.array([[0.1, -0.2, 2.5]])}
+    pts = np.column_stack([np.random.default_rng(2).normal(0, 30, (100, 3)), np.zeros(100)])
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    out = sim.deskew_frames([pts], [np.arange(100) * 10**6], tr, times=[0.0])[0]
+    ref = R.transform_pointcloud(pts, {"translation": tr["position_gps"][0], "rotation": tr["orientation_imu"][0]})
+    assert_scaled_close(out[:, :3], ref[:, :3], scale_of(pts[:, :3], tr["position_gps"][0]))
+
+
+# ---------------------------------------------------------------------------------------------
+# Path B
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case", ["mid", "before", "after", "dup", "spike", "noimu"])
+def test_compensate_point_cloud_matches_reference(mc, gpu_ctx, case):
+    g = golden("csim_pathb.npz")
+    comp = mc.MotionCompensator({}, context=gpu_ctx)
+    imu = [mc.IMUData(int(t), *map(float, gy), *map(float, ac))
+           for t, gy, ac in zip(g[f"{case}/imu_ts"], g[f"{case}/imu_gyro"], g[f"{case}/imu_accel"])]
+    xyz = g[f"{case}/xyz"]
+    pts = [mc.LiDARPoint(float(p[0]), float(p[1]), float(p[2]), int(i), int(t), int(r), int(tg))
+           for p, i, t, r, tg in zip(xyz, g[f"{case}/intensity"], g[f"{case}/ts"], g[f"{case}/ring"],
+                                     g[f"{case}/tag"])]
+    out = comp.compensate_point_cloud(pts, imu, int(g[f"{case}/frame_start"]), 100_000_000)
+    if case == "noimu":
+        assert out is pts
+        return
+    got = np.array([[p.x, p.y, p.z] for p in out])
+    assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(xyz), what=case)
+    meta = np.array([[p.intensity, p.timestamp, p.ring, p.tag] for p in out])
+    assert np.array_equal(meta, g[f"{case}/out_meta"])
+
+
+def test_compensator_disabled_and_driver(mc, gpu_ctx):
+    g = golden("csim_pathb.npz")
+    off = mc.MotionCompensator({"enable_motion_compensation": False}, context=gpu_ctx)
+    pts = [mc.LiDARPoint(1.0, 2.0, 3.0, 5, 10, 0, 0)]
+    assert off.compensate_point_cloud(pts, [mc.IMUData(0, 1, 1, 1, 0, 0, 0)], 0, 100_000_000) is pts
+    comp = mc.MotionCompensator({}, context=gpu_ctx)
+    imu = [mc.IMUData(int(t), *map(float, gy), 0.0, 0.0, 0.0) for t, gy in zip(g["mid/imu_ts"], g["mid/imu_gyro"])]
+    frames = []
+    for case in ("mid", "spike"):
+        xyz = g[f"{case}/xyz"]
+        frames.append({"timestamp": int(g[f"{case}/frame_start"]), "frame_duration_ns": 100_000_000,
+                       "points": [mc.LiDARPoint(*map(float, p), int(i), int(t), 0, 0)
+                                  for p, i, t in zip(xyz, g[f"{case}/intensity"], g[f"{case}/ts"])]})
+    frames.append({"timestamp": 0, "frame_duration_ns": 100_000_000, "points": []})
+    res = comp.apply_motion_compensation(frames, imu)
+    assert all(r["motion_compensated"] for r in res) and res[2]["points"] == []
+    for case, r in zip(("mid", "spike"), res):
+        got = np.array([[p.x, p.y, p.z] for p in r["points"]])
+        assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case)
+
+
+def test_imu_slow_path_wide_subtile(mc, gpu_ctx):
+    """1024 points spread over 1.5 s at 200 Hz IMU -> ~300 segments in one sub-tile."""
+    rng = np.random.default_rng(4)
+    ts = np.arange(0, 4_000_000_000, 5_000_000, dtype=np.int64)
+    gyro = rng.normal(0, 2.0, (len(ts), 3))
+    n = 3000
+    xyz = rng.uniform(-80, 80, (n, 3))
+    start = 1_000_000_000
+    t_abs = start + rng.integers(-500_000_000, 1_000_000_000, n)
+    comp = mc.MotionCompensator({}, context=gpu_ctx)
+    got = comp.compensate_arrays(xyz, t_abs, start, ts, gyro)
+    ref = R.compensate_arrays(xyz, t_abs, start, ts, gyro)
+    assert_scaled_close(got, ref, scale_of(xyz))
+
+
+# ---------------------------------------------------------------------------------------------
+# timing hooks and single-rank RCCL gather
+# ---------------------------------------------------------------------------------------------
+def test_timing_counts_launches(mc, gpu_ctx):
+    b, tr, times = _c2_batch(mc, gpu_ctx, frames=8, n=10_000)
+    out = gpu_ctx.batch(b.counts)
+    gpu_ctx.timing(True)
+    for _ in range(3):
+        gpu_ctx.deskew(b, out, mode="pose_slerp")
+    t = gpu_ctx.read_timing()
+    gpu_ctx.timing(False)
+    assert t["main_launches"] == 3 and t["prep_launches"] == 3 and t["main_ms"] > 0
+
+
+def test_rccl_gather_single_rank(mc, gpu_ctx):
+    dist = mc.dist
+    rdv = dist.Rendezvous(0, 1)
+    comm = dist.RcclComm(gpu_ctx, rdv)
+    try:
+        b = gpu_ctx.batch([5, 1000, 3])
+        b.synth(seed=1, frame_id_base=0)
+        merged = dist.gather_merged(gpu_ctx, comm, rdv, b)
+        assert np.array_equal(merged.download_aos(), b.download_aos())
+        assert comm.allreduce_max([1.5, -2.0]).tolist() == [1.5, -2.0]
+    finally:
+        comm.close()
