@@ -11,6 +11,7 @@ namespace mc {
 struct Tile;
 struct PoseSeg;
 struct ImuSeg;
+struct FrameWin;
 }  // namespace mc
 
 namespace mcimpl {
@@ -58,7 +59,9 @@ struct mc_batch {
   double* d_frame_time = nullptr;
   int64_t* d_frame_start = nullptr;
   float4* d_frame_tbl = nullptr;   // 3 float4 per frame (R row, t)
-  int32_t* d_frame_hint = nullptr;
+  int2* d_trange = nullptr;        // per-frame [min, max] t_ns (valid when trange_valid)
+  mc::FrameWin* d_fwin = nullptr;  // per-frame segment window (k_prep output)
+  void* d_frec = nullptr;          // 2 frame-specialised pose/IMU records per frame
   double* d_partial = nullptr;
-  bool has_times = false, has_starts = false;
+  bool has_times = false, has_starts = false, trange_valid = false;
 };

@@ -1,21 +1,22 @@
 // kernels.hpp — gfx950 (CDNA4, wave64) device code of the motion-compensation hot path.
 //
 // Kernels (DESIGN.md §4 has the roofline of each):
-//   k_prep            per step, tiny: pose selection + Euler->R per frame (LMC:804-812, 774),
-//                     quaternion segment table (SLERP), IMU segment table (CSIM:1482-1516),
-//                     per-frame segment hints.
-//   k_deskew_frame    Path A, LMC:772-776: p' = R p + t, one pose per frame (SGPR-resident).
-//   k_deskew_slerp    build-added per-point mode: quaternion SLERP + position LERP
-//                     of the pose table at each point's time, fused rotate-then-translate.
-//   k_deskew_imu      Path B, CSIM:1435-1536: gyro LERP at the point timestamp,
-//                     theta = w*dt, p' = Rx(-tx) Ry(-ty) Rz(-tz) p.
-//   k_synth / k_checksum / layout converters: input generation and staging (not the hot path).
+//   k_prep              per step, tiny: pose selection + Euler->R per frame (LMC:804-812, 774);
+//                       quaternion segment table (SLERP) / IMU record table (CSIM:1482-1516);
+//                       per-frame segment windows and their frame-specialised records.
+//   k_deskew_frame      Path A, LMC:772-776: p' = R p + t, one pose per frame (SGPR-resident).
+//   k_deskew_points<1>  build-added per-point mode: quaternion SLERP + position
+//                       LERP of the pose table at each point's time, fused rotate-then-translate.
+//   k_deskew_points<2>  Path B, CSIM:1435-1536: gyro LERP at the point timestamp,
+//                       theta = w*dt, p' = Rx(-tx) Ry(-ty) Rz(-tz) p.
+//   k_trange / k_synth / k_checksum / layout converters: staging, not the per-step path.
 //
 // Work decomposition: the batch is a "padded CSR" of frames (every frame starts at a multiple of
 // 4 points), cut into frame-aligned tiles of up to kTileGroups float4 groups.  A workgroup owns
-// one tile at a time, so the frame (and its pose) is uniform over the workgroup; every column
-// access is a 16-byte-per-lane coalesced load/store (global_load_dwordx4).  Per-point modes stage
-// the tile's pose/IMU window into LDS once per tile.
+// one (sub-)tile, so the frame and its pose window are uniform over the workgroup: the pose
+// records are read with scalar loads into SGPRs, every column access is a 16-byte-per-lane
+// coalesced global_load/store_dwordx4, and stores are non-temporal.  Frames whose points span
+// more than two pose/IMU segments stage their window in LDS (one barrier per sub-tile).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,9 +26,10 @@
 namespace mc {
 
 constexpr int kBlock = 256;                    // 4 waves of 64
-constexpr int kIters = 2;                      // float4 groups per thread per tile
+constexpr int kIters = 2;                      // float4 groups per thread per tile (frame mode)
 constexpr int kTileGroups = kBlock * kIters;   // 512 groups = 2048 points per tile
-constexpr int kWinMax = 64;                    // LDS window capacity (segments per tile)
+constexpr int kSub = kTileGroups / kBlock;     // per-point modes: sub-tiles of kBlock groups
+constexpr int kWinMax = 64;                    // LDS window capacity (segments per frame)
 
 struct Tile {
   int64_t pstart;   // padded point index of the first group (multiple of 4)
@@ -58,30 +60,53 @@ struct ImuSeg {
   double g[3];
   double dg[3];
   double inv_dt;
-  int64_t ts;    // absolute ns in the global table; frame-relative ns in an LDS window
+  int64_t ts;    // absolute ns in the global table; frame-relative ns in a frame window
+};
+
+// Per-frame segment window, written by k_prep: segments [klo, klo+W) cover every point of
+// the frame; bnd1 = frame-relative ns where segment klo+1 starts (W >= 2).
+struct FrameWin {
+  int32_t klo;
+  int32_t W;
+  int64_t bnd1;
 };
 
 struct DeskewArgs {
-  const float* __restrict__ in;    // 4 columns x|y|z|i, stride in_cap
+  const float* in;         // 4 columns x|y|z|i, stride in_cap
   int64_t in_cap;
-  const int32_t* __restrict__ tns; // t_ns column of `in` (per-point modes)
-  float* __restrict__ out;         // 4 columns, stride out_cap
+  const int32_t* tns;      // t_ns column of `in` (per-point modes)
+  float* out;              // 4 columns, stride out_cap
   int64_t out_cap;
-  const Tile* __restrict__ tiles;
+  const Tile* tiles;
   int32_t n_tiles;
-  // frame mode
-  const float4* __restrict__ frame_tbl;   // 3 float4 per frame: (R row i, t_i)
-  // per-point modes
-  const double* __restrict__ frame_time;  // seconds (SLERP)
-  const int64_t* __restrict__ frame_start;// ns (IMU)
-  const int32_t* __restrict__ frame_hint; // segment index at the frame reference time
-  const double* __restrict__ pose_time;   // T
-  const PoseSeg* __restrict__ pose_seg;   // nseg
-  const int64_t* __restrict__ imu_ts;     // M
-  const ImuSeg* __restrict__ imu_seg;     // M
-  int64_t nseg;                           // segments (SLERP: max(T-1,1); IMU: M)
-  int64_t ntab;                           // T or M (length of the time table)
+  const float4* frame_tbl; // frame mode: 3 float4 per frame (R row i, t_i)
+  const double* frame_time;
+  const int64_t* frame_start;
+  const FrameWin* fwin;    // per-point modes
+  const void* frec;        // 2 frame-specialised records per frame (PoseWin or ImuSeg)
+  const double* pose_time; // T
+  const PoseSeg* pose_seg; // nseg
+  const int64_t* imu_ts;   // M
+  const ImuSeg* imu_seg;   // M
+  int64_t nseg;            // segments (SLERP: max(T-1,1); IMU: M)
+  int64_t ntab;            // T or M (length of the time table)
 };
+
+// ---------------------------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------------------------
+// wave-uniform load through the constant address space -> s_load_dword* into SGPRs
+template <typename T>
+__device__ __forceinline__ T ldu(const T* p) {
+  static_assert(sizeof(T) % 4 == 0, "ldu needs a dword-multiple type");
+  struct Raw { int v[sizeof(T) / 4]; };
+  typedef __attribute__((address_space(4))) const int CI;
+  CI* q = (CI*)(p);
+  Raw r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) r.v[i] = q[i];
+  return __builtin_bit_cast(T, r);
+}
 
 // 16-byte non-temporal store (output is written once and never re-read by this kernel)
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -90,9 +115,6 @@ __device__ __forceinline__ void st_nt(float* p, const float4& v) {
   __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
 }
 
-// ---------------------------------------------------------------------------------------------
-// small helpers
-// ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
@@ -104,28 +126,12 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
-// number of entries of the non-decreasing table a[0..n) that are <= x, searched by galloping
-// from `hint` (an index whose entry is usually close to x).  == numpy searchsorted(a, x, 'right').
+// entries of the non-decreasing a[0..n) that are <= x  == numpy searchsorted(a, x, 'right')
 template <typename T>
-__device__ __forceinline__ int64_t upper_bound_from(const T* a, int64_t n, T x, int64_t hint) {
-  int64_t lo, hi;  // invariant: a[lo-1] <= x (or lo == 0), a[hi] > x (or hi == n)
-  if (hint < 0) hint = 0;
-  if (hint >= n) hint = n - 1;
-  if (a[hint] <= x) {
-    lo = hint + 1;
-    int64_t step = 1;
-    hi = lo;
-    while (hi < n && a[hi] <= x) { lo = hi + 1; hi = lo + step; step <<= 1; }
-    if (hi > n) hi = n;
-  } else {
-    hi = hint;
-    int64_t step = 1;
-    lo = hi - 1;
-    while (lo >= 0 && a[lo] > x) { hi = lo; lo = hi - 1 - step; step <<= 1; }
-    lo = lo < 0 ? 0 : lo + 1;
-  }
+__device__ __forceinline__ int64_t upper_bound(const T* a, int64_t n, T x) {
+  int64_t lo = 0, hi = n;
   while (lo < hi) {
-    int64_t mid = lo + ((hi - lo) >> 1);
+    const int64_t mid = lo + ((hi - lo) >> 1);
     if (a[mid] <= x) lo = mid + 1; else hi = mid;
   }
   return lo;
@@ -135,7 +141,7 @@ __device__ __forceinline__ int64_t upper_bound_from(const T* a, int64_t n, T x, 
 __device__ __forceinline__ int64_t lower_bound_f64(const double* a, int64_t n, double x) {
   int64_t lo = 0, hi = n;
   while (lo < hi) {
-    int64_t mid = lo + ((hi - lo) >> 1);
+    const int64_t mid = lo + ((hi - lo) >> 1);
     if (a[mid] < x) lo = mid + 1; else hi = mid;
   }
   return lo;
@@ -164,6 +170,70 @@ __device__ __forceinline__ void euler_xyz_quat(double r, double p, double y, dou
   q[3] = cr * cp * cy + sr * sp * sy;
 }
 
+// segment k of the pose table: shortest-arc quaternion pair, Theta, position delta
+__device__ __forceinline__ PoseSeg make_pose_seg(const double* time, const double* pos, const double* rpy,
+                                                 int64_t T, int64_t k) {
+  const int64_t k1 = (k + 1 < T) ? k + 1 : k;
+  double q0[4], q1[4];
+  euler_xyz_quat(rpy[3 * k], rpy[3 * k + 1], rpy[3 * k + 2], q0);
+  euler_xyz_quat(rpy[3 * k1], rpy[3 * k1 + 1], rpy[3 * k1 + 2], q1);
+  double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
+  if (d < 0.0) { d = -d; q1[0] = -q1[0]; q1[1] = -q1[1]; q1[2] = -q1[2]; q1[3] = -q1[3]; }
+  if (d > 1.0) d = 1.0;
+  const double th = acos(d);
+  const bool small = th < 1e-6;
+  const double inv_sin = small ? 0.0 : 1.0 / sin(th);
+  PoseSeg s;
+  s.q0 = make_float4((float)q0[0], (float)q0[1], (float)q0[2], (float)q0[3]);
+  s.q1 = make_float4((float)q1[0], (float)q1[1], (float)q1[2], (float)q1[3]);
+  const double* p0 = pos + 3 * k;
+  const double* p1 = pos + 3 * k1;
+  s.p0c = make_float4((float)p0[0], (float)p0[1], (float)p0[2], (float)d);
+  s.dpt = make_float4((float)(p1[0] - p0[0]), (float)(p1[1] - p0[1]), (float)(p1[2] - p0[2]), (float)th);
+  s.misc = make_float4((float)inv_sin, small ? 1.f : 0.f, 0.f, 0.f);
+  s.t0 = time[k];
+  const double dt = time[k1] - time[k];
+  s.inv_dt = dt > 0.0 ? 1.0 / dt : 0.0;
+  return s;
+}
+
+// IMU record k (CSIM:1482-1516): the bracketing pair (k, k+1), or the last sample alone
+__device__ __forceinline__ ImuSeg make_imu_seg(const int64_t* ts, const double* gyro, int64_t M, int64_t k) {
+  ImuSeg s;
+  const double* g = gyro + 3 * k;
+  s.g[0] = g[0]; s.g[1] = g[1]; s.g[2] = g[2];
+  if (k + 1 < M) {
+    const double* g1 = gyro + 3 * (k + 1);
+    s.dg[0] = g1[0] - g[0]; s.dg[1] = g1[1] - g[1]; s.dg[2] = g1[2] - g[2];
+    const int64_t dtn = ts[k + 1] - ts[k];
+    s.inv_dt = dtn > 0 ? 1.0 / (double)dtn : 0.0;
+  } else {
+    s.dg[0] = s.dg[1] = s.dg[2] = 0.0;
+    s.inv_dt = 0.0;
+  }
+  s.ts = ts[k];
+  return s;
+}
+
+__device__ __forceinline__ PoseWin make_pose_win(const PoseSeg& s, double tf) {
+  PoseWin w;
+  w.q0 = s.q0; w.q1 = s.q1; w.p0c = s.p0c; w.dpt = s.dpt;
+  w.inv_sin = s.misc.x;
+  w.small = s.misc.y;
+  // alpha = (tf + t_ns*1e-9 - t0) * inv_dt = t_ns * (1e-9*inv_dt) + (tf - t0)*inv_dt
+  w.off = (float)((tf - s.t0) * s.inv_dt);
+  w.scale = (float)(1e-9 * s.inv_dt);
+  return w;
+}
+
+// smallest integer n with tf + n*1e-9 >= t_abs (segment boundary in frame-relative ns)
+__device__ __forceinline__ int64_t rel_ns_ceil(double t_abs, double tf) {
+  double v = ceil((t_abs - tf) * 1e9);
+  if (v > 4.0e18) v = 4.0e18;
+  if (v < -4.0e18) v = -4.0e18;
+  return (int64_t)v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_prep: everything per step that is per frame or per pose/IMU sample (a few thousand threads)
 // ---------------------------------------------------------------------------------------------
@@ -171,14 +241,11 @@ struct PrepArgs {
   int mode;
   int pose_select;
   int32_t n_frames;
-  // trajectory
-  const double* time; const double* pos; const double* rpy; int64_t T;
-  // imu
-  const int64_t* imu_ts; const double* gyro; int64_t M;
-  // frames
-  const double* frame_time; const int64_t* frame_start;
-  // outputs
-  float4* frame_tbl; PoseSeg* pose_seg; ImuSeg* imu_seg; int32_t* frame_hint;
+  const double* time; const double* pos; const double* rpy; int64_t T;   // trajectory
+  const int64_t* imu_ts; const double* gyro; int64_t M;                  // IMU
+  const double* frame_time; const int64_t* frame_start; const int2* trange;  // frames
+  float4* frame_tbl; PoseSeg* pose_seg; ImuSeg* imu_seg;                 // outputs
+  FrameWin* fwin; void* frec;
   int64_t nseg;
 };
 
@@ -204,61 +271,53 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
     return;
   }
   if (a.mode == 1) {
-    if (gid < a.nseg) {
-      const int64_t k = gid, k1 = (k + 1 < a.T) ? k + 1 : k;
-      double q0[4], q1[4];
-      euler_xyz_quat(a.rpy[3 * k], a.rpy[3 * k + 1], a.rpy[3 * k + 2], q0);
-      euler_xyz_quat(a.rpy[3 * k1], a.rpy[3 * k1 + 1], a.rpy[3 * k1 + 2], q1);
-      double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
-      if (d < 0.0) { d = -d; q1[0] = -q1[0]; q1[1] = -q1[1]; q1[2] = -q1[2]; q1[3] = -q1[3]; }
-      if (d > 1.0) d = 1.0;
-      const double th = acos(d);
-      const bool small = th < 1e-6;
-      const double inv_sin = small ? 0.0 : 1.0 / sin(th);
-      PoseSeg s;
-      s.q0 = make_float4((float)q0[0], (float)q0[1], (float)q0[2], (float)q0[3]);
-      s.q1 = make_float4((float)q1[0], (float)q1[1], (float)q1[2], (float)q1[3]);
-      const double* p0 = a.pos + 3 * k;
-      const double* p1 = a.pos + 3 * k1;
-      s.p0c = make_float4((float)p0[0], (float)p0[1], (float)p0[2], (float)d);
-      s.dpt = make_float4((float)(p1[0] - p0[0]), (float)(p1[1] - p0[1]), (float)(p1[2] - p0[2]), (float)th);
-      s.misc = make_float4((float)inv_sin, small ? 1.f : 0.f, 0.f, 0.f);
-      s.t0 = a.time[k];
-      const double dt = a.time[k1] - a.time[k];
-      s.inv_dt = dt > 0.0 ? 1.0 / dt : 0.0;
-      a.pose_seg[k] = s;
-    }
-    if (gid < a.n_frames) {
-      int64_t k = upper_bound_from(a.time, a.T, a.frame_time[gid], (int64_t)0) - 1;
-      if (k > a.nseg - 1) k = a.nseg - 1;
-      if (k < 0) k = 0;
-      a.frame_hint[gid] = (int32_t)k;
-    }
-    return;
+    if (gid < a.nseg) a.pose_seg[gid] = make_pose_seg(a.time, a.pos, a.rpy, a.T, gid);
+  } else {
+    if (gid < a.M) a.imu_seg[gid] = make_imu_seg(a.imu_ts, a.gyro, a.M, gid);
   }
-  // mode 2: IMU records (CSIM:1482-1516)
-  if (gid < a.M) {
-    const int64_t k = gid;
-    ImuSeg s;
-    const double* g = a.gyro + 3 * k;
-    s.g[0] = g[0]; s.g[1] = g[1]; s.g[2] = g[2];
-    if (k + 1 < a.M) {
-      const double* g1 = a.gyro + 3 * (k + 1);
-      s.dg[0] = g1[0] - g[0]; s.dg[1] = g1[1] - g[1]; s.dg[2] = g1[2] - g[2];
-      const int64_t dtn = a.imu_ts[k + 1] - a.imu_ts[k];
-      s.inv_dt = dtn > 0 ? 1.0 / (double)dtn : 0.0;
+  if (gid >= a.n_frames) return;
+  // per-frame window from the frame's time span (recorded when t_ns was staged)
+  const int2 tr = a.trange[gid];
+  FrameWin fw;
+  int64_t klo = 0, khi = 0;
+  if (tr.x <= tr.y) {
+    if (a.mode == 1) {
+      const double tf = a.frame_time[gid];
+      klo = upper_bound(a.time, a.T, tf + (double)tr.x * 1e-9) - 1;
+      khi = upper_bound(a.time, a.T, tf + (double)tr.y * 1e-9) - 1;
+      klo = klo < 0 ? 0 : (klo > a.nseg - 1 ? a.nseg - 1 : klo);
+      khi = khi < 0 ? 0 : (khi > a.nseg - 1 ? a.nseg - 1 : khi);
     } else {
-      s.dg[0] = s.dg[1] = s.dg[2] = 0.0;
-      s.inv_dt = 0.0;
+      const int64_t fs = a.frame_start[gid];
+      klo = upper_bound(a.imu_ts, a.M, fs + (int64_t)tr.x) - 1;
+      khi = upper_bound(a.imu_ts, a.M, fs + (int64_t)tr.y) - 1;
+      klo = klo < 0 ? 0 : klo;
+      khi = khi < 0 ? 0 : khi;
     }
-    s.ts = a.imu_ts[k];
-    a.imu_seg[k] = s;
   }
-  if (gid < a.n_frames) {
-    int64_t k = upper_bound_from(a.imu_ts, a.M, a.frame_start[gid], (int64_t)0) - 1;
-    if (k < 0) k = 0;
-    a.frame_hint[gid] = (int32_t)k;
+  const int64_t W = khi - klo + 1;
+  fw.klo = (int32_t)klo;
+  fw.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
+  if (a.mode == 1) {
+    const double tf = a.frame_time[gid];
+    fw.bnd1 = W >= 2 ? rel_ns_ceil(a.time[klo + 1], tf) : INT64_MAX;
+    PoseWin* rec = reinterpret_cast<PoseWin*>(a.frec) + 2 * gid;
+    rec[0] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, klo), tf);
+    if (W >= 2) rec[1] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, klo + 1), tf);
+  } else {
+    const int64_t fs = a.frame_start[gid];
+    fw.bnd1 = W >= 2 ? a.imu_ts[klo + 1] - fs : INT64_MAX;
+    ImuSeg* rec = reinterpret_cast<ImuSeg*>(a.frec) + 2 * gid;
+    ImuSeg s0 = make_imu_seg(a.imu_ts, a.gyro, a.M, klo);
+    s0.ts -= fs;
+    rec[0] = s0;
+    if (W >= 2) {
+      ImuSeg s1 = make_imu_seg(a.imu_ts, a.gyro, a.M, klo + 1);
+      s1.ts -= fs;
+      rec[1] = s1;
+    }
   }
+  a.fwin[gid] = fw;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -266,10 +325,10 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-    const Tile tl = a.tiles[tile];
-    const float4 r0 = a.frame_tbl[3 * tl.frame + 0];
-    const float4 r1 = a.frame_tbl[3 * tl.frame + 1];
-    const float4 r2 = a.frame_tbl[3 * tl.frame + 2];
+    const Tile tl = ldu(a.tiles + tile);
+    const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
+    const float4 r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
+    const float4 r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
     const float* ix = a.in + tl.pstart;
     float* ox = a.out + tl.pstart;
     float4 vx[kIters], vy[kIters], vz[kIters], vi[kIters];
@@ -343,25 +402,6 @@ __device__ __forceinline__ void sincos_f32arg(float x, float& s, float& c) {
 // ---------------------------------------------------------------------------------------------
 // per-point compute bodies
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ PoseWin make_pose_win(const PoseSeg& s, double tf) {
-  PoseWin w;
-  w.q0 = s.q0; w.q1 = s.q1; w.p0c = s.p0c; w.dpt = s.dpt;
-  w.inv_sin = s.misc.x;
-  w.small = s.misc.y;
-  // alpha = (tf + t_ns*1e-9 - t0) * inv_dt = t_ns * (1e-9*inv_dt) + (tf - t0)*inv_dt
-  w.off = (float)((tf - s.t0) * s.inv_dt);
-  w.scale = (float)(1e-9 * s.inv_dt);
-  return w;
-}
-
-// smallest integer n with tf + n*1e-9 >= t_abs (boundary of a segment in frame-relative ns)
-__device__ __forceinline__ int64_t rel_ns_ceil(double t_abs, double tf) {
-  double v = ceil((t_abs - tf) * 1e9);
-  if (v > 4.0e18) v = 4.0e18;
-  if (v < -4.0e18) v = -4.0e18;
-  return (int64_t)v;
-}
-
 // quaternion SLERP + position LERP at alpha, then p' = R(q) p + pos  
 __device__ __forceinline__ void slerp_point(const PoseWin& w, int t, float& x, float& y, float& z) {
   float al = fmaf((float)t, w.scale, w.off);
@@ -393,7 +433,7 @@ __device__ __forceinline__ void slerp_point(const PoseWin& w, int t, float& x, f
 
 // Path B body (CSIM:1447-1465): w = g + alpha*dg (alpha from the bracketing IMU samples),
 // theta = w * dt, p' = Rx(-theta_x) Ry(-theta_y) Rz(-theta_z) p.  The angle is formed in f64
-// (gyro spikes at yaw wraps reach ~1e3 rad/s) and range-reduced before the f32 sincos.
+// (gyro spikes at yaw wraps reach ~1e2-1e3 rad/s) and range-reduced before the f32 polynomials.
 __device__ __forceinline__ void imu_point(const ImuSeg& w, int t, float& x, float& y, float& z) {
   double al = (double)((int64_t)t - w.ts) * w.inv_dt;
   al = al > 0.0 ? al : 0.0;
@@ -423,22 +463,39 @@ __device__ __forceinline__ int i4c(const int4& v, int c) {
 
 // window search: index of the window segment of frame-relative time t (bnd sorted, bnd[0] unused)
 __device__ __forceinline__ int win_index(const int64_t* bnd, int W, int64_t t) {
-  if (W <= 8) {
+  if (W <= 4) {
     int k = 0;
     for (int j = 1; j < W; ++j) k += (bnd[j] <= t) ? 1 : 0;
     return k;
   }
   int lo = 1, hi = W;   // count entries bnd[1..W) <= t
   while (lo < hi) {
-    int mid = (lo + hi) >> 1;
+    const int mid = (lo + hi) >> 1;
     if (bnd[mid] <= t) lo = mid + 1; else hi = mid;
   }
   return lo - 1;
 }
 
-// out-of-line per-point path for tiles whose time span covers more than kWinMax segments
 template <int MODE>
-__device__ __forceinline__ void deskew_tile_slow(const DeskewArgs& a, const Tile tl, int g0, int64_t klo) {
+__device__ __forceinline__ void point_body(const typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type& w,
+                                           int t, float& x, float& y, float& z) {
+  if constexpr (MODE == 1) slerp_point(w, t, x, y, z);
+  else imu_point(w, t, x, y, z);
+}
+
+template <typename Win>
+__device__ __forceinline__ Win select_win(bool s, const Win& a, const Win& b) {
+  struct Raw { float v[sizeof(Win) / 4]; };
+  const Raw ra = __builtin_bit_cast(Raw, a), rb = __builtin_bit_cast(Raw, b);
+  Raw r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(Win) / 4); ++i) r.v[i] = s ? rb.v[i] : ra.v[i];
+  return __builtin_bit_cast(Win, r);
+}
+
+// per-point path for frames whose points span more than kWinMax segments
+template <int MODE>
+__device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const Tile tl, int g0) {
   const int f = tl.frame;
   const int e_end = 4 * min(tl.ngroups, g0 + kBlock);
   for (int e = 4 * g0 + threadIdx.x; e < e_end; e += kBlock) {
@@ -448,12 +505,12 @@ __device__ __forceinline__ void deskew_tile_slow(const DeskewArgs& a, const Tile
     const int t = a.tns[p];
     if constexpr (MODE == 1) {
       const double tf = a.frame_time[f];
-      int64_t k = upper_bound_from(a.pose_time, a.ntab, tf + (double)t * 1e-9, klo) - 1;
+      int64_t k = upper_bound(a.pose_time, a.ntab, tf + (double)t * 1e-9) - 1;
       if (k > a.nseg - 1) k = a.nseg - 1;
       if (k < 0) k = 0;
       slerp_point(make_pose_win(a.pose_seg[k], tf), t, x, y, z);
     } else {
-      int64_t k = upper_bound_from(a.imu_ts, a.ntab, a.frame_start[f] + (int64_t)t, klo) - 1;
+      int64_t k = upper_bound(a.imu_ts, a.ntab, a.frame_start[f] + (int64_t)t) - 1;
       if (k < 0) k = 0;
       ImuSeg w = a.imu_seg[k];
       w.ts -= a.frame_start[f];
@@ -463,148 +520,108 @@ __device__ __forceinline__ void deskew_tile_slow(const DeskewArgs& a, const Tile
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// per-point modes: one kernel template, MODE 1 = SLERP, MODE 2 = IMU
-// ---------------------------------------------------------------------------------------------
-// wave-uniform copy of an LDS value into SGPRs (the W == 1 fast path: one segment per sub-tile)
-__device__ __forceinline__ float sgpr(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
-}
-__device__ __forceinline__ double sgpr(double v) {
-  const int64_t u = __builtin_bit_cast(int64_t, v);
-  const int lo = __builtin_amdgcn_readfirstlane((int)(u & 0xffffffff));
-  const int hi = __builtin_amdgcn_readfirstlane((int)(u >> 32));
-  return __builtin_bit_cast(double, ((int64_t)hi << 32) | (int64_t)(uint32_t)lo);
-}
-__device__ __forceinline__ int64_t sgpr(int64_t v) {
-  return __builtin_bit_cast(int64_t, sgpr(__builtin_bit_cast(double, v)));
-}
-__device__ __forceinline__ float4 sgpr(float4 v) { return make_float4(sgpr(v.x), sgpr(v.y), sgpr(v.z), sgpr(v.w)); }
-__device__ __forceinline__ PoseWin sgpr(const PoseWin& w) {
-  PoseWin r;
-  r.q0 = sgpr(w.q0); r.q1 = sgpr(w.q1); r.p0c = sgpr(w.p0c); r.dpt = sgpr(w.dpt);
-  r.inv_sin = sgpr(w.inv_sin); r.small = sgpr(w.small); r.off = sgpr(w.off); r.scale = sgpr(w.scale);
-  return r;
-}
-__device__ __forceinline__ ImuSeg sgpr(const ImuSeg& w) {
-  ImuSeg r;
-  for (int j = 0; j < 3; ++j) { r.g[j] = sgpr(w.g[j]); r.dg[j] = sgpr(w.dg[j]); }
-  r.inv_dt = sgpr(w.inv_dt);
-  r.ts = sgpr(w.ts);
-  return r;
-}
-
-// Per-point modes: MODE 1 = SLERP, MODE 2 = IMU.  A workgroup works on a sub-tile of
-// kBlock float4 groups (1024 points; a batch tile holds kSub of them): every thread loads one
-// float4 of each column + one int4 of t_ns, the workgroup reduces the sub-tile's time span,
-// stages the pose/IMU segments covering it into LDS, and every point then picks its segment.
-constexpr int kSub = kTileGroups / kBlock;
-
+// Per-point modes: MODE 1 = SLERP, MODE 2 = IMU.  A workgroup works on a sub-tile of kBlock
+// float4 groups (1024 points of one frame).  The frame's segment window (k_prep) decides the path,
+// uniformly for the whole workgroup:
+//   W <= 2      both frame-specialised records come in through scalar loads (SGPRs); each wave
+//               votes whether its points all sit in one segment (no LDS, no barrier);
+//   W <= 64     the window's records are staged into LDS once (one barrier), each point picks its
+//               segment by searching the boundaries;
+//   W > 64      pathological span: per-point search of the global tables.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
   using Win = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
   __shared__ Win s_win[kWinMax];
   __shared__ int64_t s_bnd[kWinMax];
-  __shared__ int s_red[2][kBlock / 64];
-  __shared__ int64_t s_hdr[2];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x;
   const int64_t n_sub = (int64_t)a.n_tiles * kSub;
+  const Win* frec = reinterpret_cast<const Win*>(a.frec);
 
   for (int64_t st = blockIdx.x; st < n_sub; st += gridDim.x) {
-    const Tile tl = a.tiles[st / kSub];
+    const Tile tl = ldu(a.tiles + st / kSub);
     const int g0 = (int)(st % kSub) * kBlock;
     if (g0 >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
     const int f = tl.frame;
+    const FrameWin fw = ldu(a.fwin + f);
+    if (fw.W > kWinMax) {
+      deskew_subtile_slow<MODE>(a, tl, g0);
+      continue;
+    }
     const int g = g0 + tid;
     const bool act = g < tl.ngroups;
     const int64_t p = tl.pstart + 4 * (int64_t)g;
 
     float4 X, Y, Z, I;
     int4 Tq;
-    int tmin = INT_MAX, tmax = INT_MIN;
     if (act) {
       Tq = *reinterpret_cast<const int4*>(a.tns + p);
       X = *reinterpret_cast<const float4*>(a.in + p);
       Y = *reinterpret_cast<const float4*>(a.in + a.in_cap + p);
       Z = *reinterpret_cast<const float4*>(a.in + 2 * a.in_cap + p);
       I = *reinterpret_cast<const float4*>(a.in + 3 * a.in_cap + p);
-      tmin = min(min(Tq.x, Tq.y), min(Tq.z, Tq.w));
-      tmax = max(max(Tq.x, Tq.y), max(Tq.z, Tq.w));
     }
-    tmin = wave_min(tmin);
-    tmax = wave_max(tmax);
-    if (lane == 0) { s_red[0][wid] = tmin; s_red[1][wid] = tmax; }
-    __syncthreads();
-    if (wid == 0 && lane < 2) {
-      int tv = s_red[lane][0];
-      for (int w = 1; w < kBlock / 64; ++w)
-        tv = lane == 0 ? min(tv, s_red[0][w]) : max(tv, s_red[1][w]);
-      // lanes 0/1 search the two window ends concurrently, galloping from the frame's hint
-      int64_t k;
-      if constexpr (MODE == 1) {
-        const double tq = a.frame_time[f] + (double)tv * 1e-9;
-        k = upper_bound_from(a.pose_time, a.ntab, tq, (int64_t)a.frame_hint[f]) - 1;
-        if (k > a.nseg - 1) k = a.nseg - 1;
-      } else {
-        const int64_t tq = a.frame_start[f] + (int64_t)tv;
-        k = upper_bound_from(a.imu_ts, a.ntab, tq, (int64_t)a.frame_hint[f]) - 1;
-      }
-      if (k < 0) k = 0;
-      s_hdr[lane] = k;
-    }
-    __syncthreads();
-    const int64_t klo = s_hdr[0];
-    const int64_t W64 = s_hdr[1] - klo + 1;
-    const int W = W64 > kWinMax ? kWinMax + 1 : (int)W64;
-    if (W > kWinMax) {
-      // pathological time span (more than kWinMax segments in 1024 points): out-of-line path
-      deskew_tile_slow<MODE>(a, tl, g0, klo);
-      __syncthreads();
-      continue;
-    }
-    if (tid < W) {
-      const int64_t k = klo + tid;
-      if constexpr (MODE == 1) {
-        const double tf = a.frame_time[f];
-        s_win[tid] = make_pose_win(a.pose_seg[k], tf);
-        s_bnd[tid] = rel_ns_ceil(a.pose_time[k], tf);
-      } else {
-        ImuSeg sg = a.imu_seg[k];
-        sg.ts -= a.frame_start[f];
-        s_win[tid] = sg;
-        s_bnd[tid] = sg.ts;
-      }
-    }
-    __syncthreads();
 
-    if (act) {
-      if (W == 1) {
-        const Win w = sgpr(s_win[0]);
+    if (fw.W <= 2) {
+      const Win r0 = ldu(frec + 2 * f);
+      bool use1 = false, mixed = false;
+      if (fw.W == 2) {
+        const int64_t b1 = fw.bnd1;
+        const bool any1 = act && ((int64_t)Tq.w >= b1 || (int64_t)Tq.x >= b1 || (int64_t)Tq.y >= b1 || (int64_t)Tq.z >= b1);
+        const bool any0 = act && ((int64_t)Tq.w < b1 || (int64_t)Tq.x < b1 || (int64_t)Tq.y < b1 || (int64_t)Tq.z < b1);
+        const bool w1 = __any(any1), w0 = __any(any0);
+        use1 = w1 && !w0;
+        mixed = w1 && w0;
+      }
+      if (act) {
+        if (!mixed) {
+          const Win w = use1 ? ldu(frec + 2 * f + 1) : r0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if constexpr (MODE == 1) slerp_point(w, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
-          else imu_point(w, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
+          for (int c = 0; c < 4; ++c) point_body<MODE>(w, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
+        } else {
+          const Win r1 = ldu(frec + 2 * f + 1);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int t = i4c(Tq, c);
+            point_body<MODE>(select_win((int64_t)t >= fw.bnd1, r0, r1), t, f4c(X, c), f4c(Y, c), f4c(Z, c));
+          }
         }
-      } else {
+      }
+    } else {
+      const int W = fw.W;
+      if (tid < W) {
+        const int64_t k = fw.klo + tid;
+        if constexpr (MODE == 1) {
+          const double tf = a.frame_time[f];
+          s_win[tid] = make_pose_win(a.pose_seg[k], tf);
+          s_bnd[tid] = rel_ns_ceil(a.pose_time[k], tf);
+        } else {
+          ImuSeg sg = a.imu_seg[k];
+          sg.ts -= a.frame_start[f];
+          s_win[tid] = sg;
+          s_bnd[tid] = sg.ts;
+        }
+      }
+      __syncthreads();
+      if (act) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int t = i4c(Tq, c);
-          const int k = win_index(s_bnd, W, (int64_t)t);
-          if constexpr (MODE == 1) slerp_point(s_win[k], t, f4c(X, c), f4c(Y, c), f4c(Z, c));
-          else imu_point(s_win[k], t, f4c(X, c), f4c(Y, c), f4c(Z, c));
+          point_body<MODE>(s_win[win_index(s_bnd, W, (int64_t)t)], t, f4c(X, c), f4c(Y, c), f4c(Z, c));
         }
       }
+      __syncthreads();  // the LDS window is rewritten by the next sub-tile
+    }
+    if (act) {
       st_nt(a.out + p, X);
       st_nt(a.out + a.out_cap + p, Y);
       st_nt(a.out + 2 * a.out_cap + p, Z);
       st_nt(a.out + 3 * a.out_cap + p, I);
     }
-    __syncthreads();  // the LDS window is rewritten by the next sub-tile
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// layout / staging kernels (not the hot path; PCIe-bound when fed from the host)
+// layout / staging kernels (not the per-step path; PCIe-bound when fed from the host)
 // ---------------------------------------------------------------------------------------------
 struct LayoutArgs {
   const Tile* tiles; int32_t n_tiles;
@@ -663,6 +680,32 @@ __global__ __launch_bounds__(kBlock) void k_column(const LayoutArgs a, const T* 
       const int64_t i = local_index(a, tl, p);
       if (DIR == 0) dst[p] = i >= 0 ? src[d0 + i] : T(0);
       else if (i >= 0) dst[d0 + i] = src[p];
+    }
+  }
+}
+
+// per-frame [min, max] of t_ns over the valid points (feeds k_prep's frame windows)
+__global__ __launch_bounds__(kBlock) void k_trange_init(int2* tr, int32_t F) {
+  const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (f < F) tr[f] = make_int2(INT_MAX, INT_MIN);
+}
+__global__ __launch_bounds__(kBlock) void k_trange(const LayoutArgs a, int2* tr) {
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = a.tiles[tile];
+    int lo = INT_MAX, hi = INT_MIN;
+    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
+      const int64_t p = tl.pstart + e;
+      if (local_index(a, tl, p) >= 0) {
+        const int t = a.tns[p];
+        lo = min(lo, t);
+        hi = max(hi, t);
+      }
+    }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if ((threadIdx.x & 63) == 0 && lo <= hi) {
+      atomicMin(&tr[tl.frame].x, lo);
+      atomicMax(&tr[tl.frame].y, hi);
     }
   }
 }

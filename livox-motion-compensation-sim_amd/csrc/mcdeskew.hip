@@ -139,6 +139,19 @@ static int download_column(mc_batch* b, const T* src_col, T* dst) {
   return MC_OK;
 }
 
+// per-frame t_ns span, recomputed whenever the t column is written (staging time, not per step)
+static int compute_trange(mc_batch* b) {
+  mc_ctx* c = b->ctx;
+  if (b->F == 0 || !b->d_t) { b->trange_valid = true; return MC_OK; }
+  hipLaunchKernelGGL(k_trange_init, dim3((b->F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, b->d_trange, b->F);
+  if (b->n_tiles > 0)
+    hipLaunchKernelGGL(k_trange, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
+                       b->d_trange);
+  HIPCHK(hipGetLastError());
+  b->trange_valid = true;
+  return MC_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
@@ -296,7 +309,11 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
   if ((r = dev_alloc(&b->d_frame_time, F))) return bail(r);
   if ((r = dev_alloc(&b->d_frame_start, F))) return bail(r);
   if ((r = dev_alloc(&b->d_frame_tbl, 3 * (size_t)F))) return bail(r);
-  if ((r = dev_alloc(&b->d_frame_hint, F))) return bail(r);
+  if ((r = dev_alloc(&b->d_trange, F))) return bail(r);
+  if ((r = dev_alloc(&b->d_fwin, F))) return bail(r);
+  if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_frec), 2 * (size_t)std::max<int>(F, 1) *
+                                                             std::max(sizeof(PoseWin), sizeof(ImuSeg)))))
+    return bail(r);
   if ((r = dev_alloc(&b->d_partial, 5 * (size_t)b->n_tiles))) return bail(r);
   hipStream_t s = c->stream;
   auto cpy = [&](void* d, const void* h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s); };
@@ -324,7 +341,9 @@ int mc_batch_destroy(mc_batch* b) {
   (void)hipStreamSynchronize(b->ctx->stream);
   dev_free(b->d_cols); dev_free(b->d_t); dev_free(b->d_counts); dev_free(b->d_poff); dev_free(b->d_doff);
   dev_free(b->d_tiles); dev_free(b->d_frame_time); dev_free(b->d_frame_start); dev_free(b->d_frame_tbl);
-  dev_free(b->d_frame_hint); dev_free(b->d_partial);
+  dev_free(b->d_trange); dev_free(b->d_fwin); dev_free(b->d_partial);
+  if (b->d_frec) (void)hipFree(b->d_frec);
+  b->d_frec = nullptr;
   delete b;
   return MC_OK;
 }
@@ -402,7 +421,10 @@ int mc_batch_upload_time_ns(mc_batch* b, const int32_t* t) {
   if (b->N == 0) return MC_OK;
   CHECK_ARG(t, "t_ns is NULL");
   DeviceGuard g(b->ctx->device);
-  return upload_column<int32_t>(b, t, b->d_t);
+  if (int r = upload_column<int32_t>(b, t, b->d_t)) return r;
+  if (int r = compute_trange(b)) return r;
+  HIPCHK(hipStreamSynchronize(b->ctx->stream));
+  return MC_OK;
 }
 
 int mc_batch_download_aos_f64(mc_batch* b, double* aos) {
@@ -449,6 +471,7 @@ int mc_batch_synth(mc_batch* b, uint64_t seed, int64_t frame_id_base) {
   hipLaunchKernelGGL(k_synth, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b), seed,
                      frame_id_base);
   HIPCHK(hipGetLastError());
+  if (int r = compute_trange(b)) return r;
   HIPCHK(hipStreamSynchronize(c->stream));
   return MC_OK;
 }
@@ -497,6 +520,8 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   if (in->F == 0) return MC_OK;
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  if (mode != MC_MODE_FRAME && !in->trange_valid)
+    if (int r = compute_trange(const_cast<mc_batch*>(in))) return r;
   const mc_batch* pb = in;  // per-frame tables live with the input batch
 
   PrepArgs pa;
@@ -506,9 +531,9 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   pa.n_frames = in->F;
   pa.time = c->d_time; pa.pos = c->d_pos; pa.rpy = c->d_rpy; pa.T = c->T;
   pa.imu_ts = c->d_imu_ts; pa.gyro = c->d_gyro; pa.M = c->M;
-  pa.frame_time = pb->d_frame_time; pa.frame_start = pb->d_frame_start;
+  pa.frame_time = pb->d_frame_time; pa.frame_start = pb->d_frame_start; pa.trange = pb->d_trange;
   pa.frame_tbl = pb->d_frame_tbl; pa.pose_seg = c->d_pose_seg; pa.imu_seg = c->d_imu_seg;
-  pa.frame_hint = pb->d_frame_hint;
+  pa.fwin = pb->d_fwin; pa.frec = pb->d_frec;
   int64_t prep_n = in->F;
   if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); prep_n = std::max<int64_t>(prep_n, pa.nseg); }
   if (mode == MC_MODE_IMU) { pa.nseg = c->M; prep_n = std::max<int64_t>(prep_n, c->M); }
@@ -525,7 +550,8 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   da.out = out->d_cols; da.out_cap = out->cap;
   da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
   da.frame_tbl = pb->d_frame_tbl;
-  da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start; da.frame_hint = pb->d_frame_hint;
+  da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start;
+  da.fwin = pb->d_fwin; da.frec = pb->d_frec;
   da.pose_time = c->d_time; da.pose_seg = c->d_pose_seg;
   da.imu_ts = c->d_imu_ts; da.imu_seg = c->d_imu_seg;
   if (mode == MC_MODE_POSE_SLERP) { da.nseg = pa.nseg; da.ntab = c->T; }
