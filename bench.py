@@ -117,7 +117,7 @@ def main():
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     rdv = mc.dist.Rendezvous(rank, world)
-    ctx = mc.Context(local_rank)
+    ctx = mc.Context()   # $MCDESKEW_DEVICE, else $LOCAL_RANK
 
     cfg, tr, times, lo = workload(rank, world, args.frames, args.points)
     counts = np.full(args.frames, args.points, dtype=np.int64)

@@ -108,11 +108,12 @@ def load(path: str | None = None):
     return lib
 
 
-def check(rc: int, what: str = "") -> None:
+def check(rc: int, what: str = "", lib=None) -> None:
     """Map a C status code to the reference-compatible Python exception."""
     if rc == MC_OK:
         return
-    msg = (_lib.mc_last_error() or b"").decode(errors="replace") if _lib is not None else ""
+    src = lib if lib is not None else _lib
+    msg = (src.mc_last_error() or b"").decode(errors="replace") if src is not None else ""
     if what:
         msg = f"{what}: {msg}"
     if rc == MC_ERR_INVALID:

@@ -25,8 +25,19 @@
 
 namespace mc {
 
+// Build-time knobs (tools/ab.py builds variants of these and times them in one process):
+#ifndef MC_KITERS
+#define MC_KITERS 2          // float4 groups per thread per tile in frame mode
+#endif
+#ifndef MC_NT_STORE
+#define MC_NT_STORE 1        // non-temporal output stores
+#endif
+#ifndef MC_POINTS_WAVES
+#define MC_POINTS_WAVES 0    // min waves/SIMD requested for the per-point kernels (0: compiler's choice)
+#endif
+
 constexpr int kBlock = 256;                    // 4 waves of 64
-constexpr int kIters = 2;                      // float4 groups per thread per tile (frame mode)
+constexpr int kIters = MC_KITERS;              // float4 groups per thread per tile (frame mode)
 constexpr int kTileGroups = kBlock * kIters;   // 512 groups = 2048 points per tile
 constexpr int kSub = kTileGroups / kBlock;     // per-point modes: sub-tiles of kBlock groups
 constexpr int kWinMax = 64;                    // LDS window capacity (segments per frame)
@@ -112,7 +123,11 @@ __device__ __forceinline__ T ldu(const T* p) {
 typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_nt(float* p, const float4& v) {
   v4f t = {v.x, v.y, v.z, v.w};
+#if MC_NT_STORE
   __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
+#else
+  *reinterpret_cast<v4f*>(p) = t;
+#endif
 }
 
 __device__ __forceinline__ int wave_min(int v) {
@@ -249,75 +264,103 @@ struct PrepArgs {
   int64_t nseg;
 };
 
+// Wave-cooperative searches over a sorted table: 64 lanes probe evenly spaced entries per round,
+// so a 3000-pose table takes 2 dependent loads and a 24000-sample IMU table 3 (instead of ~12-15
+// for a single-lane binary search).  STRICT=false: entries <= x (searchsorted 'right');
+// STRICT=true: entries < x (searchsorted 'left').  Every lane returns the same count.
+template <bool STRICT, typename T>
+__device__ __forceinline__ int64_t wave_count(const T* a, int64_t n, T x) {
+  const int lane = threadIdx.x & 63;
+  int64_t lo = 0, hi = n;  // answer in [lo, hi]
+  while (hi - lo > 64) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t idx = lo + lane * step;
+    const bool in = idx < hi && (STRICT ? a[idx] < x : a[idx] <= x);
+    const int c = __popcll(__ballot(in));
+    if (c == 0) return lo;
+    const int64_t nlo = lo + (int64_t)(c - 1) * step + 1;
+    const int64_t nhi = lo + (int64_t)c * step;
+    lo = nlo;
+    hi = nhi < hi ? nhi : hi;
+  }
+  const int64_t idx = lo + lane;
+  const bool in = idx < hi && (STRICT ? a[idx] < x : a[idx] <= x);
+  return lo + __popcll(__ballot(in));
+}
+
+// One wave per frame (frame work), then one lane per pose segment / IMU sample (table work).
 __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
-  const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (a.mode == 0) {
-    // Path A pose selection (LMC:804-812) + Euler->R (LMC:774)
-    if (gid >= a.n_frames) return;
-    int64_t idx;
-    if (a.pose_select == 1) {
-      idx = gid;  // explicit per-frame transformation (host checks T == n_frames)
-    } else {
-      idx = lower_bound_f64(a.time, a.T, a.frame_time[gid]);
-      if (idx > a.T - 1) idx = a.T - 1;
-      if (idx < 0) idx = 0;
-    }
-    double R[9];
-    euler_xyz_matrix(a.rpy[3 * idx], a.rpy[3 * idx + 1], a.rpy[3 * idx + 2], R);
-    const double* t = a.pos + 3 * idx;
-    a.frame_tbl[3 * gid + 0] = make_float4((float)R[0], (float)R[1], (float)R[2], (float)t[0]);
-    a.frame_tbl[3 * gid + 1] = make_float4((float)R[3], (float)R[4], (float)R[5], (float)t[1]);
-    a.frame_tbl[3 * gid + 2] = make_float4((float)R[6], (float)R[7], (float)R[8], (float)t[2]);
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);   // global wave id
+  if (gw >= a.n_frames) {
+    const int64_t k = (gw - a.n_frames) * 64 + lane;
+    if (a.mode == 1 && k < a.nseg) a.pose_seg[k] = make_pose_seg(a.time, a.pos, a.rpy, a.T, k);
+    if (a.mode == 2 && k < a.M) a.imu_seg[k] = make_imu_seg(a.imu_ts, a.gyro, a.M, k);
     return;
   }
-  if (a.mode == 1) {
-    if (gid < a.nseg) a.pose_seg[gid] = make_pose_seg(a.time, a.pos, a.rpy, a.T, gid);
-  } else {
-    if (gid < a.M) a.imu_seg[gid] = make_imu_seg(a.imu_ts, a.gyro, a.M, gid);
+  const int64_t f = gw;
+  if (a.mode == 0) {
+    // Path A pose selection (LMC:804-812) + Euler->R (LMC:774)
+    int64_t idx;
+    if (a.pose_select == 1) {
+      idx = f;  // explicit per-frame transformation (host checks T == n_frames)
+    } else {
+      idx = wave_count<true>(a.time, a.T, a.frame_time[f]);   // searchsorted 'left'
+      if (idx > a.T - 1) idx = a.T - 1;
+    }
+    if (lane < 3) {   // lane i writes row i of R and t_i
+      double R[9];
+      euler_xyz_matrix(a.rpy[3 * idx], a.rpy[3 * idx + 1], a.rpy[3 * idx + 2], R);
+      a.frame_tbl[3 * f + lane] = make_float4((float)R[3 * lane], (float)R[3 * lane + 1], (float)R[3 * lane + 2],
+                                              (float)a.pos[3 * idx + lane]);
+    }
+    return;
   }
-  if (gid >= a.n_frames) return;
   // per-frame window from the frame's time span (recorded when t_ns was staged)
-  const int2 tr = a.trange[gid];
-  FrameWin fw;
+  const int2 tr = a.trange[f];
   int64_t klo = 0, khi = 0;
   if (tr.x <= tr.y) {
     if (a.mode == 1) {
-      const double tf = a.frame_time[gid];
-      klo = upper_bound(a.time, a.T, tf + (double)tr.x * 1e-9) - 1;
-      khi = upper_bound(a.time, a.T, tf + (double)tr.y * 1e-9) - 1;
+      const double tf = a.frame_time[f];
+      klo = wave_count<false>(a.time, a.T, tf + (double)tr.x * 1e-9) - 1;
+      khi = wave_count<false>(a.time, a.T, tf + (double)tr.y * 1e-9) - 1;
       klo = klo < 0 ? 0 : (klo > a.nseg - 1 ? a.nseg - 1 : klo);
       khi = khi < 0 ? 0 : (khi > a.nseg - 1 ? a.nseg - 1 : khi);
     } else {
-      const int64_t fs = a.frame_start[gid];
-      klo = upper_bound(a.imu_ts, a.M, fs + (int64_t)tr.x) - 1;
-      khi = upper_bound(a.imu_ts, a.M, fs + (int64_t)tr.y) - 1;
+      const int64_t fs = a.frame_start[f];
+      klo = wave_count<false>(a.imu_ts, a.M, fs + (int64_t)tr.x) - 1;
+      khi = wave_count<false>(a.imu_ts, a.M, fs + (int64_t)tr.y) - 1;
       klo = klo < 0 ? 0 : klo;
       khi = khi < 0 ? 0 : khi;
     }
   }
   const int64_t W = khi - klo + 1;
-  fw.klo = (int32_t)klo;
-  fw.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
+  if (lane >= 2 || (lane == 1 && W < 2)) return;
+  // lane 0: record klo (+ the window header), lane 1: record klo+1
+  const int64_t k = klo + lane;
   if (a.mode == 1) {
-    const double tf = a.frame_time[gid];
-    fw.bnd1 = W >= 2 ? rel_ns_ceil(a.time[klo + 1], tf) : INT64_MAX;
-    PoseWin* rec = reinterpret_cast<PoseWin*>(a.frec) + 2 * gid;
-    rec[0] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, klo), tf);
-    if (W >= 2) rec[1] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, klo + 1), tf);
+    const double tf = a.frame_time[f];
+    reinterpret_cast<PoseWin*>(a.frec)[2 * f + lane] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, k), tf);
+    if (lane == 0) {
+      FrameWin fw;
+      fw.klo = (int32_t)klo;
+      fw.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
+      fw.bnd1 = W >= 2 ? rel_ns_ceil(a.time[klo + 1], tf) : INT64_MAX;
+      a.fwin[f] = fw;
+    }
   } else {
-    const int64_t fs = a.frame_start[gid];
-    fw.bnd1 = W >= 2 ? a.imu_ts[klo + 1] - fs : INT64_MAX;
-    ImuSeg* rec = reinterpret_cast<ImuSeg*>(a.frec) + 2 * gid;
-    ImuSeg s0 = make_imu_seg(a.imu_ts, a.gyro, a.M, klo);
-    s0.ts -= fs;
-    rec[0] = s0;
-    if (W >= 2) {
-      ImuSeg s1 = make_imu_seg(a.imu_ts, a.gyro, a.M, klo + 1);
-      s1.ts -= fs;
-      rec[1] = s1;
+    const int64_t fs = a.frame_start[f];
+    ImuSeg sg = make_imu_seg(a.imu_ts, a.gyro, a.M, k);
+    sg.ts -= fs;
+    reinterpret_cast<ImuSeg*>(a.frec)[2 * f + lane] = sg;
+    if (lane == 0) {
+      FrameWin fw;
+      fw.klo = (int32_t)klo;
+      fw.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
+      fw.bnd1 = W >= 2 ? a.imu_ts[klo + 1] - fs : INT64_MAX;
+      a.fwin[f] = fw;
     }
   }
-  a.fwin[gid] = fw;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -529,7 +572,11 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
 //               segment by searching the boundaries;
 //   W > 64      pathological span: per-point search of the global tables.
 template <int MODE>
+#if MC_POINTS_WAVES > 0
+__global__ __launch_bounds__(kBlock, MC_POINTS_WAVES) void k_deskew_points(const DeskewArgs a) {
+#else
 __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
+#endif
   using Win = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
   __shared__ Win s_win[kWinMax];
   __shared__ int64_t s_bnd[kWinMax];

@@ -534,12 +534,14 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   pa.frame_time = pb->d_frame_time; pa.frame_start = pb->d_frame_start; pa.trange = pb->d_trange;
   pa.frame_tbl = pb->d_frame_tbl; pa.pose_seg = c->d_pose_seg; pa.imu_seg = c->d_imu_seg;
   pa.fwin = pb->d_fwin; pa.frec = pb->d_frec;
-  int64_t prep_n = in->F;
-  if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); prep_n = std::max<int64_t>(prep_n, pa.nseg); }
-  if (mode == MC_MODE_IMU) { pa.nseg = c->M; prep_n = std::max<int64_t>(prep_n, c->M); }
+  // one wave per frame, then one lane per pose segment / IMU sample
+  int64_t table = 0;
+  if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); table = pa.nseg; }
+  if (mode == MC_MODE_IMU) { pa.nseg = c->M; table = c->M; }
+  const int64_t waves = in->F + (table + 63) / 64;
   {
     TimedRegion tr(c, &c->prep_ev);
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((prep_n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, pa);
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, s, pa);
   }
   HIPCHK(hipGetLastError());
   if (in->n_tiles == 0) return MC_OK;

@@ -26,12 +26,13 @@ def _f64(a, shape_tail=None):
 
 
 class Context:
-    """One device + stream.  ``device`` defaults to $LOCAL_RANK (or 0)."""
+    """One device + stream.  ``device`` defaults to $MCDESKEW_DEVICE, else $LOCAL_RANK, else 0.
+    ``lib_path`` loads an alternative build of the library (A/B variant runs in one process)."""
 
-    def __init__(self, device: int | None = None):
-        self.lib = _lib.load()
+    def __init__(self, device: int | None = None, lib_path: str | None = None):
+        self.lib = _lib.load(lib_path) if lib_path else _lib.load()
         if device is None:
-            device = int(os.environ.get("LOCAL_RANK", "0"))
+            device = int(os.environ.get("MCDESKEW_DEVICE", os.environ.get("LOCAL_RANK", "0")))
         h = c_void_p()
         check(self.lib.mc_create(int(device), ctypes.byref(h)), "mc_create")
         self.handle = h

@@ -1,0 +1,89 @@
+"""Interleaved A/B timing of library variants in ONE process on ONE device (GPU box only).
+
+Each variant .so gets its own context and its own copy of the same workload; rounds alternate
+between variants so clock / thermal drift hits all of them alike (cdna_hip_programming.md §5.4
+rule 24).  Reports median and min of the hot kernel's HIP-event time per variant.
+
+    make -C livox-motion-compensation-sim_amd/csrc variants
+    python tools/ab.py --mode pose_slerp --libs build/variants/lib_base.so,build/variants/lib_w5.so
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import mcamd as mc  # noqa: E402
+
+BYTES = {"pose_slerp": 36, "imu": 36, "frame": 32}
+
+
+def setup(lib, args):
+    ctx = mc.Context(0, lib_path=lib)
+    sim = mc.LiDARMotionSimulator({"duration": 120.0, "trajectory_type": "figure_eight", "max_speed": 12.0,
+                                   "lidar_fps": 10})
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:args.frames]
+    counts = np.full(args.frames, args.points, np.int64)
+    b_in = ctx.batch(counts, with_time=True)
+    b_out = ctx.batch(counts)
+    b_in.synth(seed=0, frame_id_base=1000)
+    b_in.set_frame_times(times)
+    b_in.set_frame_starts((times * 1e9).astype(np.int64))
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    ts, g = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    ctx.set_imu(ts, g)
+    return ctx, b_in, b_out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default=",".join(sorted(glob.glob(os.path.join(ROOT, "build", "variants", "lib_*.so")))))
+    ap.add_argument("--modes", default="pose_slerp,imu,frame")
+    ap.add_argument("--frames", type=int, default=600)
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    libs = [l for l in args.libs.split(",") if l]
+    runs = {lib: setup(lib, args) for lib in libs}
+    n = args.frames * args.points
+    out = {}
+    for mode in args.modes.split(","):
+        per = {lib: [] for lib in libs}
+        for _ in range(args.rounds):
+            for lib in libs:
+                ctx, bi, bo = runs[lib]
+                for _ in range(3):
+                    ctx.deskew(bi, bo, mode=mode)
+                ctx.sync()
+                ctx.read_timing()
+                ctx.timing(True)
+                for _ in range(args.steps):
+                    ctx.deskew(bi, bo, mode=mode)
+                ctx.sync()
+                ctx.timing(False)
+                t = ctx.read_timing()
+                per[lib].append(t["main_ms"] / t["main_launches"] * 1e3)
+        for lib in libs:
+            v = per[lib]
+            med = statistics.median(v)
+            name = os.path.basename(lib)
+            out[f"{mode}/{name}"] = {"median_us": med, "min_us": min(v),
+                                     "GBs": BYTES[mode] * n / (med * 1e-6) / 1e9}
+            print(f"{mode:10s} {name:20s} median {med:8.1f} us  min {min(v):8.1f} us  "
+                  f"{BYTES[mode] * n / (med * 1e-6) / 1e9:7.0f} GB/s", flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "ab.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
