@@ -32,6 +32,15 @@ namespace mc {
 #ifndef MC_NT_STORE
 #define MC_NT_STORE 1        // non-temporal output stores
 #endif
+#ifndef MC_FASTPATH_MAXW
+#define MC_FASTPATH_MAXW 2   // frames spanning <= this many segments take the SGPR (no-LDS) path
+#endif
+#ifndef MC_NULL_COMPUTE
+#define MC_NULL_COMPUTE 0    // diagnostic build: skip the per-point math, keep loads/stores
+#endif
+#ifndef MC_NT_LOAD
+#define MC_NT_LOAD 0         // non-temporal input loads (streamed once)
+#endif
 #ifndef MC_POINTS_WAVES
 #define MC_POINTS_WAVES 0    // min waves/SIMD requested for the per-point kernels (0: compiler's choice)
 #endif
@@ -127,6 +136,25 @@ __device__ __forceinline__ void st_nt(float* p, const float4& v) {
   __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
 #else
   *reinterpret_cast<v4f*>(p) = t;
+#endif
+}
+
+// 16-byte streaming loads of the input columns
+typedef int v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4(const float* p) {
+#if MC_NT_LOAD
+  const v4f t = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+  return make_float4(t.x, t.y, t.z, t.w);
+#else
+  return *reinterpret_cast<const float4*>(p);
+#endif
+}
+__device__ __forceinline__ int4 ld4(const int32_t* p) {
+#if MC_NT_LOAD
+  const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+  return make_int4(t.x, t.y, t.z, t.w);
+#else
+  return *reinterpret_cast<const int4*>(p);
 #endif
 }
 
@@ -379,10 +407,10 @@ __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
     for (int it = 0; it < kIters; ++it) {
       const int g = it * kBlock + threadIdx.x;
       if (g < tl.ngroups) {
-        vx[it] = *reinterpret_cast<const float4*>(ix + 4 * g);
-        vy[it] = *reinterpret_cast<const float4*>(ix + a.in_cap + 4 * g);
-        vz[it] = *reinterpret_cast<const float4*>(ix + 2 * a.in_cap + 4 * g);
-        vi[it] = *reinterpret_cast<const float4*>(ix + 3 * a.in_cap + 4 * g);
+        vx[it] = ld4(ix + 4 * g);
+        vy[it] = ld4(ix + a.in_cap + 4 * g);
+        vz[it] = ld4(ix + 2 * a.in_cap + 4 * g);
+        vi[it] = ld4(ix + 3 * a.in_cap + 4 * g);
       }
     }
 #pragma unroll
@@ -522,8 +550,12 @@ __device__ __forceinline__ int win_index(const int64_t* bnd, int W, int64_t t) {
 template <int MODE>
 __device__ __forceinline__ void point_body(const typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type& w,
                                            int t, float& x, float& y, float& z) {
+#if MC_NULL_COMPUTE
+  asm volatile("" : "+v"(x), "+v"(y), "+v"(z) : "v"(t));
+#else
   if constexpr (MODE == 1) slerp_point(w, t, x, y, z);
   else imu_point(w, t, x, y, z);
+#endif
 }
 
 template <typename Win>
@@ -601,14 +633,14 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
     float4 X, Y, Z, I;
     int4 Tq;
     if (act) {
-      Tq = *reinterpret_cast<const int4*>(a.tns + p);
-      X = *reinterpret_cast<const float4*>(a.in + p);
-      Y = *reinterpret_cast<const float4*>(a.in + a.in_cap + p);
-      Z = *reinterpret_cast<const float4*>(a.in + 2 * a.in_cap + p);
-      I = *reinterpret_cast<const float4*>(a.in + 3 * a.in_cap + p);
+      Tq = ld4(a.tns + p);
+      X = ld4(a.in + p);
+      Y = ld4(a.in + a.in_cap + p);
+      Z = ld4(a.in + 2 * a.in_cap + p);
+      I = ld4(a.in + 3 * a.in_cap + p);
     }
 
-    if (fw.W <= 2) {
+    if (fw.W <= MC_FASTPATH_MAXW) {
       const Win r0 = ldu(frec + 2 * f);
       bool use1 = false, mixed = false;
       if (fw.W == 2) {

@@ -51,16 +51,25 @@ def main():
     ap.add_argument("--points", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--grids", default="0", help="comma list of max-grid caps tried with every lib (0: one "
+                                                  "workgroup per (sub-)tile)")
     args = ap.parse_args()
     libs = [l for l in args.libs.split(",") if l]
     runs = {lib: setup(lib, args) for lib in libs}
+    grids = [int(g) for g in args.grids.split(",")]
+    if grids != [0]:   # each (lib, grid) pair becomes its own arm, sharing the lib's workload
+        runs = {f"{lib}@{g}": (*runs[lib], g) for lib in libs for g in grids}
+    else:
+        runs = {lib: (*runs[lib], 0) for lib in libs}
+    libs = list(runs)
     n = args.frames * args.points
     out = {}
     for mode in args.modes.split(","):
         per = {lib: [] for lib in libs}
         for _ in range(args.rounds):
             for lib in libs:
-                ctx, bi, bo = runs[lib]
+                ctx, bi, bo, grid = runs[lib]
+                ctx.set_max_grid(grid)
                 for _ in range(3):
                     ctx.deskew(bi, bo, mode=mode)
                 ctx.sync()
