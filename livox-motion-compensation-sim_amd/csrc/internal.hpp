@@ -20,18 +20,24 @@ int fail(int code, const char* fmt, ...);
 
 struct mc_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // main stream: staging + the deskew kernels
+  hipStream_t side = nullptr;     // per-step pose prep, pipelined one step ahead of `stream`
+  // per-step tables are double-buffered: prep of step i+1 (side) overlaps the kernel of step i
+  int buf = 0;
+  hipEvent_t ev_main_done[2] = {nullptr, nullptr};
+  hipEvent_t ev_prep_done[2] = {nullptr, nullptr};
+  hipEvent_t ev_order = nullptr;  // orders side-stream prep after async main-stream staging
   // trajectory (LMC:361-428): time, position_gps, orientation_imu
   int64_t T = 0, T_cap = 0;
   double* d_time = nullptr;
   double* d_pos = nullptr;
   double* d_rpy = nullptr;
-  mc::PoseSeg* d_pose_seg = nullptr;
+  mc::PoseSeg* d_pose_seg = nullptr;   // 2 * T_cap (double buffer)
   // IMU (CSIM:1191-1240)
   int64_t M = 0, M_cap = 0;
   int64_t* d_imu_ts = nullptr;
   double* d_gyro = nullptr;
-  mc::ImuSeg* d_imu_seg = nullptr;
+  mc::ImuSeg* d_imu_seg = nullptr;     // 2 * M_cap (double buffer)
   // staging buffer for host<->device layout conversion
   void* d_stage = nullptr;
   size_t stage_bytes = 0;
@@ -58,10 +64,12 @@ struct mc_batch {
   mc::Tile* d_tiles = nullptr;
   double* d_frame_time = nullptr;
   int64_t* d_frame_start = nullptr;
+  // k_prep outputs, double-buffered (ctx->buf selects the half): F entries per half
   float4* d_frame_tbl = nullptr;   // 3 float4 per frame (R row, t)
   int2* d_trange = nullptr;        // per-frame [min, max] t_ns (valid when trange_valid)
-  mc::FrameWin* d_fwin = nullptr;  // per-frame segment window (k_prep output)
+  mc::FrameWin* d_fwin = nullptr;  // per-frame segment window
   void* d_frec = nullptr;          // 2 frame-specialised pose/IMU records per frame
+  size_t frec_half = 0;            // bytes per half of d_frec
   double* d_partial = nullptr;
   bool has_times = false, has_starts = false, trange_valid = false;
 };

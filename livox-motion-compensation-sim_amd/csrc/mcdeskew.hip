@@ -101,18 +101,25 @@ static hipEvent_t ev_take(mc_ctx* c) {
   return e;
 }
 struct TimedRegion {
-  mc_ctx* c; std::vector<std::pair<hipEvent_t, hipEvent_t>>* v; hipEvent_t e0 = nullptr;
-  TimedRegion(mc_ctx* c_, std::vector<std::pair<hipEvent_t, hipEvent_t>>* v_) : c(c_), v(v_) {
-    if (c->timing) { e0 = ev_take(c); if (e0) (void)hipEventRecord(e0, c->stream); }
+  mc_ctx* c; std::vector<std::pair<hipEvent_t, hipEvent_t>>* v; hipStream_t s; hipEvent_t e0 = nullptr;
+  TimedRegion(mc_ctx* c_, std::vector<std::pair<hipEvent_t, hipEvent_t>>* v_, hipStream_t s_) : c(c_), v(v_), s(s_) {
+    if (c->timing) { e0 = ev_take(c); if (e0) (void)hipEventRecord(e0, s); }
   }
   ~TimedRegion() {
     if (c->timing && e0) {
       hipEvent_t e1 = ev_take(c);
-      if (e1) { (void)hipEventRecord(e1, c->stream); v->emplace_back(e0, e1); }
+      if (e1) { (void)hipEventRecord(e1, s); v->emplace_back(e0, e1); }
       else c->ev_pool.push_back(e0);
     }
   }
 };
+
+// both streams idle (before reallocating tables a pipelined prep may still read or write)
+static int sync_all(mc_ctx* c) {
+  HIPCHK(hipStreamSynchronize(c->side));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
 
 template <typename T>
 static int upload_column(mc_batch* b, const T* src, T* dst_col) {
@@ -181,7 +188,13 @@ int mc_create(int device, mc_ctx** out) {
   mc_ctx* c = new mc_ctx();
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e != hipSuccess) { delete c; return fail(MC_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    e = hipEventCreateWithFlags(&c->ev_main_done[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_prep_done[i], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming);
+  if (e != hipSuccess) { delete c; return fail(MC_ERR_HIP, "stream/event creation: %s", hipGetErrorString(e)); }
   *out = c;
   return MC_OK;
 }
@@ -189,13 +202,16 @@ int mc_create(int device, mc_ctx** out) {
 int mc_destroy(mc_ctx* c) {
   if (!c) return MC_OK;
   DeviceGuard g(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  (void)sync_all(c);
   dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
   dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
   if (c->d_stage) (void)hipFree(c->d_stage);
   for (auto& p : c->main_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->prep_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i) { (void)hipEventDestroy(c->ev_main_done[i]); (void)hipEventDestroy(c->ev_prep_done[i]); }
+  (void)hipEventDestroy(c->ev_order);
+  (void)hipStreamDestroy(c->side);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return MC_OK;
@@ -204,8 +220,7 @@ int mc_destroy(mc_ctx* c) {
 int mc_sync(mc_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   DeviceGuard g(c->device);
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return MC_OK;
+  return sync_all(c);
 }
 
 int mc_set_launch(mc_ctx* c, int32_t max_grid) {
@@ -223,14 +238,14 @@ int mc_set_trajectory(mc_ctx* c, int64_t T, const double* time, const double* po
   for (int64_t i = 1; i < T; ++i)
     CHECK_ARG(time[i] >= time[i - 1], "trajectory time must be non-decreasing (index %lld)", (long long)i);
   DeviceGuard g(c->device);
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (int r = sync_all(c)) return r;
   if (T > c->T_cap) {
     dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
     c->T_cap = 0;
     if (int r = dev_alloc(&c->d_time, T)) return r;
     if (int r = dev_alloc(&c->d_pos, 3 * T)) return r;
     if (int r = dev_alloc(&c->d_rpy, 3 * T)) return r;
-    if (int r = dev_alloc(&c->d_pose_seg, T)) return r;
+    if (int r = dev_alloc(&c->d_pose_seg, 2 * T)) return r;
     c->T_cap = T;
   }
   HIPCHK(hipMemcpyAsync(c->d_time, time, T * sizeof(double), hipMemcpyHostToDevice, c->stream));
@@ -248,13 +263,13 @@ int mc_set_imu(mc_ctx* c, int64_t M, const int64_t* ts, const double* gyro) {
   for (int64_t i = 1; i < M; ++i)
     CHECK_ARG(ts[i] >= ts[i - 1], "IMU timestamps must be non-decreasing (index %lld)", (long long)i);
   DeviceGuard g(c->device);
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (int r = sync_all(c)) return r;
   if (M > c->M_cap) {
     dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
     c->M_cap = 0;
     if (int r = dev_alloc(&c->d_imu_ts, M)) return r;
     if (int r = dev_alloc(&c->d_gyro, 3 * M)) return r;
-    if (int r = dev_alloc(&c->d_imu_seg, M)) return r;
+    if (int r = dev_alloc(&c->d_imu_seg, 2 * M)) return r;
     c->M_cap = M;
   }
   HIPCHK(hipMemcpyAsync(c->d_imu_ts, ts, M * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
@@ -308,12 +323,12 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
   if ((r = dev_alloc(&b->d_tiles, tiles.size()))) return bail(r);
   if ((r = dev_alloc(&b->d_frame_time, F))) return bail(r);
   if ((r = dev_alloc(&b->d_frame_start, F))) return bail(r);
-  if ((r = dev_alloc(&b->d_frame_tbl, 3 * (size_t)F))) return bail(r);
+  // k_prep outputs: two halves (double buffer, see mc_deskew)
+  if ((r = dev_alloc(&b->d_frame_tbl, 2 * 3 * (size_t)F))) return bail(r);
   if ((r = dev_alloc(&b->d_trange, F))) return bail(r);
-  if ((r = dev_alloc(&b->d_fwin, F))) return bail(r);
-  if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_frec), 2 * (size_t)std::max<int>(F, 1) *
-                                                             std::max(sizeof(PoseWin), sizeof(ImuSeg)))))
-    return bail(r);
+  if ((r = dev_alloc(&b->d_fwin, 2 * (size_t)F))) return bail(r);
+  b->frec_half = 2 * (size_t)std::max<int>(F, 1) * std::max(sizeof(PoseWin), sizeof(ImuSeg));
+  if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_frec), 2 * b->frec_half))) return bail(r);
   if ((r = dev_alloc(&b->d_partial, 5 * (size_t)b->n_tiles))) return bail(r);
   hipStream_t s = c->stream;
   auto cpy = [&](void* d, const void* h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s); };
@@ -338,7 +353,7 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
 int mc_batch_destroy(mc_batch* b) {
   if (!b) return MC_OK;
   DeviceGuard g(b->ctx->device);
-  (void)hipStreamSynchronize(b->ctx->stream);
+  (void)sync_all(b->ctx);
   dev_free(b->d_cols); dev_free(b->d_t); dev_free(b->d_counts); dev_free(b->d_poff); dev_free(b->d_doff);
   dev_free(b->d_tiles); dev_free(b->d_frame_time); dev_free(b->d_frame_start); dev_free(b->d_frame_tbl);
   dev_free(b->d_trange); dev_free(b->d_fwin); dev_free(b->d_partial);
@@ -519,10 +534,26 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   }
   if (in->F == 0) return MC_OK;
   DeviceGuard g(c->device);
-  hipStream_t s = c->stream;
-  if (mode != MC_MODE_FRAME && !in->trange_valid)
+  hipStream_t s = c->stream, sd = c->side;
+  if (mode != MC_MODE_FRAME && !in->trange_valid) {
+    // lazily derived frame time spans are queued on the main stream: order the prep after them
     if (int r = compute_trange(const_cast<mc_batch*>(in))) return r;
+    HIPCHK(hipEventRecord(c->ev_order, s));
+    HIPCHK(hipStreamWaitEvent(sd, c->ev_order, 0));
+  }
   const mc_batch* pb = in;  // per-frame tables live with the input batch
+
+  // Pipelining: the per-step tables come in two halves.  This step's prep runs on the side
+  // stream as soon as the deskew kernel that last read half `h` (two calls back) has finished,
+  // i.e. concurrently with the previous call's kernel; the kernel waits for its own prep.
+  const int h = c->buf;
+  c->buf ^= 1;
+  HIPCHK(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
+  float4* frame_tbl = pb->d_frame_tbl + 3 * (size_t)in->F * h;
+  FrameWin* fwin = pb->d_fwin + (size_t)in->F * h;
+  void* frec = static_cast<char*>(pb->d_frec) + pb->frec_half * h;
+  PoseSeg* pose_seg = c->d_pose_seg ? c->d_pose_seg + (size_t)c->T_cap * h : nullptr;
+  ImuSeg* imu_seg = c->d_imu_seg ? c->d_imu_seg + (size_t)c->M_cap * h : nullptr;
 
   PrepArgs pa;
   std::memset(&pa, 0, sizeof(pa));
@@ -532,30 +563,35 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   pa.time = c->d_time; pa.pos = c->d_pos; pa.rpy = c->d_rpy; pa.T = c->T;
   pa.imu_ts = c->d_imu_ts; pa.gyro = c->d_gyro; pa.M = c->M;
   pa.frame_time = pb->d_frame_time; pa.frame_start = pb->d_frame_start; pa.trange = pb->d_trange;
-  pa.frame_tbl = pb->d_frame_tbl; pa.pose_seg = c->d_pose_seg; pa.imu_seg = c->d_imu_seg;
-  pa.fwin = pb->d_fwin; pa.frec = pb->d_frec;
+  pa.frame_tbl = frame_tbl; pa.pose_seg = pose_seg; pa.imu_seg = imu_seg;
+  pa.fwin = fwin; pa.frec = frec;
   // one wave per frame, then one lane per pose segment / IMU sample
   int64_t table = 0;
   if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); table = pa.nseg; }
   if (mode == MC_MODE_IMU) { pa.nseg = c->M; table = c->M; }
   const int64_t waves = in->F + (table + 63) / 64;
   {
-    TimedRegion tr(c, &c->prep_ev);
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, s, pa);
+    TimedRegion tr(c, &c->prep_ev, sd);
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, sd, pa);
   }
   HIPCHK(hipGetLastError());
-  if (in->n_tiles == 0) return MC_OK;
+  HIPCHK(hipEventRecord(c->ev_prep_done[h], sd));
+  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
+  if (in->n_tiles == 0) {
+    HIPCHK(hipEventRecord(c->ev_main_done[h], s));
+    return MC_OK;
+  }
 
   DeskewArgs da;
   std::memset(&da, 0, sizeof(da));
   da.in = in->d_cols; da.in_cap = in->cap; da.tns = in->d_t;
   da.out = out->d_cols; da.out_cap = out->cap;
   da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
-  da.frame_tbl = pb->d_frame_tbl;
+  da.frame_tbl = frame_tbl;
   da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start;
-  da.fwin = pb->d_fwin; da.frec = pb->d_frec;
-  da.pose_time = c->d_time; da.pose_seg = c->d_pose_seg;
-  da.imu_ts = c->d_imu_ts; da.imu_seg = c->d_imu_seg;
+  da.fwin = fwin; da.frec = frec;
+  da.pose_time = c->d_time; da.pose_seg = pose_seg;
+  da.imu_ts = c->d_imu_ts; da.imu_seg = imu_seg;
   if (mode == MC_MODE_POSE_SLERP) { da.nseg = pa.nseg; da.ntab = c->T; }
   if (mode == MC_MODE_IMU) { da.nseg = c->M; da.ntab = c->M; }
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
@@ -563,12 +599,13 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   const int32_t units = mode == MC_MODE_FRAME ? in->n_tiles : in->n_tiles * kSub;
   const dim3 grid(launch_grid(c, units)), block(kBlock);
   {
-    TimedRegion tr(c, &c->main_ev);
+    TimedRegion tr(c, &c->main_ev, s);
     if (mode == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, da);
     else if (mode == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, da);
     else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, da);
   }
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_main_done[h], s));
   // per-point modes pass the timestamps through (CSIM:1472): copy the column when out != in
   if (mode != MC_MODE_FRAME && out != in && out->d_t)
     HIPCHK(hipMemcpyAsync(out->d_t, in->d_t, in->P * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
@@ -598,7 +635,7 @@ static int sum_events(mc_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>&
 int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms, int64_t* prep_n) {
   CHECK_ARG(c, "ctx is NULL");
   DeviceGuard g(c->device);
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (int r = sync_all(c)) return r;
   if (int r = sum_events(c, c->main_ev, main_ms, main_n)) return r;
   return sum_events(c, c->prep_ev, prep_ms, prep_n);
 }
