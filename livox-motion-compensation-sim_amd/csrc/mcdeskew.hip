@@ -97,7 +97,8 @@ struct DeviceGuard {
 static hipEvent_t ev_take(mc_ctx* c) {
   if (!c->ev_pool.empty()) { hipEvent_t e = c->ev_pool.back(); c->ev_pool.pop_back(); return e; }
   hipEvent_t e = nullptr;
-  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  // timing-only events: no system-scope fence (no L2 writeback/invalidate between the kernels)
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
   return e;
 }
 struct TimedRegion {
@@ -190,10 +191,12 @@ int mc_create(int device, mc_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-    e = hipEventCreateWithFlags(&c->ev_main_done[i], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_prep_done[i], hipEventDisableTiming);
+    // stream-ordering events between two queues of the same device: device-scope release only
+    const unsigned fl = hipEventDisableTiming | hipEventReleaseToDevice;
+    e = hipEventCreateWithFlags(&c->ev_main_done[i], fl);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_prep_done[i], fl);
   }
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming | hipEventReleaseToDevice);
   if (e != hipSuccess) { delete c; return fail(MC_ERR_HIP, "stream/event creation: %s", hipGetErrorString(e)); }
   *out = c;
   return MC_OK;
