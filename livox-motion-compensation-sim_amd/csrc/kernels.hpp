@@ -132,7 +132,14 @@ __device__ __forceinline__ T ldu(const T* p) {
 typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_nt(float* p, const float4& v) {
   v4f t = {v.x, v.y, v.z, v.w};
-#if MC_NT_STORE
+#if MC_NT_STORE == 2
+  // write-through: the line leaves L2 now, so the kernel ends without dirty L2 to write back
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
+#elif MC_NT_STORE == 3
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(t) : "memory");
+#elif MC_NT_STORE == 4
+  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(t) : "memory");
+#elif MC_NT_STORE
   __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
 #else
   *reinterpret_cast<v4f*>(p) = t;
