@@ -105,6 +105,39 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup):
     return t1 - t0, tm
 
 
+def timed_gather(ctx, rdv, b_in, b_out, mode, n_rank, world, timeout_s):
+    """The merged-cloud gather to rank 0 (LMC:887-889 over RCCL), after and outside the timed
+    steps, under a watchdog so that a stuck collective can never cost the throughput line.
+    Returns (report, hung).  The root's wall time is the gather time (it receives every shard)."""
+    import threading
+    res = {}
+
+    def work():
+        try:
+            comm = mc.dist.RcclComm(ctx, rdv)
+            ctx.deskew(b_in, b_out, mode=mode)
+            ctx.sync()
+            rdv.barrier()
+            t0 = time.perf_counter()
+            merged = mc.dist.gather_merged(ctx, comm, rdv, b_out, root=0)
+            dt = time.perf_counter() - t0
+            moved = 16 * n_rank * (world - 1)
+            res["report"] = {"seconds": dt, "bytes_into_root": moved, "GBs": moved / dt / 1e9,
+                             "merged_points": int(n_rank * world), "timed_on": "root wall clock"}
+            if merged is not None:
+                merged.close()
+            comm.close()
+        except Exception as e:  # report, never fail the throughput line
+            res["report"] = {"error": str(e)}
+
+    th = threading.Thread(target=work, daemon=True)
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        return {"error": f"gather did not finish within {timeout_s} s"}, True
+    return res.get("report"), False
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,6 +149,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra-modes", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL merged-cloud gather (N>1)")
+    ap.add_argument("--gather-timeout", type=float, default=120.0)
     args = ap.parse_args()
 
     rank, local_rank, world = mc.dist.env_rank()
@@ -150,23 +185,9 @@ def main():
                          "value": n_rank * world * steps / wall_max / 1e6}
 
     gather = None
-    if world > 1:
-        try:
-            comm = mc.dist.RcclComm(ctx, rdv)
-            ctx.deskew(b_in, b_out, mode=args.mode)
-            ctx.sync()
-            rdv.barrier()
-            t0 = time.perf_counter()
-            merged = mc.dist.gather_merged(ctx, comm, rdv, b_out, root=0)
-            dt = rdv.max(time.perf_counter() - t0)
-            moved = 16 * n_rank * (world - 1)
-            gather = {"seconds": dt, "bytes_into_root": moved, "GBs": moved / dt / 1e9,
-                      "merged_points": int(n_rank * world)}
-            if merged is not None:
-                merged.close()
-            comm.close()
-        except Exception as e:  # report, never fail the throughput line
-            gather = {"error": str(e)}
+    hung = False
+    if world > 1 and not args.no_gather:
+        gather, hung = timed_gather(ctx, rdv, b_in, b_out, args.mode, n_rank, world, args.gather_timeout)
 
     if rank == 0:
         r = results[args.mode]
@@ -205,6 +226,12 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args.mode, tr, times, counts, lo, args.cpu_budget)
             line["cpu_baseline"]["cores_available"] = len(os.sched_getaffinity(0))
         print(json.dumps(line), flush=True)
+    if hung:
+        # a collective is stuck inside RCCL: finalisers would block on its stream; the result
+        # line is out, so leave without running them
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     rdv.close()
 
 
