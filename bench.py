@@ -105,6 +105,32 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup):
     return t1 - t0, tm
 
 
+def measure_stager(ctx, b_in, b_out, n_rank, reps):
+    """SURVEY §8f row 1, reported beside the hot path: the device stager pair converting the
+    reference's (N,4) float64 AoS to/from the float32 SoA columns, 48 algorithmic B/point."""
+    buf = ctx.device_buffer(n_rank * 32)
+    try:
+        out = {}
+        for name, fn in (("soa_to_aos", lambda: b_in.fetch_aos_device(buf)),
+                         ("aos_to_soa", lambda: b_out.stage_aos_device(buf))):
+            for _ in range(3):
+                fn()
+            ctx.sync()
+            ctx.read_timing()
+            ctx.timing(True)
+            for _ in range(reps):
+                fn()
+            ctx.sync()
+            ctx.timing(False)
+            t = ctx.read_timing()
+            us = t["layout_ms"] / max(t["layout_launches"], 1) * 1e3
+            gbs = 48 * n_rank / (us * 1e-6) / 1e9
+            out[name] = {"kernel_avg_us": us, "GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_point": 48}
+        return out
+    finally:
+        buf.close()
+
+
 def timed_gather(ctx, rdv, b_in, b_out, mode, n_rank, world, timeout_s):
     """The merged-cloud gather to rank 0 (LMC:887-889 over RCCL), after and outside the timed
     steps, under a watchdog so that a stuck collective can never cost the throughput line.
@@ -184,6 +210,8 @@ def main():
                          "prep_avg_us": prep_avg_s * 1e6, "achieved_GBs": achieved,
                          "value": n_rank * world * steps / wall_max / 1e6}
 
+    stager = measure_stager(ctx, b_in, b_out, n_rank, min(args.steps, 50))
+
     gather = None
     hung = False
     if world > 1 and not args.no_gather:
@@ -220,6 +248,7 @@ def main():
             "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
                           "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"]}
                       for m, v in results.items()},
+            "stager": stager,
             "gather": gather,
         }
         if world == 1 and not args.no_cpu:

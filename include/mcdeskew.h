@@ -122,6 +122,18 @@ int mc_batch_download_aos_f64(mc_batch* b, double* aos_out);
 int mc_batch_download_columns_f32(mc_batch* b, float* x, float* y, float* z, float* intensity);
 int mc_batch_download_time_ns(mc_batch* b, int32_t* t_ns);
 
+/* ---- device buffers and the device-side stager ---------------------- */
+/* The stager pair converts the reference's (N,4) float64 AoS (LMC:770 in, LMC:776 out) to and
+ * from the batch's float32 SoA columns without leaving HBM; both are asynchronous on the ctx
+ * stream and timed under mc_timing_read_layout. */
+int mc_device_alloc(mc_ctx* ctx, int64_t bytes, void** dptr);
+int mc_device_free(mc_ctx* ctx, void* dptr);
+int mc_memcpy_h2d(mc_ctx* ctx, void* dptr, const void* host, int64_t bytes);
+int mc_memcpy_d2h(mc_ctx* ctx, void* host, const void* dptr, int64_t bytes);
+int mc_batch_stage_aos_f64_device(mc_batch* b, const double* d_aos, int64_t ld);
+int mc_batch_fetch_aos_f64_device(mc_batch* b, double* d_aos);
+int mc_timing_read_layout(mc_ctx* ctx, double* ms_total, int64_t* launches);
+
 /* Synthetic Mid-70 frames generated on the device (counter-hash RNG, bit-identical to
  * oracle/synth.py): frame f uses seed  seed + frame_id_base + f. */
 int mc_batch_synth(mc_batch* b, uint64_t seed, int64_t frame_id_base);

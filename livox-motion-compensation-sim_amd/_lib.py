@@ -66,6 +66,13 @@ _SIGS = {
     "mc_batch_download_aos_f64": (c_int, [c_void_p, _pd]),
     "mc_batch_download_columns_f32": (c_int, [c_void_p, _pf, _pf, _pf, _pf]),
     "mc_batch_download_time_ns": (c_int, [c_void_p, _pi32]),
+    "mc_device_alloc": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
+    "mc_device_free": (c_int, [c_void_p, c_void_p]),
+    "mc_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "mc_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "mc_batch_stage_aos_f64_device": (c_int, [c_void_p, c_void_p, c_int64]),
+    "mc_batch_fetch_aos_f64_device": (c_int, [c_void_p, c_void_p]),
+    "mc_timing_read_layout": (c_int, [c_void_p, _pd, _pi64]),
     "mc_batch_synth": (c_int, [c_void_p, c_uint64, c_int64]),
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),
     "mc_deskew": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),

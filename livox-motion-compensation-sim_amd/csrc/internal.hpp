@@ -45,7 +45,7 @@ struct mc_ctx {
   int32_t max_grid = 0;
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> main_ev, prep_ev;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> main_ev, prep_ev, layout_ev;
 };
 
 struct mc_batch {

@@ -544,6 +544,9 @@ __device__ __forceinline__ void imu_point(const ImuSeg& w, int t, float& x, floa
 __device__ __forceinline__ float& f4c(float4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
+__device__ __forceinline__ float f4g(const float4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
 __device__ __forceinline__ int i4c(const int4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
@@ -730,35 +733,75 @@ __device__ __forceinline__ int64_t local_index(const LayoutArgs& a, const Tile& 
   return i < a.counts[tl.frame] ? i : -1;
 }
 
-// host AoS (N, ld) f64 staged on the device -> padded SoA f32  (LMC:770 layout in)
+// The stager pair: the reference's (N, ld) float64 AoS [x,y,z,intensity,...]
+// (LMC:770) <-> the padded SoA float32 columns, both on the device.  One thread per float4 group
+// (4 consecutive points of one frame): 4 x 32 B of AoS = 8 contiguous 16-byte accesses per lane,
+// one 16-byte access per SoA column.  48 algorithmic bytes per point either way.
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+// AoS f64 (dense, row stride ld) -> padded SoA f32 (padding slots zeroed)
 __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const double* __restrict__ aos, int64_t ld) {
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-    const Tile tl = a.tiles[tile];
-    const int64_t d0 = a.doff[tl.frame];
-    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
-      const int64_t p = tl.pstart + e;
-      const int64_t i = local_index(a, tl, p);
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (i >= 0) {
-        const double* r = aos + (d0 + i) * ld;
-        v[0] = (float)r[0]; v[1] = (float)r[1]; v[2] = (float)r[2]; v[3] = (float)r[3];
+    const Tile tl = ldu(a.tiles + tile);
+    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int g = it * kBlock + threadIdx.x;
+      if (g >= tl.ngroups) continue;
+      const int64_t p = tl.pstart + 4 * (int64_t)g;
+      const int64_t loc = p - poff;
+      const int64_t nv = cnt - loc;                 // valid points in this group (may be >= 4)
+      const double* src = aos + (doff + loc) * ld;
+      float4 X = make_float4(0.f, 0.f, 0.f, 0.f), Y = X, Z = X, I = X;
+      if (ld == 4 && nv >= 4) {
+        const v2d* s2 = reinterpret_cast<const v2d*>(src);
+        v2d r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = __builtin_nontemporal_load(s2 + k);
+        X = make_float4((float)r[0].x, (float)r[2].x, (float)r[4].x, (float)r[6].x);
+        Y = make_float4((float)r[0].y, (float)r[2].y, (float)r[4].y, (float)r[6].y);
+        Z = make_float4((float)r[1].x, (float)r[3].x, (float)r[5].x, (float)r[7].x);
+        I = make_float4((float)r[1].y, (float)r[3].y, (float)r[5].y, (float)r[7].y);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (e < nv) {
+            const double* r = src + e * ld;
+            f4c(X, e) = (float)r[0]; f4c(Y, e) = (float)r[1]; f4c(Z, e) = (float)r[2]; f4c(I, e) = (float)r[3];
+          }
+        }
       }
-      for (int c = 0; c < 4; ++c) a.cols[c * a.cap + p] = v[c];
+      st_frame(a.cols + p, X);
+      st_frame(a.cols + a.cap + p, Y);
+      st_frame(a.cols + 2 * a.cap + p, Z);
+      st_frame(a.cols + 3 * a.cap + p, I);
     }
   }
 }
 
-// padded SoA f32 -> dense AoS (N,4) f64 on the device  (LMC:776 layout out)
+// padded SoA f32 -> dense AoS (N,4) f64  (the (N,4) float64 layout LMC:776 returns)
 __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, double* __restrict__ aos) {
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-    const Tile tl = a.tiles[tile];
-    const int64_t d0 = a.doff[tl.frame];
-    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
-      const int64_t p = tl.pstart + e;
-      const int64_t i = local_index(a, tl, p);
-      if (i >= 0) {
-        double* r = aos + (d0 + i) * 4;
-        r[0] = a.cols[p]; r[1] = a.cols[a.cap + p]; r[2] = a.cols[2 * a.cap + p]; r[3] = a.cols[3 * a.cap + p];
+    const Tile tl = ldu(a.tiles + tile);
+    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int g = it * kBlock + threadIdx.x;
+      if (g >= tl.ngroups) continue;
+      const int64_t p = tl.pstart + 4 * (int64_t)g;
+      const int64_t loc = p - poff;
+      const int64_t nv = cnt - loc;
+      const float4 X = ld4(a.cols + p), Y = ld4(a.cols + a.cap + p), Z = ld4(a.cols + 2 * a.cap + p),
+                   I = ld4(a.cols + 3 * a.cap + p);
+      v2d* dst = reinterpret_cast<v2d*>(aos + (doff + loc) * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (e < nv) {
+          const v2d xy = {(double)f4g(X, e), (double)f4g(Y, e)};
+          const v2d zi = {(double)f4g(Z, e), (double)f4g(I, e)};
+          __builtin_nontemporal_store(xy, dst + 2 * e);
+          __builtin_nontemporal_store(zi, dst + 2 * e + 1);
+        }
       }
     }
   }

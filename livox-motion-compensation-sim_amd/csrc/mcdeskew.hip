@@ -211,6 +211,7 @@ int mc_destroy(mc_ctx* c) {
   if (c->d_stage) (void)hipFree(c->d_stage);
   for (auto& p : c->main_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->prep_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
+  for (auto& p : c->layout_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) { (void)hipEventDestroy(c->ev_main_done[i]); (void)hipEventDestroy(c->ev_prep_done[i]); }
   (void)hipEventDestroy(c->ev_order);
@@ -405,6 +406,31 @@ int mc_batch_set_frame_start_ns(mc_batch* b, const int64_t* s) {
   return MC_OK;
 }
 
+// device AoS -> batch columns (async, timed as a layout kernel)
+static int launch_stage(mc_batch* b, const double* d_aos, int64_t ld) {
+  mc_ctx* c = b->ctx;
+  if (b->n_tiles == 0) return MC_OK;
+  {
+    TimedRegion tr(c, &c->layout_ev, c->stream);
+    hipLaunchKernelGGL(k_aos_to_soa, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
+                       d_aos, ld);
+  }
+  HIPCHK(hipGetLastError());
+  return MC_OK;
+}
+// batch columns -> device AoS (N,4) f64 (async, timed as a layout kernel)
+static int launch_fetch(mc_batch* b, double* d_aos) {
+  mc_ctx* c = b->ctx;
+  if (b->n_tiles == 0) return MC_OK;
+  {
+    TimedRegion tr(c, &c->layout_ev, c->stream);
+    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
+                       d_aos);
+  }
+  HIPCHK(hipGetLastError());
+  return MC_OK;
+}
+
 int mc_batch_upload_aos_f64(mc_batch* b, const double* aos, int64_t ld) {
   CHECK_ARG(b, "batch is NULL");
   if (ld < 4) return fail(MC_ERR_INDEX, "points need at least 4 columns (x,y,z,intensity); got %lld", (long long)ld);
@@ -415,9 +441,58 @@ int mc_batch_upload_aos_f64(mc_batch* b, const double* aos, int64_t ld) {
   void* st = nullptr;
   if (int r = ctx_stage(c, (size_t)b->N * ld * sizeof(double), &st)) return r;
   HIPCHK(hipMemcpyAsync(st, aos, (size_t)b->N * ld * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_aos_to_soa, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
-                     layout_of(b), static_cast<const double*>(st), ld);
-  HIPCHK(hipGetLastError());
+  if (int r = launch_stage(b, static_cast<const double*>(st), ld)) return r;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_batch_stage_aos_f64_device(mc_batch* b, const double* d_aos, int64_t ld) {
+  CHECK_ARG(b, "batch is NULL");
+  if (ld < 4) return fail(MC_ERR_INDEX, "points need at least 4 columns (x,y,z,intensity); got %lld", (long long)ld);
+  if (b->N == 0) return MC_OK;
+  CHECK_ARG(d_aos, "device points pointer is NULL");
+  DeviceGuard g(b->ctx->device);
+  return launch_stage(b, d_aos, ld);
+}
+
+int mc_batch_fetch_aos_f64_device(mc_batch* b, double* d_aos) {
+  CHECK_ARG(b, "batch is NULL");
+  if (b->N == 0) return MC_OK;
+  CHECK_ARG(d_aos, "device output pointer is NULL");
+  DeviceGuard g(b->ctx->device);
+  return launch_fetch(b, d_aos);
+}
+
+int mc_device_alloc(mc_ctx* c, int64_t bytes, void** dptr) {
+  CHECK_ARG(c && dptr, "NULL argument");
+  CHECK_ARG(bytes >= 0, "negative size");
+  DeviceGuard g(c->device);
+  *dptr = nullptr;
+  HIPCHK(hipMalloc(dptr, bytes > 0 ? (size_t)bytes : 1));
+  return MC_OK;
+}
+
+int mc_device_free(mc_ctx* c, void* dptr) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!dptr) return MC_OK;
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  HIPCHK(hipFree(dptr));
+  return MC_OK;
+}
+
+int mc_memcpy_h2d(mc_ctx* c, void* dptr, const void* host, int64_t bytes) {
+  CHECK_ARG(c && dptr && host && bytes >= 0, "bad argument");
+  DeviceGuard g(c->device);
+  HIPCHK(hipMemcpyAsync(dptr, host, (size_t)bytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_memcpy_d2h(mc_ctx* c, void* host, const void* dptr, int64_t bytes) {
+  CHECK_ARG(c && dptr && host && bytes >= 0, "bad argument");
+  DeviceGuard g(c->device);
+  HIPCHK(hipMemcpyAsync(host, dptr, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return MC_OK;
 }
@@ -453,9 +528,7 @@ int mc_batch_download_aos_f64(mc_batch* b, double* aos) {
   DeviceGuard g(c->device);
   void* st = nullptr;
   if (int r = ctx_stage(c, (size_t)b->N * 4 * sizeof(double), &st)) return r;
-  hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
-                     layout_of(b), static_cast<double*>(st));
-  HIPCHK(hipGetLastError());
+  if (int r = launch_fetch(b, static_cast<double*>(st))) return r;
   HIPCHK(hipMemcpyAsync(aos, st, (size_t)b->N * 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return MC_OK;
@@ -641,6 +714,13 @@ int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms,
   if (int r = sync_all(c)) return r;
   if (int r = sum_events(c, c->main_ev, main_ms, main_n)) return r;
   return sum_events(c, c->prep_ev, prep_ms, prep_n);
+}
+
+int mc_timing_read_layout(mc_ctx* c, double* ms, int64_t* n) {
+  CHECK_ARG(c, "ctx is NULL");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  return sum_events(c, c->layout_ev, ms, n);
 }
 
 }  // extern "C"

@@ -91,11 +91,41 @@ class Context:
         check(self.lib.mc_timing_enable(self.handle, int(bool(enable))), "timing_enable")
 
     def read_timing(self) -> dict:
-        mm, pm = c_double(), c_double()
-        mn, pn = c_int64(), c_int64()
+        mm, pm, lm = c_double(), c_double(), c_double()
+        mn, pn, ln = c_int64(), c_int64(), c_int64()
         check(self.lib.mc_timing_read(self.handle, ctypes.byref(mm), ctypes.byref(mn), ctypes.byref(pm),
                                       ctypes.byref(pn)), "timing_read")
-        return {"main_ms": mm.value, "main_launches": mn.value, "prep_ms": pm.value, "prep_launches": pn.value}
+        check(self.lib.mc_timing_read_layout(self.handle, ctypes.byref(lm), ctypes.byref(ln)), "timing_read_layout")
+        return {"main_ms": mm.value, "main_launches": mn.value, "prep_ms": pm.value, "prep_launches": pn.value,
+                "layout_ms": lm.value, "layout_launches": ln.value}
+
+    def device_buffer(self, nbytes: int) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
+
+class DeviceBuffer:
+    """Raw HBM allocation owned by a context (e.g. a device-resident (N,4) float64 AoS cloud)."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx, self.lib, self.nbytes = ctx, ctx.lib, int(nbytes)
+        p = c_void_p()
+        check(self.lib.mc_device_alloc(ctx.handle, self.nbytes, ctypes.byref(p)), "device_alloc")
+        self.ptr = p
+        self._fin = weakref.finalize(self, self.lib.mc_device_free, ctx.handle, p)
+
+    def close(self):
+        self._fin()
+
+    def to_host(self, dtype=np.float64, shape=None) -> np.ndarray:
+        out = np.empty(self.nbytes // np.dtype(dtype).itemsize, dtype)
+        check(self.lib.mc_memcpy_d2h(self.ctx.handle, out.ctypes.data_as(c_void_p), self.ptr, out.nbytes), "d2h")
+        return out.reshape(shape) if shape is not None else out
+
+    def from_host(self, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        if a.nbytes > self.nbytes:
+            raise ValueError("array larger than the device buffer")
+        check(self.lib.mc_memcpy_h2d(self.ctx.handle, self.ptr, a.ctypes.data_as(c_void_p), a.nbytes), "h2d")
 
 
 class Batch:
@@ -170,6 +200,18 @@ class Batch:
             raise ValueError("t_ns (time since frame start) must fit in int32 nanoseconds (+-2.147 s)")
         t = np.ascontiguousarray(t, dtype=np.int32)
         check(self.lib.mc_batch_upload_time_ns(self.handle, ptr(t, c_int32)), "upload_time")
+
+    def stage_aos_device(self, buf: "DeviceBuffer", ld: int = 4):
+        """Device-resident dense (N, ld) float64 AoS -> this batch's columns (async, in HBM)."""
+        if buf.nbytes < self.n_points * ld * 8:
+            raise ValueError("device buffer smaller than the batch's AoS")
+        check(self.lib.mc_batch_stage_aos_f64_device(self.handle, buf.ptr, int(ld)), "stage_aos_device")
+
+    def fetch_aos_device(self, buf: "DeviceBuffer"):
+        """This batch's columns -> device-resident dense (N,4) float64 AoS (async, in HBM)."""
+        if buf.nbytes < self.n_points * 32:
+            raise ValueError("device buffer smaller than the batch's (N,4) float64 AoS")
+        check(self.lib.mc_batch_fetch_aos_f64_device(self.handle, buf.ptr), "fetch_aos_device")
 
     def download_aos(self) -> np.ndarray:
         out = np.empty((self.n_points, 4), np.float64)

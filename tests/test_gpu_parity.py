@@ -316,3 +316,31 @@ def test_rccl_gather_single_rank(mc, gpu_ctx):
         assert comm.allreduce_max([1.5, -2.0]).tolist() == [1.5, -2.0]
     finally:
         comm.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# device stager: (N,4) f64 AoS <-> f32 SoA columns inside HBM
+# ---------------------------------------------------------------------------------------------
+def test_device_stager_roundtrip(mc, gpu_ctx):
+    counts = np.array([100_000, 3, 0, 7, 20_001, 2049])
+    b = gpu_ctx.batch(counts)
+    b.synth(seed=2, frame_id_base=0)
+    buf = gpu_ctx.device_buffer(b.n_points * 32)
+    b.fetch_aos_device(buf)
+    aos = buf.to_host(np.float64, (b.n_points, 4))
+    assert np.array_equal(aos, b.download_aos())
+    hx, hy, hz, hi, _ = synth.synth_batch(counts, seed=2, frame_id_base=0)
+    assert np.array_equal(aos, np.stack([hx, hy, hz, hi], 1).astype(np.float64))
+    b2 = gpu_ctx.batch(counts)
+    b2.stage_aos_device(buf)
+    for c1, c2 in zip(b.download_columns(), b2.download_columns()):
+        assert np.array_equal(c1, c2)
+    # wider rows (ld = 6, the reference passes extra columns through points[:, :3] / [:, 3])
+    wide = np.concatenate([aos, np.full((len(aos), 2), 7.0)], axis=1)
+    buf6 = gpu_ctx.device_buffer(wide.nbytes)
+    buf6.from_host(wide)
+    b3 = gpu_ctx.batch(counts)
+    b3.stage_aos_device(buf6, ld=6)
+    assert np.array_equal(b3.download_aos(), aos)
+    with pytest.raises(IndexError):
+        b3.stage_aos_device(buf6, ld=3)
