@@ -734,47 +734,51 @@ __device__ __forceinline__ int64_t local_index(const LayoutArgs& a, const Tile& 
 }
 
 // The stager pair: the reference's (N, ld) float64 AoS [x,y,z,intensity,...]
-// (LMC:770) <-> the padded SoA float32 columns, both on the device.  One thread per float4 group
-// (4 consecutive points of one frame): 4 x 32 B of AoS = 8 contiguous 16-byte accesses per lane,
-// one 16-byte access per SoA column.  48 algorithmic bytes per point either way.
+// (LMC:770) <-> the padded SoA float32 columns, both on the device.  48 algorithmic bytes per
+// point either way.  Mapping: one lane per 16-byte AoS chunk (half a row: (x,y) or (z,i)), so
+// every AoS access of a wave is 1 KB contiguous; the SoA side is 4-byte lanes, 2 x 128 B runs
+// per instruction.  (A lane-per-4-points mapping, 8 x 16 B at a 128-B lane stride, measured 7 %
+// / 35 % of peak.)  kStageUnroll chunks per lane are in flight at once.
 typedef double v2d __attribute__((ext_vector_type(2)));
+constexpr int kStageUnroll = 4;
 
 // AoS f64 (dense, row stride ld) -> padded SoA f32 (padding slots zeroed)
 __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const double* __restrict__ aos, int64_t ld) {
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+    const int64_t loc0 = tl.pstart - poff;
+    const int np = 4 * tl.ngroups;                                      // padded points in the tile
+    const int nv = (int)max<int64_t>(0, min<int64_t>(np, cnt - loc0)); // valid ones
+    const double* src = aos + (doff + loc0) * ld;
+    float* cx = a.cols + tl.pstart;
+    if (ld == 4) {
+      const v2d* s2 = reinterpret_cast<const v2d*>(src);
+      for (int q0 = 0; q0 < 2 * np; q0 += kStageUnroll * kBlock) {
+        v2d v[kStageUnroll];
 #pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-      const int g = it * kBlock + threadIdx.x;
-      if (g >= tl.ngroups) continue;
-      const int64_t p = tl.pstart + 4 * (int64_t)g;
-      const int64_t loc = p - poff;
-      const int64_t nv = cnt - loc;                 // valid points in this group (may be >= 4)
-      const double* src = aos + (doff + loc) * ld;
-      float4 X = make_float4(0.f, 0.f, 0.f, 0.f), Y = X, Z = X, I = X;
-      if (ld == 4 && nv >= 4) {
-        const v2d* s2 = reinterpret_cast<const v2d*>(src);
-        v2d r[8];
+        for (int u = 0; u < kStageUnroll; ++u) {
+          const int q = q0 + u * kBlock + threadIdx.x;
+          if (q < 2 * nv) v[u] = __builtin_nontemporal_load(s2 + q);
+          else v[u] = v2d{0.0, 0.0};
+        }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = __builtin_nontemporal_load(s2 + k);
-        X = make_float4((float)r[0].x, (float)r[2].x, (float)r[4].x, (float)r[6].x);
-        Y = make_float4((float)r[0].y, (float)r[2].y, (float)r[4].y, (float)r[6].y);
-        Z = make_float4((float)r[1].x, (float)r[3].x, (float)r[5].x, (float)r[7].x);
-        I = make_float4((float)r[1].y, (float)r[3].y, (float)r[5].y, (float)r[7].y);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (e < nv) {
-            const double* r = src + e * ld;
-            f4c(X, e) = (float)r[0]; f4c(Y, e) = (float)r[1]; f4c(Z, e) = (float)r[2]; f4c(I, e) = (float)r[3];
+        for (int u = 0; u < kStageUnroll; ++u) {
+          const int q = q0 + u * kBlock + threadIdx.x;
+          if (q < 2 * np) {
+            const int j = q >> 1, h = q & 1;               // point j, half h: (x,y) or (z,i)
+            cx[(2 * h) * a.cap + j] = (float)v[u].x;
+            cx[(2 * h + 1) * a.cap + j] = (float)v[u].y;
           }
         }
       }
-      st_frame(a.cols + p, X);
-      st_frame(a.cols + a.cap + p, Y);
-      st_frame(a.cols + 2 * a.cap + p, Z);
-      st_frame(a.cols + 3 * a.cap + p, I);
+    } else {
+      for (int j = threadIdx.x; j < np; j += kBlock) {
+        float r[4] = {0.f, 0.f, 0.f, 0.f};
+        if (j < nv)
+          for (int c = 0; c < 4; ++c) r[c] = (float)src[(int64_t)j * ld + c];
+        for (int c = 0; c < 4; ++c) cx[c * a.cap + j] = r[c];
+      }
     }
   }
 }
@@ -784,24 +788,25 @@ __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, doubl
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+    const int64_t loc0 = tl.pstart - poff;
+    const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
+    v2d* d2 = reinterpret_cast<v2d*>(aos + (doff + loc0) * 4);
+    const float* cx = a.cols + tl.pstart;
+    for (int q0 = 0; q0 < 2 * nv; q0 += kStageUnroll * kBlock) {
+      v2d v[kStageUnroll];
 #pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-      const int g = it * kBlock + threadIdx.x;
-      if (g >= tl.ngroups) continue;
-      const int64_t p = tl.pstart + 4 * (int64_t)g;
-      const int64_t loc = p - poff;
-      const int64_t nv = cnt - loc;
-      const float4 X = ld4(a.cols + p), Y = ld4(a.cols + a.cap + p), Z = ld4(a.cols + 2 * a.cap + p),
-                   I = ld4(a.cols + 3 * a.cap + p);
-      v2d* dst = reinterpret_cast<v2d*>(aos + (doff + loc) * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (e < nv) {
-          const v2d xy = {(double)f4g(X, e), (double)f4g(Y, e)};
-          const v2d zi = {(double)f4g(Z, e), (double)f4g(I, e)};
-          __builtin_nontemporal_store(xy, dst + 2 * e);
-          __builtin_nontemporal_store(zi, dst + 2 * e + 1);
+      for (int u = 0; u < kStageUnroll; ++u) {
+        const int q = q0 + u * kBlock + threadIdx.x;
+        if (q < 2 * nv) {
+          const int j = q >> 1, h = q & 1;
+          v[u] = v2d{(double)__builtin_nontemporal_load(cx + (2 * h) * a.cap + j),
+                     (double)__builtin_nontemporal_load(cx + (2 * h + 1) * a.cap + j)};
         }
+      }
+#pragma unroll
+      for (int u = 0; u < kStageUnroll; ++u) {
+        const int q = q0 + u * kBlock + threadIdx.x;
+        if (q < 2 * nv) __builtin_nontemporal_store(v[u], d2 + q);
       }
     }
   }
