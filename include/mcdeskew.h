@@ -134,6 +134,21 @@ int mc_batch_stage_aos_f64_device(mc_batch* b, const double* d_aos, int64_t ld);
 int mc_batch_fetch_aos_f64_device(mc_batch* b, double* d_aos);
 int mc_timing_read_layout(mc_ctx* ctx, double* ms_total, int64_t* launches);
 
+/* ---- scan_environment, the step before the path (LMC:701-770) ----------- */
+/* scene points (n, ld>=4) float64 [x, y, z, intensity, ...], copied to the device */
+int mc_set_environment(mc_ctx* ctx, int64_t n, const double* env, int64_t ld);
+/* Pass 1 for F frames: sensor pose per frame from the trajectory (pose_select as mc_deskew's
+ * frame mode; frame_times used by MC_POSE_SEARCHSORTED), visibility of every scene point,
+ * params = {range_min, range_max, fov_horizontal, fov_vertical} (degrees, full angles),
+ * systematic subsample to points_per_frame.  counts_out[F] = points each frame's scan keeps. */
+int mc_scan_count(mc_ctx* ctx, int32_t n_frames, const double* frame_times, int pose_select,
+                  const double* params, int64_t points_per_frame, int64_t* counts_out);
+/* Pass 2: writes the scans into `out` (created with counts_out as frame counts) as sensor-frame
+ * x,y,z + noise, intensity.  noise: (sum(counts), 3) float64 drawn by the caller in frame order
+ * (LMC:767 np.random.normal), or NULL for noise-free scans. */
+int mc_scan_emit(mc_ctx* ctx, mc_batch* out, const double* noise);
+int mc_timing_read_scan(mc_ctx* ctx, double* ms_total, int64_t* launches);
+
 /* Synthetic Mid-70 frames generated on the device (counter-hash RNG, bit-identical to
  * oracle/synth.py): frame f uses seed  seed + frame_id_base + f. */
 int mc_batch_synth(mc_batch* b, uint64_t seed, int64_t frame_id_base);

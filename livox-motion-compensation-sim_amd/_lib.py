@@ -73,6 +73,10 @@ _SIGS = {
     "mc_batch_stage_aos_f64_device": (c_int, [c_void_p, c_void_p, c_int64]),
     "mc_batch_fetch_aos_f64_device": (c_int, [c_void_p, c_void_p]),
     "mc_timing_read_layout": (c_int, [c_void_p, _pd, _pi64]),
+    "mc_set_environment": (c_int, [c_void_p, c_int64, _pd, c_int64]),
+    "mc_scan_count": (c_int, [c_void_p, c_int32, _pd, c_int, _pd, c_int64, _pi64]),
+    "mc_scan_emit": (c_int, [c_void_p, c_void_p, _pd]),
+    "mc_timing_read_scan": (c_int, [c_void_p, _pd, _pi64]),
     "mc_batch_synth": (c_int, [c_void_p, c_uint64, c_int64]),
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),
     "mc_deskew": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),

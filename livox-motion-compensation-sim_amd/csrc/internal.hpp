@@ -38,6 +38,19 @@ struct mc_ctx {
   int64_t* d_imu_ts = nullptr;
   double* d_gyro = nullptr;
   mc::ImuSeg* d_imu_seg = nullptr;     // 2 * M_cap (double buffer)
+  // scan_environment state (LMC:701-770): scene, per-frame f64 poses, per-(frame, tile) counts
+  int64_t E = 0, env_ld = 4;
+  double* d_env = nullptr;
+  int32_t scan_F = 0, scan_tiles = 0;
+  double* d_scan_ftime = nullptr;
+  double* d_scan_pose = nullptr;
+  int32_t* d_scan_tcount = nullptr;
+  int64_t* d_scan_toff = nullptr;
+  int64_t* d_scan_nvis = nullptr;
+  std::vector<int64_t> scan_counts;   // final per-frame counts of the last mc_scan_count
+  double scan_par[4] = {0, 0, 0, 0};  // range_min, range_max^2, fov_h/2, fov_v/2
+  int64_t scan_cap = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> scan_ev;
   // staging buffer for host<->device layout conversion
   void* d_stage = nullptr;
   size_t stage_bytes = 0;

@@ -5,6 +5,7 @@
 // plain pointers and sizes in, status codes out (thread-local message in mc_last_error()).
 #include "../../include/mcdeskew.h"
 #include "kernels.hpp"
+#include "scan.hpp"
 #include "internal.hpp"
 
 #include <algorithm>
@@ -208,8 +209,11 @@ int mc_destroy(mc_ctx* c) {
   (void)sync_all(c);
   dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
   dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
+  dev_free(c->d_env); dev_free(c->d_scan_ftime); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount);
+  dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis);
   if (c->d_stage) (void)hipFree(c->d_stage);
   for (auto& p : c->main_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
+  for (auto& p : c->scan_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->prep_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->layout_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -714,6 +718,133 @@ int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms,
   if (int r = sync_all(c)) return r;
   if (int r = sum_events(c, c->main_ev, main_ms, main_n)) return r;
   return sum_events(c, c->prep_ev, prep_ms, prep_n);
+}
+
+// ---- scan_environment (LMC:701-770) --------------------------------------------------------
+int mc_set_environment(mc_ctx* c, int64_t n, const double* env, int64_t ld) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(n >= 0, "negative scene size");
+  if (ld < 4) return fail(MC_ERR_INDEX, "scene points need at least 4 columns; got %lld", (long long)ld);
+  CHECK_ARG(n == 0 || env, "scene pointer is NULL");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  dev_free(c->d_env);
+  c->E = 0;
+  if (int r = dev_alloc(&c->d_env, (size_t)std::max<int64_t>(n, 1) * ld)) return r;
+  if (n > 0) {
+    HIPCHK(hipMemcpyAsync(c->d_env, env, (size_t)n * ld * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  c->E = n;
+  c->env_ld = ld;
+  return MC_OK;
+}
+
+int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_select, const double* params,
+                  int64_t cap, int64_t* counts_out) {
+  CHECK_ARG(c && params && counts_out, "NULL argument");
+  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(cap >= 1, "points_per_frame must be >= 1");
+  CHECK_ARG(pose_select == MC_POSE_SEARCHSORTED || pose_select == MC_POSE_DIRECT, "unknown pose_select");
+  if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
+  if (pose_select == MC_POSE_DIRECT && c->T != F)
+    return fail(MC_ERR_INVALID, "MC_POSE_DIRECT needs one pose per frame (T=%lld, frames=%d)", (long long)c->T, F);
+  CHECK_ARG(pose_select == MC_POSE_DIRECT || F == 0 || frame_times, "frame times are NULL");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  const int32_t tiles = (int32_t)((c->E + kScanTile - 1) / kScanTile);
+  dev_free(c->d_scan_ftime); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount); dev_free(c->d_scan_toff);
+  dev_free(c->d_scan_nvis);
+  c->scan_F = 0;
+  if (int r = dev_alloc(&c->d_scan_ftime, std::max(F, 1))) return r;
+  if (int r = dev_alloc(&c->d_scan_pose, 12 * (size_t)std::max(F, 1))) return r;
+  if (int r = dev_alloc(&c->d_scan_tcount, (size_t)std::max(F, 1) * std::max(tiles, 1))) return r;
+  if (int r = dev_alloc(&c->d_scan_toff, (size_t)std::max(F, 1) * std::max(tiles, 1))) return r;
+  if (int r = dev_alloc(&c->d_scan_nvis, std::max(F, 1))) return r;
+  c->scan_par[0] = params[0];
+  c->scan_par[1] = params[1] * params[1];   // LMC:715 max_range_sq
+  c->scan_par[2] = params[2] / 2;           // LMC:740
+  c->scan_par[3] = params[3] / 2;           // LMC:741
+  c->scan_cap = cap;
+  c->scan_counts.assign(F, 0);
+  c->scan_F = F;
+  c->scan_tiles = tiles;
+  if (F == 0) return MC_OK;
+  if (pose_select == MC_POSE_SEARCHSORTED)
+    HIPCHK(hipMemcpyAsync(c->d_scan_ftime, frame_times, F * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_scan_pose, dim3((F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->d_time, c->d_pos,
+                     c->d_rpy, c->T, c->d_scan_ftime, F, pose_select, c->d_scan_pose);
+  HIPCHK(hipGetLastError());
+  std::vector<int64_t> nvis(F, 0), toff((size_t)F * std::max(tiles, 1), 0);
+  if (tiles > 0) {
+    ScanParams sp{c->scan_par[0], c->scan_par[1], c->scan_par[2], c->scan_par[3], cap};
+    {
+      TimedRegion tr(c, &c->scan_ev, c->stream);
+      hipLaunchKernelGGL(k_scan_count, dim3(tiles, F), dim3(kBlock), 0, c->stream, c->d_env, c->env_ld, c->E,
+                         c->d_scan_pose, sp, c->d_scan_tcount);
+    }
+    HIPCHK(hipGetLastError());
+    std::vector<int32_t> tc((size_t)F * tiles);
+    HIPCHK(hipMemcpyAsync(tc.data(), c->d_scan_tcount, tc.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int32_t f = 0; f < F; ++f) {
+      int64_t run = 0;
+      for (int32_t t = 0; t < tiles; ++t) { toff[(size_t)f * tiles + t] = run; run += tc[(size_t)f * tiles + t]; }
+      nvis[f] = run;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_scan_toff, toff.data(), (size_t)F * tiles * sizeof(int64_t), hipMemcpyHostToDevice,
+                          c->stream));
+  }
+  HIPCHK(hipMemcpyAsync(c->d_scan_nvis, nvis.data(), F * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int32_t f = 0; f < F; ++f) {
+    // LMC:757-762: every (n // cap)-th visible point, at most cap of them
+    const int64_t n = nvis[f];
+    int64_t k = n;
+    if (n > cap) {
+      const int64_t step = n / cap;
+      k = std::min<int64_t>(cap, (n + step - 1) / step);
+    }
+    c->scan_counts[f] = k;
+    counts_out[f] = k;
+  }
+  return MC_OK;
+}
+
+int mc_scan_emit(mc_ctx* c, mc_batch* out, const double* noise) {
+  CHECK_ARG(c && out, "NULL argument");
+  CHECK_ARG(out->ctx == c, "batch belongs to another context");
+  if (out->counts != c->scan_counts)
+    return fail(MC_ERR_INVALID, "output batch frame counts differ from the last mc_scan_count");
+  if (out->F == 0 || out->N == 0 || c->scan_tiles == 0) return MC_OK;
+  DeviceGuard g(c->device);
+  const double* d_noise = nullptr;
+  if (noise) {
+    void* st = nullptr;
+    if (int r = ctx_stage(c, (size_t)out->N * 3 * sizeof(double), &st)) return r;
+    HIPCHK(hipMemcpyAsync(st, noise, (size_t)out->N * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    d_noise = static_cast<const double*>(st);
+  }
+  ScanEmitArgs ea;
+  ea.env = c->d_env; ea.ld = c->env_ld; ea.E = c->E;
+  ea.pose = c->d_scan_pose;
+  ea.sp = ScanParams{c->scan_par[0], c->scan_par[1], c->scan_par[2], c->scan_par[3], c->scan_cap};
+  ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.noise = d_noise;
+  ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.cap = out->cap;
+  {
+    TimedRegion tr(c, &c->scan_ev, c->stream);
+    hipLaunchKernelGGL(k_scan_emit, dim3(c->scan_tiles, out->F), dim3(kBlock), 0, c->stream, ea);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_timing_read_scan(mc_ctx* c, double* ms, int64_t* n) {
+  CHECK_ARG(c, "ctx is NULL");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  return sum_events(c, c->scan_ev, ms, n);
 }
 
 int mc_timing_read_layout(mc_ctx* c, double* ms, int64_t* n) {

@@ -84,6 +84,44 @@ class Context:
                                  _lib.POSE_SELECT[pose_select]), f"deskew[{mode}]")
         return out
 
+    # ---- scan_environment (LMC:701-770) ----------------------------------------------------
+    def set_environment(self, environment):
+        """Static scene (E, >=4) float64 [x, y, z, intensity] (LMC:430-699's output), to HBM."""
+        env = np.asarray(environment)
+        if env.ndim != 2:
+            raise IndexError(f"too many indices for array: array is {env.ndim}-dimensional, but 2 were indexed")
+        env = np.ascontiguousarray(env, dtype=np.float64)
+        check(self.lib.mc_set_environment(self.handle, env.shape[0], ptr(env, c_double), env.shape[1]),
+              "set_environment")
+
+    def scan(self, frame_times, config: dict, pose_select: str = "searchsorted", rng=np.random,
+             out: "Batch | None" = None) -> "Batch":
+        """All frames' local scans of the scene (LMC:701-770 once per frame of LMC:802-831) in two
+        launches: visibility counts per (frame, scene tile), then in-order compaction, the systematic
+        subsample and the range noise.  The trajectory must be set (pose per frame as in
+        ``deskew(mode='frame')``).  The noise is drawn here from ``rng`` (numpy's global RNG by
+        default) in frame order, exactly as the reference's per-frame ``np.random.normal`` calls
+        consume it (LMC:765-768), so seeded runs reproduce the reference's scans."""
+        t = np.ascontiguousarray(np.atleast_1d(frame_times), dtype=np.float64)
+        F = len(t)
+        par = np.array([config["range_min"], config["range_max"], config["fov_horizontal"],
+                        config["fov_vertical"]], np.float64)
+        counts = np.zeros(F, np.int64)
+        check(self.lib.mc_scan_count(self.handle, F, ptr(t, c_double), _lib.POSE_SELECT[pose_select],
+                                     ptr(par, c_double), int(config["points_per_frame"]), ptr(counts, c_int64)),
+              "scan_count")
+        if out is None or not np.array_equal(out.counts, counts):
+            out = Batch(self, counts)
+        noise = None
+        std = config["lidar_range_noise"]
+        if std > 0 and counts.sum() > 0:
+            # one draw of sum(n_f) x 3 consumes the legacy normal stream exactly like F per-frame
+            # draws of n_f x 3 (frames with no visible point draw nothing in the reference either)
+            noise = np.ascontiguousarray(rng.normal(0, std, (int(counts.sum()), 3)), dtype=np.float64)
+        check(self.lib.mc_scan_emit(self.handle, out.handle, ptr(noise, c_double) if noise is not None else None),
+              "scan_emit")
+        return out
+
     def set_max_grid(self, max_grid: int):
         check(self.lib.mc_set_launch(self.handle, int(max_grid)), "set_launch")
 
@@ -96,8 +134,10 @@ class Context:
         check(self.lib.mc_timing_read(self.handle, ctypes.byref(mm), ctypes.byref(mn), ctypes.byref(pm),
                                       ctypes.byref(pn)), "timing_read")
         check(self.lib.mc_timing_read_layout(self.handle, ctypes.byref(lm), ctypes.byref(ln)), "timing_read_layout")
+        sm, sn = c_double(), c_int64()
+        check(self.lib.mc_timing_read_scan(self.handle, ctypes.byref(sm), ctypes.byref(sn)), "timing_read_scan")
         return {"main_ms": mm.value, "main_launches": mn.value, "prep_ms": pm.value, "prep_launches": pn.value,
-                "layout_ms": lm.value, "layout_launches": ln.value}
+                "layout_ms": lm.value, "layout_launches": ln.value, "scan_ms": sm.value, "scan_launches": sn.value}
 
     def device_buffer(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)

@@ -165,6 +165,73 @@ class LiDARMotionSimulator:
         ctx.deskew(bin_, bout, mode="pose_slerp")
         return bout.split(bout.download_aos())
 
+    # ---- scanning (LMC:701-770) and the frame loop (LMC:778-858) ----------------------------
+    def _load_environment(self, environment) -> np.ndarray:
+        """Upload the scene once per distinct array (identity, buffer, shape and sum)."""
+        env = np.asarray(environment)
+        if env.ndim != 2:
+            raise IndexError(f"too many indices for array: array is {env.ndim}-dimensional, but 2 were indexed")
+        key = (id(environment), env.__array_interface__["data"][0], env.shape, float(np.sum(env[:, :4])))
+        if getattr(self, "_env_key", None) != key:
+            self.context.set_environment(env)
+            self._env_key = key
+        return env
+
+    def scan_environment(self, environment, sensor_pose):
+        """LMC:701-770: the sensor-frame scan of ``environment`` from one pose (``position`` and
+        ``orientation`` rad), (n, 4) [x, y, z, intensity]; draws the range noise from the global
+        RNG like the reference."""
+        self._load_environment(environment)
+        ctx = self.context
+        ctx.set_trajectory([0.0], np.asarray(sensor_pose["position"], np.float64).reshape(1, 3),
+                           np.asarray(sensor_pose["orientation"], np.float64).reshape(1, 3))
+        scans = ctx.scan([0.0], self.config, pose_select="direct")
+        return scans.download_aos() if scans.n_points else np.zeros((0, 4))
+
+    def scan_frames(self, environment, trajectory: dict, times: Optional[np.ndarray] = None):
+        """Every frame's scan (LMC:802-817 pose selection + 815 scan) as one device batch, noise
+        drawn in frame order from the global RNG.  Returns the device ``Batch`` of local scans."""
+        if times is None:
+            times = self.lidar_times()
+        self._load_environment(environment)
+        ctx = self.context
+        ctx.set_trajectory(trajectory["time"], trajectory["position_gps"], trajectory["orientation_imu"])
+        return ctx.scan(np.asarray(times, np.float64), self.config, pose_select="searchsorted")
+
+    def simulate_frames(self, environment, trajectory: dict, times: Optional[np.ndarray] = None) -> dict:
+        """The frame loop of run_simulation (LMC:802-850) with both point stages on the GPU: the
+        scans are produced into HBM and aligned there (MC_POSE_SEARCHSORTED) without a host round
+        trip in between.  Returns run_simulation's dict (LMC:852-858)."""
+        if times is None:
+            times = self.lidar_times()
+        times = np.asarray(times, np.float64)
+        scans = self.scan_frames(environment, trajectory, times)
+        scans.set_frame_times(times)
+        aligned_b = self.context.deskew(scans, None, mode="frame", pose_select="searchsorted")
+        local = scans.split(scans.download_aos())
+        aligned = aligned_b.split(aligned_b.download_aos())
+        idx = np.clip(np.searchsorted(trajectory["time"], times), 0, len(trajectory["time"]) - 1)
+        raw, motion = [], []
+        for i, (t, k) in enumerate(zip(times, idx)):
+            pose = {"position": trajectory["position_gps"][k], "orientation": trajectory["orientation_imu"][k],
+                    "velocity": trajectory["velocity"][k]}
+            raw.append({"frame_id": i, "timestamp": t, "points_local": local[i], "sensor_pose": pose})
+            p, o, v = pose["position"], pose["orientation"], pose["velocity"]
+            motion.append({"frame_id": i, "timestamp": t,
+                           "gps_lat": p[1] / 111320.0 + 40.0,
+                           "gps_lon": p[0] / (111320.0 * np.cos(np.radians(40.0))) - 74.0,
+                           "gps_alt": p[2], "imu_roll": o[0], "imu_pitch": o[1], "imu_yaw": o[2],
+                           "vel_x": v[0], "vel_y": v[1], "vel_z": v[2]})
+        return {"raw_scans": raw, "aligned_pointclouds": aligned, "motion_data": motion,
+                "trajectory": trajectory, "environment": environment}
+
+    def run_simulation(self, environment):
+        """LMC:778-858 given the scene: trajectory + sensor noise (LMC:784-785, global RNG), then
+        simulate_frames over the lidar time grid.  Scene synthesis (LMC:430-699) is not provided
+        (DESIGN.md §6): pass the environment array."""
+        trajectory = self.add_sensor_noise(self.generate_trajectory())
+        return self.simulate_frames(environment, trajectory, self.lidar_times())
+
     @staticmethod
     def merge_aligned(aligned: List[np.ndarray]) -> np.ndarray:
         """LMC:887-889: frame-ordered concatenation of the aligned clouds."""

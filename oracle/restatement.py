@@ -23,7 +23,7 @@ import numpy as np
 
 __all__ = [
     "euler_xyz_matrix", "euler_xyz_quat", "select_pose_index", "transform_pointcloud",
-    "align_frames", "merge_aligned", "imu_interpolate_gyro", "compensate_arrays",
+    "align_frames", "merge_aligned", "scan_environment", "imu_interpolate_gyro", "compensate_arrays",
     "compensate_point_cloud_loop", "slerp_pose", "deskew_pose_slerp",
 ]
 
@@ -92,6 +92,38 @@ def align_frames(scans, trajectory, times) -> list:
         out.append(transform_pointcloud(scan, {"translation": trajectory["position_gps"][k],
                                                "rotation": trajectory["orientation_imu"][k]}))
     return out
+
+
+def scan_environment(environment, sensor_pose, config, rng=np.random) -> np.ndarray:
+    """LMC:701-770: local scan of the scene from a pose.  Range prefilter on the world distance
+    (709-723), R^T (p - t) into the sensor frame (726-728), FOV mask on atan2 / asin in degrees and
+    range_min (735-745), systematic subsample to points_per_frame (754-762), N(0, range_noise)
+    added to the kept points from the global RNG (765-768); returns (n, 4) [x, y, z, intensity]."""
+    env = np.asarray(environment, dtype=np.float64)
+    pos = np.asarray(sensor_pose["position"], dtype=np.float64)
+    d2 = np.sum((env[:, :3] - pos) ** 2, axis=1)
+    keep = d2 <= config["range_max"] ** 2
+    if not np.any(keep):
+        return np.zeros((0, 4))
+    envf = env[keep]
+    Rm = euler_xyz_matrix(np.asarray(sensor_pose["orientation"], dtype=np.float64))
+    loc = (Rm.T @ (envf[:, :3] - pos).T).T
+    rng_ = np.sqrt(d2[keep])
+    az = np.arctan2(loc[:, 1], loc[:, 0]) * 180 / np.pi
+    el = np.arcsin(np.clip(loc[:, 2] / np.maximum(rng_, 1e-6), -1, 1)) * 180 / np.pi
+    fov = ((np.abs(az) <= config["fov_horizontal"] / 2) & (np.abs(el) <= config["fov_vertical"] / 2)
+           & (rng_ >= config["range_min"]))
+    if not np.any(fov):
+        return np.zeros((0, 4))
+    pts = loc[fov]
+    inten = envf[fov, 3]
+    n, cap = len(pts), config["points_per_frame"]
+    if n > cap:
+        sel = np.arange(0, n, n // cap)[:cap]
+        pts, inten = pts[sel], inten[sel]
+    if config["lidar_range_noise"] > 0:
+        pts = pts + rng.normal(0, config["lidar_range_noise"], pts.shape)
+    return np.column_stack([pts, inten])
 
 
 def merge_aligned(aligned) -> np.ndarray:

@@ -91,6 +91,20 @@ def make_lmc(lmc):
     np.savez_compressed(os.path.join(HERE, "lmc_frames.npz"), **out)
 
 
+def make_env(lmc):
+    """The scene each scenario scans and the global RNG state right before the reference's frame
+    loop (LMC:802): run_simulation draws trajectory noise (LMC:785) and the environment (LMC:789)
+    first, so replaying those steps from a fresh seed-42 construction reproduces both."""
+    for name, cfg in SCENARIOS.items():
+        sim = lmc.LiDARMotionSimulator(dict(cfg))
+        sim.add_sensor_noise(sim.generate_trajectory())
+        env = sim.generate_environment_pointcloud()
+        kind, keys, pos, has_gauss, cached = np.random.get_state()
+        np.savez_compressed(os.path.join(HERE, f"lmc_env_{name}.npz"), environment=env,
+                            rng_keys=keys, rng_pos=np.int64(pos), rng_has_gauss=np.int64(has_gauss),
+                            rng_cached=np.float64(cached))
+
+
 def make_kat(lmc):
     rng = np.random.default_rng(7)
     sim = lmc.LiDARMotionSimulator()
@@ -225,6 +239,7 @@ def make_synth():
 def main():
     lmc, csim = import_reference()
     make_lmc(lmc)
+    make_env(lmc)
     make_kat(lmc)
     make_config(lmc)
     make_pathb(csim)

@@ -163,6 +163,36 @@ def test_synth_generator_matches_committed_vectors():
     assert t[0] == 0 and (np.diff(t) >= 0).all() and t[-1] < 100_000_000
 
 
+def restore_rng(env_fixture):
+    np.random.set_state(("MT19937", env_fixture["rng_keys"], int(env_fixture["rng_pos"]),
+                         int(env_fixture["rng_has_gauss"]), float(env_fixture["rng_cached"])))
+
+
+@pytest.mark.parametrize("name", list(SCEN))
+def test_scan_environment_replays_reference_frame_loop(name):
+    """LMC:802-832 replayed with the oracle's scan: every frame's point count and the recorded
+    frames' local scans and aligned clouds match the reference run (same RNG stream)."""
+    g = golden("lmc_frames.npz")
+    e = golden(f"lmc_env_{name}.npz")
+    tr = golden(f"lmc_traj_{name}.npz")
+    m = pkg()
+    cfg = dict(m.default_config(), **CFGS[name])
+    times = m.trajectory.lidar_times(cfg)
+    restore_rng(e)
+    idx = R.select_pose_index(tr["time"], times)
+    counts = []
+    want = set(SCEN[name])
+    for f, t in enumerate(times):
+        pose = {"position": tr["position_gps"][idx[f]], "orientation": tr["orientation_imu"][idx[f]]}
+        scan = R.scan_environment(e["environment"], pose, cfg)
+        counts.append(len(scan))
+        if f in want:
+            np.testing.assert_allclose(scan, g[f"{name}/{f}/points_local"], rtol=0, atol=1e-9)
+            al = R.transform_pointcloud(scan, {"translation": pose["position"], "rotation": pose["orientation"]})
+            np.testing.assert_allclose(al, g[f"{name}/{f}/aligned"], rtol=0, atol=1e-9)
+    assert np.array_equal(np.array(counts), g[f"{name}/frame_counts"])
+
+
 def test_golden_files_are_data_only():
     for f in os.listdir(GOLDEN):
         assert f.endswith((".npz", ".json", ".py")), f
