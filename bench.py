@@ -131,6 +131,51 @@ def measure_stager(ctx, b_in, b_out, n_rank, reps):
         buf.close()
 
 
+def measure_scan(ctx, cfg, tr, reps, cpu_budget):
+    """SURVEY §8f row 2, reported beside the hot path: scan_environment for every frame of the
+    urban_complex run (1200 frames, LMC:792-815) against a scene the size of the reference's urban
+    scene (29,000 points, LMC:430-699), noise on.  Unit: scene points tested per second (F x E)."""
+    rng = np.random.default_rng(7)
+    E = 29_000
+    env = np.column_stack([rng.uniform(-200, 200, E), rng.uniform(-200, 200, E), rng.uniform(-25, 70, E),
+                           rng.uniform(0, 1, E)])
+    times = mc.trajectory.lidar_times(cfg)[:1200]
+    F = len(times)
+    scfg = dict(mc.default_config(), **URBAN)
+    ctx.set_environment(env)
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    out = ctx.scan(times, scfg)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = ctx.scan(times, scfg, out=out)
+    wall = (time.perf_counter() - t0) / reps
+    ctx.read_timing()
+    ctx.timing(True)
+    for _ in range(reps):
+        out = ctx.scan(times, scfg, out=out)
+    ctx.timing(False)
+    tm = ctx.read_timing()
+    kern = tm["scan_ms"] / max(tm["scan_launches"], 1) * 2 / 1e3    # count + emit per scan
+    rep = {"workload": f"{F} frames x {E} scene pts (urban_complex run, synthetic scene)",
+           "wall_ms": wall * 1e3, "kernels_ms": kern * 1e3, "Mtests_s_wall": F * E / wall / 1e6,
+           "Mtests_s_kernels": F * E / kern / 1e6, "points_out": int(out.n_points),
+           "note": "wall includes host noise draw (numpy normal) + H2D of the noise"}
+    if cpu_budget > 0:
+        from oracle import restatement as R
+        idx = R.select_pose_index(tr["time"], times)
+        t_cpu, f = 0.0, 0
+        while f < F and t_cpu < cpu_budget:
+            pose = {"position": tr["position_gps"][idx[f]], "orientation": tr["orientation_imu"][idx[f]]}
+            t1 = time.perf_counter()
+            R.scan_environment(env, pose, scfg)
+            t_cpu += time.perf_counter() - t1
+            f += 1
+        rep["cpu_baseline"] = {"Mtests_s": f * E / t_cpu / 1e6, "cores": 1, "kind": "port",
+                               "sample": f"{f} frames, oracle numpy restatement"}
+    return rep
+
+
 def timed_gather(ctx, rdv, b_in, b_out, mode, n_rank, world, timeout_s):
     """The merged-cloud gather to rank 0 (LMC:887-889 over RCCL), after and outside the timed
     steps, under a watchdog so that a stuck collective can never cost the throughput line.
@@ -211,6 +256,10 @@ def main():
                          "value": n_rank * world * steps / wall_max / 1e6}
 
     stager = measure_stager(ctx, b_in, b_out, n_rank, min(args.steps, 50))
+    scan = None
+    if not args.no_extra_modes:
+        scan = measure_scan(ctx, cfg, tr, 10, 0.0 if (args.no_cpu or world > 1) else 3.0)
+        ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
 
     gather = None
     hung = False
@@ -249,6 +298,7 @@ def main():
                           "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"]}
                       for m, v in results.items()},
             "stager": stager,
+            "scan_environment": scan,
             "gather": gather,
         }
         if world == 1 and not args.no_cpu:
