@@ -61,6 +61,7 @@ extern "C" {
 #define MC_ERR_STATE -4     /* missing prerequisite (e.g. no trajectory uploaded) */
 #define MC_ERR_INDEX -5     /* column count < 4: Python maps to IndexError (LMC:776) */
 #define MC_ERR_COMM -6      /* RCCL failure                                       */
+#define MC_ERR_SPACE -7     /* output buffer too small (the size needed is reported) */
 
 /* deskew modes */
 #define MC_MODE_FRAME 0      /* Path A: one SE(3) pose per frame, p' = R(rpy) p + t   (LMC:772-776)    */
@@ -148,6 +149,28 @@ int mc_scan_count(mc_ctx* ctx, int32_t n_frames, const double* frame_times, int 
  * (LMC:767 np.random.normal), or NULL for noise-free scans. */
 int mc_scan_emit(mc_ctx* ctx, mc_batch* out, const double* noise);
 int mc_timing_read_scan(mc_ctx* ctx, double* ms_total, int64_t* launches);
+
+/* ---- output codecs, encoded from a device (N, ld) float64 AoS cloud whose
+ * frames lie back to back (counts[f] rows each): the array layout the reference hands its writers.
+ * Both are synchronous and timed under mc_timing_read_codec. ------------------------------------ */
+/* LVX v1.1 layout (LMC:113-132): byte offset of every frame; frame_pos[F] = file size. Host only. */
+int mc_lvx_layout(int32_t n_frames, const int64_t* counts, int64_t* frame_pos);
+/* The whole LVX v1.1 file of LivoxLVXWriter.write_compatible_lvx (LMC:57-272) into d_out
+ * (>= frame_pos[F] bytes, 2-byte aligned): 88-byte file header, per frame a 24-byte header
+ * (offset, next offset, frame_ids[f]) and 96-point packages stamped timestamp_ns[f]
+ * (= int(timestamp * 1e9), LMC:176).  ld >= 3; has_intensity[f] == 0 gives reflectivity 128
+ * (LMC:268); has_intensity NULL means (ld > 3).  A NaN coordinate or intensity -> MC_ERR_INVALID
+ * (the reference's int(nan) fails its write). */
+int mc_lvx_encode(mc_ctx* ctx, const double* d_aos, int64_t ld, int32_t n_frames, const int64_t* counts,
+                  const uint64_t* frame_ids, const uint64_t* timestamp_ns, const uint8_t* has_intensity,
+                  void* d_out, int64_t out_bytes);
+/* ASCII PCD point lines of save_pcd (LMC:946-948, "%.6f %.6f %.6f %.6f\n", Python's correctly
+ * rounded formatting) for F clouds, back to back in d_out; body_pos[F+1] receives each cloud's byte
+ * offset (body_pos[F] = total).  If out_bytes < total: MC_ERR_SPACE, body_pos filled, nothing
+ * written.  |value| >= 2^107 -> MC_ERR_INVALID (beyond the device formatter). */
+int mc_pcd_encode(mc_ctx* ctx, const double* d_aos, int64_t ld, int32_t n_frames, const int64_t* counts,
+                  void* d_out, int64_t out_bytes, int64_t* body_pos);
+int mc_timing_read_codec(mc_ctx* ctx, double* ms_total, int64_t* launches);
 
 /* Synthetic Mid-70 frames generated on the device (counter-hash RNG, bit-identical to
  * oracle/synth.py): frame f uses seed  seed + frame_id_base + f. */

@@ -19,6 +19,7 @@ MC_ERR_NOMEM = -3
 MC_ERR_STATE = -4
 MC_ERR_INDEX = -5
 MC_ERR_COMM = -6
+MC_ERR_SPACE = -7
 
 MC_MODE_FRAME = 0
 MC_MODE_POSE_SLERP = 1
@@ -77,6 +78,11 @@ _SIGS = {
     "mc_scan_count": (c_int, [c_void_p, c_int32, _pd, c_int, _pd, c_int64, _pi64]),
     "mc_scan_emit": (c_int, [c_void_p, c_void_p, _pd]),
     "mc_timing_read_scan": (c_int, [c_void_p, _pd, _pi64]),
+    "mc_lvx_layout": (c_int, [c_int32, _pi64, _pi64]),
+    "mc_lvx_encode": (c_int, [c_void_p, c_void_p, c_int64, c_int32, _pi64, POINTER(c_uint64), POINTER(c_uint64),
+                              POINTER(ctypes.c_uint8), c_void_p, c_int64]),
+    "mc_pcd_encode": (c_int, [c_void_p, c_void_p, c_int64, c_int32, _pi64, c_void_p, c_int64, _pi64]),
+    "mc_timing_read_codec": (c_int, [c_void_p, _pd, _pi64]),
     "mc_batch_synth": (c_int, [c_void_p, c_uint64, c_int64]),
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),
     "mc_deskew": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),

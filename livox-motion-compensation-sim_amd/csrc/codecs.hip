@@ -1,0 +1,207 @@
+// codecs.hip — host side of the output codecs in include/mcdeskew.h:
+// LVX v1.1 files (LMC:24-272) and ASCII PCD bodies (LMC:932-948) encoded on the device from a
+// device-resident (N, ld) float64 AoS cloud.
+#include "codecs.hpp"
+#include "hostutil.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+using namespace mc;
+
+namespace {
+
+int codec_scratch(mc_ctx* c, size_t bytes, char** out) {
+  if (bytes > c->codec_bytes) {
+    if (c->d_codec) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->d_codec); c->d_codec = nullptr; }
+    c->codec_bytes = 0;
+    HIPCHK(hipMalloc(&c->d_codec, bytes));
+    c->codec_bytes = bytes;
+  }
+  if (!c->d_codec_err) {
+    if (int r = dev_alloc(&c->d_codec_err, 1)) return r;
+  }
+  *out = static_cast<char*>(c->d_codec);
+  return MC_OK;
+}
+
+// the 88 bytes ahead of the first frame: public header (LMC:86-101), private header (LMC:104-110),
+// device info block (LMC:146-172)
+void lvx_file_header(uint8_t h[kLvxFileHdr]) {
+  std::memset(h, 0, kLvxFileHdr);
+  std::memcpy(h, "livox_tech", 10);
+  h[16] = 1; h[17] = 1;
+  const uint32_t magic = 0xAC0EA767u, dur = 50;
+  std::memcpy(h + 20, &magic, 4);
+  std::memcpy(h + 24, &dur, 4);
+  h[28] = 1;                                       // device count
+  std::memcpy(h + 29, "3GGDJ6K00200101", 15);      // LiDAR SN (16 B, NUL-terminated)
+  h[29 + 33] = 1;                                  // device type
+}
+
+int check_frames(int32_t F, const int64_t* counts, std::vector<int64_t>& doff) {
+  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(F == 0 || counts, "counts is NULL");
+  doff.assign((size_t)F + 1, 0);
+  for (int32_t f = 0; f < F; ++f) {
+    CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
+    doff[f + 1] = doff[f] + counts[f];
+  }
+  return MC_OK;
+}
+
+template <typename T>
+size_t put(std::vector<uint8_t>& blob, const T* src, size_t n) {
+  const size_t at = (blob.size() + 7) & ~size_t(7);
+  blob.resize(at + n * sizeof(T));
+  if (n) std::memcpy(blob.data() + at, src, n * sizeof(T));
+  return at;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_lvx_layout(int32_t F, const int64_t* counts, int64_t* pos) {
+  CHECK_ARG(pos, "frame_pos is NULL");
+  std::vector<int64_t> doff;
+  if (int r = check_frames(F, counts, doff)) return r;
+  pos[0] = kLvxFileHdr;
+  for (int32_t f = 0; f < F; ++f)
+    pos[f + 1] = pos[f] + kLvxFrameHdr + (counts[f] + kLvxPkgPoints - 1) / kLvxPkgPoints * kLvxPkg;
+  return MC_OK;
+}
+
+int mc_lvx_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const int64_t* counts,
+                  const uint64_t* frame_ids, const uint64_t* ts_ns, const uint8_t* has_int, void* d_out,
+                  int64_t out_bytes) {
+  CHECK_ARG(c && d_out, "NULL argument");
+  if (ld < 3) return fail(MC_ERR_INDEX, "LVX points need at least 3 columns; got %lld", (long long)ld);
+  std::vector<int64_t> doff;
+  if (int r = check_frames(F, counts, doff)) return r;
+  CHECK_ARG(F == 0 || (frame_ids && ts_ns), "frame_ids / timestamp_ns are NULL");
+  CHECK_ARG(doff[F] == 0 || d_aos, "points pointer is NULL");
+  CHECK_ARG(((uintptr_t)d_out & 1) == 0, "d_out must be 2-byte aligned");
+  std::vector<int64_t> pos((size_t)F + 1), units((size_t)F + 1, 0);
+  mc_lvx_layout(F, counts, pos.data());
+  if (out_bytes < pos[F])
+    return fail(MC_ERR_SPACE, "LVX output needs %lld bytes, buffer has %lld", (long long)pos[F], (long long)out_bytes);
+  for (int32_t f = 0; f < F; ++f) units[f + 1] = units[f] + (counts[f] + kLvxPkgPoints - 1) / kLvxPkgPoints;
+  const int64_t n_pkg = units[F];
+  CHECK_ARG(n_pkg < (int64_t)INT32_MAX, "too many packages for one launch");
+  DeviceGuard g(c->device);
+
+  std::vector<uint8_t> blob;
+  const size_t o_doff = put(blob, doff.data(), doff.size());
+  const size_t o_unit = put(blob, units.data(), units.size());
+  const size_t o_pos = put(blob, pos.data(), (size_t)F);
+  const size_t o_ids = put(blob, frame_ids, (size_t)F);
+  const size_t o_ts = put(blob, ts_ns, (size_t)F);
+  const size_t o_hi = has_int ? put(blob, has_int, (size_t)F) : 0;
+  char* d = nullptr;
+  if (int r = codec_scratch(c, blob.size(), &d)) return r;
+  HIPCHK(hipMemcpyAsync(d, blob.data(), blob.size(), hipMemcpyHostToDevice, c->stream));
+  uint8_t hdr[kLvxFileHdr];
+  lvx_file_header(hdr);
+  HIPCHK(hipMemcpyAsync(d_out, hdr, kLvxFileHdr, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_codec_err, 0, sizeof(int), c->stream));
+
+  LvxArgs a;
+  a.src = CodecFrames{d_aos, ld, reinterpret_cast<const int64_t*>(d + o_doff),
+                      reinterpret_cast<const int64_t*>(d + o_unit), F};
+  a.frame_pos = reinterpret_cast<const int64_t*>(d + o_pos);
+  a.frame_id = reinterpret_cast<const uint64_t*>(d + o_ids);
+  a.ts_ns = reinterpret_cast<const uint64_t*>(d + o_ts);
+  a.has_int = has_int ? reinterpret_cast<const uint8_t*>(d + o_hi) : nullptr;
+  a.out = static_cast<uint16_t*>(d_out);
+  a.err = c->d_codec_err;
+  {
+    TimedRegion tr(c, &c->codec_ev, c->stream);
+    if (F > 0)
+      hipLaunchKernelGGL(k_lvx_frames, dim3((F + kCodecBlock - 1) / kCodecBlock), dim3(kCodecBlock), 0, c->stream,
+                         a, (int64_t)0);
+    if (n_pkg > 0)
+      hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
+  }
+  HIPCHK(hipGetLastError());
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, c->d_codec_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (err) return fail(MC_ERR_INVALID, "cannot convert float NaN to integer (NaN coordinate or intensity)");
+  return MC_OK;
+}
+
+int mc_pcd_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const int64_t* counts, void* d_out,
+                  int64_t out_bytes, int64_t* body_pos) {
+  CHECK_ARG(c && body_pos, "NULL argument");
+  if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 0 with size %lld", (long long)ld);
+  std::vector<int64_t> doff;
+  if (int r = check_frames(F, counts, doff)) return r;
+  CHECK_ARG(doff[F] == 0 || d_aos, "points pointer is NULL");
+  std::vector<int64_t> units((size_t)F + 1, 0);
+  for (int32_t f = 0; f < F; ++f) units[f + 1] = units[f] + (counts[f] + kCodecBlock - 1) / kCodecBlock;
+  const int64_t n_tiles = units[F];
+  CHECK_ARG(n_tiles < (int64_t)INT32_MAX, "too many tiles for one launch");
+  if (n_tiles == 0) {
+    std::fill(body_pos, body_pos + F + 1, (int64_t)0);
+    return MC_OK;
+  }
+  DeviceGuard g(c->device);
+  std::vector<uint8_t> blob;
+  const size_t o_doff = put(blob, doff.data(), doff.size());
+  const size_t o_unit = put(blob, units.data(), units.size());
+  const size_t o_tb = put(blob, (const int32_t*)nullptr, 0);
+  blob.resize(o_tb + (size_t)n_tiles * sizeof(int32_t));
+  const size_t o_tp = put(blob, (const int64_t*)nullptr, 0);
+  blob.resize(o_tp + (size_t)n_tiles * sizeof(int64_t));
+  char* d = nullptr;
+  if (int r = codec_scratch(c, blob.size(), &d)) return r;
+  HIPCHK(hipMemcpyAsync(d, blob.data(), o_tb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_codec_err, 0, sizeof(int), c->stream));
+  PcdArgs a;
+  a.src = CodecFrames{d_aos, ld, reinterpret_cast<const int64_t*>(d + o_doff),
+                      reinterpret_cast<const int64_t*>(d + o_unit), F};
+  a.tile_bytes = reinterpret_cast<int32_t*>(d + o_tb);
+  a.tile_pos = reinterpret_cast<const int64_t*>(d + o_tp);
+  a.out = static_cast<char*>(d_out);
+  a.err = c->d_codec_err;
+  {
+    TimedRegion tr(c, &c->codec_ev, c->stream);
+    hipLaunchKernelGGL(k_pcd_measure, dim3((uint32_t)n_tiles), dim3(kCodecBlock), 0, c->stream, a);
+  }
+  HIPCHK(hipGetLastError());
+  std::vector<int32_t> tb((size_t)n_tiles);
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(tb.data(), a.tile_bytes, tb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(&err, c->d_codec_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (err) return fail(MC_ERR_INVALID, "a value has |v| >= 2^107, beyond the device %%.6f formatter");
+  std::vector<int64_t> tpos((size_t)n_tiles);
+  int64_t run = 0;
+  for (int32_t f = 0; f < F; ++f) {
+    body_pos[f] = run;
+    for (int64_t t = units[f]; t < units[f + 1]; ++t) { tpos[t] = run; run += tb[t]; }
+  }
+  body_pos[F] = run;
+  if (out_bytes < run)
+    return fail(MC_ERR_SPACE, "PCD text needs %lld bytes, buffer has %lld", (long long)run, (long long)out_bytes);
+  CHECK_ARG(d_out, "d_out is NULL");
+  HIPCHK(hipMemcpyAsync(d + o_tp, tpos.data(), tpos.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  {
+    TimedRegion tr(c, &c->codec_ev, c->stream);
+    hipLaunchKernelGGL(k_pcd_write, dim3((uint32_t)n_tiles), dim3(kCodecBlock), 0, c->stream, a);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_timing_read_codec(mc_ctx* c, double* ms, int64_t* n) {
+  CHECK_ARG(c, "ctx is NULL");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  return sum_events(c, c->codec_ev, ms, n);
+}
+
+}  // extern "C"

@@ -51,6 +51,11 @@ struct mc_ctx {
   double scan_par[4] = {0, 0, 0, 0};  // range_min, range_max^2, fov_h/2, fov_v/2
   int64_t scan_cap = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> scan_ev;
+  // output codecs: per-call frame / unit tables carved from one scratch buffer, error flag
+  void* d_codec = nullptr;
+  size_t codec_bytes = 0;
+  int* d_codec_err = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> codec_ev;
   // staging buffer for host<->device layout conversion
   void* d_stage = nullptr;
   size_t stage_bytes = 0;

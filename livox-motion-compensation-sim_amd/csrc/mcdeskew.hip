@@ -7,6 +7,7 @@
 #include "kernels.hpp"
 #include "scan.hpp"
 #include "internal.hpp"
+#include "hostutil.hpp"
 
 #include <algorithm>
 #include <cstdarg>
@@ -30,48 +31,6 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 }  // namespace mcimpl
-using mcimpl::fail;
-
-#define HIPCHK(expr)                                                                        \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
-    if (e_ != hipSuccess)                                                                   \
-      return fail(e_ == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP, "%s failed: %s", \
-                  #expr, hipGetErrorString(e_));                                            \
-  } while (0)
-
-#define CHECK_ARG(cond, ...) \
-  do {                       \
-    if (!(cond)) return fail(MC_ERR_INVALID, __VA_ARGS__); \
-  } while (0)
-
-// ------------------------------------------------------------------------------------------------
-// small device-buffer helpers
-// ------------------------------------------------------------------------------------------------
-template <typename T>
-static int dev_alloc(T** p, size_t n) {
-  *p = nullptr;
-  if (n == 0) n = 1;
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)));
-  return MC_OK;
-}
-template <typename T>
-static void dev_free(T*& p) {
-  if (p) (void)hipFree(p);
-  p = nullptr;
-}
-
-static int ctx_stage(mc_ctx* c, size_t bytes, void** out) {
-  if (bytes > c->stage_bytes) {
-    if (c->d_stage) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->d_stage); c->d_stage = nullptr; }
-    c->stage_bytes = 0;
-    HIPCHK(hipMalloc(&c->d_stage, bytes));
-    c->stage_bytes = bytes;
-  }
-  *out = c->d_stage;
-  return MC_OK;
-}
-
 static int launch_grid(const mc_ctx* c, int32_t n_tiles) {
   int g = n_tiles;
   if (c->max_grid > 0 && g > c->max_grid) g = c->max_grid;
@@ -84,43 +43,6 @@ static LayoutArgs layout_of(const mc_batch* b) {
   a.poff = b->d_poff; a.doff = b->d_doff; a.counts = b->d_counts;
   a.cols = b->d_cols; a.cap = b->cap; a.tns = b->d_t;
   return a;
-}
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    (void)hipGetDevice(&prev);
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-};
-
-// event timing around the hot kernels
-static hipEvent_t ev_take(mc_ctx* c) {
-  if (!c->ev_pool.empty()) { hipEvent_t e = c->ev_pool.back(); c->ev_pool.pop_back(); return e; }
-  hipEvent_t e = nullptr;
-  // timing-only events: no system-scope fence (no L2 writeback/invalidate between the kernels)
-  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
-  return e;
-}
-struct TimedRegion {
-  mc_ctx* c; std::vector<std::pair<hipEvent_t, hipEvent_t>>* v; hipStream_t s; hipEvent_t e0 = nullptr;
-  TimedRegion(mc_ctx* c_, std::vector<std::pair<hipEvent_t, hipEvent_t>>* v_, hipStream_t s_) : c(c_), v(v_), s(s_) {
-    if (c->timing) { e0 = ev_take(c); if (e0) (void)hipEventRecord(e0, s); }
-  }
-  ~TimedRegion() {
-    if (c->timing && e0) {
-      hipEvent_t e1 = ev_take(c);
-      if (e1) { (void)hipEventRecord(e1, s); v->emplace_back(e0, e1); }
-      else c->ev_pool.push_back(e0);
-    }
-  }
-};
-
-// both streams idle (before reallocating tables a pipelined prep may still read or write)
-static int sync_all(mc_ctx* c) {
-  HIPCHK(hipStreamSynchronize(c->side));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return MC_OK;
 }
 
 template <typename T>
@@ -211,6 +133,9 @@ int mc_destroy(mc_ctx* c) {
   dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
   dev_free(c->d_env); dev_free(c->d_scan_ftime); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount);
   dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis);
+  if (c->d_codec) (void)hipFree(c->d_codec);
+  dev_free(c->d_codec_err);
+  for (auto& p : c->codec_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   if (c->d_stage) (void)hipFree(c->d_stage);
   for (auto& p : c->main_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->scan_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
@@ -698,19 +623,6 @@ int mc_timing_enable(mc_ctx* c, int enable) {
   return MC_OK;
 }
 
-static int sum_events(mc_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int64_t* n) {
-  double tot = 0.0;
-  for (auto& p : v) {
-    float m = 0.f;
-    HIPCHK(hipEventElapsedTime(&m, p.first, p.second));
-    tot += m;
-  }
-  if (ms) *ms = tot;
-  if (n) *n = (int64_t)v.size();
-  for (auto& p : v) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
-  v.clear();
-  return MC_OK;
-}
 
 int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms, int64_t* prep_n) {
   CHECK_ARG(c, "ctx is NULL");

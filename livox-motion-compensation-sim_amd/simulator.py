@@ -11,8 +11,10 @@ launch over a ragged batch of frames:
   deskew_frames(frames, t_ns, ...)            per-point SLERP/LERP pose   (build-added mode)
   merge_aligned(aligned)                      LMC:887-889 np.vstack
 
-Scene synthesis, scanning, file export, plots and reports (LMC:430-770, 860-1173) are outside
-the hot path and not provided.
+Around the path, also on the GPU: scan_environment / scan_frames / simulate_frames / run_simulation
+(LMC:701-858, the scan feeding the alignment without leaving HBM) and the byte-exact writers
+save_pcd / save_lvx (LMC:932-990).  Scene synthesis, CSV/LAS export, plots and reports
+(LMC:430-699, 860-931, 950-963, 992-1173) are not provided.
 """
 from __future__ import annotations
 
@@ -21,6 +23,7 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
+from . import codecs as _codecs
 from . import config as _config
 from . import trajectory as _traj
 from .runtime import Context, default_context
@@ -231,6 +234,23 @@ class LiDARMotionSimulator:
         (DESIGN.md §6): pass the environment array."""
         trajectory = self.add_sensor_noise(self.generate_trajectory())
         return self.simulate_frames(environment, trajectory, self.lidar_times())
+
+    # ---- file output (LMC:932-948, 965-990) ----------------------------------------------------
+    def save_pcd(self, points, filename):
+        """LMC:932-948: ASCII PCD v0.7, lines formatted on the GPU (byte-identical)."""
+        _codecs.save_pcd(points, filename, self.context)
+
+    def save_lvx(self, results, base_filename):
+        """LMC:965-990: the raw (local) scans of ``results`` as ``<base_filename>.lvx``."""
+        frames_data = [{"frame_id": s["frame_id"], "timestamp": s["timestamp"], "points": s["points_local"]}
+                       for s in results["raw_scans"]]
+        print("Generating corrected LVX format...")
+        try:
+            _codecs.LivoxLVXWriter(self.context).write_compatible_lvx(f"{base_filename}.lvx", frames_data)
+            print(f"✅ Corrected LVX format: {base_filename}.lvx")
+        except Exception as e:
+            print(f"❌ LVX generation failed: {e}")
+        print(f"Processed {len(frames_data)} frames with corrected LVX implementation")
 
     @staticmethod
     def merge_aligned(aligned: List[np.ndarray]) -> np.ndarray:

@@ -6,4 +6,4 @@ and bench.py's cpu_baseline leg may import this package, and only as the checker
 baseline; the product package never does.  Parity: pinned against golden vectors generated from
 the reference itself (tests/golden/make_golden.py).
 """
-from . import restatement, synth  # noqa: F401
+from . import codecs, restatement, synth  # noqa: F401

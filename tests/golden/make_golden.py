@@ -236,8 +236,71 @@ def make_synth():
                                                    t.astype(np.float64).sum()]))
 
 
+PCD_TRICKY = [0.0078125, -0.0078125, -0.0, 0.0, -1e-9, 1e-9, 5e-7, -5e-7, 1.5e-6, 2.5e-6, 1e-7, 1 / 3, -2 / 3,
+              999999.9999995, 123456.7890125, 0.0000015, 1e20, -3.4e30, 2.0 ** 53 + 2, 0.1, 0.2, 0.3, 1e-300,
+              4.0000005, 12.3456785, 7.5e-7, 2.5e-7, 99.9999995, -99.9999995, 1e15 + 0.5, 65504.0]
+
+
+def make_codecs(lmc):
+    """LVX v1.1 packer (LMC:24-272) and ASCII PCD writer (LMC:932-948) outputs, byte for byte."""
+    import tempfile
+    rng = np.random.default_rng(77)
+    w = lmc.LivoxLVXWriter()
+    out = {}
+
+    def frame(n, ncol=4, scale=40.0):
+        p = rng.normal(0, scale, (n, 3))
+        cols = [p] + ([rng.uniform(-0.2, 1.2, (n, 1))] if ncol > 3 else [])
+        return np.hstack(cols)
+
+    clip = frame(96)
+    clip[:8, 0] = [3e6, -3e6, 1.0005, -0.0009, 2147483.6475, -2147483.6485, 1e300, -1e300]
+    clip[:6, 3] = [1.5, -0.5, 0.999999, 1.0, 0.0, 254.5 / 255]
+    frames = [
+        {"frame_id": 0, "timestamp": 0.0, "points": frame(97)},
+        {"frame_id": 1, "timestamp": 0.1, "points": np.zeros((0, 4))},
+        {"frame_id": 2, "timestamp": 0.2, "points": clip},
+        {"frame_id": 7, "timestamp": 12.345678912, "points": frame(1)},
+        {"frame_id": 8, "timestamp": 119.9, "points": frame(300, ncol=3)},
+        {"frame_id": 9, "timestamp": 120.0, "points": frame(1000, scale=0.01)},
+    ]
+    with tempfile.TemporaryDirectory() as d:
+        fn = os.path.join(d, "t.lvx")
+        with contextlib.redirect_stdout(io.StringIO()):
+            ok = w.write_compatible_lvx(fn, frames)
+        assert ok
+        with open(fn, "rb") as fh:
+            out["lvx/bytes"] = np.frombuffer(fh.read(), np.uint8)
+        for i, fr in enumerate(frames):
+            out[f"lvx/{i}/points"] = fr["points"]
+            out[f"lvx/{i}/frame_id"] = np.int64(fr["frame_id"])
+            out[f"lvx/{i}/timestamp"] = np.float64(fr["timestamp"])
+        out["lvx/n_frames"] = np.int64(len(frames))
+        # a NaN coordinate: the writer's int() raises inside its try -> returns False
+        bad = [{"frame_id": 0, "timestamp": 0.0, "points": np.array([[np.nan, 0, 0, 0.5]])}]
+        with contextlib.redirect_stdout(io.StringIO()):
+            out["lvx/nan_ok"] = np.bool_(w.write_compatible_lvx(os.path.join(d, "bad.lvx"), bad))
+
+        sim = lmc.LiDARMotionSimulator()
+        t = np.array(PCD_TRICKY, np.float64)
+        n4 = (len(t) + 3) // 4 * 4
+        tricky = np.resize(t, n4).reshape(-1, 4)
+        specials = np.array([[np.inf, -np.inf, np.nan, 1.0], [-np.nan, 0.5, 2.0, -np.inf]])
+        cases = {"tricky": tricky, "specials": specials, "random": frame(2000, scale=60.0),
+                 "f32": frame(500).astype(np.float32).astype(np.float64), "empty": np.zeros((0, 4)),
+                 "wide": np.hstack([frame(10), np.full((10, 2), 9.0)])}
+        for name, pts in cases.items():
+            fn = os.path.join(d, f"{name}.pcd")
+            sim.save_pcd(pts, fn)
+            with open(fn, "rb") as fh:
+                out[f"pcd/{name}/bytes"] = np.frombuffer(fh.read(), np.uint8)
+            out[f"pcd/{name}/points"] = pts
+    np.savez_compressed(os.path.join(HERE, "codecs.npz"), **out)
+
+
 def main():
     lmc, csim = import_reference()
+    make_codecs(lmc)
     make_lmc(lmc)
     make_env(lmc)
     make_kat(lmc)

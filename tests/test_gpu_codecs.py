@@ -1,0 +1,110 @@
+"""GPU codecs byte for byte against files the reference itself wrote
+(tests/golden/codecs.npz: LVX v1.1 via LivoxLVXWriter.write_compatible_lvx LMC:57-272, ASCII PCD
+via save_pcd LMC:932-948) and against the pinned oracle (oracle/codecs.py) on larger inputs."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import codecs as C
+
+pytestmark = pytest.mark.gpu
+
+
+def golden_frames(g):
+    return [{"frame_id": int(g[f"lvx/{i}/frame_id"]), "timestamp": float(g[f"lvx/{i}/timestamp"]),
+             "points": g[f"lvx/{i}/points"]} for i in range(int(g["lvx/n_frames"]))]
+
+
+def test_lvx_file_matches_reference_bytes(mc, gpu_ctx, tmp_path):
+    g = golden("codecs.npz")
+    frames = golden_frames(g)
+    assert mc.codecs.encode_lvx(frames, gpu_ctx) == g["lvx/bytes"].tobytes()
+    w = mc.LivoxLVXWriter(gpu_ctx)
+    fn = str(tmp_path / "t.lvx")
+    assert w.write_compatible_lvx(fn, frames) is True
+    with open(fn, "rb") as f:
+        assert f.read() == g["lvx/bytes"].tobytes()
+
+
+def test_lvx_failures_like_reference(mc, gpu_ctx, tmp_path):
+    w = mc.LivoxLVXWriter(gpu_ctx)
+    bad = [{"frame_id": 0, "timestamp": 0.0, "points": np.array([[np.nan, 0, 0, 0.5]])}]
+    assert w.write_compatible_lvx(str(tmp_path / "b.lvx"), bad) is False
+    bad_i = [{"frame_id": 0, "timestamp": 0.0, "points": np.array([[1.0, 0, 0, np.nan]])}]
+    assert w.write_compatible_lvx(str(tmp_path / "c.lvx"), bad_i) is False
+    neg_ts = [{"frame_id": 0, "timestamp": -1.0, "points": np.zeros((3, 4))}]
+    assert w.write_compatible_lvx(str(tmp_path / "d.lvx"), neg_ts) is False
+    with pytest.raises(ValueError):
+        w.write_compatible_lvx("", [{"frame_id": 0, "timestamp": 0.0, "points": np.zeros((1, 4))}])
+    with pytest.raises(ValueError):
+        w.write_compatible_lvx(str(tmp_path / "e.lvx"), [])
+
+
+def test_lvx_large_ragged_vs_oracle(mc, gpu_ctx):
+    rng = np.random.default_rng(5)
+    frames = []
+    for i, n in enumerate([0, 1, 95, 96, 97, 191, 192, 5000, 20011, 0, 3]):
+        p = np.column_stack([rng.normal(0, 10 ** rng.uniform(-3, 7), (n, 3)), rng.uniform(-0.5, 1.5, n)])
+        if n > 10:
+            p[::7, 0] = np.round(p[::7, 0], 3)          # exact-mm values (truncation boundary)
+        frames.append({"frame_id": 3 * i + 1, "timestamp": 0.05 * i + 1e-3, "points": p})
+    assert mc.codecs.encode_lvx(frames, gpu_ctx) == C.lvx_bytes(frames)
+
+
+@pytest.mark.parametrize("case", ["tricky", "specials", "random", "f32", "empty", "wide"])
+def test_pcd_matches_reference_bytes(mc, gpu_ctx, tmp_path, case):
+    g = golden("codecs.npz")
+    pts = g[f"pcd/{case}/points"]
+    want = g[f"pcd/{case}/bytes"].tobytes()
+    fn = str(tmp_path / f"{case}.pcd")
+    mc.codecs.save_pcd(pts, fn, gpu_ctx)
+    with open(fn, "rb") as f:
+        assert f.read() == want
+
+
+def test_pcd_batched_frames_long_lines_and_limits(mc, gpu_ctx):
+    g = golden("codecs.npz")
+    rng = np.random.default_rng(8)
+    mags = 10.0 ** rng.uniform(-12, 31, (3000, 4))
+    huge = rng.choice([-1, 1], (3000, 4)) * mags           # lines up to ~150 B: exceeds the LDS tile
+    ties = (rng.integers(-2 ** 20, 2 ** 20, (1000, 4)) / 128.0)   # many exact half-way cases
+    clouds = [g["pcd/tricky/points"], huge, np.zeros((0, 4)), ties, g["pcd/random/points"]]
+    got = mc.codecs.encode_pcd_frames(clouds, gpu_ctx)
+    for c, b in zip(clouds, got):
+        assert b == C.pcd_ascii_bytes(c)
+    with pytest.raises(ValueError):
+        mc.codecs.encode_pcd(np.array([[1e33, 0, 0, 0]]), gpu_ctx)
+    with pytest.raises(IndexError):
+        mc.codecs.encode_pcd(np.zeros((2, 3)), gpu_ctx)
+
+
+def test_codecs_from_device_batch(mc, gpu_ctx):
+    counts = np.array([1000, 0, 2500, 96], np.int64)
+    b = gpu_ctx.batch(counts, with_time=True)
+    b.synth(seed=3, frame_id_base=50)
+    host = b.split(b.download_aos())
+    pcds = mc.codecs.encode_pcd_batch(b)
+    for h, p in zip(host, pcds):
+        assert p == C.pcd_ascii_bytes(h)
+    ids, ts = [5, 6, 7, 8], [0.1, 0.2, 0.3, 0.4]
+    lvx = mc.codecs.encode_lvx_batch(b, ids, ts)
+    ref = C.lvx_bytes([{"frame_id": i, "timestamp": t, "points": h} for i, t, h in zip(ids, ts, host)])
+    assert lvx == ref
+
+
+def test_simulator_save_lvx_and_pcd(mc, gpu_ctx, tmp_path):
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    rng = np.random.default_rng(1)
+    scans = [{"frame_id": i, "timestamp": 0.1 * i, "points_local": rng.normal(0, 20, (n, 4))}
+             for i, n in enumerate([10, 0, 200])]
+    base = str(tmp_path / "run")
+    sim.save_lvx({"raw_scans": scans}, base)
+    with open(base + ".lvx", "rb") as f:
+        data = f.read()
+    assert data == C.lvx_bytes([{"frame_id": s["frame_id"], "timestamp": s["timestamp"],
+                                 "points": s["points_local"]} for s in scans])
+    sim.save_pcd(scans[2]["points_local"], os.path.join(tmp_path, "f.pcd"))
+    with open(os.path.join(tmp_path, "f.pcd"), "rb") as f:
+        assert f.read() == C.pcd_ascii_bytes(scans[2]["points_local"])

@@ -198,3 +198,23 @@ def test_golden_files_are_data_only():
         assert f.endswith((".npz", ".json", ".py")), f
     with open(os.path.join(GOLDEN, "lmc_config.json")) as fh:
         json.load(fh)
+
+
+def test_lvx_packer_bytes_match_reference():
+    from oracle import codecs as C
+    g = golden("codecs.npz")
+    frames = [{"frame_id": int(g[f"lvx/{i}/frame_id"]), "timestamp": float(g[f"lvx/{i}/timestamp"]),
+               "points": g[f"lvx/{i}/points"]} for i in range(int(g["lvx/n_frames"]))]
+    assert C.lvx_bytes(frames) == g["lvx/bytes"].tobytes()
+    pos = C.lvx_frame_positions([len(f["points"]) for f in frames])
+    assert pos[-1] == len(g["lvx/bytes"])
+    assert not bool(g["lvx/nan_ok"])
+    with pytest.raises(ValueError):
+        C.lvx_bytes([{"frame_id": 0, "timestamp": 0.0, "points": np.array([[np.nan, 0, 0, 0.5]])}])
+
+
+@pytest.mark.parametrize("case", ["tricky", "specials", "random", "f32", "empty", "wide"])
+def test_pcd_ascii_bytes_match_reference(case):
+    from oracle import codecs as C
+    g = golden("codecs.npz")
+    assert C.pcd_ascii_bytes(g[f"pcd/{case}/points"]) == g[f"pcd/{case}/bytes"].tobytes()
