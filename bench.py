@@ -176,6 +176,76 @@ def measure_scan(ctx, cfg, tr, reps, cpu_budget):
     return rep
 
 
+def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
+    """SURVEY §8f row 3, reported beside the hot path: the byte-exact writers (LVX v1.1 LMC:24-272,
+    ASCII PCD LMC:932-948) encoding the rank's whole deskewed batch from a device (N,4) f64 cloud.
+    Kernel time only (HIP events); HBM bytes = 32 B/pt read + the encoded bytes written."""
+    from ctypes import c_int64, c_uint64
+    counts = np.ascontiguousarray(b_out.counts, np.int64)
+    F = len(counts)
+    src = ctx.device_buffer(n_rank * 32)
+    b_out.fetch_aos_device(src)
+    rep = {}
+    try:
+        pos = mc.codecs.lvx_layout(counts)
+        ids = np.arange(F, dtype=np.uint64)
+        ts = (np.arange(F) * 100_000_000).astype(np.uint64)
+        out = ctx.device_buffer(int(pos[-1]))
+        ptr = mc._lib.ptr
+
+        def lvx():
+            mc._lib.check(ctx.lib.mc_lvx_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), ptr(ids, c_uint64),
+                                                ptr(ts, c_uint64), None, out.ptr, int(pos[-1])), "lvx_encode")
+        lvx()
+        ctx.read_timing()
+        ctx.timing(True)
+        for _ in range(reps):
+            lvx()
+        ctx.timing(False)
+        ms = ctx.read_timing()["codec_ms"] / reps
+        out.close()
+        alg = 32 * n_rank + int(pos[-1])
+        rep["lvx"] = {"file_bytes": int(pos[-1]), "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
+                      "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
+                      "bytes_per_point": alg / n_rank}
+        bpos = np.zeros(F + 1, np.int64)
+        cap = n_rank * 48
+        out = ctx.device_buffer(cap)
+
+        def pcd():
+            mc._lib.check(ctx.lib.mc_pcd_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), out.ptr, cap,
+                                                ptr(bpos, c_int64)), "pcd_encode")
+        pcd()
+        ctx.read_timing()
+        ctx.timing(True)
+        for _ in range(reps):
+            pcd()
+        ctx.timing(False)
+        ms = ctx.read_timing()["codec_ms"] / reps
+        out.close()
+        text = int(bpos[-1])
+        alg = 32 * n_rank + text
+        rep["pcd_ascii"] = {"text_bytes": text, "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
+                            "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
+                            "bytes_per_point": alg / n_rank, "note": "measure + write passes"}
+        if cpu_budget > 0:
+            from oracle import codecs as C
+            host = b_out.download_aos()[:int(counts[0])]
+            t0 = time.perf_counter()
+            C.lvx_bytes([{"frame_id": 0, "timestamp": 0.0, "points": host}])
+            t1 = time.perf_counter()
+            k = min(len(host), 20_000)
+            C.pcd_ascii_bytes(host[:k])
+            t2 = time.perf_counter()
+            rep["cpu_baseline"] = {"lvx_Mpoints_s": len(host) / (t1 - t0) / 1e6,
+                                   "pcd_Mpoints_s": k / (t2 - t1) / 1e6, "cores": 1, "kind": "port",
+                                   "sample": f"LVX 1 frame x {len(host)} pts (vectorised numpy oracle), "
+                                             f"PCD {k} pts (Python float formatting, as the reference)"}
+    finally:
+        src.close()
+    return rep
+
+
 def timed_gather(ctx, rdv, b_in, b_out, mode, n_rank, world, timeout_s):
     """The merged-cloud gather to rank 0 (LMC:887-889 over RCCL), after and outside the timed
     steps, under a watchdog so that a stuck collective can never cost the throughput line.
@@ -256,10 +326,12 @@ def main():
                          "value": n_rank * world * steps / wall_max / 1e6}
 
     stager = measure_stager(ctx, b_in, b_out, n_rank, min(args.steps, 50))
-    scan = None
+    scan = codecs = None
     if not args.no_extra_modes:
         scan = measure_scan(ctx, cfg, tr, 10, 0.0 if (args.no_cpu or world > 1) else 3.0)
         ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+        ctx.deskew(b_in, b_out, mode=args.mode)
+        codecs = measure_codecs(ctx, b_out, n_rank, 5, 0.0 if (args.no_cpu or world > 1) else 1.0)
 
     gather = None
     hung = False
@@ -299,6 +371,7 @@ def main():
                       for m, v in results.items()},
             "stager": stager,
             "scan_environment": scan,
+            "codecs": codecs,
             "gather": gather,
         }
         if world == 1 and not args.no_cpu:

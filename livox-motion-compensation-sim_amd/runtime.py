@@ -134,10 +134,12 @@ class Context:
         check(self.lib.mc_timing_read(self.handle, ctypes.byref(mm), ctypes.byref(mn), ctypes.byref(pm),
                                       ctypes.byref(pn)), "timing_read")
         check(self.lib.mc_timing_read_layout(self.handle, ctypes.byref(lm), ctypes.byref(ln)), "timing_read_layout")
-        sm, sn = c_double(), c_int64()
+        sm, sn, cm, cn = c_double(), c_int64(), c_double(), c_int64()
         check(self.lib.mc_timing_read_scan(self.handle, ctypes.byref(sm), ctypes.byref(sn)), "timing_read_scan")
+        check(self.lib.mc_timing_read_codec(self.handle, ctypes.byref(cm), ctypes.byref(cn)), "timing_read_codec")
         return {"main_ms": mm.value, "main_launches": mn.value, "prep_ms": pm.value, "prep_launches": pn.value,
-                "layout_ms": lm.value, "layout_launches": ln.value, "scan_ms": sm.value, "scan_launches": sn.value}
+                "layout_ms": lm.value, "layout_launches": ln.value, "scan_ms": sm.value, "scan_launches": sn.value,
+                "codec_ms": cm.value, "codec_launches": cn.value}
 
     def device_buffer(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
