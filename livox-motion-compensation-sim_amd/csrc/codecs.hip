@@ -87,8 +87,8 @@ int mc_lvx_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
   mc_lvx_layout(F, counts, pos.data());
   if (out_bytes < pos[F])
     return fail(MC_ERR_SPACE, "LVX output needs %lld bytes, buffer has %lld", (long long)pos[F], (long long)out_bytes);
-  for (int32_t f = 0; f < F; ++f) units[f + 1] = units[f] + (counts[f] + kLvxPkgPoints - 1) / kLvxPkgPoints;
-  const int64_t n_pkg = units[F];
+  for (int32_t f = 0; f < F; ++f) units[f + 1] = units[f] + (counts[f] + kLvxUnitPoints - 1) / kLvxUnitPoints;
+  const int64_t n_pkg = units[F];   // units of up to kLvxPkgPerWG packages
   CHECK_ARG(n_pkg < (int64_t)INT32_MAX, "too many packages for one launch");
   DeviceGuard g(c->device);
 
@@ -109,12 +109,12 @@ int mc_lvx_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
 
   LvxArgs a;
   a.src = CodecFrames{d_aos, ld, reinterpret_cast<const int64_t*>(d + o_doff),
-                      reinterpret_cast<const int64_t*>(d + o_unit), F};
+                      reinterpret_cast<const int64_t*>(d + o_unit), F, n_pkg};
   a.frame_pos = reinterpret_cast<const int64_t*>(d + o_pos);
   a.frame_id = reinterpret_cast<const uint64_t*>(d + o_ids);
   a.ts_ns = reinterpret_cast<const uint64_t*>(d + o_ts);
   a.has_int = has_int ? reinterpret_cast<const uint8_t*>(d + o_hi) : nullptr;
-  a.out = static_cast<uint16_t*>(d_out);
+  a.out = static_cast<char*>(d_out);
   a.err = c->d_codec_err;
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
@@ -161,14 +161,14 @@ int mc_pcd_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
   HIPCHK(hipMemsetAsync(c->d_codec_err, 0, sizeof(int), c->stream));
   PcdArgs a;
   a.src = CodecFrames{d_aos, ld, reinterpret_cast<const int64_t*>(d + o_doff),
-                      reinterpret_cast<const int64_t*>(d + o_unit), F};
+                      reinterpret_cast<const int64_t*>(d + o_unit), F, n_tiles};
   a.tile_bytes = reinterpret_cast<int32_t*>(d + o_tb);
   a.tile_pos = reinterpret_cast<const int64_t*>(d + o_tp);
   a.out = static_cast<char*>(d_out);
   a.err = c->d_codec_err;
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    hipLaunchKernelGGL(k_pcd_measure, dim3((uint32_t)n_tiles), dim3(kCodecBlock), 0, c->stream, a);
+    hipLaunchKernelGGL(k_pcd_measure, dim3((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG)), dim3(kCodecBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());
   std::vector<int32_t> tb((size_t)n_tiles);
@@ -190,7 +190,7 @@ int mc_pcd_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
   HIPCHK(hipMemcpyAsync(d + o_tp, tpos.data(), tpos.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    hipLaunchKernelGGL(k_pcd_write, dim3((uint32_t)n_tiles), dim3(kCodecBlock), 0, c->stream, a);
+    hipLaunchKernelGGL(k_pcd_write, dim3((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG)), dim3(kCodecBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

@@ -4,8 +4,12 @@
 //   LVX v1.1 packer  LMC:24-272   96-point packages of 14-byte records (int32 mm + reflectivity)
 //   ASCII PCD body   LMC:932-948  "%.6f %.6f %.6f %.6f\n" per point, correctly rounded
 //
-// Both are byte-producing, HBM-bound passes.  Frames map to "units" (LVX packages, PCD tiles of
-// kBlock points) through a per-frame prefix, so one launch covers every frame of a batch.
+// Both produce byte streams whose records are not 4-byte aligned (14-byte LVX records, variable
+// PCD lines).  Each workgroup therefore assembles its contiguous piece of the output in LDS at the
+// same offset modulo 16 as in HBM, then stores it with 16-byte stores by consecutive lanes; only
+// the two partial 16-byte chunks at the ends of the piece are written with narrow stores.
+// Frames map to "units" (LVX package chunks, PCD tiles) through a per-frame prefix, so one launch
+// covers every frame of a batch.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,15 +22,19 @@ constexpr int kLvxRec = 14;
 constexpr int kLvxPkgHdr = 22;
 constexpr int kLvxPkg = kLvxPkgHdr + kLvxPkgPoints * kLvxRec;   // 1366 bytes
 constexpr int kLvxFrameHdr = 24;
-constexpr int kLvxPkgWords = kLvxPkg / 2;                       // every offset in the file is even
 constexpr int kLvxFileHdr = 88;
-constexpr int kPcdTileText = 16384;                             // LDS text buffer per tile of kBlock lines
+constexpr int kLvxPkgPerWG = 8;                                 // one unit = up to 8 packages of a frame
+constexpr int kLvxUnitPoints = kLvxPkgPerWG * kLvxPkgPoints;    // 768
+constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment shift
+constexpr int kPcdTilesPerWG = 4;                               // PCD tiles of kCodecBlock lines per workgroup
+constexpr int kPcdTileText = 16384;                             // LDS text buffer per tile
 
 struct CodecFrames {
   const double* aos; int64_t ld;
   const int64_t* doff;       // [F+1] dense row offset of each frame
-  const int64_t* unit_off;   // [F+1] prefix of per-frame units (LVX packages / PCD tiles)
+  const int64_t* unit_off;   // [F+1] prefix of per-frame units
   int32_t F;
+  int64_t n_units;           // unit_off[F]
 };
 
 // frame owning unit u: last f with unit_off[f] <= u (frames without units are skipped over)
@@ -39,6 +47,27 @@ __device__ __forceinline__ int32_t codec_frame_of(const int64_t* __restrict__ un
   return lo - 1;
 }
 
+// advance a workgroup-uniform frame cursor to unit u (units of a workgroup are consecutive)
+__device__ __forceinline__ int32_t codec_advance(const int64_t* __restrict__ unit_off, int32_t f, int64_t u) {
+  while (unit_off[f + 1] <= u) ++f;
+  return f;
+}
+
+// Store LDS bytes [lo, hi) to g + [lo, hi), where lds and g agree modulo 16: whole 16-byte chunks
+// with dwordx4 stores, the partial chunks at either end byte by byte.  All threads participate.
+__device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const char* lds, int lo, int hi) {
+  const int c0 = lo >> 4, c1 = (hi + 15) >> 4;
+  for (int c = c0 + threadIdx.x; c < c1; c += kCodecBlock) {
+    const int b0 = c << 4;
+    if (b0 >= lo && b0 + 16 <= hi) {
+      *reinterpret_cast<uint4*>(g + b0) = *reinterpret_cast<const uint4*>(lds + b0);
+    } else {
+      const int e = b0 + 16 < hi ? b0 + 16 : hi;
+      for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];
+    }
+  }
+}
+
 // ---- LVX v1.1 -------------------------------------------------------------------------------
 struct LvxArgs {
   CodecFrames src;
@@ -46,7 +75,7 @@ struct LvxArgs {
   const uint64_t* frame_id;     // [F]
   const uint64_t* ts_ns;        // [F] package timestamp, int(timestamp * 1e9) (LMC:176)
   const uint8_t* has_int;       // [F] frame has an intensity column (else reflectivity 128), or null
-  uint16_t* out;                // file base
+  char* out;                    // file base
   int* err;                     // set to 1 on a NaN coordinate / intensity (LMC:259, 268 int(nan))
 };
 
@@ -57,44 +86,71 @@ __device__ __forceinline__ int32_t lvx_fixed(double v, double scale, double lo, 
   return (int32_t)fmin(fmax(s, lo), hi);
 }
 
-// one workgroup per 96-point package: 683 little-endian 16-bit words (header + records + padding)
+// One unit = up to 8 consecutive packages of one frame = one contiguous byte range of the file.
+// Phase 1: a thread per point slot writes its 14-byte record (7 halfwords, zero for the padding
+// slots of the last package, LMC:245-248) and threads 0..k*11 the 22-byte package headers
+// (LMC:204-237) into LDS.  Phase 2: codec_store_piece.
 __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
+  __shared__ uint4 s_buf[kLvxLds / 16 + 1];
+  uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
   const int64_t u = blockIdx.x;
   const int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u);
-  const int64_t p = u - a.src.unit_off[f];
-  const int64_t row0 = a.src.doff[f] + p * kLvxPkgPoints;
-  const int64_t rem = a.src.doff[f + 1] - row0;
-  const int n = rem < kLvxPkgPoints ? (int)rem : kLvxPkgPoints;
-  const int64_t word0 = (a.frame_pos[f] + kLvxFrameHdr + p * kLvxPkg) >> 1;
+  const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
+  const int64_t frow = a.src.doff[f];
+  const int64_t fcount = a.src.doff[f + 1] - frow;
+  const int64_t fpkgs = (fcount + kLvxPkgPoints - 1) / kLvxPkgPoints;
+  const int k = (int)((fpkgs - pkg0) < kLvxPkgPerWG ? (fpkgs - pkg0) : kLvxPkgPerWG);
+  const int64_t rem = fcount - pkg0 * kLvxPkgPoints;
+  const int n = (int)(rem < k * kLvxPkgPoints ? rem : k * kLvxPkgPoints);
+  const int64_t S = a.frame_pos[f] + kLvxFrameHdr + pkg0 * kLvxPkg;   // even
+  const int shift = (int)(S & 15);
   const uint64_t ts = a.ts_ns[f];
   const bool hi = a.has_int ? a.has_int[f] != 0 : a.src.ld > 3;
-  const double* __restrict__ aos = a.src.aos;
   const int64_t ld = a.src.ld;
-  for (int w = threadIdx.x; w < kLvxPkgWords; w += kCodecBlock) {
-    uint32_t v;
-    if (w < kLvxPkgHdr / 2) {
-      // LMC:204-237: dev 0, version 5, slot 0, lidar 1, reserved, status 0 (4 B), ts type 1,
-      // data type 2, reserved (3 B), timestamp (8 B)
-      constexpr uint32_t kHdr[7] = {0x0500u, 0x0100u, 0x0000u, 0x0000u, 0x0100u, 0x0002u, 0x0000u};
-      v = w < 7 ? kHdr[w] : (uint32_t)(ts >> (16 * (w - 7))) & 0xffffu;
-    } else {
-      const int k = 2 * w - kLvxPkgHdr;
-      const int r = k / kLvxRec;
-      const int o = k - r * kLvxRec;
-      if (r >= n) {
-        v = 0;                                                  // LMC:245-248 zero padding
+  const double* __restrict__ base = a.src.aos + (frow + pkg0 * kLvxPkgPoints) * ld;
+
+  for (int i = threadIdx.x; i < k * kLvxPkgPoints; i += kCodecBlock) {
+    const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
+    uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
+    uint32_t x = 0, y = 0, z = 0, refl = 0;
+    if (i < n) {
+      const double* q = base + (int64_t)i * ld;
+      double v0, v1, v2, v3 = 0.0;
+      if (ld == 4) {
+        const double2 p01 = *reinterpret_cast<const double2*>(q);
+        const double2 p23 = *reinterpret_cast<const double2*>(q + 2);
+        v0 = p01.x; v1 = p01.y; v2 = p23.x; v3 = p23.y;
       } else {
-        const double* q = aos + (row0 + r) * ld;
-        if (o < 12) {
-          const uint32_t mm = (uint32_t)lvx_fixed(q[o >> 2], 1000.0, -2147483648.0, 2147483647.0, a.err);
-          v = (o & 2) ? mm >> 16 : mm & 0xffffu;
-        } else {
-          v = hi ? (uint32_t)lvx_fixed(q[3], 255.0, 0.0, 255.0, a.err) : 128u;   // tag byte 0
-        }
+        v0 = q[0]; v1 = q[1]; v2 = q[2];
+        if (ld > 3) v3 = q[3];
       }
+      x = (uint32_t)lvx_fixed(v0, 1000.0, -2147483648.0, 2147483647.0, a.err);
+      y = (uint32_t)lvx_fixed(v1, 1000.0, -2147483648.0, 2147483647.0, a.err);
+      z = (uint32_t)lvx_fixed(v2, 1000.0, -2147483648.0, 2147483647.0, a.err);
+      refl = hi ? (uint32_t)lvx_fixed(v3, 255.0, 0.0, 255.0, a.err) : 128u;   // tag byte 0
     }
-    a.out[word0 + w] = (uint16_t)v;
+    r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
+    r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
+    r[4] = (uint16_t)z; r[5] = (uint16_t)(z >> 16);
+    r[6] = (uint16_t)refl;
   }
+  // dev 0, version 5 | slot 0, lidar 1 | reserved, status (4 B) | ts type 1 | data type 2 |
+  // reserved (3 B) | timestamp (8 B)
+  for (int h = threadIdx.x; h < k * (kLvxPkgHdr / 2); h += kCodecBlock) {
+    const int pk = h / (kLvxPkgHdr / 2), w = h - pk * (kLvxPkgHdr / 2);
+    uint32_t v;
+    switch (w) {
+      case 0: v = 0x0500u; break;
+      case 1: v = 0x0100u; break;
+      case 4: v = 0x0100u; break;
+      case 5: v = 0x0002u; break;
+      case 7: case 8: case 9: case 10: v = (uint32_t)(ts >> (16 * (w - 7))) & 0xffffu; break;
+      default: v = 0u;
+    }
+    s16[((shift + pk * kLvxPkg) >> 1) + w] = (uint16_t)v;
+  }
+  __syncthreads();
+  codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
 }
 
 // LMC:178-193: frame header = own offset, next frame's offset (0 for the last), frame_id
@@ -104,20 +160,29 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_frames(const LvxArgs a, int
   const uint64_t q[3] = {(uint64_t)a.frame_pos[f],
                          f + 1 < a.src.F ? (uint64_t)a.frame_pos[f + 1] : (uint64_t)next_of_last_frame,
                          a.frame_id[f]};
-  uint16_t* o = a.out + (a.frame_pos[f] >> 1);
+  uint16_t* o = reinterpret_cast<uint16_t*>(a.out + a.frame_pos[f]);
 #pragma unroll
   for (int i = 0; i < 12; ++i) o[i] = (uint16_t)(q[i >> 2] >> (16 * (i & 3)));
 }
 
 // ---- "%.6f" (Python's correctly rounded fixed-point float formatting) -------------------------
 // v = m * 2^e exactly; N = round-half-even(|v| * 10^6) in 128-bit integer arithmetic, printed as
-// N / 10^6 "." N % 10^6.  Finite |v| < 2^107 (~1.6e32) is supported; larger values set the error
-// flag (the host reports it).
+// ip = N / 10^6, "." and the six digits of N % 10^6.  |v| < 2^107 (~1.6e32) is supported; larger
+// values set the error flag.  |v| < 4294.97 (N < 2^32, every LiDAR coordinate) stays in 32-bit
+// integer arithmetic.
 struct Fmt6 {
-  unsigned __int128 N;
+  unsigned __int128 ip;
+  uint32_t fp;
+  int nd;      // digits of ip
+  int len;     // characters
   int kind;    // 0 finite, 1 inf, 2 nan, 3 out of range
   bool neg;
 };
+
+__device__ __forceinline__ int u32_digits(uint32_t x) {
+  return 1 + (x >= 10u) + (x >= 100u) + (x >= 1000u) + (x >= 10000u) + (x >= 100000u) + (x >= 1000000u) +
+         (x >= 10000000u) + (x >= 100000000u) + (x >= 1000000000u);
+}
 
 __device__ __forceinline__ Fmt6 fmt6_prepare(double v) {
   Fmt6 r;
@@ -125,15 +190,19 @@ __device__ __forceinline__ Fmt6 fmt6_prepare(double v) {
   r.neg = (bits >> 63) != 0;
   const int ex = (int)((bits >> 52) & 0x7ff);
   const uint64_t frac = bits & ((1ull << 52) - 1);
-  r.N = 0;
-  if (ex == 0x7ff) { r.kind = frac ? 2 : 1; return r; }
-  r.kind = 0;
+  r.ip = 0; r.fp = 0; r.nd = 1;
+  if (ex == 0x7ff) {                                // "nan" (Python drops a NaN's sign) / "inf" / "-inf"
+    r.kind = frac ? 2 : 1;
+    r.len = 3 + (r.kind == 1 && r.neg ? 1 : 0);
+    return r;
+  }
   const uint64_t m = ex ? (frac | (1ull << 52)) : frac;
   const int e = ex ? ex - 1075 : -1074;
   const unsigned __int128 P = (unsigned __int128)m * 1000000u;   // < 2^73
+  unsigned __int128 N = 0;
   if (e >= 0) {
-    if (e > 54) { r.kind = 3; return r; }
-    r.N = P << e;
+    if (e > 54) { r.kind = 3; r.len = 0; return r; }
+    N = P << e;
   } else if (-e < 74) {
     const int s = -e;
     const unsigned __int128 one = 1;
@@ -141,55 +210,53 @@ __device__ __forceinline__ Fmt6 fmt6_prepare(double v) {
     const unsigned __int128 rem = P & ((one << s) - 1);
     const unsigned __int128 half = one << (s - 1);
     if (rem > half || (rem == half && (q & 1))) ++q;
-    r.N = q;
+    N = q;
   }
+  r.kind = 0;
+  if ((uint64_t)(N >> 32) == 0) {
+    const uint32_t n = (uint32_t)N;
+    const uint32_t ip = n / 1000000u;
+    r.ip = ip;
+    r.fp = n - ip * 1000000u;
+    r.nd = u32_digits(ip);
+  } else {
+    const unsigned __int128 ip = (uint64_t)(N >> 64) == 0 ? (unsigned __int128)((uint64_t)N / 1000000u)
+                                                          : N / 1000000u;
+    r.ip = ip;
+    r.fp = (uint32_t)(N - ip * 1000000u);
+    int d = 1;
+    for (unsigned __int128 x = ip; x >= 10; x /= 10) ++d;
+    r.nd = d;
+  }
+  r.len = (r.neg ? 1 : 0) + r.nd + 7;
   return r;
 }
 
-__device__ __forceinline__ int u128_digits(unsigned __int128 x) {
-  int d = 1;
-  if ((uint64_t)(x >> 64) == 0) {
-    uint64_t y = (uint64_t)x;
-    while (y >= 10) { y /= 10; ++d; }
-    return d;
-  }
-  while (x >= 10) { x /= 10; ++d; }
-  return d;
-}
-
-__device__ __forceinline__ int fmt6_len(const Fmt6& f) {
-  if (f.kind == 2) return 3;                      // "nan" (Python drops a NaN's sign)
-  if (f.kind == 1) return 3 + (f.neg ? 1 : 0);    // "inf" / "-inf"
-  if (f.kind == 3) return 0;
-  const unsigned __int128 ip = (uint64_t)(f.N >> 64) == 0 ? (unsigned __int128)((uint64_t)f.N / 1000000u)
-                                                          : f.N / 1000000u;
-  return (f.neg ? 1 : 0) + u128_digits(ip) + 7;
-}
-
-// writes fmt6_len(f) characters at p (generic pointer: LDS or global)
+// writes f.len characters at p (generic pointer: LDS or global)
 __device__ __forceinline__ void fmt6_write(const Fmt6& f, char* p) {
   if (f.kind == 3) return;
   if (f.kind == 2) { p[0] = 'n'; p[1] = 'a'; p[2] = 'n'; return; }
   if (f.neg) *p++ = '-';
   if (f.kind == 1) { p[0] = 'i'; p[1] = 'n'; p[2] = 'f'; return; }
-  unsigned __int128 ip;
-  uint32_t fp;
-  if ((uint64_t)(f.N >> 64) == 0) {
-    const uint64_t n = (uint64_t)f.N;
-    ip = n / 1000000u;
-    fp = (uint32_t)(n - (uint64_t)ip * 1000000u);
-  } else {
-    ip = f.N / 1000000u;
-    fp = (uint32_t)(f.N - ip * 1000000u);
+  const int nd = f.nd;
+  uint32_t fp = f.fp;
+#pragma unroll
+  for (int i = 6; i >= 1; --i) {
+    const uint32_t q = fp / 10u;
+    p[nd + i] = (char)('0' + (fp - q * 10u));
+    fp = q;
   }
-  const int nd = u128_digits(ip);
-  for (int i = 6; i >= 1; --i) { p[nd + i] = (char)('0' + fp % 10); fp /= 10; }
   p[nd] = '.';
-  if ((uint64_t)(ip >> 64) == 0) {
-    uint64_t y = (uint64_t)ip;
-    for (int i = nd - 1; i >= 0; --i) { p[i] = (char)('0' + y % 10); y /= 10; }
+  if ((uint64_t)(f.ip >> 32) == 0) {
+    uint32_t y = (uint32_t)f.ip;
+    for (int i = nd - 1; i >= 0; --i) {
+      const uint32_t q = y / 10u;
+      p[i] = (char)('0' + (y - q * 10u));
+      y = q;
+    }
   } else {
-    for (int i = nd - 1; i >= 0; --i) { p[i] = (char)('0' + (uint32_t)(ip % 10)); ip /= 10; }
+    unsigned __int128 y = f.ip;
+    for (int i = nd - 1; i >= 0; --i) { p[i] = (char)('0' + (uint32_t)(y % 10)); y /= 10; }
   }
 }
 
@@ -206,27 +273,35 @@ struct PcdLine {
   int len;
 };
 
-__device__ __forceinline__ void pcd_line(const double* __restrict__ q, PcdLine& L, int* err) {
+__device__ __forceinline__ void pcd_line(const double* __restrict__ q, int64_t ld, PcdLine& L, int* err) {
+  double c[4];
+  if (ld == 4) {
+    const double2 p01 = *reinterpret_cast<const double2*>(q);
+    const double2 p23 = *reinterpret_cast<const double2*>(q + 2);
+    c[0] = p01.x; c[1] = p01.y; c[2] = p23.x; c[3] = p23.y;
+  } else {
+    c[0] = q[0]; c[1] = q[1]; c[2] = q[2]; c[3] = q[3];
+  }
   L.len = 4;                                       // 3 separators + newline
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    L.v[c] = fmt6_prepare(q[c]);
-    if (L.v[c].kind == 3) *err = 1;
-    L.len += fmt6_len(L.v[c]);
+  for (int k = 0; k < 4; ++k) {
+    L.v[k] = fmt6_prepare(c[k]);
+    if (L.v[k].kind == 3) *err = 1;
+    L.len += L.v[k].len;
   }
 }
 
 __device__ __forceinline__ void pcd_emit(const PcdLine& L, char* p) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    fmt6_write(L.v[c], p);
-    p += fmt6_len(L.v[c]);
-    *p++ = c < 3 ? ' ' : '\n';
+  for (int k = 0; k < 4; ++k) {
+    fmt6_write(L.v[k], p);
+    p += L.v[k].len;
+    *p++ = k < 3 ? ' ' : '\n';
   }
 }
 
 __device__ __forceinline__ int64_t pcd_row(const CodecFrames& s, int64_t u, int32_t& f, bool& valid) {
-  f = codec_frame_of(s.unit_off, s.F, u);
+  f = codec_advance(s.unit_off, f, u);
   const int64_t row = s.doff[f] + (u - s.unit_off[f]) * kCodecBlock + threadIdx.x;
   valid = row < s.doff[f + 1];
   return row;
@@ -255,40 +330,56 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
 
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
-  int32_t f; bool valid;
-  const int64_t row = pcd_row(a.src, blockIdx.x, f, valid);
-  int len = 0;
-  if (valid) {
-    PcdLine L;
-    pcd_line(a.src.aos + row * a.src.ld, L, a.err);
-    len = L.len;
+  const int64_t u0 = (int64_t)blockIdx.x * kPcdTilesPerWG;
+  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  for (int j = 0; j < kPcdTilesPerWG; ++j) {
+    const int64_t u = u0 + j;
+    if (u >= a.src.n_units) break;
+    bool valid;
+    const int64_t row = pcd_row(a.src, u, f, valid);
+    int len = 0;
+    if (valid) {
+      PcdLine L;
+      pcd_line(a.src.aos + row * a.src.ld, a.src.ld, L, a.err);
+      len = L.len;
+    }
+    int total;
+    block_scan(len, s_wave, total);
+    if (threadIdx.x == 0) a.tile_bytes[u] = total;
+    __syncthreads();   // s_wave is reused by the next tile
   }
-  int total;
-  block_scan(len, s_wave, total);
-  if (threadIdx.x == 0) a.tile_bytes[blockIdx.x] = total;
 }
 
-// every tile formats its lines into LDS at their block-scan offsets, then the whole tile text is
-// stored with consecutive lanes on consecutive bytes (a tile larger than the LDS buffer — only
-// possible with extreme magnitudes — is written line by line straight to HBM instead)
+// every tile formats its lines into LDS (at the tile's HBM offset modulo 16) and stores the text
+// with codec_store_piece; a tile larger than the LDS buffer — only possible with extreme
+// magnitudes — is written line by line straight to HBM instead
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
-  __shared__ char s_text[kPcdTileText];
-  int32_t f; bool valid;
-  const int64_t row = pcd_row(a.src, blockIdx.x, f, valid);
-  PcdLine L;
-  L.len = 0;
-  if (valid) pcd_line(a.src.aos + row * a.src.ld, L, a.err);
-  int total;
-  const int incl = block_scan(L.len, s_wave, total);
-  const int excl = incl - L.len;
-  char* const g = a.out + a.tile_pos[blockIdx.x];
-  if (total <= kPcdTileText) {
-    if (valid) pcd_emit(L, s_text + excl);
-    __syncthreads();
-    for (int i = threadIdx.x; i < total; i += kCodecBlock) g[i] = s_text[i];
-  } else if (valid) {
-    pcd_emit(L, g + excl);
+  __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
+  char* const s_text = reinterpret_cast<char*>(s_text4);
+  const int64_t u0 = (int64_t)blockIdx.x * kPcdTilesPerWG;
+  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  for (int j = 0; j < kPcdTilesPerWG; ++j) {
+    const int64_t u = u0 + j;
+    if (u >= a.src.n_units) break;
+    bool valid;
+    const int64_t row = pcd_row(a.src, u, f, valid);
+    PcdLine L;
+    L.len = 0;
+    if (valid) pcd_line(a.src.aos + row * a.src.ld, a.src.ld, L, a.err);
+    int total;
+    const int incl = block_scan(L.len, s_wave, total);
+    const int excl = incl - L.len;
+    const int64_t G = a.tile_pos[u];
+    const int shift = (int)(G & 15);
+    if (total + shift <= kPcdTileText) {
+      if (valid) pcd_emit(L, s_text + shift + excl);
+      __syncthreads();
+      codec_store_piece(a.out + (G - shift), s_text, shift, shift + total);
+    } else if (valid) {
+      pcd_emit(L, a.out + G + excl);
+    }
+    __syncthreads();   // s_wave / s_text are reused by the next tile
   }
 }
 
