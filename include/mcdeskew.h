@@ -182,6 +182,14 @@ int mc_batch_checksum(mc_batch* b, double* sums5);
 /* out must have the same frame counts as in (it may be the same batch: in-place). */
 int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select);
 
+/* CoordinateTransformer.transform_points (CSIM:153-233) / _transform_coordinates (CSIM:2107-2163):
+ * p' = A p + b with one 3x4 [A | b] matrix (row-major float64, 12 values) for all frames
+ * (n_mats == 1) or one per frame (n_mats == n_frames).  w_column != 0: the intensity column is the
+ * homogeneous w of (N,4) input (p' = A p + b w, CSIM:226-229).  The 4th column passes through.
+ * Synchronous; timed with the deskew kernels (mc_timing_read main). */
+int mc_transform_affine(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int32_t n_mats, const double* mats,
+                        int w_column);
+
 /* HIP-event timing of the hot kernels (main deskew kernel and the pose-prep kernel) */
 int mc_timing_enable(mc_ctx* ctx, int enable);
 int mc_timing_read(mc_ctx* ctx, double* main_ms_total, int64_t* main_launches,

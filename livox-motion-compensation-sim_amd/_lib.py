@@ -86,6 +86,7 @@ _SIGS = {
     "mc_batch_synth": (c_int, [c_void_p, c_uint64, c_int64]),
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),
     "mc_deskew": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
+    "mc_transform_affine": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, _pd, c_int]),
     "mc_timing_enable": (c_int, [c_void_p, c_int]),
     "mc_timing_read": (c_int, [c_void_p, _pd, _pi64, _pd, _pi64]),
     "mc_set_launch": (c_int, [c_void_p, c_int32]),

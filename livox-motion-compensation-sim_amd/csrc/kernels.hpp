@@ -410,7 +410,10 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Path A: frame mode (LMC:772-776).  One pose per tile -> uniform (SGPR) operands.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
+// kW: homogeneous input whose 4th column is w (CSIM:226-229 applies T to (N,4) points as they are),
+// p' = A p + b w; otherwise p' = A p + b with the 4th column passed through.
+template <bool kW>
+__device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
     const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
@@ -433,14 +436,16 @@ __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
     for (int it = 0; it < kIters; ++it) {
       const int g = it * kBlock + threadIdx.x;
       if (g < tl.ngroups) {
-        float4 X = vx[it], Y = vy[it], Z = vz[it];
+        float4 X = vx[it], Y = vy[it], Z = vz[it], W = vi[it];
         float4 ox4, oy4, oz4;
-#define MC_XF(c)                                                         \
-  ox4.c = fmaf(r0.x, X.c, fmaf(r0.y, Y.c, fmaf(r0.z, Z.c, r0.w)));       \
-  oy4.c = fmaf(r1.x, X.c, fmaf(r1.y, Y.c, fmaf(r1.z, Z.c, r1.w)));       \
-  oz4.c = fmaf(r2.x, X.c, fmaf(r2.y, Y.c, fmaf(r2.z, Z.c, r2.w)));
+#define MC_T(r, c) (kW ? r.w * W.c : r.w)
+#define MC_XF(c)                                                              \
+  ox4.c = fmaf(r0.x, X.c, fmaf(r0.y, Y.c, fmaf(r0.z, Z.c, MC_T(r0, c))));     \
+  oy4.c = fmaf(r1.x, X.c, fmaf(r1.y, Y.c, fmaf(r1.z, Z.c, MC_T(r1, c))));     \
+  oz4.c = fmaf(r2.x, X.c, fmaf(r2.y, Y.c, fmaf(r2.z, Z.c, MC_T(r2, c))));
         MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
 #undef MC_XF
+#undef MC_T
         st_frame(ox + 4 * g, ox4);
         st_frame(ox + a.out_cap + 4 * g, oy4);
         st_frame(ox + 2 * a.out_cap + 4 * g, oz4);
@@ -449,6 +454,11 @@ __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
     }
   }
 }
+
+__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) { deskew_frame_body<false>(a); }
+
+// CoordinateTransformer.transform_points on homogeneous (N,4) input (CSIM:214-233)
+__global__ __launch_bounds__(kBlock) void k_affine_w(const DeskewArgs a) { deskew_frame_body<true>(a); }
 
 // ---------------------------------------------------------------------------------------------
 // bounded-argument sin/cos.  ocml's sincosf carries a Payne-Hanek branch for huge arguments that

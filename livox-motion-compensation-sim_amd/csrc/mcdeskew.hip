@@ -617,6 +617,47 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   return MC_OK;
 }
 
+int mc_transform_affine(mc_ctx* c, const mc_batch* in, mc_batch* out, int32_t n_mats, const double* mats,
+                        int w_column) {
+  CHECK_ARG(c && in && out && mats, "NULL argument");
+  CHECK_ARG(in->ctx == c && out->ctx == c, "batches belong to another context");
+  CHECK_ARG(in->counts == out->counts, "input and output batches have different frame counts");
+  CHECK_ARG(n_mats == 1 || n_mats == in->F, "need 1 or n_frames matrices (got %d for %d frames)", n_mats, in->F);
+  if (in->F == 0) return MC_OK;
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  // the frame table half not used by the last mc_deskew; main-stream order protects the previous
+  // reader of this half, the event hands it back to the next pipelined prep
+  const int h = c->buf;
+  c->buf ^= 1;
+  std::vector<float4> tbl(3 * (size_t)in->F);
+  for (int32_t f = 0; f < in->F; ++f) {
+    const double* m = mats + 12 * (size_t)(n_mats == 1 ? 0 : f);
+    for (int r = 0; r < 3; ++r)
+      tbl[3 * (size_t)f + r] = make_float4((float)m[4 * r], (float)m[4 * r + 1], (float)m[4 * r + 2], (float)m[4 * r + 3]);
+  }
+  float4* frame_tbl = in->d_frame_tbl + 3 * (size_t)in->F * h;
+  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
+  HIPCHK(hipMemcpyAsync(frame_tbl, tbl.data(), tbl.size() * sizeof(float4), hipMemcpyHostToDevice, s));
+  if (in->n_tiles > 0) {
+    DeskewArgs da;
+    std::memset(&da, 0, sizeof(da));
+    da.in = in->d_cols; da.in_cap = in->cap;
+    da.out = out->d_cols; da.out_cap = out->cap;
+    da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
+    da.frame_tbl = frame_tbl;
+    const dim3 grid(launch_grid(c, in->n_tiles)), block(kBlock);
+    TimedRegion tr(c, &c->main_ev, s);
+    if (w_column) hipLaunchKernelGGL(k_affine_w, grid, block, 0, s, da);
+    else hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, da);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_main_done[h], s));
+  // the host table must outlive the (possibly pageable-staged) copy
+  HIPCHK(hipStreamSynchronize(s));
+  return MC_OK;
+}
+
 int mc_timing_enable(mc_ctx* c, int enable) {
   CHECK_ARG(c, "ctx is NULL");
   c->timing = enable != 0;

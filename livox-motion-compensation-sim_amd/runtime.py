@@ -84,6 +84,21 @@ class Context:
                                  _lib.POSE_SELECT[pose_select]), f"deskew[{mode}]")
         return out
 
+    def transform_affine(self, inp: "Batch", out: "Batch | None" = None, mats=None, w_column: bool = False) -> "Batch":
+        """p' = A p + b (CSIM:214-233) with one 3x4 [A | b] for all frames or one per frame;
+        ``w_column``: the 4th column is the homogeneous w (p' = A p + b w).  Synchronous."""
+        m = np.ascontiguousarray(mats, dtype=np.float64)
+        if m.ndim == 2:
+            m = m[None]
+        if m.shape[1:] not in ((3, 4), (4, 4)):
+            raise ValueError(f"expected (3,4) / (4,4) matrices, got {np.shape(mats)}")
+        m = np.ascontiguousarray(m[:, :3, :4])
+        if out is None:
+            out = Batch(self, inp.counts, with_time=False)
+        check(self.lib.mc_transform_affine(self.handle, inp.handle, out.handle, len(m), ptr(m, c_double),
+                                           int(bool(w_column))), "transform_affine")
+        return out
+
     # ---- scan_environment (LMC:701-770) ----------------------------------------------------
     def set_environment(self, environment):
         """Static scene (E, >=4) float64 [x, y, z, intensity] (LMC:430-699's output), to HBM."""

@@ -273,3 +273,22 @@ def deskew_pose_slerp(xyz, t_ns, t_frame: float, trajectory) -> np.ndarray:
     tq = float(t_frame) + np.asarray(t_ns, dtype=np.int64) * 1e-9
     R, p = slerp_pose(trajectory["time"], trajectory["position_gps"], trajectory["orientation_imu"], tq)
     return np.einsum("nij,nj->ni", R, xyz) + p
+
+
+# ----------------------------------------------------------------------------------------------
+# CoordinateTransformer (CSIM:153-233)
+# ----------------------------------------------------------------------------------------------
+def create_transform_matrix(translation, rotation) -> np.ndarray:
+    """CSIM:187-212: 4x4 [Rz(yaw) Ry(pitch) Rx(roll) | t]."""
+    T = np.eye(4)
+    T[:3, :3] = euler_xyz_matrix(np.asarray(rotation, dtype=np.float64))
+    T[:3, 3] = translation
+    return T
+
+
+def transform_points_h(points, T) -> np.ndarray:
+    """CSIM:214-233: (N,3) gets w = 1; any other width is used as homogeneous as it is."""
+    p = np.asarray(points, dtype=np.float64)
+    if p.shape[1] == 3:
+        p = np.column_stack([p, np.ones(len(p))])
+    return (np.asarray(T) @ p.T).T[:, :3]

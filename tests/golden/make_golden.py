@@ -298,8 +298,53 @@ def make_codecs(lmc):
     np.savez_compressed(os.path.join(HERE, "codecs.npz"), **out)
 
 
+def make_coords(csim):
+    """CoordinateTransformer (CSIM:153-233) and _transform_coordinates (CSIM:2107-2163)."""
+    rng = np.random.default_rng(21)
+    ct = csim.CoordinateTransformer()
+    ct.set_transformation("sensor", "local", [10.0, -5.0, 2.0], [0.1, -0.2, 2.5])
+    p3 = rng.normal(0, 30, (200, 3))
+    p4 = np.column_stack([rng.normal(0, 30, (50, 3)), rng.uniform(0, 1, 50)])
+    out = {"p3": p3, "p4": p4}
+    with contextlib.redirect_stderr(io.StringIO()):
+        for a, b in [("sensor", "vehicle"), ("sensor", "local"), ("local", "sensor"), ("sensor", "sensor"),
+                     ("vehicle", "sensor")]:
+            out[f"tp/{a}/{b}"] = ct.transform_points(p3, a, b)
+        out["tp4/sensor/local"] = ct.transform_points(p4, "sensor", "local")
+        out["T/sensor/local"] = ct.transformations[("sensor", "local")]
+        out["T/local/sensor"] = ct.transformations[("local", "sensor")]
+
+        class Stub:
+            coordinate_transformer = ct
+
+            def _find_closest_gps_sample(self, gps, ts):
+                return csim.LiDARMotionSimulator._find_closest_gps_sample(self, gps, ts)
+
+        counts = [40, 0, 7]
+        frames = []
+        for i, n in enumerate(counts):
+            xyz = rng.normal(0, 20, (n, 3))
+            pts = [csim.LiDARPoint(x=float(x), y=float(y), z=float(z), intensity=int(k % 256),
+                                   timestamp=int(1_000_000 * k), ring=0, tag=0) for k, (x, y, z) in enumerate(xyz)]
+            frames.append({"frame_id": i, "timestamp": int(i * 100_000_000), "points": pts})
+            out[f"tc/in/{i}"] = xyz.reshape(n, 3)
+        gps = [csim.GPSData(timestamp=0, latitude=40.0, longitude=-74.0, altitude=10.0, velocity_x=0.0,
+                            velocity_y=0.0, velocity_z=0.0, heading=0.0)]
+        for target in ("vehicle", "local", "utm"):
+            res = csim.LiDARMotionSimulator._transform_coordinates(Stub(), frames, target, gps)
+            for i, fr in enumerate(res):
+                out[f"tc/{target}/{i}"] = np.array([[p.x, p.y, p.z] for p in fr["points"]]).reshape(-1, 3)
+                out[f"tc/{target}/{i}/meta"] = np.array([[p.intensity, p.timestamp] for p in fr["points"]],
+                                                        np.int64).reshape(-1, 2)
+                assert fr["coordinate_system"] == target
+        out["tc/n_frames"] = np.int64(len(counts))
+        out["utm_available"] = np.bool_(csim.UTM_AVAILABLE)
+    np.savez_compressed(os.path.join(HERE, "coords.npz"), **out)
+
+
 def main():
     lmc, csim = import_reference()
+    make_coords(csim)
     make_codecs(lmc)
     make_lmc(lmc)
     make_env(lmc)

@@ -218,3 +218,19 @@ def test_pcd_ascii_bytes_match_reference(case):
     from oracle import codecs as C
     g = golden("codecs.npz")
     assert C.pcd_ascii_bytes(g[f"pcd/{case}/points"]) == g[f"pcd/{case}/bytes"].tobytes()
+
+
+def test_coordinate_transformer_matches_reference():
+    g = golden("coords.npz")
+    T = R.create_transform_matrix([10.0, -5.0, 2.0], [0.1, -0.2, 2.5])
+    np.testing.assert_allclose(T, g["T/sensor/local"], atol=1e-14)
+    np.testing.assert_allclose(np.linalg.inv(T), g["T/local/sensor"], atol=1e-12)
+    np.testing.assert_allclose(R.transform_points_h(g["p3"], T), g["tp/sensor/local"], atol=1e-12)
+    np.testing.assert_allclose(R.transform_points_h(g["p3"], np.linalg.inv(T)), g["tp/local/sensor"], atol=1e-12)
+    np.testing.assert_allclose(R.transform_points_h(g["p4"], T), g["tp4/sensor/local"], atol=1e-12)
+    Tsv = np.eye(4)
+    Tsv[2, 3] = 1.5
+    np.testing.assert_allclose(R.transform_points_h(g["p3"], Tsv), g["tp/sensor/vehicle"], atol=1e-12)
+    assert np.array_equal(g["tp/vehicle/sensor"], g["p3"])          # missing pair: input unchanged
+    for i in range(int(g["tc/n_frames"])):
+        assert np.array_equal(g[f"tc/utm/{i}"], g[f"tc/in/{i}"])    # utm package absent: unchanged
