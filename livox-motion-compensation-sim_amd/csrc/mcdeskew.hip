@@ -696,7 +696,7 @@ int mc_set_environment(mc_ctx* c, int64_t n, const double* env, int64_t ld) {
 int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_select, const double* params,
                   int64_t cap, int64_t* counts_out) {
   CHECK_ARG(c && params && counts_out, "NULL argument");
-  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(F >= 0 && F <= 65535 * kScanFrames, "n_frames must be in [0, %d]", 65535 * kScanFrames);
   CHECK_ARG(cap >= 1, "points_per_frame must be >= 1");
   CHECK_ARG(pose_select == MC_POSE_SEARCHSORTED || pose_select == MC_POSE_DIRECT, "unknown pose_select");
   if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
@@ -730,11 +730,11 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   HIPCHK(hipGetLastError());
   std::vector<int64_t> nvis(F, 0), toff((size_t)F * std::max(tiles, 1), 0);
   if (tiles > 0) {
-    ScanParams sp{c->scan_par[0], c->scan_par[1], c->scan_par[2], c->scan_par[3], cap};
+    const ScanParams sp = make_scan_params(c->scan_par, cap);
     {
       TimedRegion tr(c, &c->scan_ev, c->stream);
-      hipLaunchKernelGGL(k_scan_count, dim3(tiles, F), dim3(kBlock), 0, c->stream, c->d_env, c->env_ld, c->E,
-                         c->d_scan_pose, sp, c->d_scan_tcount);
+      hipLaunchKernelGGL(k_scan_count, dim3(tiles, (F + kScanFrames - 1) / kScanFrames), dim3(kBlock), 0, c->stream,
+                         c->d_env, c->env_ld, c->E, c->d_scan_pose, F, sp, c->d_scan_tcount);
     }
     HIPCHK(hipGetLastError());
     std::vector<int32_t> tc((size_t)F * tiles);
@@ -780,13 +780,14 @@ int mc_scan_emit(mc_ctx* c, mc_batch* out, const double* noise) {
   }
   ScanEmitArgs ea;
   ea.env = c->d_env; ea.ld = c->env_ld; ea.E = c->E;
-  ea.pose = c->d_scan_pose;
-  ea.sp = ScanParams{c->scan_par[0], c->scan_par[1], c->scan_par[2], c->scan_par[3], c->scan_cap};
+  ea.pose = c->d_scan_pose; ea.F = out->F;
+  ea.sp = make_scan_params(c->scan_par, c->scan_cap);
   ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.noise = d_noise;
   ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.cap = out->cap;
   {
     TimedRegion tr(c, &c->scan_ev, c->stream);
-    hipLaunchKernelGGL(k_scan_emit, dim3(c->scan_tiles, out->F), dim3(kBlock), 0, c->stream, ea);
+    hipLaunchKernelGGL(k_scan_emit, dim3(c->scan_tiles, (out->F + kScanFrames - 1) / kScanFrames), dim3(kBlock), 0,
+                       c->stream, ea);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

@@ -7,6 +7,9 @@
 // with the reference's operation order (no FMA contraction in the distance sum, the same degree
 // conversions), so the kept point sets are the reference's; the range noise (LMC:765-768) is drawn
 // by the host from numpy's global RNG in frame order and added here.
+//
+// A workgroup owns a tile of kScanTile scene points held in registers and tests it against
+// kScanFrames frames (scene re-reads from L2 drop by that factor).
 #pragma once
 #include "kernels.hpp"
 
@@ -14,11 +17,25 @@ namespace mc {
 
 constexpr int kScanRounds = 4;                       // scene points per thread per tile
 constexpr int kScanTile = kScanRounds * kBlock;      // 1024 scene points per workgroup
+constexpr int kScanFrames = 8;                       // frames per workgroup
 
 struct ScanParams {
   double range_min, range_max_sq, half_fov_h, half_fov_v;
   int64_t cap;         // points_per_frame
+  double tan_h, sin_v; // tan / sin of the half FOVs: transcendental-free decisions away from the edges
+  int fast;            // both half FOVs in [0, 89) degrees
 };
+
+inline ScanParams make_scan_params(const double par[4], int64_t cap) {
+  ScanParams sp;
+  sp.range_min = par[0]; sp.range_max_sq = par[1]; sp.half_fov_h = par[2]; sp.half_fov_v = par[3];
+  sp.cap = cap;
+  const double d2r = 3.141592653589793 / 180.0;
+  sp.fast = par[2] >= 0.0 && par[2] < 89.0 && par[3] >= 0.0 && par[3] < 89.0;
+  sp.tan_h = sp.fast ? std::tan(par[2] * d2r) : 0.0;
+  sp.sin_v = sp.fast ? std::sin(par[3] * d2r) : 0.0;
+  return sp;
+}
 
 // f64 sensor pose per frame: R (row-major, 9) + position (3), pose selection as in LMC:804-812
 __global__ __launch_bounds__(kBlock) void k_scan_pose(const double* time, const double* pos, const double* rpy,
@@ -39,53 +56,95 @@ __global__ __launch_bounds__(kBlock) void k_scan_pose(const double* time, const 
   for (int k = 0; k < 3; ++k) pose[12 * f + 9 + k] = pos[3 * idx + k];
 }
 
-// LMC:713-745 for one scene point; returns visibility and the sensor-frame coordinates
-__device__ __forceinline__ bool scan_visible(const double* __restrict__ P, const double* __restrict__ e,
+// the reference's degree comparisons (LMC:735-744), for points near an FOV edge only: kept out of
+// line so the rarely taken transcendental code does not inflate the register budget of the loop
+__device__ __noinline__ bool scan_fov_exact(double lx, double ly, double s, int az_in, int el_in, double half_h,
+                                            double half_v) {
+  if (az_in < 0 && !(fabs(atan2(ly, lx) * 180.0 / 3.141592653589793) <= half_h)) return false;
+  if (el_in < 0 && !(fabs(asin(s) * 180.0 / 3.141592653589793) <= half_v)) return false;
+  return true;
+}
+
+// LMC:713-745 for one scene point (ex, ey, ez); returns visibility and the sensor-frame coordinates
+__device__ __forceinline__ bool scan_visible(const double* __restrict__ P, double ex, double ey, double ez,
                                              const ScanParams& sp, double& lx, double& ly, double& lz) {
 #pragma clang fp contract(off)
-  const double dx = e[0] - P[9], dy = e[1] - P[10], dz = e[2] - P[11];
+  const double dx = ex - P[9], dy = ey - P[10], dz = ez - P[11];
   const double d2 = dx * dx + dy * dy + dz * dz;              // np.sum(.., axis=1) order
   if (!(d2 <= sp.range_max_sq)) return false;                 // LMC:718
   lx = P[0] * dx + P[3] * dy + P[6] * dz;                      // R^T (p - t), LMC:727-728
   ly = P[1] * dx + P[4] * dy + P[7] * dz;
   lz = P[2] * dx + P[5] * dy + P[8] * dz;
   const double r = sqrt(d2);                                   // LMC:732
-  const double az = atan2(ly, lx) * 180.0 / 3.141592653589793;
-  double s = lz / fmax(r, 1e-6);
+  if (!(r >= sp.range_min)) return false;                      // LMC:745
+  double s = lz / fmax(r, 1e-6);                               // LMC:738-739
   s = fmin(fmax(s, -1.0), 1.0);
-  const double el = asin(s) * 180.0 / 3.141592653589793;
-  return fabs(az) <= sp.half_fov_h && fabs(el) <= sp.half_fov_v && r >= sp.range_min;
+  // Away from the FOV edges the degree comparisons of LMC:743-744 are decided exactly by
+  // |ly| <= tan(h) lx (lx > 0) and |s| <= sin(v) (both FOVs below 90 degrees; atan2 / asin are
+  // monotonic there).  Within a relative 1e-9 of an edge the reference's own expressions decide.
+  int az_in = -1, el_in = -1;
+  if (sp.fast) {
+    const double m = 1e-9 * r;
+    const double a = fabs(ly) - sp.tan_h * lx;
+    if (lx > m) az_in = a < -m ? 1 : (a > m ? 0 : -1);
+    else if (lx < -m) az_in = 0;
+    const double e = fabs(s) - sp.sin_v;
+    el_in = e < -1e-12 ? 1 : (e > 1e-12 ? 0 : -1);
+  }
+  if (az_in == 0 || el_in == 0) return false;
+  if (az_in < 0 || el_in < 0) return scan_fov_exact(lx, ly, s, az_in, el_in, sp.half_fov_h, sp.half_fov_v);
+  return true;
 }
 
-// pass 1: visible scene points per (frame, tile)
-__global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict__ env, int64_t ld, int64_t E,
-                                                       const double* __restrict__ pose, ScanParams sp,
-                                                       int32_t* __restrict__ tile_count) {
-  __shared__ int s_cnt[kBlock / 64];
-  const int f = blockIdx.y;
+// the workgroup's scene tile, kScanRounds points per thread, in registers
+struct ScanTile {
+  double x[kScanRounds], y[kScanRounds], z[kScanRounds];
+  bool in[kScanRounds];
+};
+
+__device__ __forceinline__ void scan_load_tile(const double* __restrict__ env, int64_t ld, int64_t E, ScanTile& t) {
   const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
-  const double* P = pose + 12 * (int64_t)f;
-  int n = 0;
 #pragma unroll
   for (int r = 0; r < kScanRounds; ++r) {
     const int64_t e = t0 + r * kBlock + threadIdx.x;
-    double lx, ly, lz;
-    if (e < E && scan_visible(P, env + e * ld, sp, lx, ly, lz)) ++n;
+    t.in[r] = e < E;
+    const double* q = env + (t.in[r] ? e : 0) * ld;
+    t.x[r] = q[0]; t.y[r] = q[1]; t.z[r] = q[2];
   }
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = n;
+}
+
+// pass 1: visible scene points per (frame, tile) -> tile_count[f * n_tiles + tile]
+__global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict__ env, int64_t ld, int64_t E,
+                                                       const double* __restrict__ pose, int32_t F, ScanParams sp,
+                                                       int32_t* __restrict__ tile_count) {
+  __shared__ int s_cnt[kScanFrames][kBlock / 64];
+  ScanTile t;
+  scan_load_tile(env, ld, E, t);
+  const int f0 = blockIdx.y * kScanFrames;
+  const int nf = F - f0 < kScanFrames ? F - f0 : kScanFrames;
+  for (int j = 0; j < nf; ++j) {
+    const double* P = pose + 12 * (int64_t)(f0 + j);
+    int n = 0;
+#pragma unroll
+    for (int r = 0; r < kScanRounds; ++r) {
+      double lx, ly, lz;
+      if (t.in[r] && scan_visible(P, t.x[r], t.y[r], t.z[r], sp, lx, ly, lz)) ++n;
+    }
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+    if ((threadIdx.x & 63) == 0) s_cnt[j][threadIdx.x >> 6] = n;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < nf) {
     int tot = 0;
-    for (int w = 0; w < kBlock / 64; ++w) tot += s_cnt[w];
-    tile_count[(int64_t)f * gridDim.x + blockIdx.x] = tot;
+    for (int w = 0; w < kBlock / 64; ++w) tot += s_cnt[threadIdx.x][w];
+    tile_count[(int64_t)(f0 + threadIdx.x) * gridDim.x + blockIdx.x] = tot;
   }
 }
 
 // pass 2: in-order compaction + systematic subsample + noise, written into the output batch
 struct ScanEmitArgs {
   const double* env; int64_t ld; int64_t E;
-  const double* pose; ScanParams sp;
+  const double* pose; int32_t F; ScanParams sp;
   const int64_t* tile_off;   // [F][n_tiles] exclusive visible-point offset of the tile in its frame
   const int64_t* nvis;       // [F] visible points before subsampling
   const double* noise;       // (N_out, 3) in the batch's dense order, or nullptr
@@ -94,44 +153,58 @@ struct ScanEmitArgs {
 };
 
 __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
-  __shared__ int s_cnt[kBlock / 64];
-  const int f = blockIdx.y;
+  __shared__ int s_cnt[kScanRounds][kBlock / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  ScanTile t;
+  scan_load_tile(a.env, a.ld, a.E, t);
   const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
-  const double* P = a.pose + 12 * (int64_t)f;
-  const int64_t nv = a.nvis[f];
-  const int64_t step = nv > a.sp.cap ? nv / a.sp.cap : 1;    // LMC:757-760
-  const int64_t poff = a.poff[f], doff = a.doff[f];
-  int64_t base = a.tile_off[(int64_t)f * gridDim.x + blockIdx.x];
-  for (int r = 0; r < kScanRounds; ++r) {
-    const int64_t e = t0 + r * kBlock + threadIdx.x;
-    double lx = 0, ly = 0, lz = 0;
-    const bool vis = e < a.E && scan_visible(P, a.env + e * a.ld, a.sp, lx, ly, lz);
-    const unsigned long long m = __ballot(vis);
-    const int rank = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) s_cnt[wid] = __popcll(m);
+  const int f0 = blockIdx.y * kScanFrames;
+  const int nf = a.F - f0 < kScanFrames ? a.F - f0 : kScanFrames;
+  for (int j = 0; j < nf; ++j) {
+    const int f = f0 + j;
+    const double* P = a.pose + 12 * (int64_t)f;
+    bool vis[kScanRounds];
+    double lx[kScanRounds], ly[kScanRounds], lz[kScanRounds];
+    int rank[kScanRounds];
+#pragma unroll
+    for (int r = 0; r < kScanRounds; ++r) {
+      lx[r] = ly[r] = lz[r] = 0.0;
+      vis[r] = t.in[r] && scan_visible(P, t.x[r], t.y[r], t.z[r], a.sp, lx[r], ly[r], lz[r]);
+      const unsigned long long m = __ballot(vis[r]);
+      rank[r] = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) s_cnt[r][wid] = __popcll(m);
+    }
     __syncthreads();
-    int before = 0, total = 0;
-    for (int w = 0; w < kBlock / 64; ++w) {
-      const int c = s_cnt[w];
-      before += w < wid ? c : 0;
-      total += c;
-    }
-    if (vis) {
-      const int64_t idx = base + before + rank;               // index among the frame's visible points
-      if (idx % step == 0 && idx / step < a.sp.cap) {
-        const int64_t o = idx / step;
-        double nx = 0, ny = 0, nz = 0;
-        if (a.noise) { const double* q = a.noise + 3 * (doff + o); nx = q[0]; ny = q[1]; nz = q[2]; }
-        const int64_t p = poff + o;
-        a.cols[p] = (float)(lx + nx);
-        a.cols[a.cap + p] = (float)(ly + ny);
-        a.cols[2 * a.cap + p] = (float)(lz + nz);
-        a.cols[3 * a.cap + p] = (float)a.env[e * a.ld + 3];
+    const int64_t nv = a.nvis[f];
+    const int64_t step = nv > a.sp.cap ? nv / a.sp.cap : 1;    // LMC:757-760
+    const int64_t poff = a.poff[f], doff = a.doff[f];
+    int64_t base = a.tile_off[(int64_t)f * gridDim.x + blockIdx.x];
+#pragma unroll
+    for (int r = 0; r < kScanRounds; ++r) {
+      int before = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) {
+        const int c = s_cnt[r][w];
+        before += w < wid ? c : 0;
+        total += c;
       }
+      if (vis[r]) {
+        const int64_t idx = base + before + rank[r];          // index among the frame's visible points
+        if (idx % step == 0 && idx / step < a.sp.cap) {
+          const int64_t o = idx / step;
+          double nx = 0, ny = 0, nz = 0;
+          if (a.noise) { const double* q = a.noise + 3 * (doff + o); nx = q[0]; ny = q[1]; nz = q[2]; }
+          const int64_t p = poff + o;
+          const int64_t e = t0 + r * kBlock + threadIdx.x;
+          a.cols[p] = (float)(lx[r] + nx);
+          a.cols[a.cap + p] = (float)(ly[r] + ny);
+          a.cols[2 * a.cap + p] = (float)(lz[r] + nz);
+          a.cols[3 * a.cap + p] = (float)a.env[e * a.ld + 3];
+        }
+      }
+      base += total;
     }
-    base += total;
-    __syncthreads();   // s_cnt is rewritten by the next round
+    __syncthreads();   // s_cnt is rewritten by the next frame
   }
 }
 

@@ -126,6 +126,30 @@ def test_scan_edge_cases(mc, gpu_ctx):
         sim.scan_environment(np.zeros((5, 3)), pose)
 
 
+def test_scan_fov_edges_decided_like_reference(mc, gpu_ctx):
+    """Points at +-1e-12 .. 1e-3 degrees from the FOV edges: the kernel's transcendental-free test
+    must defer to the reference's atan2 / asin comparisons near the edges (LMC:735-745)."""
+    cfg = dict(lidar_range_noise=0.0, points_per_frame=10 ** 6)
+    sim = mc.LiDARMotionSimulator(cfg, context=gpu_ctx)
+    h, v = sim.config["fov_horizontal"] / 2, sim.config["fov_vertical"] / 2
+    offs = np.concatenate([-np.logspace(-12, -3, 40), [0.0], np.logspace(-12, -3, 40)])
+    pts = []
+    for r in (1.0, 17.3, 80.0):
+        for d in offs:
+            a = np.radians(h + d)
+            pts.append([r * np.cos(a), r * np.sin(a), 0.0, 0.5])
+            pts.append([r * np.cos(a), -r * np.sin(a), 0.1, 0.5])
+            e = np.radians(v + d)
+            pts.append([r * np.cos(e), 0.0, r * np.sin(e), 0.5])
+            pts.append([r * np.cos(e), 0.0, -r * np.sin(e), 0.5])
+    env = np.array(pts)
+    pose = {"position": np.zeros(3), "orientation": np.zeros(3)}
+    ref = R.scan_environment(env, pose, sim.config)
+    out = sim.scan_environment(env, pose)
+    assert out.shape == ref.shape
+    assert_scaled_close(out, ref, scale_of(ref[:, :3]), what="fov edges")
+
+
 def test_scan_noise_consumes_global_rng_like_reference(mc, gpu_ctx):
     cfg = dict(points_per_frame=3000, lidar_range_noise=0.02)
     sim = mc.LiDARMotionSimulator(cfg, context=gpu_ctx)
