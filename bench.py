@@ -39,37 +39,68 @@ def workload(rank, world, frames, points):
     return cfg, tr, times[lo:lo + frames], lo
 
 
-def cpu_baseline(mode, tr, times, counts, frame_lo, budget_s):
-    """The oracle (numpy restatement, 1 thread) on a bounded sample of the same frames."""
-    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+def _cpu_frames(mode, tr, times, counts, frame_lo, budget_s, f_first=0, f_step=1):
+    """The oracle on frames f_first, f_first+f_step, ... until budget_s of compute; 1 BLAS thread.
+    Returns (points, seconds, frames)."""
+    from threadpoolctl import threadpool_limits
     from oracle import restatement as R
     from oracle import synth
     done = 0
     t_total = 0.0
-    f = 0
+    nf = 0
     ts_imu = gyro = None
     if mode == "imu":
         ts_imu, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
-    while f < len(counts) and t_total < budget_s:
-        x, y, z, i, t = synth.synth_frame(int(counts[f]), 0, 1000 + frame_lo + f)
-        pts = np.column_stack([x, y, z, i]).astype(np.float64)
-        t0 = time.perf_counter()
-        if mode == "frame":
-            k = int(R.select_pose_index(tr["time"], times[f]))
-            R.transform_pointcloud(pts, {"translation": tr["position_gps"][k], "rotation": tr["orientation_imu"][k]})
-        elif mode == "pose_slerp":
-            out = R.deskew_pose_slerp(pts[:, :3], t, times[f], tr)
-            np.column_stack([out, pts[:, 3]])
-        else:
-            st = int(times[f] * 1e9)
-            out = R.compensate_arrays(pts[:, :3], st + t.astype(np.int64), st, ts_imu, gyro)
-            np.column_stack([out, pts[:, 3]])
-        t_total += time.perf_counter() - t0
-        done += int(counts[f])
-        f += 1
-    return {"value": done / t_total / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
-            "sample": f"{f} of {len(counts)} frames x {int(counts[0])} pts (oracle numpy restatement, "
-                      f"same synthetic frames, generation excluded, {t_total:.1f} s)"}
+    with threadpool_limits(limits=1):
+        for f in range(f_first, len(counts), f_step):
+            if t_total >= budget_s:
+                break
+            x, y, z, i, t = synth.synth_frame(int(counts[f]), 0, 1000 + frame_lo + f)
+            pts = np.column_stack([x, y, z, i]).astype(np.float64)
+            t0 = time.perf_counter()
+            if mode == "frame":
+                k = int(R.select_pose_index(tr["time"], times[f]))
+                R.transform_pointcloud(pts, {"translation": tr["position_gps"][k], "rotation": tr["orientation_imu"][k]})
+            elif mode == "pose_slerp":
+                out = R.deskew_pose_slerp(pts[:, :3], t, times[f], tr)
+                np.column_stack([out, pts[:, 3]])
+            else:
+                st = int(times[f] * 1e9)
+                out = R.compensate_arrays(pts[:, :3], st + t.astype(np.int64), st, ts_imu, gyro)
+                np.column_stack([out, pts[:, 3]])
+            t_total += time.perf_counter() - t0
+            done += int(counts[f])
+            nf += 1
+    return done, t_total, nf
+
+
+def _cpu_worker(job):
+    return _cpu_frames(*job)
+
+
+def cpu_baselines(mode, tr, times, counts, frame_lo, budget_s, procs):
+    """The oracle (numpy restatement of the reference's op sequence) on the same synthetic frames,
+    generation excluded: one core, then `procs` processes (one BLAS thread each) splitting the
+    frames round-robin.  Runs before the GPU is touched (the pool is spawned)."""
+    import multiprocessing as mp
+    done, secs, nf = _cpu_frames(mode, tr, times, counts, frame_lo, budget_s)
+    single = {"value": done / secs / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
+              "sample": f"{nf} of {len(counts)} frames x {int(counts[0])} pts (oracle numpy restatement, "
+                        f"same synthetic frames, generation excluded, {secs:.1f} s)"}
+    if procs <= 1:
+        return single
+    jobs = [(mode, tr, times, counts, frame_lo, budget_s, p, procs) for p in range(procs)]
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    pts = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    frames = sum(r[2] for r in res)
+    multi = {"value": pts / wall / 1e6, "unit": "Mpoints/s", "cores": procs, "kind": "port",
+             "sample": f"{frames} of {len(counts)} frames x {int(counts[0])} pts over {procs} processes "
+                       f"(1 BLAS thread each, round-robin frames), rate = points / slowest worker's compute time",
+             "single_core": single}
+    return multi
+
 
 
 def load_traffic(mode, frames, points):
@@ -287,7 +318,9 @@ def main():
     ap.add_argument("--mode", default="pose_slerp", choices=list(BYTES_PER_POINT))
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--points", type=int, default=100_000)
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work (per process)")
+    ap.add_argument("--cpu-procs", type=int, default=16, help="processes for the all-cores CPU baseline "
+                    "(the box's CPU share per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra-modes", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL merged-cloud gather (N>1)")
@@ -298,10 +331,16 @@ def main():
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     rdv = mc.dist.Rendezvous(rank, world)
-    ctx = mc.Context()   # $MCDESKEW_DEVICE, else $LOCAL_RANK
-
     cfg, tr, times, lo = workload(rank, world, args.frames, args.points)
     counts = np.full(args.frames, args.points, dtype=np.int64)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # before the GPU is initialised: the all-cores leg spawns worker processes
+        cpu = cpu_baselines(args.mode, tr, times, counts, lo, args.cpu_budget,
+                            min(args.cpu_procs, len(os.sched_getaffinity(0))))
+        cpu["cores_available"] = len(os.sched_getaffinity(0))
+    ctx = mc.Context()   # $MCDESKEW_DEVICE, else $LOCAL_RANK
+
     b_in = ctx.batch(counts, with_time=True)
     b_out = ctx.batch(counts)
     b_in.synth(seed=0, frame_id_base=1000 + lo)
@@ -374,9 +413,8 @@ def main():
             "codecs": codecs,
             "gather": gather,
         }
-        if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(args.mode, tr, times, counts, lo, args.cpu_budget)
-            line["cpu_baseline"]["cores_available"] = len(os.sched_getaffinity(0))
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     if hung:
         # a collective is stuck inside RCCL: finalisers would block on its stream; the result
