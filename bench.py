@@ -30,8 +30,25 @@ BYTES_PER_POINT = {"pose_slerp": 36, "imu": 36, "frame": 32}   # SURVEY §8d alg
 HBM_PEAK_GBS = 8000.0                                          # MI355X_MICROARCH.md chip table
 
 
-def workload(rank, world, frames, points):
-    cfg = dict(URBAN, duration=max(URBAN["duration"], frames * world / URBAN["lidar_fps"]))
+SCENARIOS = {   # LMC:1182-1204 (BASELINE configs 2 / 4 / 5: urban; 3: parking; 1: highway)
+    "urban_complex": URBAN,
+    "parking_detailed": {"duration": 30.0, "trajectory_type": "circular", "environment_complexity": "medium",
+                         "max_speed": 5.0, "lidar_fps": 20},
+    "highway_simple": {"duration": 60.0, "trajectory_type": "linear", "environment_complexity": "simple",
+                       "max_speed": 25.0, "lidar_fps": 15},
+}
+
+
+def config_label(scenario, frames, points):
+    if scenario == "urban_complex" and points >= 1_000_000:
+        return "BASELINE config 5 shape: 1M-pt dense frames"
+    return {"urban_complex": "BASELINE config 2 (config 4 at 8 GPUs)", "parking_detailed": "BASELINE config 3",
+            "highway_simple": "BASELINE config 1 scenario"}[scenario]
+
+
+def workload(rank, world, frames, points, scenario="urban_complex"):
+    base = SCENARIOS[scenario]
+    cfg = dict(base, duration=max(base["duration"], frames * world / base["lidar_fps"]))
     sim = mc.LiDARMotionSimulator(cfg)
     tr = sim.add_sensor_noise(sim.generate_trajectory())
     times = sim.lidar_times()
@@ -325,13 +342,15 @@ def main():
     ap.add_argument("--no-extra-modes", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL merged-cloud gather (N>1)")
     ap.add_argument("--gather-timeout", type=float, default=120.0)
+    ap.add_argument("--scenario", default="urban_complex", choices=list(SCENARIOS),
+                    help="pose table of this LMC scenario (BASELINE config 3 = parking_detailed)")
     args = ap.parse_args()
 
     rank, local_rank, world = mc.dist.env_rank()
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     rdv = mc.dist.Rendezvous(rank, world)
-    cfg, tr, times, lo = workload(rank, world, args.frames, args.points)
+    cfg, tr, times, lo = workload(rank, world, args.frames, args.points, args.scenario)
     counts = np.full(args.frames, args.points, dtype=np.int64)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -392,10 +411,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 (f64 pose/angle setup)",
-            "data": "synthetic Mid-70 frames (counter-hash generator, on device); reference urban_complex "
+            "data": f"synthetic Mid-70 frames (counter-hash generator, on device); reference {args.scenario} "
                     "pose table, seed 42",
-            "config": {"workload": f"urban_complex figure_eight, {args.frames} frames x {args.points} pts per GPU "
-                                   f"(BASELINE config 2; weak scaling over {world} GPU)",
+            "config": {"workload": f"{args.scenario} {cfg['trajectory_type']}, {args.frames} frames x {args.points} "
+                                   f"pts per GPU ({config_label(args.scenario, args.frames, args.points)}; "
+                                   f"weak scaling over {world} GPU)",
+                       "scenario": args.scenario,
                        "mode": args.mode, "frames_per_gpu": args.frames, "points_per_frame": args.points,
                        "global_frames": args.frames * world, "parallelism": f"frame-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": r["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
