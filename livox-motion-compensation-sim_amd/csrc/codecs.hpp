@@ -184,7 +184,35 @@ __device__ __forceinline__ int u32_digits(uint32_t x) {
          (x >= 10000000u) + (x >= 100000000u) + (x >= 1000000000u);
 }
 
+__device__ __noinline__ Fmt6 fmt6_prepare_exact(double v);
+
+// Common case, |v| < 4294: y = |v| * 1e6 in double is within 2.4e-7 of the exact product, so
+// unless y's fraction is within 1e-6 of one half the rounded integer is floor(y) or floor(y) + 1
+// as decided by the fraction — no 128-bit arithmetic.  Otherwise (and for NaN / inf / large
+// magnitudes) the exact path decides.
 __device__ __forceinline__ Fmt6 fmt6_prepare(double v) {
+  const double a = fabs(v);
+  if (a < 4294.0) {
+    const double y = a * 1000000.0;
+    const double fl = floor(y);
+    const double fr = y - fl;
+    if (fabs(fr - 0.5) > 1e-6) {
+      Fmt6 r;
+      const uint32_t n = (uint32_t)fl + (fr > 0.5 ? 1u : 0u);
+      const uint32_t ip = n / 1000000u;
+      r.neg = signbit(v);
+      r.kind = 0;
+      r.ip = ip;
+      r.fp = n - ip * 1000000u;
+      r.nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
+      r.len = (r.neg ? 1 : 0) + r.nd + 7;
+      return r;
+    }
+  }
+  return fmt6_prepare_exact(v);
+}
+
+__device__ __noinline__ Fmt6 fmt6_prepare_exact(double v) {
   Fmt6 r;
   const uint64_t bits = (uint64_t)__double_as_longlong(v);
   r.neg = (bits >> 63) != 0;
