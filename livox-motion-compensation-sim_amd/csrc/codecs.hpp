@@ -260,6 +260,16 @@ __device__ __noinline__ Fmt6 fmt6_prepare_exact(double v) {
   return r;
 }
 
+// the last min(n, 3) decimal digits of x < 1000 at q[3-n .. 2] (q[0..2] = hundreds, tens, units)
+__device__ __forceinline__ void put3(char* q, uint32_t x, int n) {
+  const uint32_t h = __umul24(x, 41u) >> 12;
+  const uint32_t r = x - h * 100u;
+  const uint32_t t = __umul24(r, 103u) >> 10;
+  if (n >= 3) q[0] = (char)('0' + h);
+  if (n >= 2) q[1] = (char)('0' + t);
+  q[2] = (char)('0' + (r - t * 10u));
+}
+
 // writes f.len characters at p (generic pointer: LDS or global)
 __device__ __forceinline__ void fmt6_write(const Fmt6& f, char* p) {
   if (f.kind == 3) return;
@@ -267,6 +277,19 @@ __device__ __forceinline__ void fmt6_write(const Fmt6& f, char* p) {
   if (f.neg) *p++ = '-';
   if (f.kind == 1) { p[0] = 'i'; p[1] = 'n'; p[2] = 'f'; return; }
   const int nd = f.nd;
+  if (nd <= 4) {
+    // ip < 10^4: 24-bit multiply-shift digit extraction ((x*41)>>12 == x/100 for x < 1000,
+    // (x*103)>>10 == x/10 for x < 100, (x*8389)>>23 == x/1000 for x < 10^4)
+    const uint32_t ip = (uint32_t)f.ip;
+    const uint32_t th = __umul24(ip, 8389u) >> 23;
+    put3(p + nd - 3, ip - th * 1000u, nd);
+    if (nd == 4) p[0] = (char)('0' + th);
+    p[nd] = '.';
+    const uint32_t fh = f.fp / 1000u;
+    put3(p + nd + 1, fh, 3);
+    put3(p + nd + 4, f.fp - fh * 1000u, 3);
+    return;
+  }
   uint32_t fp = f.fp;
 #pragma unroll
   for (int i = 6; i >= 1; --i) {
