@@ -47,6 +47,8 @@ struct mc_ctx {
   int32_t* d_scan_tcount = nullptr;
   int64_t* d_scan_toff = nullptr;
   int64_t* d_scan_nvis = nullptr;
+  uint32_t* d_scan_bits = nullptr;    // pass-1 visibility words
+  size_t scan_bits_cap = 0;
   std::vector<int64_t> scan_counts;   // final per-frame counts of the last mc_scan_count
   double scan_par[4] = {0, 0, 0, 0};  // range_min, range_max^2, fov_h/2, fov_v/2
   int64_t scan_cap = 0;

@@ -132,7 +132,7 @@ int mc_destroy(mc_ctx* c) {
   dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
   dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
   dev_free(c->d_env); dev_free(c->d_scan_ftime); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount);
-  dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis);
+  dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis); dev_free(c->d_scan_bits);
   if (c->d_codec) (void)hipFree(c->d_codec);
   dev_free(c->d_codec_err);
   for (auto& p : c->codec_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
@@ -731,10 +731,17 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   std::vector<int64_t> nvis(F, 0), toff((size_t)F * std::max(tiles, 1), 0);
   if (tiles > 0) {
     const ScanParams sp = make_scan_params(c->scan_par, cap);
+    const size_t words = (size_t)tiles * ((F + kScanFrames - 1) / kScanFrames) * kBlock;
+    if (words > c->scan_bits_cap) {
+      dev_free(c->d_scan_bits);
+      c->scan_bits_cap = 0;
+      if (int r = dev_alloc(&c->d_scan_bits, words)) return r;
+      c->scan_bits_cap = words;
+    }
     {
       TimedRegion tr(c, &c->scan_ev, c->stream);
       hipLaunchKernelGGL(k_scan_count, dim3(tiles, (F + kScanFrames - 1) / kScanFrames), dim3(kBlock), 0, c->stream,
-                         c->d_env, c->env_ld, c->E, c->d_scan_pose, F, sp, c->d_scan_tcount);
+                         c->d_env, c->env_ld, c->E, c->d_scan_pose, F, sp, c->d_scan_tcount, c->d_scan_bits);
     }
     HIPCHK(hipGetLastError());
     std::vector<int32_t> tc((size_t)F * tiles);
@@ -782,7 +789,7 @@ int mc_scan_emit(mc_ctx* c, mc_batch* out, const double* noise) {
   ea.env = c->d_env; ea.ld = c->env_ld; ea.E = c->E;
   ea.pose = c->d_scan_pose; ea.F = out->F;
   ea.sp = make_scan_params(c->scan_par, c->scan_cap);
-  ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.noise = d_noise;
+  ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.vis_bits = c->d_scan_bits; ea.noise = d_noise;
   ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.cap = out->cap;
   {
     TimedRegion tr(c, &c->scan_ev, c->stream);

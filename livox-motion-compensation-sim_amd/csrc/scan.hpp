@@ -22,8 +22,9 @@ constexpr int kScanFrames = 8;                       // frames per workgroup
 struct ScanParams {
   double range_min, range_max_sq, half_fov_h, half_fov_v;
   int64_t cap;         // points_per_frame
-  double tan_h, sin_v; // tan / sin of the half FOVs: transcendental-free decisions away from the edges
-  int fast;            // both half FOVs in [0, 89) degrees
+  double tan_h, sin_v2;        // tan / sin^2 of the half FOVs: decisions away from the edges
+  double rmin2_lo, rmin2_hi;   // range_min^2 (1 -+ 1e-12)
+  int fast;                    // both half FOVs in [0, 89) degrees
 };
 
 inline ScanParams make_scan_params(const double par[4], int64_t cap) {
@@ -33,7 +34,11 @@ inline ScanParams make_scan_params(const double par[4], int64_t cap) {
   const double d2r = 3.141592653589793 / 180.0;
   sp.fast = par[2] >= 0.0 && par[2] < 89.0 && par[3] >= 0.0 && par[3] < 89.0;
   sp.tan_h = sp.fast ? std::tan(par[2] * d2r) : 0.0;
-  sp.sin_v = sp.fast ? std::sin(par[3] * d2r) : 0.0;
+  const double sv = sp.fast ? std::sin(par[3] * d2r) : 0.0;
+  sp.sin_v2 = sv * sv;
+  // a non-positive range_min passes every point (sqrt(d2) >= 0)
+  sp.rmin2_lo = par[0] > 0.0 ? par[0] * par[0] * (1.0 - 1e-12) : -1.0;
+  sp.rmin2_hi = par[0] > 0.0 ? par[0] * par[0] * (1.0 + 1e-12) : -1.0;
   return sp;
 }
 
@@ -75,25 +80,30 @@ __device__ __forceinline__ bool scan_visible(const double* __restrict__ P, doubl
   lx = P[0] * dx + P[3] * dy + P[6] * dz;                      // R^T (p - t), LMC:727-728
   ly = P[1] * dx + P[4] * dy + P[7] * dz;
   lz = P[2] * dx + P[5] * dy + P[8] * dz;
+  // Away from the edges the tests of LMC:732-745 are decided without sqrt / division / atan2 /
+  // asin: r >= range_min by d2 against range_min^2, |az| <= h by |ly| <= tan(h) lx (lx > 0),
+  // |el| <= v by lz^2 <= sin(v)^2 d2 (both FOVs below 90 degrees, where atan2 / asin are
+  // monotonic).  Within a relative 1e-9 of any edge the reference's own expressions decide.
+  int r_in = -1, az_in = -1, el_in = -1;
+  if (sp.fast) {
+    r_in = d2 > sp.rmin2_hi ? 1 : (d2 < sp.rmin2_lo ? 0 : -1);
+    const double m = 1e-9 * (fabs(lx) + fabs(ly) + fabs(lz));
+    const double a = fabs(ly) - sp.tan_h * lx;
+    if (lx > m) az_in = a < -m ? 1 : (a > m ? 0 : -1);
+    else if (lx < -m) az_in = 0;
+    if (d2 > 1e-10) {
+      const double e = lz * lz - sp.sin_v2 * d2;
+      const double me = 1e-9 * d2;
+      el_in = e < -me ? 1 : (e > me ? 0 : -1);
+    }
+    if (r_in == 0 || az_in == 0 || el_in == 0) return false;
+    if (r_in == 1 && az_in == 1 && el_in == 1) return true;
+  }
   const double r = sqrt(d2);                                   // LMC:732
   if (!(r >= sp.range_min)) return false;                      // LMC:745
   double s = lz / fmax(r, 1e-6);                               // LMC:738-739
   s = fmin(fmax(s, -1.0), 1.0);
-  // Away from the FOV edges the degree comparisons of LMC:743-744 are decided exactly by
-  // |ly| <= tan(h) lx (lx > 0) and |s| <= sin(v) (both FOVs below 90 degrees; atan2 / asin are
-  // monotonic there).  Within a relative 1e-9 of an edge the reference's own expressions decide.
-  int az_in = -1, el_in = -1;
-  if (sp.fast) {
-    const double m = 1e-9 * r;
-    const double a = fabs(ly) - sp.tan_h * lx;
-    if (lx > m) az_in = a < -m ? 1 : (a > m ? 0 : -1);
-    else if (lx < -m) az_in = 0;
-    const double e = fabs(s) - sp.sin_v;
-    el_in = e < -1e-12 ? 1 : (e > 1e-12 ? 0 : -1);
-  }
-  if (az_in == 0 || el_in == 0) return false;
-  if (az_in < 0 || el_in < 0) return scan_fov_exact(lx, ly, s, az_in, el_in, sp.half_fov_h, sp.half_fov_v);
-  return true;
+  return scan_fov_exact(lx, ly, s, az_in, el_in, sp.half_fov_h, sp.half_fov_v);
 }
 
 // the workgroup's scene tile, kScanRounds points per thread, in registers
@@ -113,26 +123,35 @@ __device__ __forceinline__ void scan_load_tile(const double* __restrict__ env, i
   }
 }
 
-// pass 1: visible scene points per (frame, tile) -> tile_count[f * n_tiles + tile]
+static_assert(kScanFrames * kScanRounds == 32, "one 32-bit visibility word per thread and workgroup");
+
+// pass 1: visible scene points per (frame, tile) -> tile_count[f * n_tiles + tile], and the
+// visibility bits (bit j*kScanRounds + r: frame f0+j, round r) that pass 2 consumes
 __global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict__ env, int64_t ld, int64_t E,
                                                        const double* __restrict__ pose, int32_t F, ScanParams sp,
-                                                       int32_t* __restrict__ tile_count) {
+                                                       int32_t* __restrict__ tile_count,
+                                                       uint32_t* __restrict__ vis_bits) {
   __shared__ int s_cnt[kScanFrames][kBlock / 64];
   ScanTile t;
   scan_load_tile(env, ld, E, t);
   const int f0 = blockIdx.y * kScanFrames;
   const int nf = F - f0 < kScanFrames ? F - f0 : kScanFrames;
+  uint32_t bits = 0;
   for (int j = 0; j < nf; ++j) {
     const double* P = pose + 12 * (int64_t)(f0 + j);
     int n = 0;
 #pragma unroll
     for (int r = 0; r < kScanRounds; ++r) {
       double lx, ly, lz;
-      if (t.in[r] && scan_visible(P, t.x[r], t.y[r], t.z[r], sp, lx, ly, lz)) ++n;
+      if (t.in[r] && scan_visible(P, t.x[r], t.y[r], t.z[r], sp, lx, ly, lz)) {
+        ++n;
+        bits |= 1u << (j * kScanRounds + r);
+      }
     }
     for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
     if ((threadIdx.x & 63) == 0) s_cnt[j][threadIdx.x >> 6] = n;
   }
+  vis_bits[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x] = bits;
   __syncthreads();
   if (threadIdx.x < nf) {
     int tot = 0;
@@ -147,6 +166,7 @@ struct ScanEmitArgs {
   const double* pose; int32_t F; ScanParams sp;
   const int64_t* tile_off;   // [F][n_tiles] exclusive visible-point offset of the tile in its frame
   const int64_t* nvis;       // [F] visible points before subsampling
+  const uint32_t* vis_bits;  // pass 1's visibility words
   const double* noise;       // (N_out, 3) in the batch's dense order, or nullptr
   const int64_t* poff; const int64_t* doff;
   float* cols; int64_t cap;
@@ -160,6 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
   const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
   const int f0 = blockIdx.y * kScanFrames;
   const int nf = a.F - f0 < kScanFrames ? a.F - f0 : kScanFrames;
+  const uint32_t bits = a.vis_bits[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x];
   for (int j = 0; j < nf; ++j) {
     const int f = f0 + j;
     const double* P = a.pose + 12 * (int64_t)f;
@@ -168,8 +189,16 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
     int rank[kScanRounds];
 #pragma unroll
     for (int r = 0; r < kScanRounds; ++r) {
+      vis[r] = (bits >> (j * kScanRounds + r)) & 1u;
       lx[r] = ly[r] = lz[r] = 0.0;
-      vis[r] = t.in[r] && scan_visible(P, t.x[r], t.y[r], t.z[r], a.sp, lx[r], ly[r], lz[r]);
+      if (vis[r]) {
+        // the sensor-frame point exactly as pass 1 (and LMC:727-728) computed it
+#pragma clang fp contract(off)
+        const double dx = t.x[r] - P[9], dy = t.y[r] - P[10], dz = t.z[r] - P[11];
+        lx[r] = P[0] * dx + P[3] * dy + P[6] * dz;
+        ly[r] = P[1] * dx + P[4] * dy + P[7] * dz;
+        lz[r] = P[2] * dx + P[5] * dy + P[8] * dz;
+      }
       const unsigned long long m = __ballot(vis[r]);
       rank[r] = __popcll(m & ((1ull << lane) - 1ull));
       if (lane == 0) s_cnt[r][wid] = __popcll(m);
