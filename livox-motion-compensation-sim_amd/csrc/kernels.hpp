@@ -751,9 +751,67 @@ __device__ __forceinline__ int64_t local_index(const LayoutArgs& a, const Tile& 
 // / 35 % of peak.)  kStageUnroll chunks per lane are in flight at once.
 typedef double v2d __attribute__((ext_vector_type(2)));
 constexpr int kStageUnroll = 4;
+#ifndef MC_STAGE_LDS
+#define MC_STAGE_LDS 1       // transpose each tile through LDS (16-byte lanes on both sides):
+                             // -11 % / -15 % kernel time vs the direct mapping (tools/ab_stager.py)
+#endif
+#ifndef MC_STAGE_ST
+#define MC_STAGE_ST 1        // LDS stager output stores (st_pol policy)
+#endif
+constexpr int kTilePts = 4 * kTileGroups;
+constexpr int kStageRow = kTilePts + 16;   // LDS row pad: the 4 rows start in different banks
+
+// LDS-transposed stager: the tile's 4 x 2048 float32 values sit in LDS between a 16-byte-per-lane
+// AoS pass and a float4-per-lane SoA pass.
+__device__ __forceinline__ void stage_tile_lds_in(const LayoutArgs& a, const Tile& tl, const v2d* __restrict__ s2,
+                                                  int nv, float (*s)[kStageRow]) {
+  const int np = 4 * tl.ngroups;
+  for (int q = threadIdx.x; q < 2 * np; q += kBlock) {
+    const v2d v = q < 2 * nv ? __builtin_nontemporal_load(s2 + q) : v2d{0.0, 0.0};
+    const int j = q >> 1, h = q & 1;
+    s[2 * h][j] = (float)v.x;
+    s[2 * h + 1][j] = (float)v.y;
+  }
+  __syncthreads();
+  float* cx = a.cols + tl.pstart;
+  for (int g = threadIdx.x; g < tl.ngroups; g += kBlock)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      st_pol<MC_STAGE_ST>(cx + c * a.cap + 4 * g, *reinterpret_cast<const float4*>(&s[c][4 * g]));
+  __syncthreads();
+}
+
+__device__ __forceinline__ void stage_tile_lds_out(const LayoutArgs& a, const Tile& tl, v2d* __restrict__ d2, int nv,
+                                                   float (*s)[kStageRow]) {
+  const float* cx = a.cols + tl.pstart;
+  for (int g = threadIdx.x; g < (nv + 3) / 4; g += kBlock)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      *reinterpret_cast<float4*>(&s[c][4 * g]) = ld4(cx + c * a.cap + 4 * g);
+  __syncthreads();
+  for (int q = threadIdx.x; q < 2 * nv; q += kBlock) {
+    const int j = q >> 1, h = q & 1;
+    const v2d v = {(double)s[2 * h][j], (double)s[2 * h + 1][j]};
+    st_pol<MC_STAGE_ST>(reinterpret_cast<float*>(d2 + q), __builtin_bit_cast(float4, v));
+  }
+  __syncthreads();
+}
 
 // AoS f64 (dense, row stride ld) -> padded SoA f32 (padding slots zeroed)
 __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const double* __restrict__ aos, int64_t ld) {
+#if MC_STAGE_LDS
+  __shared__ float s_t[4][kStageRow];
+  if (ld == 4) {
+    for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+      const Tile tl = ldu(a.tiles + tile);
+      const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+      const int64_t loc0 = tl.pstart - poff;
+      const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
+      stage_tile_lds_in(a, tl, reinterpret_cast<const v2d*>(aos + (doff + loc0) * 4), nv, s_t);
+    }
+    return;
+  }
+#endif
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
@@ -795,6 +853,17 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
 
 // padded SoA f32 -> dense AoS (N,4) f64  (the (N,4) float64 layout LMC:776 returns)
 __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, double* __restrict__ aos) {
+#if MC_STAGE_LDS
+  __shared__ float s_t[4][kStageRow];
+  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const Tile tl = ldu(a.tiles + tile);
+    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+    const int64_t loc0 = tl.pstart - poff;
+    const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
+    stage_tile_lds_out(a, tl, reinterpret_cast<v2d*>(aos + (doff + loc0) * 4), nv, s_t);
+  }
+  return;
+#endif
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);

@@ -1,0 +1,74 @@
+"""Interleaved A/B of the device stager pair (SoA f32 <-> AoS f64) across library variants, one
+process, one device (GPU box only).  Also checks that every variant's round trip is bit-identical.
+
+    make -C livox-motion-compensation-sim_amd/csrc variants VARIANTS="base:-DMC_KITERS=2 lds:-DMC_STAGE_LDS=1"
+    python tools/ab_stager.py --libs build/variants/lib_base.so,build/variants/lib_lds.so
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import mcamd as mc  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--frames", type=int, default=600)
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    libs = [l for l in args.libs.split(",") if l]
+    counts = np.full(args.frames, args.points, np.int64)
+    counts[::7] -= 3                                    # ragged frames: partial groups and tiles
+    n = int(counts.sum())
+    runs = {}
+    for lib in libs:
+        ctx = mc.Context(0, lib_path=lib)
+        b = ctx.batch(counts)
+        b.synth(seed=1, frame_id_base=1000)
+        back = ctx.batch(counts)
+        buf = ctx.device_buffer(n * 32)
+        runs[lib] = (ctx, b, back, buf)
+    ref = None
+    for lib, (ctx, b, back, buf) in runs.items():
+        b.fetch_aos_device(buf)
+        back.stage_aos_device(buf)
+        ck = (b.checksum().tolist(), back.checksum().tolist())
+        assert ck[0][:4] == ck[1][:4], (lib, ck)
+        ref = ref or ck
+        assert ck == ref, (lib, ck, ref)
+    res = {lib: {"soa_to_aos": [], "aos_to_soa": []} for lib in libs}
+    for _ in range(args.rounds):
+        for lib, (ctx, b, back, buf) in runs.items():
+            for name, fn in (("soa_to_aos", lambda: b.fetch_aos_device(buf)),
+                             ("aos_to_soa", lambda: back.stage_aos_device(buf))):
+                fn()
+                ctx.sync()
+                ctx.read_timing()
+                ctx.timing(True)
+                for _ in range(args.reps):
+                    fn()
+                ctx.sync()
+                ctx.timing(False)
+                t = ctx.read_timing()
+                res[lib][name].append(t["layout_ms"] / t["layout_launches"] * 1e3)
+    out = {}
+    for lib, d in res.items():
+        out[os.path.basename(lib)] = {k: {"median_us": statistics.median(v), "min_us": min(v),
+                                          "frac_median": 48 * n / (statistics.median(v) * 1e-6) / 8e12}
+                                      for k, v in d.items()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
