@@ -48,8 +48,36 @@ def run_pass(mode, counter, outdir, frames, points):
     return statistics.median(vals), len(vals)
 
 
+AUX = ["k_soa_to_aos", "k_aos_to_soa", "k_lvx_packages", "k_pcd_measure", "k_pcd_write", "k_scan_count",
+       "k_scan_emit"]
+
+
+def run_aux(counter, outdir):
+    """One counter pass over tools/aux_kernels.py; returns ({kernel: median KiB}, alg bytes)."""
+    d = os.path.join(outdir, f"pmc_aux_{counter}")
+    cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d,
+           "-o", "run", "--", sys.executable, os.path.join(ROOT, "tools", "aux_kernels.py")]
+    env = dict(os.environ, TMPDIR="/tmp")
+    r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout[-2000:] + r.stderr[-4000:])
+        raise SystemExit(f"rocprofv3 aux pass {counter} failed rc={r.returncode}")
+    alg = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["algorithmic_bytes_per_launch"]
+    vals = {k: [] for k in AUX}
+    for fn in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                for k in AUX:
+                    if f"mc::{k}(" in row.get("Kernel_Name", ""):
+                        vals[k].append(float(row["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items() if v}, alg
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--aux", action="store_true", help="the kernels around the path (tools/aux_kernels.py)")
     ap.add_argument("--modes", default="pose_slerp,frame,imu")
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--points", type=int, default=100_000)
@@ -62,7 +90,20 @@ def main():
     if os.path.exists(path):
         with open(path) as f:
             res = json.load(f)
-    for mode in args.modes.split(","):
+    if args.aux:
+        fetch, alg = run_aux("FETCH_SIZE", outdir)
+        write, _ = run_aux("WRITE_SIZE", outdir)
+        for k in AUX:
+            if k not in fetch or k not in write:
+                continue
+            f_b, w_b = fetch[k] * 1024 * 2, write[k] * 1024
+            res[f"aux:{k}"] = {"kernel": k, "fetch_bytes_per_launch": f_b, "write_bytes_per_launch": w_b,
+                               "hbm_bytes_per_launch": f_b + w_b, "algorithmic_bytes_per_launch": alg[k],
+                               "traffic_over_algorithmic": (f_b + w_b) / alg[k], "tag": args.tag,
+                               "note": "tools/aux_kernels.py workload; FETCH_SIZE x2 (gfx950 correction)"}
+            print(k, json.dumps(res[f"aux:{k}"]))
+        args.modes = ""
+    for mode in [m for m in args.modes.split(",") if m]:
         fetch_kib, n1 = run_pass(mode, "FETCH_SIZE", outdir, args.frames, args.points)
         write_kib, n2 = run_pass(mode, "WRITE_SIZE", outdir, args.frames, args.points)
         fetch = fetch_kib * 1024 * 2      # gfx950: FETCH_SIZE reports half of a wide coalesced read
