@@ -120,6 +120,17 @@ def cpu_baselines(mode, tr, times, counts, frame_lo, budget_s, procs):
 
 
 
+def aux_traffic(*kernels):
+    """PMC traffic / algorithmic bytes of the kernels around the path (tools/pmc_traffic.py --aux)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    got = {k: d[f"aux:{k}"]["traffic_over_algorithmic"] for k in kernels if f"aux:{k}" in d}
+    return got or None
+
+
 def load_traffic(mode, frames, points):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
@@ -173,7 +184,8 @@ def measure_stager(ctx, b_in, b_out, n_rank, reps):
             t = ctx.read_timing()
             us = t["layout_ms"] / max(t["layout_launches"], 1) * 1e3
             gbs = 48 * n_rank / (us * 1e-6) / 1e9
-            out[name] = {"kernel_avg_us": us, "GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_point": 48}
+            out[name] = {"kernel_avg_us": us, "GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_point": 48,
+                         "traffic_over_algorithmic": aux_traffic("k_" + name)}
         return out
     finally:
         buf.close()
@@ -255,7 +267,7 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
         alg = 32 * n_rank + int(pos[-1])
         rep["lvx"] = {"file_bytes": int(pos[-1]), "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
                       "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
-                      "bytes_per_point": alg / n_rank}
+                      "bytes_per_point": alg / n_rank, "traffic_over_algorithmic": aux_traffic("k_lvx_packages")}
         bpos = np.zeros(F + 1, np.int64)
         cap = n_rank * 48
         out = ctx.device_buffer(cap)
@@ -275,7 +287,8 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
         alg = 32 * n_rank + text
         rep["pcd_ascii"] = {"text_bytes": text, "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
                             "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
-                            "bytes_per_point": alg / n_rank, "note": "measure + write passes"}
+                            "bytes_per_point": alg / n_rank, "note": "measure + write passes",
+                            "traffic_over_algorithmic": aux_traffic("k_pcd_measure", "k_pcd_write")}
         if cpu_budget > 0:
             from oracle import codecs as C
             host = b_out.download_aos()[:int(counts[0])]
