@@ -179,6 +179,61 @@ def test_full_size_c2_per_point_modes_sampled(mc, gpu_ctx, mode):
         assert np.max(np.abs(nout - nin) / nin) < 1e-5
 
 
+def _scenario_batch(mc, ctx, name, frames, n, seed):
+    sim = mc.LiDARMotionSimulator(dict(CFGS[name]), context=ctx)   # seeds np.random (LMC:288): noise on
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:frames]
+    b = ctx.batch(np.full(frames, n), with_time=True)
+    b.synth(seed=seed, frame_id_base=1000)
+    b.set_frame_times(times)
+    b.set_frame_starts((times * 1e9).astype(np.int64))
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    ts, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    ctx.set_imu(ts, gyro)
+    return b, tr, times, ts, gyro
+
+
+def _check_frames(mc, ctx, b, tr, times, ts, gyro, mode, frames_to_check, n, seed):
+    out = ctx.deskew(b, mode=mode)
+    ox, oy, oz, oi = out.download_columns()
+    hx, hy, hz, hi, ht = synth.synth_batch(b.counts, seed=seed, frame_id_base=1000)
+    assert np.array_equal(oi, hi)
+    idx = R.select_pose_index(tr["time"], times)
+    for f in frames_to_check:
+        s = slice(f * n, (f + 1) * n)
+        p = np.stack([hx[s], hy[s], hz[s]], axis=1).astype(np.float64)
+        got = np.stack([ox[s], oy[s], oz[s]], axis=1)
+        if mode == "frame":
+            k = idx[f]
+            ref = R.transform_pointcloud(np.column_stack([p, hi[s]]),
+                                         {"translation": tr["position_gps"][k], "rotation": tr["orientation_imu"][k]})[:, :3]
+            sc = scale_of(p, tr["position_gps"][k])
+        elif mode == "pose_slerp":
+            ref = R.deskew_pose_slerp(p, ht[s], times[f], tr)
+            _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[f] + ht[s] * 1e-9)
+            sc = scale_of(p, pos)
+        else:
+            st = int(times[f] * 1e9)
+            ref = R.compensate_arrays(p, st + ht[s].astype(np.int64), st, ts, gyro)
+            sc = scale_of(p)
+        assert_scaled_close(got, ref, sc, what=f"{mode} frame {f}")
+
+
+@pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
+def test_config1_highway_10x20k_all_points(mc, gpu_ctx, mode):
+    """BASELINE config 1 (highway_simple, linear, 10 frames x 20k points): every point, every mode."""
+    b, tr, times, ts, gyro = _scenario_batch(mc, gpu_ctx, "highway_simple", 10, 20_000, seed=5)
+    _check_frames(mc, gpu_ctx, b, tr, times, ts, gyro, mode, range(10), 20_000, seed=5)
+
+
+@pytest.mark.parametrize("mode", ["pose_slerp", "frame"])
+def test_config3_parking_600x100k_sampled(mc, gpu_ctx, mode):
+    """BASELINE config 3 (parking_detailed, circular, IMU/GPS noise on, SLERP-heavy): 600 x 100k,
+    frames sampled across the run including the yaw wrap region."""
+    b, tr, times, ts, gyro = _scenario_batch(mc, gpu_ctx, "parking_detailed", 600, 100_000, seed=9)
+    _check_frames(mc, gpu_ctx, b, tr, times, ts, gyro, mode, [0, 1, 150, 299, 300, 301, 450, 599], 100_000, seed=9)
+
+
 # ---------------------------------------------------------------------------------------------
 # per-point SLERP mode
 # ---------------------------------------------------------------------------------------------
