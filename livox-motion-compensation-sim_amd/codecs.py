@@ -153,6 +153,13 @@ class LivoxLVXWriter:
 
 # ---- ASCII PCD -------------------------------------------------------------------------------
 def _pcd_encode_device(ctx: Context, d_aos, ld, counts) -> List[bytes]:
+    """Per cloud the PCD header + point lines."""
+    counts = np.ascontiguousarray(counts, np.int64)
+    return [pcd_header(c) + body for c, body in zip(counts, _pcd_bodies_device(ctx, d_aos, ld, counts))]
+
+
+def _pcd_bodies_device(ctx: Context, d_aos, ld, counts) -> List[bytes]:
+    """Per cloud its point lines only (LMC:946-948)."""
     counts = np.ascontiguousarray(counts, np.int64)
     F = len(counts)
     pos = np.zeros(F + 1, np.int64)
@@ -166,10 +173,10 @@ def _pcd_encode_device(ctx: Context, d_aos, ld, counts) -> List[bytes]:
                 cap = int(pos[-1])        # exact size now known: one more pass
                 continue
             check(rc, "pcd_encode")
-            text = out.to_host(np.uint8)[:int(pos[-1])].tobytes() if pos[-1] else b""
+            text = out.to_host(np.uint8, count=int(pos[-1])).tobytes() if pos[-1] else b""
         finally:
             out.close()
-        return [pcd_header(c) + text[pos[f]:pos[f + 1]] for f, c in enumerate(counts)]
+        return [text[pos[f]:pos[f + 1]] for f in range(F)]
     raise _lib.McError("pcd_encode: output size changed between passes")
 
 
@@ -179,6 +186,16 @@ def encode_pcd_frames(clouds: Sequence[np.ndarray], context: Context | None = No
     buf, counts, _ = _device_cloud(ctx, [np.asarray(c, np.float64) for c in clouds], 4)
     try:
         return _pcd_encode_device(ctx, buf.ptr, 4, counts)
+    finally:
+        buf.close()
+
+
+def encode_pcd_bodies(clouds: Sequence[np.ndarray], context: Context | None = None) -> List[bytes]:
+    """Per cloud its point lines without the header (merged files reuse the frames' lines)."""
+    ctx = context or default_context()
+    buf, counts, _ = _device_cloud(ctx, [np.asarray(c, np.float64) for c in clouds], 4)
+    try:
+        return _pcd_bodies_device(ctx, buf.ptr, 4, counts)
     finally:
         buf.close()
 

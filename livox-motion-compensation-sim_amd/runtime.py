@@ -173,8 +173,9 @@ class DeviceBuffer:
     def close(self):
         self._fin()
 
-    def to_host(self, dtype=np.float64, shape=None) -> np.ndarray:
-        out = np.empty(self.nbytes // np.dtype(dtype).itemsize, dtype)
+    def to_host(self, dtype=np.float64, shape=None, count=None) -> np.ndarray:
+        n = self.nbytes // np.dtype(dtype).itemsize
+        out = np.empty(n if count is None else min(int(count), n), dtype)
         check(self.lib.mc_memcpy_d2h(self.ctx.handle, out.ctypes.data_as(c_void_p), self.ptr, out.nbytes), "d2h")
         return out.reshape(shape) if shape is not None else out
 

@@ -13,11 +13,13 @@ launch over a ragged batch of frames:
 
 Around the path, also on the GPU: scan_environment / scan_frames / simulate_frames / run_simulation
 (LMC:701-858, the scan feeding the alignment without leaving HBM) and the byte-exact writers
-save_pcd / save_lvx (LMC:932-990).  Scene synthesis, CSV/LAS export, plots and reports
-(LMC:430-699, 860-931, 950-963, 992-1173) are not provided.
+save_pcd / save_lvx / save_results (LMC:860-990; CSVs through pandas, LAS through laspy when it is
+installed, as in the reference).  Scene synthesis, plots and reports (LMC:430-699, 992-1173) are
+not provided.
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -240,6 +242,68 @@ class LiDARMotionSimulator:
         """LMC:932-948: ASCII PCD v0.7, lines formatted on the GPU (byte-identical)."""
         _codecs.save_pcd(points, filename, self.context)
 
+    def save_las(self, points, filename):
+        """LMC:950-963 through laspy (a host file format; raises ImportError without laspy)."""
+        import laspy   # noqa: F401  (optional dependency, as in the reference)
+        header = laspy.LasHeader(point_format=3, version="1.2")
+        las = laspy.LasData(header)
+        las.x, las.y, las.z = points[:, 0], points[:, 1], points[:, 2]
+        las.intensity = (points[:, 3] * 65535).astype(np.uint16)
+        las.write(filename)
+
+    def save_results(self, results, output_dir="lidar_simulation_output"):
+        """LMC:860-931: motion / trajectory CSVs, per-frame raw and aligned PCDs, the merged PCDs,
+        LAS and LVX.  Every PCD's point lines come from one GPU launch pair over all frames; the
+        merged files reuse the frames' lines (a vstack of the clouds prints the same lines)."""
+        import pandas as pd
+        os.makedirs(output_dir, exist_ok=True)
+        print(f"Saving results to {output_dir}...")
+        pd.DataFrame(results["motion_data"]).to_csv(os.path.join(output_dir, "motion_data.csv"), index=False)
+        raw = [s["points_local"] for s in results["raw_scans"]]
+        aligned = list(results["aligned_pointclouds"])
+        bodies = _codecs.encode_pcd_bodies(raw + aligned, self.context) if raw or aligned else []
+        raw_b, al_b = bodies[:len(raw)], bodies[len(raw):]
+        pcd_dir = os.path.join(output_dir, "raw_scans_pcd")
+        os.makedirs(pcd_dir, exist_ok=True)
+        for s, pts, body in zip(results["raw_scans"], raw, raw_b):
+            _write(os.path.join(pcd_dir, f'frame_{s["frame_id"]:04d}.pcd'), _codecs.pcd_header(len(pts)) + body)
+        aligned_dir = os.path.join(output_dir, "aligned_scans_pcd")
+        os.makedirs(aligned_dir, exist_ok=True)
+        for i, (pts, body) in enumerate(zip(aligned, al_b)):
+            _write(os.path.join(aligned_dir, f"aligned_frame_{i:04d}.pcd"), _codecs.pcd_header(len(pts)) + body)
+        merged_aligned = None
+        if aligned and all(len(pc) > 0 for pc in aligned):      # LMC:887
+            n = sum(len(pc) for pc in aligned)
+            _write(os.path.join(output_dir, "merged_aligned.pcd"), _codecs.pcd_header(n) + b"".join(al_b))
+            merged_aligned = self.merge_aligned(aligned)
+        else:
+            print("Warning: No aligned point clouds to merge")
+        keep = [i for i, pts in enumerate(raw) if len(pts) > 0]
+        if keep:
+            n = sum(len(raw[i]) for i in keep)
+            _write(os.path.join(output_dir, "merged_raw_overlapped.pcd"),
+                   _codecs.pcd_header(n) + b"".join(raw_b[i] for i in keep))
+        else:
+            print("Warning: No raw point clouds to merge")
+        try:
+            if merged_aligned is None:
+                raise NameError("name 'merged_aligned' is not defined")   # LMC:903 on the skipped merge
+            self.save_las(merged_aligned, os.path.join(output_dir, "merged_aligned.las"))
+            print("LAS format saved successfully")
+        except Exception as e:
+            print(f"Could not save LAS format: {e}")
+        try:
+            self.save_lvx(results, os.path.join(output_dir, "lidar_data"))
+            print("LVX formats saved successfully")
+        except Exception as e:
+            print(f"Could not save LVX formats: {e}")
+        tr = results["trajectory"]
+        pd.DataFrame({"time": tr["time"], "x": tr["position"][:, 0], "y": tr["position"][:, 1],
+                      "z": tr["position"][:, 2], "x_gps": tr["position_gps"][:, 0], "y_gps": tr["position_gps"][:, 1],
+                      "z_gps": tr["position_gps"][:, 2]}).to_csv(os.path.join(output_dir, "trajectory.csv"), index=False)
+        print("Results saved successfully!")
+        return output_dir
+
     def save_lvx(self, results, base_filename):
         """LMC:965-990: the raw (local) scans of ``results`` as ``<base_filename>.lvx``."""
         frames_data = [{"frame_id": s["frame_id"], "timestamp": s["timestamp"], "points": s["points_local"]}
@@ -266,3 +330,8 @@ def _stack_aos(frames: List[np.ndarray]) -> np.ndarray:
     if len(frames) == 1:
         return np.ascontiguousarray(frames[0][:, :ld], dtype=np.float64)
     return np.ascontiguousarray(np.concatenate([f[:, :ld] for f in frames]), dtype=np.float64)
+
+
+def _write(path: str, data: bytes) -> None:
+    with open(path, "wb") as f:
+        f.write(data)

@@ -342,8 +342,54 @@ def make_coords(csim):
     np.savez_compressed(os.path.join(HERE, "coords.npz"), **out)
 
 
+def make_save_results(lmc):
+    """LMC:860-931 on a small results dict: every file save_results writes, byte for byte."""
+    import tempfile
+    rng = np.random.default_rng(31)
+    n_frames = 4
+    sizes = [50, 0, 130, 7]
+    tr = {"time": np.linspace(0, 1, 6), "position": rng.normal(0, 10, (6, 3)),
+          "position_gps": rng.normal(0, 10, (6, 3))}
+    raw, aligned, motion = [], [], []
+    for i, n in enumerate(sizes):
+        loc = np.column_stack([rng.normal(0, 30, (n, 3)), rng.uniform(0, 1, n)]).reshape(n, 4)
+        al = np.column_stack([rng.normal(0, 300, (n, 3)), loc[:, 3]]).reshape(n, 4)
+        pose = {"position": tr["position_gps"][i], "orientation": rng.normal(0, 0.1, 3),
+                "velocity": rng.normal(0, 5, 3)}
+        raw.append({"frame_id": i, "timestamp": 0.1 * i, "points_local": loc, "sensor_pose": pose})
+        aligned.append(al)
+        motion.append({"frame_id": i, "timestamp": 0.1 * i, "gps_lat": 40.0 + i * 1e-5, "gps_lon": -74.0,
+                       "gps_alt": 1.5, "imu_roll": 0.01 * i, "imu_pitch": -0.02, "imu_yaw": 1.0 + i,
+                       "vel_x": 3.0, "vel_y": 0.5 * i, "vel_z": 0.0})
+    results = {"raw_scans": raw, "aligned_pointclouds": aligned, "motion_data": motion, "trajectory": tr}
+    out = {}
+    for tag, res in (("gap", results),
+                     ("full", dict(results, aligned_pointclouds=[a for a in aligned if len(a)],
+                                   raw_scans=[s for s in raw if len(s["points_local"])]))):
+        sim = lmc.LiDARMotionSimulator()
+        with tempfile.TemporaryDirectory() as d, contextlib.redirect_stdout(io.StringIO()):
+            sim.save_results(res, d)
+            for root, _, files in os.walk(d):
+                for fn in sorted(files):
+                    p = os.path.join(root, fn)
+                    with open(p, "rb") as fh:
+                        out[f"{tag}/{os.path.relpath(p, d)}"] = np.frombuffer(fh.read(), np.uint8)
+        for i, s in enumerate(res["raw_scans"]):
+            out[f"{tag}/in/raw/{i}"] = s["points_local"]
+            out[f"{tag}/in/frame_id/{i}"] = np.int64(s["frame_id"])
+        for i, a in enumerate(res["aligned_pointclouds"]):
+            out[f"{tag}/in/aligned/{i}"] = a
+    for k in ("time", "position", "position_gps"):
+        out[f"in/trajectory/{k}"] = tr[k]
+    out["in/motion"] = np.array([[m[c] for c in motion[0]] for m in motion], np.float64)
+    out["in/motion_cols"] = np.array(list(motion[0]))
+    out["in/n_frames"] = np.int64(n_frames)
+    np.savez_compressed(os.path.join(HERE, "save_results.npz"), **out)
+
+
 def main():
     lmc, csim = import_reference()
+    make_save_results(lmc)
     make_coords(csim)
     make_codecs(lmc)
     make_lmc(lmc)

@@ -108,3 +108,41 @@ def test_simulator_save_lvx_and_pcd(mc, gpu_ctx, tmp_path):
     sim.save_pcd(scans[2]["points_local"], os.path.join(tmp_path, "f.pcd"))
     with open(os.path.join(tmp_path, "f.pcd"), "rb") as f:
         assert f.read() == C.pcd_ascii_bytes(scans[2]["points_local"])
+
+
+@pytest.mark.parametrize("tag", ["gap", "full"])
+def test_save_results_files_match_reference(mc, gpu_ctx, tmp_path, tag):
+    """LMC:860-931: every file save_results writes (CSVs, per-frame and merged PCDs, LVX), byte for
+    byte against the reference's own output directory (tests/golden/save_results.npz)."""
+    g = golden("save_results.npz")
+    cols = [str(c) for c in g["in/motion_cols"]]
+    motion = []
+    for row in g["in/motion"]:
+        m = {c: float(v) for c, v in zip(cols, row)}
+        m["frame_id"] = int(m["frame_id"])
+        motion.append(m)
+    raw = []
+    i = 0
+    while f"{tag}/in/raw/{i}" in g:
+        fid = int(g[f"{tag}/in/frame_id/{i}"])
+        raw.append({"frame_id": fid, "timestamp": 0.1 * fid, "points_local": g[f"{tag}/in/raw/{i}"]})
+        i += 1
+    aligned = []
+    i = 0
+    while f"{tag}/in/aligned/{i}" in g:
+        aligned.append(g[f"{tag}/in/aligned/{i}"])
+        i += 1
+    tr = {k: g[f"in/trajectory/{k}"] for k in ("time", "position", "position_gps")}
+    results = {"raw_scans": raw, "aligned_pointclouds": aligned, "motion_data": motion, "trajectory": tr}
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    sim.save_results(results, str(tmp_path))
+    want = {k[len(tag) + 1:]: g[k].tobytes() for k in g.files if k.startswith(tag + "/") and "/in/" not in k}
+    got = {}
+    for root, _, files in os.walk(tmp_path):
+        for fn in files:
+            p = os.path.join(root, fn)
+            with open(p, "rb") as f:
+                got[os.path.relpath(p, tmp_path)] = f.read()
+    assert sorted(got) == sorted(want)
+    for k in want:
+        assert got[k] == want[k], k
