@@ -41,3 +41,7 @@ cd "$ROOT"
 timeout -k 10 1200 python tools/pmc_traffic.py --tag "$TAG" > "$OUT/pmc_$TAG.log" 2>&1
 stop_if_fault $? pmc
 tail -5 "$OUT/pmc_$TAG.log"
+
+timeout -k 10 900 python tools/pmc_traffic.py --aux --tag "$TAG" > "$OUT/pmc_aux_$TAG.log" 2>&1
+stop_if_fault $? pmc_aux
+tail -8 "$OUT/pmc_aux_$TAG.log"
