@@ -110,7 +110,6 @@ class CoordinateTransformer:
 def transform_arrays(frames: Sequence[np.ndarray], T, context: Context | None = None) -> List[np.ndarray]:
     """T @ [p, 1] (or T @ p for (N,4) homogeneous rows) for every cloud; one matrix for all, or one
     per cloud ((F,4,4) / (F,3,4)).  Returns (N_i, 3) float64 arrays."""
-    ctx = context or default_context()
     arrs = [np.asarray(f) for f in frames]
     if any(a.ndim != 2 for a in arrs):
         raise IndexError("tuple index out of range")     # points.shape[1] on a 1-D array (CSIM:223)
@@ -123,6 +122,7 @@ def transform_arrays(frames: Sequence[np.ndarray], T, context: Context | None = 
     if not arrs or counts.sum() == 0:
         return [np.zeros((len(a), 3)) for a in arrs]
     homog = widths == {4}
+    ctx = context or default_context()
     b = ctx.batch(counts)
     try:
         xyz = np.concatenate([a[:, :3] for a in arrs]).astype(np.float32)

@@ -7,7 +7,7 @@ import re
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, ROOT, pkg
+from conftest import GOLDEN, ROOT, golden, pkg
 
 
 def test_default_config_is_the_reference_dict():
@@ -121,3 +121,35 @@ def test_imu_stream_shape():
     ts, g = m.trajectory.imu_from_trajectory(tr, 200.0)
     assert ts.dtype == np.int64 and g.shape == (len(ts), 3)
     assert ts[0] == 0 and np.all(np.diff(ts) > 0) and np.all(g[0] == 0)
+
+
+def test_lvx_layout_is_host_only_and_matches_oracle():
+    from oracle import codecs as C
+    m = pkg()
+    counts = [0, 1, 95, 96, 97, 100_000]
+    assert np.array_equal(m.codecs.lvx_layout(counts), C.lvx_frame_positions(counts))
+    with pytest.raises(ValueError):
+        m.codecs.lvx_layout([3, -1])
+
+
+def test_coordinate_transformer_host_matrices_match_reference():
+    g = golden("coords.npz")
+    m = pkg()
+    ct = m.CoordinateTransformer()          # no device touched until points are transformed
+    ct.set_transformation("sensor", "local", [10.0, -5.0, 2.0], [0.1, -0.2, 2.5])
+    np.testing.assert_allclose(ct.transformations[("sensor", "local")], g["T/sensor/local"], atol=1e-15)
+    np.testing.assert_allclose(ct.transformations[("local", "sensor")], g["T/local/sensor"], atol=1e-15)
+    p = g["p3"]
+    assert ct.transform_points(p, "vehicle", "sensor") is p      # missing pair: the input itself
+    T = ct.transformations[("sensor", "vehicle")]
+    assert T[2, 3] == 1.5 and np.array_equal(T[:3, :3], np.eye(3))
+    with pytest.raises(IndexError):
+        m.coords.transform_arrays([np.zeros(3)], np.eye(4))
+
+
+def test_pcd_header_matches_reference_files():
+    g = golden("codecs.npz")
+    m = pkg()
+    for case in ("tricky", "random", "empty"):
+        pts = g[f"pcd/{case}/points"]
+        assert g[f"pcd/{case}/bytes"].tobytes().startswith(m.codecs.pcd_header(len(pts)))
