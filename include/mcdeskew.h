@@ -9,7 +9,9 @@
  *
  *   reference (file:line)                                      replaced by
  *   ---------------------------------------------------------  -----------------------------
- *   LiDARMotionSimulator.transform_pointcloud  LMC:772-776     mc_batch_upload_aos_f64 +
+ *   LiDARMotionSimulator.transform_pointcloud  LMC:772-776     mc_transform_pointcloud_f64 (one
+ *                                                              call, host arrays, float64), or
+ *                                                              mc_batch_upload_aos_f64 +
  *                                                              mc_deskew(MC_MODE_FRAME,
  *                                                              MC_POSE_DIRECT) +
  *                                                              mc_batch_download_aos_f64
@@ -181,6 +183,13 @@ int mc_batch_checksum(mc_batch* b, double* sums5);
 /* ---- the hot path --------------------------------------------------------- */
 /* out must have the same frame counts as in (it may be the same batch: in-place). */
 int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select);
+
+/* One call of transform_pointcloud (LMC:772-776) on host arrays: points (n, ld>=4) float64 rows,
+ * rpy / translation (3,) float64 -> out (n, 4) float64 = [R_xyz(rpy) p + t, intensity], computed in
+ * float64 by a kernel that reads and writes pinned, device-mapped host memory (no DMA round trips:
+ * the latency path for the reference's one-frame-per-call use).  ld < 4 -> MC_ERR_INDEX. */
+int mc_transform_pointcloud_f64(mc_ctx* ctx, const double* points, int64_t n, int64_t ld, const double* rpy,
+                                const double* translation, double* out);
 
 /* CoordinateTransformer.transform_points (CSIM:153-233) / _transform_coordinates (CSIM:2107-2163):
  * p' = A p + b with one 3x4 [A | b] matrix (row-major float64, 12 values) for all frames

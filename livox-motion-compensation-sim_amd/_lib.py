@@ -87,6 +87,7 @@ _SIGS = {
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),
     "mc_deskew": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "mc_transform_affine": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, _pd, c_int]),
+    "mc_transform_pointcloud_f64": (c_int, [c_void_p, _pd, c_int64, c_int64, _pd, _pd, _pd]),
     "mc_timing_enable": (c_int, [c_void_p, c_int]),
     "mc_timing_read": (c_int, [c_void_p, _pd, _pi64, _pd, _pi64]),
     "mc_set_launch": (c_int, [c_void_p, c_int32]),

@@ -58,6 +58,9 @@ struct mc_ctx {
   size_t codec_bytes = 0;
   int* d_codec_err = nullptr;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> codec_ev;
+  // pinned, device-mapped host buffer of the single-call drop-in path
+  void* h_pin = nullptr;
+  size_t pin_bytes = 0;
   // staging buffer for host<->device layout conversion
   void* d_stage = nullptr;
   size_t stage_bytes = 0;

@@ -457,6 +457,28 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
 
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) { deskew_frame_body<false>(a); }
 
+// Single-call drop-in of transform_pointcloud (LMC:772-776) on host-resident (n, ld) float64 rows:
+// reads and writes pinned, device-mapped host memory directly (no DMA round trips for the small
+// frames the reference transforms one call at a time), float64 math like the reference.
+__global__ __launch_bounds__(kBlock) void k_transform_host_f64(const double* __restrict__ in, int64_t n, int64_t ld,
+                                                               double roll, double pitch, double yaw, double tx,
+                                                               double ty, double tz, double* __restrict__ out) {
+  __shared__ double s_R[9];
+  if (threadIdx.x == 0) euler_xyz_matrix(roll, pitch, yaw, s_R);
+  __syncthreads();
+  const double R0 = s_R[0], R1 = s_R[1], R2 = s_R[2], R3 = s_R[3], R4 = s_R[4], R5 = s_R[5], R6 = s_R[6],
+               R7 = s_R[7], R8 = s_R[8];
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double* q = in + i * ld;
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    double* o = out + 4 * i;
+    o[0] = R0 * x + R1 * y + R2 * z + tx;
+    o[1] = R3 * x + R4 * y + R5 * z + ty;
+    o[2] = R6 * x + R7 * y + R8 * z + tz;
+    o[3] = w;
+  }
+}
+
 // CoordinateTransformer.transform_points on homogeneous (N,4) input (CSIM:214-233)
 __global__ __launch_bounds__(kBlock) void k_affine_w(const DeskewArgs a) { deskew_frame_body<true>(a); }
 

@@ -135,6 +135,7 @@ int mc_destroy(mc_ctx* c) {
   dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis); dev_free(c->d_scan_bits);
   if (c->d_codec) (void)hipFree(c->d_codec);
   dev_free(c->d_codec_err);
+  if (c->h_pin) (void)hipHostFree(c->h_pin);
   for (auto& p : c->codec_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   if (c->d_stage) (void)hipFree(c->d_stage);
   for (auto& p : c->main_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
@@ -614,6 +615,37 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   // per-point modes pass the timestamps through (CSIM:1472): copy the column when out != in
   if (mode != MC_MODE_FRAME && out != in && out->d_t)
     HIPCHK(hipMemcpyAsync(out->d_t, in->d_t, in->P * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  return MC_OK;
+}
+
+int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
+                                const double* translation, double* out) {
+  CHECK_ARG(c && rpy && translation, "NULL argument");
+  CHECK_ARG(n >= 0, "negative point count");
+  if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 1 with size %lld", (long long)ld);
+  if (n == 0) return MC_OK;
+  CHECK_ARG(points && out, "NULL points / out");
+  DeviceGuard g(c->device);
+  const size_t in_b = (size_t)n * ld * sizeof(double), out_b = (size_t)n * 4 * sizeof(double);
+  const size_t off = (in_b + 255) & ~size_t(255);
+  if (off + out_b > c->pin_bytes) {
+    if (c->h_pin) { (void)hipStreamSynchronize(c->stream); (void)hipHostFree(c->h_pin); c->h_pin = nullptr; }
+    c->pin_bytes = 0;
+    HIPCHK(hipHostMalloc(&c->h_pin, off + out_b, hipHostMallocMapped | hipHostMallocCoherent));
+    c->pin_bytes = off + out_b;
+  }
+  char* pin = static_cast<char*>(c->h_pin);
+  std::memcpy(pin, points, in_b);
+  const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
+  {
+    TimedRegion tr(c, &c->main_ev, c->stream);
+    hipLaunchKernelGGL(k_transform_host_f64, dim3(grid), dim3(kBlock), 0, c->stream,
+                       reinterpret_cast<const double*>(pin), n, ld, rpy[0], rpy[1], rpy[2], translation[0],
+                       translation[1], translation[2], reinterpret_cast<double*>(pin + off));
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  std::memcpy(out, pin + off, out_b);
   return MC_OK;
 }
 

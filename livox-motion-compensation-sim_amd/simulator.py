@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import os
 from collections import OrderedDict
+from ctypes import c_double
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -28,6 +29,7 @@ import numpy as np
 from . import codecs as _codecs
 from . import config as _config
 from . import trajectory as _traj
+from ._lib import check, ptr
 from .runtime import Context, default_context
 
 
@@ -97,11 +99,18 @@ class LiDARMotionSimulator:
         points (N, >=4) -> new (N, 4) float64 array; input untouched; (0,4) -> (0,4).
         """
         points = self._check_points(points)
-        rot = np.asarray(transformation["rotation"], dtype=np.float64).reshape(3)
-        trans = np.asarray(transformation["translation"], dtype=np.float64).reshape(3)
+        rot = np.ascontiguousarray(transformation["rotation"], dtype=np.float64).reshape(3)
+        trans = np.ascontiguousarray(transformation["translation"], dtype=np.float64).reshape(3)
         if points.shape[0] == 0:
             return np.zeros((0, 4))
-        return self.align_frames([points], [{"translation": trans, "rotation": rot}])[0]
+        # one frame per call (the reference's loop): the float64 kernel on pinned host memory
+        p = np.ascontiguousarray(points, dtype=np.float64)
+        out = np.empty((p.shape[0], 4))
+        ctx = self.context
+        check(ctx.lib.mc_transform_pointcloud_f64(ctx.handle, ptr(p, c_double), p.shape[0], p.shape[1],
+                                                  ptr(rot, c_double), ptr(trans, c_double), ptr(out, c_double)),
+              "transform_pointcloud")
+        return out
 
     def align_frames(self, frames: List[np.ndarray], transformations: List[dict]) -> List[np.ndarray]:
         """Batched transform_pointcloud: frame i uses transformations[i]; one kernel launch."""

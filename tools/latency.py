@@ -1,0 +1,59 @@
+"""Per-call latency of the drop-in entry points on host arrays at the reference's native frame size
+(~1.6k points per urban_complex frame), next to the oracle on one core.
+
+    python tools/latency.py [--points 1600] [--calls 300]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import mcamd as mc  # noqa: E402
+from oracle import restatement as R  # noqa: E402
+
+
+def timed(fn, calls):
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        fn()
+    return (time.perf_counter() - t0) / calls
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=1600)
+    ap.add_argument("--calls", type=int, default=300)
+    ap.add_argument("--frames", type=int, default=1200)
+    args = ap.parse_args()
+    rng = np.random.default_rng(0)
+    pts = np.column_stack([rng.normal(0, 30, (args.points, 3)), rng.uniform(0, 1, args.points)])
+    pose = {"translation": np.array([12.0, -3.0, 0.5]), "rotation": np.array([0.01, -0.02, 1.3])}
+    sim = mc.LiDARMotionSimulator({"duration": 120.0, "trajectory_type": "figure_eight", "lidar_fps": 10})
+    out = {"points_per_frame": args.points}
+    out["transform_pointcloud_us"] = timed(lambda: sim.transform_pointcloud(pts, pose), args.calls) * 1e6
+    out["oracle_transform_pointcloud_us"] = timed(lambda: R.transform_pointcloud(pts, pose), args.calls) * 1e6
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:args.frames]
+    scans = [pts] * args.frames
+    t = timed(lambda: sim.run_alignment(scans, tr, times), 5)
+    out["run_alignment_frames"] = args.frames
+    out["run_alignment_ms"] = t * 1e3
+    out["run_alignment_us_per_frame"] = t / args.frames * 1e6
+    idx = R.select_pose_index(tr["time"], times)
+    t = timed(lambda: [R.transform_pointcloud(s, {"translation": tr["position_gps"][k],
+                                                  "rotation": tr["orientation_imu"][k]})
+                       for s, k in zip(scans, idx)], 2)
+    out["oracle_loop_us_per_frame"] = t / args.frames * 1e6
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
