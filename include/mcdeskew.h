@@ -191,6 +191,13 @@ int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose
 int mc_transform_pointcloud_f64(mc_ctx* ctx, const double* points, int64_t n, int64_t ld, const double* rpy,
                                 const double* translation, double* out);
 
+/* The frame loop (LMC:802-832) on host arrays: frames[f] (counts[f], lds[f] >= 4) float64 rows
+ * -> outs[f] (counts[f], 4) float64, pose per frame from the uploaded trajectory (pose_select as
+ * mc_deskew's frame mode; frame_times for MC_POSE_SEARCHSORTED), float64 math, one launch over
+ * all frames on pinned, device-mapped host memory (host copies on 16 threads above 8 MB). */
+int mc_align_frames_host_f64(mc_ctx* ctx, int32_t n_frames, const double* const* frames, const int64_t* counts,
+                             const int64_t* lds, const double* frame_times, int pose_select, double* const* outs);
+
 /* CoordinateTransformer.transform_points (CSIM:153-233) / _transform_coordinates (CSIM:2107-2163):
  * p' = A p + b with one 3x4 [A | b] matrix (row-major float64, 12 values) for all frames
  * (n_mats == 1) or one per frame (n_mats == n_frames).  w_column != 0: the intensity column is the

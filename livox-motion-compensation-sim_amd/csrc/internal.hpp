@@ -3,7 +3,13 @@
 #include <hip/hip_runtime_api.h>
 #include <hip/hip_vector_types.h>
 #include <stdint.h>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -16,7 +22,55 @@ struct FrameWin;
 
 namespace mcimpl {
 int fail(int code, const char* fmt, ...);
-}
+
+// Persistent host worker pool for the host-side row copies of the host<->device pipeline.
+class HostPool {
+ public:
+  explicit HostPool(int threads) {
+    for (int k = 0; k < threads; ++k) th_.emplace_back([this] { work(); });
+  }
+  ~HostPool() {
+    { std::lock_guard<std::mutex> l(m_); stop_ = true; }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // fn(i) for i in [0, n) on the pool's threads; returns when all are done
+  void run(int64_t n, const std::function<void(int64_t)>& fn) {
+    if (n <= 0) return;
+    std::unique_lock<std::mutex> l(m_);
+    fn_ = &fn; n_ = n; next_ = 0; busy_ = (int)th_.size(); ++gen_;
+    cv_.notify_all();
+    done_.wait(l, [this] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> l(m_);
+      cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      const std::function<void(int64_t)>* fn = fn_;
+      const int64_t n = n_;
+      l.unlock();
+      for (int64_t i = next_++; i < n; i = next_++) (*fn)(i);
+      l.lock();
+      if (--busy_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int64_t)>* fn_ = nullptr;
+  int64_t n_ = 0;
+  std::atomic<int64_t> next_{0};
+  int busy_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+}  // namespace mcimpl
 
 struct mc_ctx {
   int device = 0;
@@ -61,6 +115,10 @@ struct mc_ctx {
   // pinned, device-mapped host buffer of the single-call drop-in path
   void* h_pin = nullptr;
   size_t pin_bytes = 0;
+  // host <-> device row pipeline (double-buffered pinned and device chunks, in + out)
+  void* h_pipe = nullptr;
+  void* d_pipe = nullptr;
+  std::unique_ptr<mcimpl::HostPool> pool;
   // staging buffer for host<->device layout conversion
   void* d_stage = nullptr;
   size_t stage_bytes = 0;

@@ -457,6 +457,58 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
 
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) { deskew_frame_body<false>(a); }
 
+// Many frames on host-resident rows (LMC:802-832 on host arrays): frame f's rows [doff[f],
+// doff[f+1]) of the pinned input get pose[12 f ..] = R (row-major) | t (float64, from k_scan_pose).
+// Rows [r0, r0 + n) of the concatenated frames (a pipeline chunk); in / out hold (n, 4) rows.
+__global__ __launch_bounds__(kBlock) void k_align_rows_f64(const double* __restrict__ in, int64_t n, int64_t r0,
+                                                           const int64_t* __restrict__ doff, int32_t F,
+                                                           const double* __restrict__ pose, double* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = r0 + i;
+    int32_t lo = 0, hi = F;                      // last f with doff[f] <= row
+    while (hi - lo > 1) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (doff[mid] <= row) lo = mid; else hi = mid;
+    }
+    const double* P = pose + 12 * (int64_t)lo;
+    const double2 p01 = *reinterpret_cast<const double2*>(in + 4 * i);
+    const double2 p23 = *reinterpret_cast<const double2*>(in + 4 * i + 2);
+    const double x = p01.x, y = p01.y, z = p23.x, w = p23.y;
+    double* o = out + 4 * i;
+    *reinterpret_cast<double2*>(o) = double2{P[0] * x + P[1] * y + P[2] * z + P[9], P[3] * x + P[4] * y + P[5] * z + P[10]};
+    *reinterpret_cast<double2*>(o + 2) = double2{P[6] * x + P[7] * y + P[8] * z + P[11], w};
+  }
+}
+
+// the 12-double pose (R row-major | t) of explicit Euler angles and translation
+__global__ void k_pose_from_rpy(double roll, double pitch, double yaw, double tx, double ty, double tz,
+                                double* __restrict__ pose) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    euler_xyz_matrix(roll, pitch, yaw, pose);
+    pose[9] = tx; pose[10] = ty; pose[11] = tz;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_align_host_f64(const double* __restrict__ in, int64_t n, int64_t ld,
+                                                           const int64_t* __restrict__ doff, int32_t F,
+                                                           const double* __restrict__ pose, double* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    int32_t lo = 0, hi = F;                      // last f with doff[f] <= i
+    while (hi - lo > 1) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (doff[mid] <= i) lo = mid; else hi = mid;
+    }
+    const double* P = pose + 12 * (int64_t)lo;
+    const double* q = in + i * ld;
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    double* o = out + 4 * i;
+    o[0] = P[0] * x + P[1] * y + P[2] * z + P[9];
+    o[1] = P[3] * x + P[4] * y + P[5] * z + P[10];
+    o[2] = P[6] * x + P[7] * y + P[8] * z + P[11];
+    o[3] = w;
+  }
+}
+
 // Single-call drop-in of transform_pointcloud (LMC:772-776) on host-resident (n, ld) float64 rows:
 // reads and writes pinned, device-mapped host memory directly (no DMA round trips for the small
 // frames the reference transforms one call at a time), float64 math like the reference.

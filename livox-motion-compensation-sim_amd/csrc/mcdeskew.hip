@@ -10,10 +10,14 @@
 #include "hostutil.hpp"
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace mc;
@@ -136,6 +140,8 @@ int mc_destroy(mc_ctx* c) {
   if (c->d_codec) (void)hipFree(c->d_codec);
   dev_free(c->d_codec_err);
   if (c->h_pin) (void)hipHostFree(c->h_pin);
+  if (c->h_pipe) (void)hipHostFree(c->h_pipe);
+  if (c->d_pipe) (void)hipFree(c->d_pipe);
   for (auto& p : c->codec_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   if (c->d_stage) (void)hipFree(c->d_stage);
   for (auto& p : c->main_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
@@ -618,6 +624,14 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   return MC_OK;
 }
 
+constexpr int64_t kPipeRows = 1 << 20;                                 // 32 MB of (n,4) float64
+constexpr size_t kPipeBytes = (size_t)kPipeRows * 4 * sizeof(double);
+constexpr int64_t kZeroCopyRows = 1 << 15;                             // below: zero-copy kernels
+constexpr int kPoolThreads = 16;                                       // the box's CPU share per GPU
+constexpr int64_t kJobRows = 8192;                                     // rows per host copy job (256 KB)
+static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
+                        const int64_t* d_doff, const double* d_pose, double* const* outs);
+
 int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
                                 const double* translation, double* out) {
   CHECK_ARG(c && rpy && translation, "NULL argument");
@@ -626,6 +640,22 @@ int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int6
   if (n == 0) return MC_OK;
   CHECK_ARG(points && out, "NULL points / out");
   DeviceGuard g(c->device);
+  if (n >= kZeroCopyRows) {                     // large: the DMA row pipeline with one frame
+    if (int r = sync_all(c)) return r;
+    void* st = nullptr;
+    if (int r = ctx_stage(c, 2 * sizeof(int64_t) + 12 * sizeof(double), &st)) return r;
+    int64_t* d_doff = static_cast<int64_t*>(st);
+    double* d_pose = reinterpret_cast<double*>(d_doff + 2);
+    const std::vector<int64_t> doff{0, n};
+    HIPCHK(hipMemcpyAsync(d_doff, doff.data(), 2 * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_pose_from_rpy, dim3(1), dim3(64), 0, c->stream, rpy[0], rpy[1], rpy[2], translation[0],
+                       translation[1], translation[2], d_pose);
+    HIPCHK(hipGetLastError());
+    const double* fr[1] = {points};
+    const int64_t lds[1] = {ld};
+    double* const outs[1] = {out};
+    return row_pipeline(c, fr, lds, doff, d_doff, d_pose, outs);
+  }
   const size_t in_b = (size_t)n * ld * sizeof(double), out_b = (size_t)n * 4 * sizeof(double);
   const size_t off = (in_b + 255) & ~size_t(255);
   if (off + out_b > c->pin_bytes) {
@@ -646,6 +676,157 @@ int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int6
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   std::memcpy(out, pin + off, out_b);
+  return MC_OK;
+}
+
+// ---- host arrays <-> device: the row pipeline ------------------------------------------------
+// Rows of the concatenated frames travel in chunks: the host pool copies a chunk into pinned
+// memory (compacting rows to 4 columns), DMA to HBM, k_align_rows_f64, DMA back, the pool copies
+// the rows out to the caller's arrays — chunk k's host copies overlap chunk k±1's DMA and kernel.
+
+static void host_rows(mc_ctx* c, const std::vector<int64_t>& doff, int64_t r0, int64_t r1,
+                      const std::function<void(int32_t, int64_t, int64_t)>& seg) {
+  // segments (frame, row_a, row_b) of [r0, r1), at most kJobRows rows each, run on the pool
+  std::vector<std::array<int64_t, 3>> jobs;
+  int32_t f = (int32_t)(std::upper_bound(doff.begin(), doff.end(), r0) - doff.begin()) - 1;
+  for (; f < (int32_t)doff.size() - 1 && doff[f] < r1; ++f)
+    for (int64_t a = std::max(doff[f], r0), e = std::min(doff[f + 1], r1); a < e; a += kJobRows)
+      jobs.push_back({f, a, std::min(a + kJobRows, e)});
+  if (!c->pool) c->pool.reset(new mcimpl::HostPool(kPoolThreads));
+  c->pool->run((int64_t)jobs.size(), [&](int64_t j) { seg((int32_t)jobs[j][0], jobs[j][1], jobs[j][2]); });
+}
+
+static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
+                        const int64_t* d_doff, const double* d_pose, double* const* outs) {
+  const int32_t F = (int32_t)doff.size() - 1;
+  const int64_t n = doff[F];
+  if (!c->h_pipe) HIPCHK(hipHostMalloc(&c->h_pipe, 4 * kPipeBytes, hipHostMallocDefault));
+  if (!c->d_pipe) HIPCHK(hipMalloc(&c->d_pipe, 4 * kPipeBytes));
+  double* pin[4];
+  double* dev[4];
+  for (int k = 0; k < 4; ++k) {
+    pin[k] = reinterpret_cast<double*>(static_cast<char*>(c->h_pipe) + k * kPipeBytes);
+    dev[k] = reinterpret_cast<double*>(static_cast<char*>(c->d_pipe) + k * kPipeBytes);
+  }
+  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
+  for (int b = 0; b < 2; ++b) {
+    HIPCHK(hipEventCreateWithFlags(&ev_in[b], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_out[b], hipEventDisableTiming));
+  }
+  hipStream_t s = c->stream;
+  auto copy_out = [&](int64_t k) {
+    const int64_t r0 = k * kPipeRows, r1 = std::min(n, r0 + kPipeRows);
+    const double* src = pin[2 + (k & 1)];
+    host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t e) {
+      std::memcpy(outs[f] + 4 * (a - doff[f]), src + 4 * (a - r0), (size_t)(e - a) * 4 * sizeof(double));
+    });
+  };
+  const int64_t K = (n + kPipeRows - 1) / kPipeRows;
+  int rc = MC_OK;
+  for (int64_t k = 0; k < K && rc == MC_OK; ++k) {
+    const int b = (int)(k & 1);
+    const int64_t r0 = k * kPipeRows, r1 = std::min(n, r0 + kPipeRows), m = r1 - r0;
+    if (k >= 2) (void)hipEventSynchronize(ev_in[b]);                 // pinned input b is free again
+    double* dst = pin[b];
+    host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t e) {
+      const int64_t ld = lds[f];
+      const double* sp = frames[f] + (a - doff[f]) * ld;
+      double* dp = dst + 4 * (a - r0);
+      if (ld == 4) {
+        std::memcpy(dp, sp, (size_t)(e - a) * 4 * sizeof(double));
+      } else {
+        for (int64_t i = 0; i < e - a; ++i) std::memcpy(dp + 4 * i, sp + i * ld, 4 * sizeof(double));
+      }
+    });
+    hipError_t e = hipMemcpyAsync(dev[b], pin[b], (size_t)m * 32, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(ev_in[b], s);
+    if (e == hipSuccess) {
+      TimedRegion tr(c, &c->main_ev, s);
+      hipLaunchKernelGGL(k_align_rows_f64, dim3((unsigned)std::min<int64_t>((m + kBlock - 1) / kBlock, 4096)),
+                         dim3(kBlock), 0, s, dev[b], m, r0, d_doff, F, d_pose, dev[2 + b]);
+    }
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess && k >= 1) {                                // chunk k-1's rows are back: copy out
+      e = hipEventSynchronize(ev_out[b ^ 1]);
+      if (e == hipSuccess) copy_out(k - 1);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(pin[2 + b], dev[2 + b], (size_t)m * 32, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(ev_out[b], s);
+    if (e != hipSuccess) rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
+  }
+  if (rc == MC_OK && K > 0) {
+    const hipError_t e = hipEventSynchronize(ev_out[(K - 1) & 1]);
+    if (e == hipSuccess) copy_out(K - 1);
+    else rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
+  }
+  (void)hipStreamSynchronize(s);
+  for (int b = 0; b < 2; ++b) { (void)hipEventDestroy(ev_in[b]); (void)hipEventDestroy(ev_out[b]); }
+  return rc;
+}
+
+int mc_align_frames_host_f64(mc_ctx* c, int32_t F, const double* const* frames, const int64_t* counts,
+                             const int64_t* lds, const double* frame_times, int pose_select, double* const* outs) {
+  CHECK_ARG(c && (F == 0 || (frames && counts && lds && outs)), "NULL argument");
+  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(pose_select == MC_POSE_SEARCHSORTED || pose_select == MC_POSE_DIRECT, "unknown pose_select");
+  if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
+  if (pose_select == MC_POSE_DIRECT && c->T != F)
+    return fail(MC_ERR_INVALID, "MC_POSE_DIRECT needs one pose per frame (T=%lld, frames=%d)", (long long)c->T, F);
+  CHECK_ARG(pose_select == MC_POSE_DIRECT || F == 0 || frame_times, "frame times are NULL");
+  std::vector<int64_t> doff((size_t)F + 1, 0);
+  for (int32_t f = 0; f < F; ++f) {
+    CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
+    if (counts[f] > 0 && lds[f] < 4)
+      return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 1 with size %lld", (long long)lds[f]);
+    CHECK_ARG(counts[f] == 0 || (frames[f] && outs[f]), "NULL frame pointer at frame %d", f);
+    doff[f + 1] = doff[f] + counts[f];
+  }
+  const int64_t n = doff[F];
+  if (n == 0) return MC_OK;
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  // per-frame float64 pose (k_scan_pose: pose selection LMC:804-812 + Euler -> R) in device scratch
+  void* st = nullptr;
+  const size_t tab_b = ((size_t)F + 1) * sizeof(int64_t) + (size_t)F * sizeof(double) + 12 * (size_t)F * sizeof(double);
+  if (int r = ctx_stage(c, tab_b, &st)) return r;
+  int64_t* d_doff = static_cast<int64_t*>(st);
+  double* d_ft = reinterpret_cast<double*>(d_doff + F + 1);
+  double* d_pose = d_ft + F;
+  HIPCHK(hipMemcpyAsync(d_doff, doff.data(), doff.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  if (pose_select == MC_POSE_SEARCHSORTED)
+    HIPCHK(hipMemcpyAsync(d_ft, frame_times, F * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_scan_pose, dim3((F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->d_time, c->d_pos,
+                     c->d_rpy, c->T, d_ft, F, pose_select, d_pose);
+  HIPCHK(hipGetLastError());
+  if (n >= kZeroCopyRows) return row_pipeline(c, frames, lds, doff, d_doff, d_pose, outs);
+
+  // small: the kernel reads and writes pinned, device-mapped host memory [rows (n,4) | out (n,4)]
+  const size_t rows_b = (size_t)n * 4 * sizeof(double);
+  if (2 * rows_b > c->pin_bytes) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->h_pin) { (void)hipHostFree(c->h_pin); c->h_pin = nullptr; }
+    c->pin_bytes = 0;
+    HIPCHK(hipHostMalloc(&c->h_pin, 2 * rows_b, hipHostMallocMapped | hipHostMallocCoherent));
+    c->pin_bytes = 2 * rows_b;
+  }
+  double* pin_in = static_cast<double*>(c->h_pin);
+  double* pin_out = pin_in + 4 * n;
+  for (int32_t f = 0; f < F; ++f) {
+    const int64_t m = counts[f], ld = lds[f];
+    double* dst = pin_in + 4 * doff[f];
+    if (ld == 4) std::memcpy(dst, frames[f], (size_t)m * 4 * sizeof(double));
+    else for (int64_t i = 0; i < m; ++i) std::memcpy(dst + 4 * i, frames[f] + i * ld, 4 * sizeof(double));
+  }
+  {
+    TimedRegion tr(c, &c->main_ev, c->stream);
+    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
+    hipLaunchKernelGGL(k_align_host_f64, dim3(grid), dim3(kBlock), 0, c->stream, pin_in, n, (int64_t)4, d_doff, F,
+                       d_pose, pin_out);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int32_t f = 0; f < F; ++f)
+    if (counts[f]) std::memcpy(outs[f], pin_out + 4 * doff[f], (size_t)counts[f] * 4 * sizeof(double));
   return MC_OK;
 }
 

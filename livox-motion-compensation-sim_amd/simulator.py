@@ -21,11 +21,12 @@ from __future__ import annotations
 
 import os
 from collections import OrderedDict
-from ctypes import c_double
+from ctypes import c_double, c_int64
 from typing import Dict, List, Optional
 
 import numpy as np
 
+from . import _lib
 from . import codecs as _codecs
 from . import config as _config
 from . import trajectory as _traj
@@ -121,15 +122,29 @@ class LiDARMotionSimulator:
             return []
         rot = np.stack([np.asarray(t["rotation"], np.float64).reshape(3) for t in transformations])
         trans = np.stack([np.asarray(t["translation"], np.float64).reshape(3) for t in transformations])
-        counts = np.array([f.shape[0] for f in frames], np.int64)
-        if counts.sum() == 0:
+        if sum(f.shape[0] for f in frames) == 0:
             return [np.zeros((0, 4)) for _ in frames]
+        self.context.set_trajectory(np.arange(len(frames), dtype=np.float64), trans, rot)
+        return self._align_host(frames, None, _lib.MC_POSE_DIRECT)
+
+    def _align_host(self, frames, times, pose_select) -> List[np.ndarray]:
+        """Host arrays in, host arrays out: one float64 launch over all frames on pinned,
+        device-mapped memory (mc_align_frames_host_f64); poses from the uploaded trajectory."""
         ctx = self.context
-        bin_, bout = self._io_batches(counts)
-        ctx.set_trajectory(np.arange(len(frames), dtype=np.float64), trans, rot)
-        bin_.upload_aos(_stack_aos(frames))
-        ctx.deskew(bin_, bout, mode="frame", pose_select="direct")
-        return bout.split(bout.download_aos())
+        src = [f if f.dtype == np.float64 and f.flags.c_contiguous else np.ascontiguousarray(f, dtype=np.float64)
+               for f in frames]
+        F = len(src)
+        counts = np.fromiter((f.shape[0] for f in src), np.int64, F)
+        lds = np.fromiter((f.shape[1] for f in src), np.int64, F)
+        offs = np.concatenate([[0], np.cumsum(counts)])
+        out = np.empty((int(offs[-1]), 4))                     # one allocation; frames are views
+        fp = np.fromiter((f.__array_interface__["data"][0] for f in src), np.uintp, F)
+        op = (out.__array_interface__["data"][0] + 32 * offs[:-1]).astype(np.uintp)
+        t = None if times is None else np.ascontiguousarray(times, dtype=np.float64)
+        check(ctx.lib.mc_align_frames_host_f64(ctx.handle, F, fp.ctypes.data, ptr(counts, c_int64),
+                                               ptr(lds, c_int64), ptr(t, c_double), pose_select, op.ctypes.data),
+              "align_frames")
+        return [out[offs[f]:offs[f + 1]] for f in range(F)]
 
     def run_alignment(self, scans: List[np.ndarray], trajectory: dict,
                       times: Optional[np.ndarray] = None) -> List[np.ndarray]:
@@ -142,16 +157,10 @@ class LiDARMotionSimulator:
         if len(times) != len(scans):
             raise ValueError("one frame time per scan expected")
         scans = [self._check_points(s) for s in scans]
-        counts = np.array([s.shape[0] for s in scans], np.int64)
-        if not scans or counts.sum() == 0:
+        if not scans or sum(s.shape[0] for s in scans) == 0:
             return [np.zeros((0, 4)) for _ in scans]
-        ctx = self.context
-        bin_, bout = self._io_batches(counts)
-        ctx.set_trajectory(trajectory["time"], trajectory["position_gps"], trajectory["orientation_imu"])
-        bin_.set_frame_times(times)
-        bin_.upload_aos(_stack_aos(scans))
-        ctx.deskew(bin_, bout, mode="frame", pose_select="searchsorted")
-        return bout.split(bout.download_aos())
+        self.context.set_trajectory(trajectory["time"], trajectory["position_gps"], trajectory["orientation_imu"])
+        return self._align_host(scans, times, _lib.MC_POSE_SEARCHSORTED)
 
     def deskew_frames(self, frames: List[np.ndarray], t_ns: List[np.ndarray], trajectory: dict,
                       times: Optional[np.ndarray] = None) -> List[np.ndarray]:

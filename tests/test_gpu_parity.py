@@ -399,3 +399,34 @@ def test_device_stager_roundtrip(mc, gpu_ctx):
     assert np.array_equal(b3.download_aos(), aos)
     with pytest.raises(IndexError):
         b3.stage_aos_device(buf6, ld=3)
+
+
+def test_host_array_paths_zero_copy_and_pipeline(mc, gpu_ctx):
+    """transform_pointcloud / align_frames / run_alignment on host arrays: the zero-copy kernels
+    below 32k rows and the chunked DMA pipeline above (1M-row chunks), ragged frames, empty
+    frames, wider rows, float64 results against the oracle."""
+    rng = np.random.default_rng(12)
+    sim = mc.LiDARMotionSimulator(dict(CFGS["urban_complex"]), context=gpu_ctx)
+    for n in (5, 40_000, 1_300_000):
+        pts = np.column_stack([rng.normal(0, 50, (n, 3)), rng.uniform(0, 1, n), rng.normal(0, 1, n)])
+        pose = {"translation": rng.normal(0, 500, 3), "rotation": rng.uniform(-np.pi, np.pi, 3)}
+        out = sim.transform_pointcloud(pts, pose)
+        ref = R.transform_pointcloud(pts, pose)
+        np.testing.assert_allclose(out, ref, rtol=0, atol=1e-9 * (1 + np.abs(ref).max()))
+        assert np.array_equal(out[:, 3], pts[:, 3])
+    tr = traj_of("urban_complex")
+    sizes = [0, 17, 300_000, 0, 1_100_001, 5, 900_000, 64]
+    scans = [np.column_stack([rng.normal(0, 40, (m, 3)), rng.uniform(0, 1, m)] +
+                             ([rng.normal(0, 1, (m, 2))] if i % 3 == 1 else [])) for i, m in enumerate(sizes)]
+    times = np.linspace(0, 119.9, len(sizes))
+    got = sim.run_alignment(scans, tr, times)
+    ref = R.align_frames(scans, tr, times)
+    for g, r, s in zip(got, ref, scans):
+        assert g.shape == r.shape
+        if len(r):
+            np.testing.assert_allclose(g, r, rtol=0, atol=1e-9 * (1 + np.abs(r).max()))
+            assert np.array_equal(g[:, 3], s[:, 3])
+    small = [s[:50] for s in scans]
+    poses = [{"translation": rng.normal(0, 100, 3), "rotation": rng.uniform(-1, 1, 3)} for _ in small]
+    for g, s, p in zip(sim.align_frames(small, poses), small, poses):
+        np.testing.assert_allclose(g, R.transform_pointcloud(s, p), rtol=0, atol=1e-9)
