@@ -38,11 +38,11 @@
  *    mc_deskew is asynchronous (mc_sync() waits for it).
  *  - One context per thread and device.
  *
- * Device layout of a batch ("padded CSR"): n_frames ragged
- * frames; frame f holds count[f] points stored at [poff[f], poff[f]+count[f])
- * of five columns x, y, z, intensity (float32) and t_ns (int32, nanoseconds
- * since the frame start); poff[f] is a multiple of 4 so every frame starts
- * 16-byte aligned.
+ * Device layout of a batch ("blocked CSR"): n_frames ragged
+ * frames; frame f holds count[f] points at padded indices [poff[f], poff[f]+count[f]);
+ * poff[f] is a multiple of 256, so every frame starts on a block.  Block k holds
+ * points 256k..256k+255 as C runs of 256 values: x, y, z, intensity (float32) and,
+ * with MC_BATCH_WITH_TIME, t_ns (int32, nanoseconds since the frame start).
  */
 #ifndef MCDESKEW_H_
 #define MCDESKEW_H_
@@ -217,7 +217,7 @@ int mc_set_launch(mc_ctx* ctx, int32_t max_grid);
 int mc_comm_unique_id(char id_out[128]);
 int mc_comm_init(mc_ctx* ctx, int nranks, int rank, const char id[128], mc_comm** out);
 int mc_comm_destroy(mc_comm* comm);
-/* ragged gather of every rank's batch columns (x,y,z,intensity, padded layout) into `merged`
+/* ragged gather of every rank's batch columns (x,y,z,intensity; blocked layout) into `merged`
  * on `root`, in rank order (== np.vstack of the frame-ordered shards).  `merged` is ignored on
  * non-root ranks and on root must have been created with the concatenated frame counts. */
 int mc_comm_gather_batch(mc_comm* comm, const mc_batch* local, int root, mc_batch* merged);

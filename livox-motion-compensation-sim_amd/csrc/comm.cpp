@@ -2,8 +2,11 @@
 //
 // The reference concatenates the frame-ordered aligned clouds with np.vstack (LMC:887-889).
 // Frames shard across ranks as contiguous, point-balanced ranges, so the merged cloud is the
-// rank-ordered concatenation of every rank's (padded-CSR) columns: one ragged gather to root,
-// written as grouped ncclSend/ncclRecv per column (no reduction collective is involved).
+// rank-ordered concatenation of every rank's blocked columns (frames start on 256-point block
+// boundaries, so a rank's shard is one contiguous run of blocks): one ragged gather to root, one
+// grouped ncclSend/ncclRecv per rank (no reduction collective is involved).  A shard whose
+// column count differs from the merged batch's (t_ns carried on one side only) lands in a
+// staging area and is re-pitched block by block with one 2-D copy.
 // librccl is dlopen'ed on first use so the core library loads without it.
 #include "../../include/mcdeskew.h"
 #include "internal.hpp"
@@ -69,7 +72,9 @@ struct mc_comm {
   mc_ctx* ctx = nullptr;
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
-  int64_t* d_scratch = nullptr;  // nranks int64 for the padded-size allgather
+  int64_t* d_scratch = nullptr;  // 2 (nranks + 1) int64 for the (padded size, columns) allgather
+  float* d_stage = nullptr;      // root: shards whose column count differs from the merged batch
+  int64_t stage_cap = 0;
   double* d_red = nullptr;       // reduction buffer
   int64_t red_cap = 0;
 };
@@ -110,7 +115,7 @@ int mc_comm_init(mc_ctx* ctx, int nranks, int rank, const char id_in[128], mc_co
   c->rank = rank;
   ncclResult_t r = g_rccl.CommInitRank(&c->comm, nranks, id, rank);
   if (r != ncclSuccess) { delete c; return fail(MC_ERR_COMM, "ncclCommInitRank: %s", g_rccl.GetErrorString(r)); }
-  if (hipMalloc(&c->d_scratch, sizeof(int64_t) * (nranks + 1)) != hipSuccess) {
+  if (hipMalloc(&c->d_scratch, sizeof(int64_t) * 2 * (nranks + 1)) != hipSuccess) {
     g_rccl.CommDestroy(c->comm);
     delete c;
     return fail(MC_ERR_NOMEM, "hipMalloc failed");
@@ -126,6 +131,7 @@ int mc_comm_destroy(mc_comm* c) {
   if (c->comm) g_rccl.CommDestroy(c->comm);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
   if (c->d_red) (void)hipFree(c->d_red);
+  if (c->d_stage) (void)hipFree(c->d_stage);
   delete c;
   return MC_OK;
 }
@@ -136,45 +142,70 @@ int mc_comm_gather_batch(mc_comm* c, const mc_batch* local, int root, mc_batch* 
   if (local->ctx != c->ctx) return fail(MC_ERR_INVALID, "batch belongs to another context");
   HIPCHK(hipSetDevice(c->ctx->device));
   hipStream_t s = c->ctx->stream;
-  // every rank's padded length (the merged layout is the rank-ordered concatenation)
-  int64_t mine = local->P;
-  HIPCHK(hipMemcpyAsync(c->d_scratch + c->nranks, &mine, sizeof(int64_t), hipMemcpyHostToDevice, s));
-  NCCLCHK(g_rccl.AllGather(c->d_scratch + c->nranks, c->d_scratch, 1, ncclInt64, c->comm, s));
-  std::vector<int64_t> P(c->nranks);
-  HIPCHK(hipMemcpyAsync(P.data(), c->d_scratch, sizeof(int64_t) * c->nranks, hipMemcpyDeviceToHost, s));
+  // every rank's padded length and column count (the merged layout is the rank-ordered concatenation)
+  const int64_t mine[2] = {local->P, local->C};
+  HIPCHK(hipMemcpyAsync(c->d_scratch + 2 * c->nranks, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+  NCCLCHK(g_rccl.AllGather(c->d_scratch + 2 * c->nranks, c->d_scratch, 2, ncclInt64, c->comm, s));
+  std::vector<int64_t> PC(2 * c->nranks);
+  HIPCHK(hipMemcpyAsync(PC.data(), c->d_scratch, sizeof(int64_t) * 2 * c->nranks, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (c->rank == root) {
-    if (!merged) return fail(MC_ERR_INVALID, "root needs a merged batch");
-    int64_t tot = 0;
-    for (int64_t v : P) tot += v;
-    if (tot != merged->P)
-      return fail(MC_ERR_INVALID, "merged batch holds %lld padded points, ranks sent %lld", (long long)merged->P,
-                  (long long)tot);
-  }
-  NCCLCHK(g_rccl.GroupStart());
-  if (c->rank == root) {
-    int64_t off = 0;
-    for (int q = 0; q < c->nranks; ++q) {
-      for (int col = 0; col < 4; ++col) {
-        float* dst = merged->d_cols + col * merged->cap + off;
-        if (P[q] == 0) continue;
-        if (q == root) {
-          if (hipMemcpyAsync(dst, local->d_cols + col * local->cap, P[q] * sizeof(float), hipMemcpyDeviceToDevice, s) !=
-              hipSuccess) {
-            g_rccl.GroupEnd();
-            return fail(MC_ERR_HIP, "local copy failed");
-          }
-        } else {
-          NCCLCHK(g_rccl.Recv(dst, (size_t)P[q], ncclFloat32, q, c->comm, s));
-        }
-      }
-      off += P[q];
+  auto P = [&](int q) { return PC[2 * q]; };
+  auto C = [&](int q) { return PC[2 * q + 1]; };
+  if (c->rank != root) {
+    if (local->P > 0) {
+      NCCLCHK(g_rccl.GroupStart());
+      NCCLCHK(g_rccl.Send(local->d_cols, (size_t)(local->C * local->P), ncclFloat32, root, c->comm, s));
+      NCCLCHK(g_rccl.GroupEnd());
     }
-  } else if (local->P > 0) {
-    for (int col = 0; col < 4; ++col)
-      NCCLCHK(g_rccl.Send(local->d_cols + col * local->cap, (size_t)local->P, ncclFloat32, root, c->comm, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MC_OK;
+  }
+  if (!merged) return fail(MC_ERR_INVALID, "root needs a merged batch");
+  int64_t tot = 0, staged = 0;
+  for (int q = 0; q < c->nranks; ++q) {
+    tot += P(q);
+    if (q != root && C(q) != merged->C) staged += C(q) * P(q);
+  }
+  if (tot != merged->P)
+    return fail(MC_ERR_INVALID, "merged batch holds %lld padded points, ranks sent %lld", (long long)merged->P,
+                (long long)tot);
+  if (staged > c->stage_cap) {
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    c->d_stage = nullptr;
+    c->stage_cap = 0;
+    HIPCHK(hipMalloc(&c->d_stage, staged * sizeof(float)));
+    c->stage_cap = staged;
+  }
+  // copy the first min(C) columns of every block of a shard into the merged batch at `off`
+  auto repitch = [&](const float* src, int64_t cs, int64_t np, int64_t off) {
+    const int64_t cm = merged->C, w = std::min(cs, cm);
+    return hipMemcpy2DAsync(merged->d_cols + off * cm, (size_t)(cm * mcimpl::kBatchBlock * sizeof(float)), src,
+                            (size_t)(cs * mcimpl::kBatchBlock * sizeof(float)), (size_t)(w * mcimpl::kBatchBlock * sizeof(float)),
+                            (size_t)(np / mcimpl::kBatchBlock), hipMemcpyDeviceToDevice, s);
+  };
+  std::vector<int64_t> off(c->nranks), soff(c->nranks, -1);
+  NCCLCHK(g_rccl.GroupStart());
+  for (int64_t q = 0, o = 0, so = 0; q < c->nranks; o += P(q), ++q) {
+    off[q] = o;
+    if (q == root || P(q) == 0) continue;
+    float* dst = merged->d_cols + o * merged->C;   // o is a multiple of kBatchBlock
+    if (C(q) != merged->C) {
+      dst = c->d_stage + so;
+      soff[q] = so;
+      so += C(q) * P(q);
+    }
+    NCCLCHK(g_rccl.Recv(dst, (size_t)(C(q) * P(q)), ncclFloat32, (int)q, c->comm, s));
   }
   NCCLCHK(g_rccl.GroupEnd());
+  if (P(root) > 0) {
+    if (local->C == merged->C)
+      HIPCHK(hipMemcpyAsync(merged->d_cols + off[root] * merged->C, local->d_cols,
+                            (size_t)(local->C * local->P) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    else
+      HIPCHK(repitch(local->d_cols, local->C, local->P, off[root]));
+  }
+  for (int q = 0; q < c->nranks; ++q)
+    if (soff[q] >= 0) HIPCHK(repitch(c->d_stage + soff[q], C(q), P(q), off[q]));
   HIPCHK(hipStreamSynchronize(s));
   return MC_OK;
 }

@@ -22,6 +22,7 @@ struct FrameWin;
 
 namespace mcimpl {
 int fail(int code, const char* fmt, ...);
+constexpr int64_t kBatchBlock = 256;   // points per block of the blocked batch layout (= mc::kBlkPts)
 
 // Persistent host worker pool for the host-side row copies of the host<->device pipeline.
 class HostPool {
@@ -133,12 +134,14 @@ struct mc_batch {
   mc_ctx* ctx = nullptr;
   int32_t F = 0;
   int64_t N = 0;    // valid points
-  int64_t P = 0;    // padded points (poff[F])
-  int64_t cap = 0;  // column stride (>= P, multiple of 64)
+  int64_t P = 0;    // padded points (poff[F]; every frame starts on a kBlkPts boundary)
+  int32_t C = 4;    // columns per block: x | y | z | intensity [| t_ns]
   std::vector<int64_t> counts, poff, doff;
   int32_t n_tiles = 0;
-  float* d_cols = nullptr;    // x | y | z | intensity, each `cap` floats
-  int32_t* d_t = nullptr;     // t_ns (optional)
+  // blocked columns: block k (points 256k .. 256k+255) holds its C columns of 256 values back to
+  // back, C * P values in all (mc::bidx); t_ns, when present, is column 4 (int32 bits)
+  float* d_cols = nullptr;
+  bool has_t() const { return C == 5; }
   int64_t* d_counts = nullptr;
   int64_t* d_poff = nullptr;
   int64_t* d_doff = nullptr;

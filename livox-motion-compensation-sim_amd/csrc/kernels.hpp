@@ -54,8 +54,18 @@ constexpr int kTileGroups = kBlock * kIters;   // 512 groups = 2048 points per t
 constexpr int kSub = kTileGroups / kBlock;     // per-point modes: sub-tiles of kBlock groups
 constexpr int kWinMax = 64;                    // LDS window capacity (segments per frame)
 
+// Blocked column layout ("AoSoA"): a batch is a sequence of 256-point blocks, each holding its C
+// columns (x, y, z, intensity [, t_ns]) of 256 values back to back.  A wave's float4 access to
+// one column is 1 KB contiguous, and a workgroup's whole working set is one contiguous stretch
+// of HBM instead of C streams a batch apart (+4-5 % on a 5-in / 4-out pass, tools/layout_probe.hip).
+// Frames start at multiples of kBlkPts, so tiles and frame ranges are whole blocks.
+constexpr int kBlkPts = 256;
+__host__ __device__ __forceinline__ int64_t bidx(int C, int c, int64_t p) {
+  return ((p >> 8) * C + c) * kBlkPts + (p & (kBlkPts - 1));
+}
+
 struct Tile {
-  int64_t pstart;   // padded point index of the first group (multiple of 4)
+  int64_t pstart;   // padded point index of the first group (multiple of kBlkPts)
   int32_t frame;    // frame id (uniform over the tile)
   int32_t ngroups;  // float4 groups in this tile (<= kTileGroups)
 };
@@ -95,11 +105,11 @@ struct FrameWin {
 };
 
 struct DeskewArgs {
-  const float* in;         // 4 columns x|y|z|i, stride in_cap
-  int64_t in_cap;
-  const int32_t* tns;      // t_ns column of `in` (per-point modes)
-  float* out;              // 4 columns, stride out_cap
-  int64_t out_cap;
+  const float* in;         // blocked columns x|y|z|i[|t_ns], in_C of them
+  int64_t in_C;
+  int32_t copy_t;          // per-point modes, out != in and out_C == 5: pass t_ns through (CSIM:1472)
+  float* out;              // blocked columns, out_C of them
+  int64_t out_C;
   const Tile* tiles;
   int32_t n_tiles;
   const float4* frame_tbl; // frame mode: 3 float4 per frame (R row i, t_i)
@@ -419,17 +429,19 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
     const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
     const float4 r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
     const float4 r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
-    const float* ix = a.in + tl.pstart;
-    float* ox = a.out + tl.pstart;
+    // group g of the tile: block pstart/256 + g/64, offset 4 (g % 64) inside it
+    const float* ix = a.in + bidx((int)a.in_C, 0, tl.pstart);
+    float* ox = a.out + bidx((int)a.out_C, 0, tl.pstart);
     float4 vx[kIters], vy[kIters], vz[kIters], vi[kIters];
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
       const int g = it * kBlock + threadIdx.x;
       if (g < tl.ngroups) {
-        vx[it] = ld4(ix + 4 * g);
-        vy[it] = ld4(ix + a.in_cap + 4 * g);
-        vz[it] = ld4(ix + 2 * a.in_cap + 4 * g);
-        vi[it] = ld4(ix + 3 * a.in_cap + 4 * g);
+        const float* q = ix + (int64_t)(g >> 6) * a.in_C * kBlkPts + 4 * (g & 63);
+        vx[it] = ld4(q);
+        vy[it] = ld4(q + kBlkPts);
+        vz[it] = ld4(q + 2 * kBlkPts);
+        vi[it] = ld4(q + 3 * kBlkPts);
       }
     }
 #pragma unroll
@@ -446,10 +458,11 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
         MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
 #undef MC_XF
 #undef MC_T
-        st_frame(ox + 4 * g, ox4);
-        st_frame(ox + a.out_cap + 4 * g, oy4);
-        st_frame(ox + 2 * a.out_cap + 4 * g, oz4);
-        st_frame(ox + 3 * a.out_cap + 4 * g, vi[it]);
+        float* o = ox + (int64_t)(g >> 6) * a.out_C * kBlkPts + 4 * (g & 63);
+        st_frame(o, ox4);
+        st_frame(o + kBlkPts, oy4);
+        st_frame(o + 2 * kBlkPts, oz4);
+        st_frame(o + 3 * kBlkPts, vi[it]);
       }
     }
   }
@@ -678,9 +691,10 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
   const int e_end = 4 * min(tl.ngroups, g0 + kBlock);
   for (int e = 4 * g0 + threadIdx.x; e < e_end; e += kBlock) {
     const int64_t p = tl.pstart + e;
-    float x = a.in[p], y = a.in[a.in_cap + p], z = a.in[2 * a.in_cap + p];
-    const float in = a.in[3 * a.in_cap + p];
-    const int t = a.tns[p];
+    const float* q = a.in + bidx((int)a.in_C, 0, p);
+    float x = q[0], y = q[kBlkPts], z = q[2 * kBlkPts];
+    const float in = q[3 * kBlkPts];
+    const int t = __builtin_bit_cast(int, q[4 * kBlkPts]);
     if constexpr (MODE == 1) {
       const double tf = a.frame_time[f];
       int64_t k = upper_bound(a.pose_time, a.ntab, tf + (double)t * 1e-9) - 1;
@@ -694,7 +708,9 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
       w.ts -= a.frame_start[f];
       imu_point(w, t, x, y, z);
     }
-    a.out[p] = x; a.out[a.out_cap + p] = y; a.out[2 * a.out_cap + p] = z; a.out[3 * a.out_cap + p] = in;
+    float* o = a.out + bidx((int)a.out_C, 0, p);
+    o[0] = x; o[kBlkPts] = y; o[2 * kBlkPts] = z; o[3 * kBlkPts] = in;
+    if (a.copy_t) o[4 * kBlkPts] = __builtin_bit_cast(float, t);
   }
 }
 
@@ -735,12 +751,13 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
 
     float4 X, Y, Z, I;
     int4 Tq;
+    const float* q = a.in + bidx((int)a.in_C, 0, p);   // the float4 group never straddles a block
     if (act) {
-      Tq = ld4(a.tns + p);
-      X = ld4(a.in + p);
-      Y = ld4(a.in + a.in_cap + p);
-      Z = ld4(a.in + 2 * a.in_cap + p);
-      I = ld4(a.in + 3 * a.in_cap + p);
+      Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts));
+      X = ld4(q);
+      Y = ld4(q + kBlkPts);
+      Z = ld4(q + 2 * kBlkPts);
+      I = ld4(q + 3 * kBlkPts);
     }
 
     if (fw.W <= MC_FASTPATH_MAXW) {
@@ -794,10 +811,12 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
       __syncthreads();  // the LDS window is rewritten by the next sub-tile
     }
     if (act) {
-      st_points(a.out + p, X);
-      st_points(a.out + a.out_cap + p, Y);
-      st_points(a.out + 2 * a.out_cap + p, Z);
-      st_points(a.out + 3 * a.out_cap + p, I);
+      float* o = a.out + bidx((int)a.out_C, 0, p);
+      st_points(o, X);
+      st_points(o + kBlkPts, Y);
+      st_points(o + 2 * kBlkPts, Z);
+      st_points(o + 3 * kBlkPts, I);
+      if (a.copy_t) st_points(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
     }
   }
 }
@@ -808,7 +827,11 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
 struct LayoutArgs {
   const Tile* tiles; int32_t n_tiles;
   const int64_t* poff; const int64_t* doff; const int64_t* counts;
-  float* cols; int64_t cap; int32_t* tns;
+  float* cols; int32_t C;   // blocked columns x|y|z|i[|t_ns]; C == 5 carries the t_ns column
+  __device__ __forceinline__ float& col(int c, int64_t p) const { return cols[bidx(C, c, p)]; }
+  __device__ __forceinline__ int32_t& tns(int64_t p) const {
+    return reinterpret_cast<int32_t*>(cols)[bidx(C, 4, p)];
+  }
 };
 
 // per element of the padded layout: its frame-local index, or -1 for a padding slot
@@ -847,21 +870,22 @@ __device__ __forceinline__ void stage_tile_lds_in(const LayoutArgs& a, const Til
     s[2 * h + 1][j] = (float)v.y;
   }
   __syncthreads();
-  float* cx = a.cols + tl.pstart;
+  float* cx = a.cols + bidx(a.C, 0, tl.pstart);
   for (int g = threadIdx.x; g < tl.ngroups; g += kBlock)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      st_pol<MC_STAGE_ST>(cx + c * a.cap + 4 * g, *reinterpret_cast<const float4*>(&s[c][4 * g]));
+      st_pol<MC_STAGE_ST>(cx + ((g >> 6) * a.C + c) * kBlkPts + 4 * (g & 63),
+                          *reinterpret_cast<const float4*>(&s[c][4 * g]));
   __syncthreads();
 }
 
 __device__ __forceinline__ void stage_tile_lds_out(const LayoutArgs& a, const Tile& tl, v2d* __restrict__ d2, int nv,
                                                    float (*s)[kStageRow]) {
-  const float* cx = a.cols + tl.pstart;
+  const float* cx = a.cols + bidx(a.C, 0, tl.pstart);
   for (int g = threadIdx.x; g < (nv + 3) / 4; g += kBlock)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      *reinterpret_cast<float4*>(&s[c][4 * g]) = ld4(cx + c * a.cap + 4 * g);
+      *reinterpret_cast<float4*>(&s[c][4 * g]) = ld4(cx + ((g >> 6) * a.C + c) * kBlkPts + 4 * (g & 63));
   __syncthreads();
   for (int q = threadIdx.x; q < 2 * nv; q += kBlock) {
     const int j = q >> 1, h = q & 1;
@@ -893,7 +917,6 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
     const int np = 4 * tl.ngroups;                                      // padded points in the tile
     const int nv = (int)max<int64_t>(0, min<int64_t>(np, cnt - loc0)); // valid ones
     const double* src = aos + (doff + loc0) * ld;
-    float* cx = a.cols + tl.pstart;
     if (ld == 4) {
       const v2d* s2 = reinterpret_cast<const v2d*>(src);
       for (int q0 = 0; q0 < 2 * np; q0 += kStageUnroll * kBlock) {
@@ -909,8 +932,8 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
           const int q = q0 + u * kBlock + threadIdx.x;
           if (q < 2 * np) {
             const int j = q >> 1, h = q & 1;               // point j, half h: (x,y) or (z,i)
-            cx[(2 * h) * a.cap + j] = (float)v[u].x;
-            cx[(2 * h + 1) * a.cap + j] = (float)v[u].y;
+            a.col(2 * h, tl.pstart + j) = (float)v[u].x;
+            a.col(2 * h + 1, tl.pstart + j) = (float)v[u].y;
           }
         }
       }
@@ -919,7 +942,7 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
         float r[4] = {0.f, 0.f, 0.f, 0.f};
         if (j < nv)
           for (int c = 0; c < 4; ++c) r[c] = (float)src[(int64_t)j * ld + c];
-        for (int c = 0; c < 4; ++c) cx[c * a.cap + j] = r[c];
+        for (int c = 0; c < 4; ++c) a.col(c, tl.pstart + j) = r[c];
       }
     }
   }
@@ -944,7 +967,6 @@ __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, doubl
     const int64_t loc0 = tl.pstart - poff;
     const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
     v2d* d2 = reinterpret_cast<v2d*>(aos + (doff + loc0) * 4);
-    const float* cx = a.cols + tl.pstart;
     for (int q0 = 0; q0 < 2 * nv; q0 += kStageUnroll * kBlock) {
       v2d v[kStageUnroll];
 #pragma unroll
@@ -952,8 +974,8 @@ __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, doubl
         const int q = q0 + u * kBlock + threadIdx.x;
         if (q < 2 * nv) {
           const int j = q >> 1, h = q & 1;
-          v[u] = v2d{(double)__builtin_nontemporal_load(cx + (2 * h) * a.cap + j),
-                     (double)__builtin_nontemporal_load(cx + (2 * h + 1) * a.cap + j)};
+          v[u] = v2d{(double)__builtin_nontemporal_load(&a.col(2 * h, tl.pstart + j)),
+                     (double)__builtin_nontemporal_load(&a.col(2 * h + 1, tl.pstart + j))};
         }
       }
 #pragma unroll
@@ -965,17 +987,19 @@ __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, doubl
   }
 }
 
-// dense column (N) <-> padded column; DIR 0: dense->padded (padding zeroed), 1: padded->dense
+// dense column (N) <-> blocked column c; DIR 0: dense->blocked (padding zeroed), 1: blocked->dense
 template <typename T, int DIR>
-__global__ __launch_bounds__(kBlock) void k_column(const LayoutArgs a, const T* __restrict__ src, T* __restrict__ dst) {
+__global__ __launch_bounds__(kBlock) void k_column(const LayoutArgs a, int c, const T* __restrict__ src,
+                                                   T* __restrict__ dst) {
+  T* colv = reinterpret_cast<T*>(a.cols);
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = a.tiles[tile];
     const int64_t d0 = a.doff[tl.frame];
     for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
       const int64_t p = tl.pstart + e;
       const int64_t i = local_index(a, tl, p);
-      if (DIR == 0) dst[p] = i >= 0 ? src[d0 + i] : T(0);
-      else if (i >= 0) dst[d0 + i] = src[p];
+      if (DIR == 0) colv[bidx(a.C, c, p)] = i >= 0 ? src[d0 + i] : T(0);
+      else if (i >= 0) dst[d0 + i] = colv[bidx(a.C, c, p)];
     }
   }
 }
@@ -992,7 +1016,7 @@ __global__ __launch_bounds__(kBlock) void k_trange(const LayoutArgs a, int2* tr)
     for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
       const int64_t p = tl.pstart + e;
       if (local_index(a, tl, p) >= 0) {
-        const int t = a.tns[p];
+        const int t = a.tns(p);
         lo = min(lo, t);
         hi = max(hi, t);
       }
@@ -1041,8 +1065,8 @@ __global__ __launch_bounds__(kBlock) void k_synth(const LayoutArgs a, uint64_t s
         in = u3;
         t = (int32_t)((i * 100000000ll) / n);                  // spread over the 0.1 s frame
       }
-      a.cols[p] = x; a.cols[a.cap + p] = y; a.cols[2 * a.cap + p] = z; a.cols[3 * a.cap + p] = in;
-      if (a.tns) a.tns[p] = t;
+      a.col(0, p) = x; a.col(1, p) = y; a.col(2, p) = z; a.col(3, p) = in;
+      if (a.C == 5) a.tns(p) = t;
     }
   }
 }
@@ -1056,8 +1080,8 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const LayoutArgs a, double*
     for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
       const int64_t p = tl.pstart + e;
       if (local_index(a, tl, p) >= 0) {
-        for (int c = 0; c < 4; ++c) acc[c] += (double)a.cols[c * a.cap + p];
-        if (a.tns) acc[4] += (double)a.tns[p];
+        for (int c = 0; c < 4; ++c) acc[c] += (double)a.col(c, p);
+        if (a.C == 5) acc[4] += (double)a.tns(p);
       }
     }
     for (int c = 0; c < 5; ++c) s[c][threadIdx.x] = acc[c];

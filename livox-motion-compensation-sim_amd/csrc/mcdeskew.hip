@@ -41,33 +41,35 @@ static int launch_grid(const mc_ctx* c, int32_t n_tiles) {
   return g < 1 ? 1 : g;
 }
 
+static_assert(mcimpl::kBatchBlock == kBlkPts, "batch block size");
+
 static LayoutArgs layout_of(const mc_batch* b) {
   LayoutArgs a;
   a.tiles = b->d_tiles; a.n_tiles = b->n_tiles;
   a.poff = b->d_poff; a.doff = b->d_doff; a.counts = b->d_counts;
-  a.cols = b->d_cols; a.cap = b->cap; a.tns = b->d_t;
+  a.cols = b->d_cols; a.C = b->C;
   return a;
 }
 
 template <typename T>
-static int upload_column(mc_batch* b, const T* src, T* dst_col) {
+static int upload_column(mc_batch* b, const T* src, int col) {
   mc_ctx* c = b->ctx;
   void* st = nullptr;
   if (int r = ctx_stage(c, (size_t)b->N * sizeof(T), &st)) return r;
   HIPCHK(hipMemcpyAsync(st, src, (size_t)b->N * sizeof(T), hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL((k_column<T, 0>), dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
-                     layout_of(b), static_cast<const T*>(st), dst_col);
+                     layout_of(b), col, static_cast<const T*>(st), static_cast<T*>(nullptr));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return MC_OK;
 }
 template <typename T>
-static int download_column(mc_batch* b, const T* src_col, T* dst) {
+static int download_column(mc_batch* b, int col, T* dst) {
   mc_ctx* c = b->ctx;
   void* st = nullptr;
   if (int r = ctx_stage(c, (size_t)b->N * sizeof(T), &st)) return r;
   hipLaunchKernelGGL((k_column<T, 1>), dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
-                     layout_of(b), src_col, static_cast<T*>(st));
+                     layout_of(b), col, static_cast<const T*>(nullptr), static_cast<T*>(st));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(dst, st, (size_t)b->N * sizeof(T), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -77,7 +79,7 @@ static int download_column(mc_batch* b, const T* src_col, T* dst) {
 // per-frame t_ns span, recomputed whenever the t column is written (staging time, not per step)
 static int compute_trange(mc_batch* b) {
   mc_ctx* c = b->ctx;
-  if (b->F == 0 || !b->d_t) { b->trange_valid = true; return MC_OK; }
+  if (b->F == 0 || !b->has_t()) { b->trange_valid = true; return MC_OK; }
   hipLaunchKernelGGL(k_trange_init, dim3((b->F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, b->d_trange, b->F);
   if (b->n_tiles > 0)
     hipLaunchKernelGGL(k_trange, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
@@ -237,7 +239,7 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
     if (b->counts[f] < 0) { delete b; return fail(MC_ERR_INVALID, "frame %d has a negative count", f); }
     const int64_t groups = (b->counts[f] + 3) / 4;
     b->doff[f + 1] = b->doff[f] + b->counts[f];
-    b->poff[f + 1] = b->poff[f] + 4 * groups;
+    b->poff[f + 1] = b->poff[f] + (b->counts[f] + kBlkPts - 1) / kBlkPts * kBlkPts;
     for (int64_t g0 = 0; g0 < groups; g0 += kTileGroups) {
       Tile t;
       t.pstart = b->poff[f] + 4 * g0;
@@ -249,14 +251,13 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
   if (tiles.size() > (size_t)INT32_MAX) { delete b; return fail(MC_ERR_INVALID, "too many tiles"); }
   b->N = b->doff[F];
   b->P = b->poff[F];
-  b->cap = ((b->P + 63) / 64) * 64;
+  b->C = (flags & MC_BATCH_WITH_TIME) ? 5 : 4;
+  const size_t col_vals = (size_t)b->C * (size_t)std::max<int64_t>(b->P, kBlkPts);
   b->n_tiles = (int32_t)tiles.size();
   DeviceGuard g(c->device);
   int r = MC_OK;
   auto bail = [&](int code) { mc_batch_destroy(b); return code; };
-  if ((r = dev_alloc(&b->d_cols, 4 * (size_t)std::max<int64_t>(b->cap, 64)))) return bail(r);
-  if (flags & MC_BATCH_WITH_TIME)
-    if ((r = dev_alloc(&b->d_t, (size_t)std::max<int64_t>(b->cap, 64)))) return bail(r);
+  if ((r = dev_alloc(&b->d_cols, col_vals))) return bail(r);
   if ((r = dev_alloc(&b->d_counts, F + 1))) return bail(r);
   if ((r = dev_alloc(&b->d_poff, F + 1))) return bail(r);
   if ((r = dev_alloc(&b->d_doff, F + 1))) return bail(r);
@@ -281,9 +282,7 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
       return bail(fail(MC_ERR_HIP, "tile table upload failed"));
   }
   // zero the columns so padding slots are defined even before the first upload
-  if (hipMemsetAsync(b->d_cols, 0, 4 * (size_t)std::max<int64_t>(b->cap, 64) * sizeof(float), s) != hipSuccess)
-    return bail(fail(MC_ERR_HIP, "memset failed"));
-  if (b->d_t && hipMemsetAsync(b->d_t, 0, (size_t)std::max<int64_t>(b->cap, 64) * sizeof(int32_t), s) != hipSuccess)
+  if (hipMemsetAsync(b->d_cols, 0, col_vals * sizeof(float), s) != hipSuccess)
     return bail(fail(MC_ERR_HIP, "memset failed"));
   if (hipStreamSynchronize(s) != hipSuccess) return bail(fail(MC_ERR_HIP, "sync failed"));
   *out = b;
@@ -294,7 +293,7 @@ int mc_batch_destroy(mc_batch* b) {
   if (!b) return MC_OK;
   DeviceGuard g(b->ctx->device);
   (void)sync_all(b->ctx);
-  dev_free(b->d_cols); dev_free(b->d_t); dev_free(b->d_counts); dev_free(b->d_poff); dev_free(b->d_doff);
+  dev_free(b->d_cols); dev_free(b->d_counts); dev_free(b->d_poff); dev_free(b->d_doff);
   dev_free(b->d_tiles); dev_free(b->d_frame_time); dev_free(b->d_frame_start); dev_free(b->d_frame_tbl);
   dev_free(b->d_trange); dev_free(b->d_fwin); dev_free(b->d_partial);
   if (b->d_frec) (void)hipFree(b->d_frec);
@@ -440,17 +439,17 @@ int mc_batch_upload_columns_f32(mc_batch* b, const float* x, const float* y, con
   const float* src[4] = {x, y, z, in};
   for (int k = 0; k < 4; ++k)
     if (src[k])
-      if (int r = upload_column<float>(b, src[k], b->d_cols + k * b->cap)) return r;
+      if (int r = upload_column<float>(b, src[k], k)) return r;
   return MC_OK;
 }
 
 int mc_batch_upload_time_ns(mc_batch* b, const int32_t* t) {
   CHECK_ARG(b, "batch is NULL");
-  if (!b->d_t) return fail(MC_ERR_STATE, "batch was created without MC_BATCH_WITH_TIME");
+  if (!b->has_t()) return fail(MC_ERR_STATE, "batch was created without MC_BATCH_WITH_TIME");
   if (b->N == 0) return MC_OK;
   CHECK_ARG(t, "t_ns is NULL");
   DeviceGuard g(b->ctx->device);
-  if (int r = upload_column<int32_t>(b, t, b->d_t)) return r;
+  if (int r = upload_column<int32_t>(b, t, 4)) return r;
   if (int r = compute_trange(b)) return r;
   HIPCHK(hipStreamSynchronize(b->ctx->stream));
   return MC_OK;
@@ -477,17 +476,17 @@ int mc_batch_download_columns_f32(mc_batch* b, float* x, float* y, float* z, flo
   float* dst[4] = {x, y, z, in};
   for (int k = 0; k < 4; ++k)
     if (dst[k])
-      if (int r = download_column<float>(b, b->d_cols + k * b->cap, dst[k])) return r;
+      if (int r = download_column<float>(b, k, dst[k])) return r;
   return MC_OK;
 }
 
 int mc_batch_download_time_ns(mc_batch* b, int32_t* t) {
   CHECK_ARG(b, "batch is NULL");
-  if (!b->d_t) return fail(MC_ERR_STATE, "batch was created without MC_BATCH_WITH_TIME");
+  if (!b->has_t()) return fail(MC_ERR_STATE, "batch was created without MC_BATCH_WITH_TIME");
   if (b->N == 0) return MC_OK;
   CHECK_ARG(t, "t_ns is NULL");
   DeviceGuard g(b->ctx->device);
-  return download_column<int32_t>(b, b->d_t, t);
+  return download_column<int32_t>(b, 4, t);
 }
 
 int mc_batch_synth(mc_batch* b, uint64_t seed, int64_t frame_id_base) {
@@ -538,11 +537,11 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   } else if (mode == MC_MODE_POSE_SLERP) {
     if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
     if (!in->has_times) return fail(MC_ERR_STATE, "frame times not set (mc_batch_set_frame_times)");
-    if (!in->d_t) return fail(MC_ERR_STATE, "input batch has no t_ns column");
+    if (!in->has_t()) return fail(MC_ERR_STATE, "input batch has no t_ns column");
   } else {
     if (c->M < 1) return fail(MC_ERR_STATE, "no IMU samples uploaded (mc_set_imu)");
     if (!in->has_starts) return fail(MC_ERR_STATE, "frame start times not set (mc_batch_set_frame_start_ns)");
-    if (!in->d_t) return fail(MC_ERR_STATE, "input batch has no t_ns column");
+    if (!in->has_t()) return fail(MC_ERR_STATE, "input batch has no t_ns column");
   }
   if (in->F == 0) return MC_OK;
   DeviceGuard g(c->device);
@@ -596,8 +595,10 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
 
   DeskewArgs da;
   std::memset(&da, 0, sizeof(da));
-  da.in = in->d_cols; da.in_cap = in->cap; da.tns = in->d_t;
-  da.out = out->d_cols; da.out_cap = out->cap;
+  da.in = in->d_cols; da.in_C = in->C;
+  da.out = out->d_cols; da.out_C = out->C;
+  // per-point modes pass the timestamps through (CSIM:1472) when out is another batch with t_ns
+  da.copy_t = mode != MC_MODE_FRAME && out != in && out->has_t();
   da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
   da.frame_tbl = frame_tbl;
   da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start;
@@ -618,9 +619,6 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_main_done[h], s));
-  // per-point modes pass the timestamps through (CSIM:1472): copy the column when out != in
-  if (mode != MC_MODE_FRAME && out != in && out->d_t)
-    HIPCHK(hipMemcpyAsync(out->d_t, in->d_t, in->P * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
   return MC_OK;
 }
 
@@ -855,8 +853,8 @@ int mc_transform_affine(mc_ctx* c, const mc_batch* in, mc_batch* out, int32_t n_
   if (in->n_tiles > 0) {
     DeskewArgs da;
     std::memset(&da, 0, sizeof(da));
-    da.in = in->d_cols; da.in_cap = in->cap;
-    da.out = out->d_cols; da.out_cap = out->cap;
+    da.in = in->d_cols; da.in_C = in->C;
+    da.out = out->d_cols; da.out_C = out->C;
     da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
     da.frame_tbl = frame_tbl;
     const dim3 grid(launch_grid(c, in->n_tiles)), block(kBlock);
@@ -1003,7 +1001,7 @@ int mc_scan_emit(mc_ctx* c, mc_batch* out, const double* noise) {
   ea.pose = c->d_scan_pose; ea.F = out->F;
   ea.sp = make_scan_params(c->scan_par, c->scan_cap);
   ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.vis_bits = c->d_scan_bits; ea.noise = d_noise;
-  ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.cap = out->cap;
+  ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.C = out->C;
   {
     TimedRegion tr(c, &c->scan_ev, c->stream);
     hipLaunchKernelGGL(k_scan_emit, dim3(c->scan_tiles, (out->F + kScanFrames - 1) / kScanFrames), dim3(kBlock), 0,

@@ -169,7 +169,7 @@ struct ScanEmitArgs {
   const uint32_t* vis_bits;  // pass 1's visibility words
   const double* noise;       // (N_out, 3) in the batch's dense order, or nullptr
   const int64_t* poff; const int64_t* doff;
-  float* cols; int64_t cap;
+  float* cols; int32_t C;   // the output batch's blocked columns (kernels.hpp bidx)
 };
 
 __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
@@ -225,10 +225,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
           if (a.noise) { const double* q = a.noise + 3 * (doff + o); nx = q[0]; ny = q[1]; nz = q[2]; }
           const int64_t p = poff + o;
           const int64_t e = t0 + r * kBlock + threadIdx.x;
-          a.cols[p] = (float)(lx[r] + nx);
-          a.cols[a.cap + p] = (float)(ly[r] + ny);
-          a.cols[2 * a.cap + p] = (float)(lz[r] + nz);
-          a.cols[3 * a.cap + p] = (float)a.env[e * a.ld + 3];
+          float* q = a.cols + bidx(a.C, 0, p);
+          q[0] = (float)(lx[r] + nx);
+          q[kBlkPts] = (float)(ly[r] + ny);
+          q[2 * kBlkPts] = (float)(lz[r] + nz);
+          q[3 * kBlkPts] = (float)a.env[e * a.ld + 3];
         }
       }
       base += total;
