@@ -376,6 +376,10 @@ def main():
     b_in = ctx.batch(counts, with_time=True)
     b_out = ctx.batch(counts)
     b_in.synth(seed=0, frame_id_base=1000 + lo)
+    # frame mode deskews the reference's (N,4) points (LMC:772-776): no t_ns column, 4 per block
+    b_xyz = ctx.batch(counts)
+    b_xyz.synth(seed=0, frame_id_base=1000 + lo)
+    b_xyz.set_frame_times(times)
     b_in.set_frame_times(times)
     b_in.set_frame_starts((times * 1e9).astype(np.int64))
     ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
@@ -387,7 +391,7 @@ def main():
     results = {}
     for mode in modes:
         steps = args.steps if mode == args.mode else max(10, args.steps // 4)
-        wall, tm = run_mode(ctx, rdv, mode, b_in, b_out, steps, args.warmup)
+        wall, tm = run_mode(ctx, rdv, mode, b_xyz if mode == "frame" else b_in, b_out, steps, args.warmup)
         wall_max = rdv.max(wall)
         main_avg_s = tm["main_ms"] / max(tm["main_launches"], 1) / 1e3
         prep_avg_s = tm["prep_ms"] / max(tm["prep_launches"], 1) / 1e3
@@ -396,7 +400,7 @@ def main():
                          "prep_avg_us": prep_avg_s * 1e6, "achieved_GBs": achieved,
                          "value": n_rank * world * steps / wall_max / 1e6}
 
-    stager = measure_stager(ctx, b_in, b_out, n_rank, min(args.steps, 50))
+    stager = measure_stager(ctx, b_xyz, b_out, n_rank, min(args.steps, 50))
     scan = codecs = None
     if not args.no_extra_modes:
         scan = measure_scan(ctx, cfg, tr, 10, 0.0 if (args.no_cpu or world > 1) else 3.0)
@@ -407,7 +411,8 @@ def main():
     gather = None
     hung = False
     if world > 1 and not args.no_gather:
-        gather, hung = timed_gather(ctx, rdv, b_in, b_out, args.mode, n_rank, world, args.gather_timeout)
+        gather, hung = timed_gather(ctx, rdv, b_xyz if args.mode == "frame" else b_in, b_out, args.mode, n_rank,
+                                    world, args.gather_timeout)
 
     if rank == 0:
         r = results[args.mode]

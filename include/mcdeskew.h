@@ -19,7 +19,7 @@
  *                                                              mc_batch_set_frame_times +
  *                                                              mc_deskew(MC_MODE_FRAME,
  *                                                              MC_POSE_SEARCHSORTED)
- *   save_results merge (np.vstack)             LMC:887-889     padded-CSR batch layout;
+ *   save_results merge (np.vstack)             LMC:887-889     blocked-CSR batch layout;
  *                                                              mc_comm_gather_batch (multi-GPU)
  *   MotionCompensator.compensate_point_cloud   CSIM:1435-1480  mc_set_imu + mc_deskew(MC_MODE_IMU)
  *     _interpolate_imu_data                    CSIM:1482-1516    (per-point gyro LERP in-kernel)

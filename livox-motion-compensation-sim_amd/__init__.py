@@ -11,7 +11,7 @@ Drop-in surface (reference file:line in each docstring):
   LiDARPoint, IMUData    livox_mid70_complete_simulator.py:97-129
   LivoxLVXWriter, codecs lidar_motion_compensation.py:24-272, 932-948 (byte-exact LVX / PCD)
   CoordinateTransformer  livox_mid70_complete_simulator.py:145-233, 2107-2180 (coords)
-Device layer: Context, Batch (padded-CSR float32 columns in HBM); multi-GPU: dist.
+Device layer: Context, Batch (blocked-CSR float32 columns in HBM); multi-GPU: dist.
 """
 from . import _lib, codecs, config, coords, dist, runtime, trajectory  # noqa: F401
 from .coords import CoordinateSystem, CoordinateTransformer, GPSData  # noqa: F401

@@ -35,6 +35,12 @@ namespace mc {
 #ifndef MC_STORE_POINTS
 #define MC_STORE_POINTS 2    // per-point kernels output stores: sc1 write-through (see st_pol)
 #endif
+#ifndef MC_STORE_IMU
+#define MC_STORE_IMU 1       // the IMU kernel's output stores: nt (-4 % vs sc1, tools/ab.py)
+#endif
+#ifndef MC_FRAME_SLEEP
+#define MC_FRAME_SLEEP 0     // diagnostic: s_sleep between the frame kernel's loads and stores
+#endif
 #ifndef MC_FASTPATH_MAXW
 #define MC_FASTPATH_MAXW 2   // frames spanning <= this many segments take the SGPR (no-LDS) path
 #endif
@@ -163,7 +169,10 @@ __device__ __forceinline__ void st_pol(float* p, const float4& v) {
   }
 }
 __device__ __forceinline__ void st_frame(float* p, const float4& v) { st_pol<MC_STORE_FRAME>(p, v); }
-__device__ __forceinline__ void st_points(float* p, const float4& v) { st_pol<MC_STORE_POINTS>(p, v); }
+template <int MODE>
+__device__ __forceinline__ void st_points(float* p, const float4& v) {
+  st_pol<MODE == 2 ? MC_STORE_IMU : MC_STORE_POINTS>(p, v);
+}
 
 // 16-byte streaming loads of the input columns
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -444,6 +453,9 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
         vi[it] = ld4(q + 3 * kBlkPts);
       }
     }
+#if MC_FRAME_SLEEP
+    __builtin_amdgcn_s_sleep(MC_FRAME_SLEEP);
+#endif
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
       const int g = it * kBlock + threadIdx.x;
@@ -812,11 +824,11 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
     }
     if (act) {
       float* o = a.out + bidx((int)a.out_C, 0, p);
-      st_points(o, X);
-      st_points(o + kBlkPts, Y);
-      st_points(o + 2 * kBlkPts, Z);
-      st_points(o + 3 * kBlkPts, I);
-      if (a.copy_t) st_points(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
+      st_points<MODE>(o, X);
+      st_points<MODE>(o + kBlkPts, Y);
+      st_points<MODE>(o + 2 * kBlkPts, Z);
+      st_points<MODE>(o + 3 * kBlkPts, I);
+      if (a.copy_t) st_points<MODE>(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
     }
   }
 }

@@ -1,4 +1,4 @@
-"""Device context and padded-CSR frame batches — thin Python objects over the C-ABI handles.
+"""Device context and blocked-CSR frame batches — thin Python objects over the C-ABI handles.
 
 A ``Context`` is one HIP device + stream (one per process/rank, like the C-ABI's mc_ctx).  A
 ``Batch`` is a device-resident ragged batch of frames laid out as float32 columns
@@ -187,7 +187,7 @@ class DeviceBuffer:
 
 
 class Batch:
-    """Device-resident ragged frame batch (padded CSR, float32 SoA columns in HBM)."""
+    """Device-resident ragged frame batch (blocked CSR: 256-point blocks of float32 columns in HBM)."""
 
     def __init__(self, ctx: Context, counts, with_time: bool = False):
         self.ctx = ctx

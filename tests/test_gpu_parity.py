@@ -276,6 +276,40 @@ def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
         assert_scaled_close(out[f][:, :3], ref, scale_of(frames[f][:, :3], p), what=f"frame {f}")
 
 
+@pytest.mark.parametrize("mode", ["pose_slerp", "imu"])
+def test_per_point_modes_pass_t_ns_through(mc, gpu_ctx, mode):
+    """CSIM:1472 keeps each point's timestamp: out-of-place deskew into a batch with t_ns copies
+    the column from inside the kernel (fast and out-of-line paths); in place leaves it as is; the
+    result equals the in-place run and a 4-column output batch."""
+    rng = np.random.default_rng(4)
+    T = 4000
+    time = np.linspace(0, 40, T)
+    tr = {"time": time, "position_gps": np.cumsum(rng.normal(0, 0.2, (T, 3)), axis=0),
+          "orientation_imu": np.cumsum(rng.normal(0, 0.05, (T, 3)), axis=0)}
+    counts = np.array([5000, 3, 0, 1024, 70_001])
+    t_ns = np.concatenate([rng.integers(-2_000_000_000, 2_000_000_000, counts[0]),   # slow path
+                           rng.integers(0, 100_000_000, int(counts[1:].sum()))]).astype(np.int32)
+    pts = np.column_stack([rng.uniform(-90, 90, (int(counts.sum()), 3)), rng.uniform(0, 1, int(counts.sum()))])
+    b = gpu_ctx.batch(counts, with_time=True)
+    b.upload_aos(pts)
+    b.upload_time(t_ns)
+    if mode == "pose_slerp":
+        gpu_ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+        b.set_frame_times(np.array([1.0, 0.2, 5.0, 20.0, 39.0]))
+    else:
+        ts = np.arange(0, 40_000_000_000, 5_000_000, dtype=np.int64)
+        gpu_ctx.set_imu(ts, rng.normal(0, 0.3, (len(ts), 3)))
+        b.set_frame_starts(np.array([3, 1, 5, 20, 30], np.int64) * 10**9)
+    out_t = gpu_ctx.deskew(b, gpu_ctx.batch(counts, with_time=True), mode=mode)
+    out_4 = gpu_ctx.deskew(b, gpu_ctx.batch(counts), mode=mode)
+    got = out_t.download_aos()
+    assert np.array_equal(out_t.download_time(), t_ns)
+    assert np.array_equal(out_4.download_aos(), got)
+    gpu_ctx.deskew(b, b, mode=mode)
+    assert np.array_equal(b.download_aos(), got)
+    assert np.array_equal(b.download_time(), t_ns)
+
+
 def test_slerp_single_pose_table(mc, gpu_ctx):
     tr = {"time": np.array([3.0]), "position_gps": np.array([[1.0, 2.0, 3.0]]),
           "orientation_imu": np.array([[0.1, -0.2, 2.5]])}
@@ -369,6 +403,12 @@ def test_rccl_gather_single_rank(mc, gpu_ctx):
         merged = dist.gather_merged(gpu_ctx, comm, rdv, b)
         assert np.array_equal(merged.download_aos(), b.download_aos())
         assert comm.allreduce_max([1.5, -2.0]).tolist() == [1.5, -2.0]
+        # a shard carrying t_ns (5 columns per block) into a 4-column merged batch: re-pitched copy
+        bt = gpu_ctx.batch([300, 0, 70_000, 1], with_time=True)
+        bt.synth(seed=3, frame_id_base=0)
+        merged = dist.gather_merged(gpu_ctx, comm, rdv, bt)
+        assert not merged.with_time
+        assert np.array_equal(merged.download_aos(), bt.download_aos())
     finally:
         comm.close()
 

@@ -38,10 +38,13 @@ def setup(lib, args):
     b_in.synth(seed=0, frame_id_base=1000)
     b_in.set_frame_times(times)
     b_in.set_frame_starts((times * 1e9).astype(np.int64))
+    b_xyz = ctx.batch(counts)                     # frame mode: the reference's (N,4) points, no t_ns
+    b_xyz.synth(seed=0, frame_id_base=1000)
+    b_xyz.set_frame_times(times)
     ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
     ts, g = mc.trajectory.imu_from_trajectory(tr, 200.0)
     ctx.set_imu(ts, g)
-    return ctx, b_in, b_out
+    return ctx, (b_in, b_xyz), b_out
 
 
 def main():
@@ -70,7 +73,8 @@ def main():
         wall = {lib: [] for lib in libs}
         for _ in range(args.rounds):
             for lib in libs:
-                ctx, bi, bo, grid = runs[lib]
+                ctx, (bt, bx), bo, grid = runs[lib]
+                bi = bx if mode == "frame" else bt
                 ctx.set_max_grid(grid)
                 for _ in range(3):
                     ctx.deskew(bi, bo, mode=mode)
