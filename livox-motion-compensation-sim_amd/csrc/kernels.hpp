@@ -38,9 +38,6 @@ namespace mc {
 #ifndef MC_STORE_IMU
 #define MC_STORE_IMU 1       // the IMU kernel's output stores: nt (-4 % vs sc1, tools/ab.py)
 #endif
-#ifndef MC_FRAME_SLEEP
-#define MC_FRAME_SLEEP 0     // diagnostic: s_sleep between the frame kernel's loads and stores
-#endif
 #ifndef MC_FASTPATH_MAXW
 #define MC_FASTPATH_MAXW 2   // frames spanning <= this many segments take the SGPR (no-LDS) path
 #endif
@@ -453,9 +450,6 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
         vi[it] = ld4(q + 3 * kBlkPts);
       }
     }
-#if MC_FRAME_SLEEP
-    __builtin_amdgcn_s_sleep(MC_FRAME_SLEEP);
-#endif
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
       const int g = it * kBlock + threadIdx.x;

@@ -614,7 +614,8 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   {
     TimedRegion tr(c, &c->main_ev, s);
     if (mode == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, da);
-    else if (mode == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, da);
+    else if (mode == MC_MODE_POSE_SLERP)
+      hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, da);
     else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, da);
   }
   HIPCHK(hipGetLastError());
