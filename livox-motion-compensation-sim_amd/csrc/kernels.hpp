@@ -30,7 +30,7 @@ namespace mc {
 #define MC_KITERS 2          // float4 groups per thread per tile in frame mode
 #endif
 #ifndef MC_STORE_FRAME
-#define MC_STORE_FRAME 1     // frame kernel output stores: nt (see st_pol)
+#define MC_STORE_FRAME 4     // frame kernel output stores: sc1 nt (see st_pol; -3 % vs nt with MC_FRAME_SUB)
 #endif
 #ifndef MC_STORE_POINTS
 #define MC_STORE_POINTS 2    // per-point kernels output stores: sc1 write-through (see st_pol)
@@ -474,7 +474,44 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) { deskew_frame_body<false>(a); }
+#ifndef MC_FRAME_SUB
+#define MC_FRAME_SUB 1       // frame kernel over kBlock-group sub-tiles, one group per thread (-3 %)
+#endif
+// the per-point kernels' decomposition applied to frame mode (MC_FRAME_SUB=1)
+__device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a) {
+  const int64_t n_sub = (int64_t)a.n_tiles * kSub;
+  for (int64_t st = blockIdx.x; st < n_sub; st += gridDim.x) {
+    const Tile tl = ldu(a.tiles + st / kSub);
+    const int g = (int)(st % kSub) * kBlock + threadIdx.x;
+    if (g >= tl.ngroups) continue;
+    const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
+    const float4 r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
+    const float4 r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
+    const int64_t p = tl.pstart + 4 * (int64_t)g;
+    const float* q = a.in + bidx((int)a.in_C, 0, p);
+    const float4 X = ld4(q), Y = ld4(q + kBlkPts), Z = ld4(q + 2 * kBlkPts), I = ld4(q + 3 * kBlkPts);
+    float4 ox4, oy4, oz4;
+#define MC_XF(c)                                                  \
+  ox4.c = fmaf(r0.x, X.c, fmaf(r0.y, Y.c, fmaf(r0.z, Z.c, r0.w))); \
+  oy4.c = fmaf(r1.x, X.c, fmaf(r1.y, Y.c, fmaf(r1.z, Z.c, r1.w))); \
+  oz4.c = fmaf(r2.x, X.c, fmaf(r2.y, Y.c, fmaf(r2.z, Z.c, r2.w)));
+    MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
+#undef MC_XF
+    float* o = a.out + bidx((int)a.out_C, 0, p);
+    st_frame(o, ox4);
+    st_frame(o + kBlkPts, oy4);
+    st_frame(o + 2 * kBlkPts, oz4);
+    st_frame(o + 3 * kBlkPts, I);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
+#if MC_FRAME_SUB
+  deskew_frame_sub(a);
+#else
+  deskew_frame_body<false>(a);
+#endif
+}
 
 // Many frames on host-resident rows (LMC:802-832 on host arrays): frame f's rows [doff[f],
 // doff[f+1]) of the pinned input get pose[12 f ..] = R (row-major) | t (float64, from k_scan_pose).

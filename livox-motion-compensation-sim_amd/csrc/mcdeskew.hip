@@ -609,7 +609,7 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   if (mode == MC_MODE_IMU) { da.nseg = c->M; da.ntab = c->M; }
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
-  const int32_t units = mode == MC_MODE_FRAME ? in->n_tiles : in->n_tiles * kSub;
+  const int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
   const dim3 grid(launch_grid(c, units)), block(kBlock);
   {
     TimedRegion tr(c, &c->main_ev, s);

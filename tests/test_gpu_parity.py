@@ -179,6 +179,44 @@ def test_full_size_c2_per_point_modes_sampled(mc, gpu_ctx, mode):
         assert np.max(np.abs(nout - nin) / nin) < 1e-5
 
 
+def test_max_size_c4_on_one_gpu_past_int32_indices(mc, gpu_ctx):
+    """BASELINE config 4's whole job (6000 x 100k, urban poses over 600 s) on ONE device: 600 M
+    points, 3.0 G values in the 5-column input (past 2^31), 12 GB in + 9.6 GB out.  SLERP into a
+    4-column batch, then frame mode in place on that output; frames at both ends and across the
+    2^31-value boundary are checked against the oracle."""
+    F, n = 6000, 100_000
+    cfg = dict(CFGS["urban_complex"], duration=600.0)
+    sim = mc.LiDARMotionSimulator(cfg, context=gpu_ctx)
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:F]
+    assert len(times) == F
+    b = gpu_ctx.batch(np.full(F, n), with_time=True)
+    b.synth(seed=7, frame_id_base=1000)
+    b.set_frame_times(times)
+    gpu_ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    out = gpu_ctx.deskew(b, gpu_ctx.batch(b.counts), mode="pose_slerp")
+    b.close()
+    g = np.stack(out.download_columns()[:3], axis=1)
+    out.set_frame_times(times)
+    gpu_ctx.deskew(out, out, mode="frame")
+    h = np.stack(out.download_columns()[:3], axis=1)
+    idx = R.select_pose_index(tr["time"], times)
+    edge = (2 ** 31) // (5 * n)          # first frames whose t_ns column lies past 2^31 values
+    for f in [0, 1, edge - 1, edge, edge + 1, 4297, F - 2, F - 1]:
+        x, y, z, _, t = synth.synth_frame(n, 7, 1000 + f)
+        p = np.stack([x, y, z], axis=1).astype(np.float64)
+        s = slice(f * n, (f + 1) * n)
+        ref = R.deskew_pose_slerp(p, t, times[f], tr)
+        _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[f] + t * 1e-9)
+        assert_scaled_close(g[s], ref, scale_of(p, pos), what=f"slerp frame {f}")
+        k = idx[f]
+        gp = g[s].astype(np.float64)
+        ref2 = R.transform_pointcloud(np.column_stack([gp, np.zeros(n)]),
+                                      {"translation": tr["position_gps"][k], "rotation": tr["orientation_imu"][k]})
+        assert_scaled_close(h[s], ref2[:, :3], scale_of(gp, tr["position_gps"][k]), what=f"frame {f}")
+    out.close()
+
+
 def _scenario_batch(mc, ctx, name, frames, n, seed):
     sim = mc.LiDARMotionSimulator(dict(CFGS[name]), context=ctx)   # seeds np.random (LMC:288): noise on
     tr = sim.add_sensor_noise(sim.generate_trajectory())

@@ -13,6 +13,7 @@ import argparse
 import glob
 import json
 import os
+import random
 import statistics
 import time
 import sys
@@ -71,8 +72,11 @@ def main():
     for mode in args.modes.split(","):
         per = {lib: [] for lib in libs}
         wall = {lib: [] for lib in libs}
+        order = list(libs)
+        rng = random.Random(1)
         for _ in range(args.rounds):
-            for lib in libs:
+            rng.shuffle(order)             # arm position within a round must not decide the result
+            for lib in order:
                 ctx, (bt, bx), bo, grid = runs[lib]
                 bi = bx if mode == "frame" else bt
                 ctx.set_max_grid(grid)
