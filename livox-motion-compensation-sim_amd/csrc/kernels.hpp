@@ -41,6 +41,9 @@ namespace mc {
 #ifndef MC_FASTPATH_MAXW
 #define MC_FASTPATH_MAXW 2   // frames spanning <= this many segments take the SGPR (no-LDS) path
 #endif
+#ifndef MC_SUBTILE_WIN
+#define MC_SUBTILE_WIN 1     // per sub-tile segment windows for frames wider than the SGPR path
+#endif
 #ifndef MC_NULL_COMPUTE
 #define MC_NULL_COMPUTE 0    // diagnostic build: skip the per-point math, keep loads/stores
 #endif
@@ -120,6 +123,8 @@ struct DeskewArgs {
   const int64_t* frame_start;
   const FrameWin* fwin;    // per-point modes
   const void* frec;        // 2 frame-specialised records per frame (PoseWin or ImuSeg)
+  const FrameWin* swin;    // per sub-tile: the same, for frames whose window exceeds MC_FASTPATH_MAXW
+  const void* srec;        // 2 frame-specialised records per sub-tile
   const double* pose_time; // T
   const PoseSeg* pose_seg; // nseg
   const int64_t* imu_ts;   // M
@@ -322,6 +327,10 @@ struct PrepArgs {
   float4* frame_tbl; PoseSeg* pose_seg; ImuSeg* imu_seg;                 // outputs
   FrameWin* fwin; void* frec;
   int64_t nseg;
+  // per sub-tile windows for frames whose window is wider than MC_FASTPATH_MAXW
+  const int32_t* ftile;    // first tile of frame f (F+1 entries)
+  const int2* strange;     // per sub-tile [min, max] t_ns (recorded with trange)
+  FrameWin* swin; void* srec;
 };
 
 // Wave-cooperative searches over a sorted table: 64 lanes probe evenly spaced entries per round,
@@ -395,30 +404,58 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
     }
   }
   const int64_t W = khi - klo + 1;
-  if (lane >= 2 || (lane == 1 && W < 2)) return;
-  // lane 0: record klo (+ the window header), lane 1: record klo+1
-  const int64_t k = klo + lane;
-  if (a.mode == 1) {
-    const double tf = a.frame_time[f];
-    reinterpret_cast<PoseWin*>(a.frec)[2 * f + lane] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, k), tf);
-    if (lane == 0) {
-      FrameWin fw;
-      fw.klo = (int32_t)klo;
-      fw.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
-      fw.bnd1 = W >= 2 ? rel_ns_ceil(a.time[klo + 1], tf) : INT64_MAX;
-      a.fwin[f] = fw;
+  const double tf = a.mode == 1 ? a.frame_time[f] : 0.0;
+  const int64_t fs = a.mode == 2 ? a.frame_start[f] : 0;
+  // frame-relative ns where segment k starts (the LDS path's s_bnd, the SGPR path's bnd1)
+  auto bound = [&](int64_t k) -> int64_t {
+    return a.mode == 1 ? rel_ns_ceil(a.time[k], tf) : a.imu_ts[k] - fs;
+  };
+  auto record = [&](int64_t k, void* dst, int64_t slot) {
+    if (a.mode == 1) {
+      reinterpret_cast<PoseWin*>(dst)[slot] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, k), tf);
+    } else {
+      ImuSeg sg = make_imu_seg(a.imu_ts, a.gyro, a.M, k);
+      sg.ts -= fs;
+      reinterpret_cast<ImuSeg*>(dst)[slot] = sg;
     }
-  } else {
-    const int64_t fs = a.frame_start[f];
-    ImuSeg sg = make_imu_seg(a.imu_ts, a.gyro, a.M, k);
-    sg.ts -= fs;
-    reinterpret_cast<ImuSeg*>(a.frec)[2 * f + lane] = sg;
-    if (lane == 0) {
-      FrameWin fw;
-      fw.klo = (int32_t)klo;
-      fw.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
-      fw.bnd1 = W >= 2 ? a.imu_ts[klo + 1] - fs : INT64_MAX;
-      a.fwin[f] = fw;
+  };
+  auto window = [&](int64_t k0, int64_t n) {
+    FrameWin w;
+    w.klo = (int32_t)k0;
+    w.W = n > kWinMax ? kWinMax + 1 : (int32_t)n;
+    w.bnd1 = n >= 2 ? bound(k0 + 1) : INT64_MAX;
+    return w;
+  };
+  // lane 0: record klo (+ the window header), lane 1: record klo+1
+  if (lane < 2 && !(lane == 1 && W < 2)) {
+    record(klo + lane, a.frec, 2 * f + lane);
+    if (lane == 0) a.fwin[f] = window(klo, W);
+  }
+  if (!MC_SUBTILE_WIN || W <= MC_FASTPATH_MAXW || !a.swin) return;
+  // A wide frame (IMU: ~20 samples per 0.1 s frame): each 1024-point sub-tile of a time-ordered
+  // frame spans ~1 ms, so its own window is 1-2 segments and takes the SGPR path (no LDS staging,
+  // no barrier: -10 % kernel time on SLERP, tools/ab.py).  Lane per sub-tile; segment of t =
+  // last k in [klo, khi] with bound(k) <= t (klo if none), as the kernel's window search.
+  auto seg_of = [&](int64_t t) {
+    int64_t lo = klo, hi = khi;   // invariant: answer in [lo, hi]
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (bound(mid) <= t) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  const int64_t st0 = (int64_t)a.ftile[f] * kSub, st1 = (int64_t)a.ftile[f + 1] * kSub;
+  for (int64_t st = st0 + lane; st < st1; st += 64) {
+    const int2 r = a.strange[st];
+    int64_t k0 = klo, n = 1;
+    if (r.x <= r.y) {
+      k0 = seg_of(r.x);
+      n = seg_of(r.y) - k0 + 1;
+    }
+    a.swin[st] = window(k0, n);
+    if (n <= MC_FASTPATH_MAXW) {
+      record(k0, a.srec, 2 * st);
+      if (n >= 2) record(k0 + 1, a.srec, 2 * st + 1);
     }
   }
 }
@@ -777,13 +814,19 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
   const int tid = threadIdx.x;
   const int64_t n_sub = (int64_t)a.n_tiles * kSub;
   const Win* frec = reinterpret_cast<const Win*>(a.frec);
+  const Win* srec = reinterpret_cast<const Win*>(a.srec);
 
   for (int64_t st = blockIdx.x; st < n_sub; st += gridDim.x) {
     const Tile tl = ldu(a.tiles + st / kSub);
+    const FrameWin sw = ldu(a.swin + st);   // independent of the tile: issued with it
     const int g0 = (int)(st % kSub) * kBlock;
     if (g0 >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
     const int f = tl.frame;
-    const FrameWin fw = ldu(a.fwin + f);
+    const FrameWin ff = ldu(a.fwin + f);
+    // frames wider than the SGPR path take their sub-tile's own window (k_prep)
+    const bool sub = MC_SUBTILE_WIN && ff.W > MC_FASTPATH_MAXW;
+    const FrameWin fw = sub ? sw : ff;
+    const Win* rec = sub ? srec + 2 * st : frec + 2 * f;
     if (fw.W > kWinMax) {
       deskew_subtile_slow<MODE>(a, tl, g0);
       continue;
@@ -804,7 +847,7 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
     }
 
     if (fw.W <= MC_FASTPATH_MAXW) {
-      const Win r0 = ldu(frec + 2 * f);
+      const Win r0 = ldu(rec);
       bool use1 = false, mixed = false;
       if (fw.W == 2) {
         const int64_t b1 = fw.bnd1;
@@ -816,11 +859,11 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
       }
       if (act) {
         if (!mixed) {
-          const Win w = use1 ? ldu(frec + 2 * f + 1) : r0;
+          const Win w = use1 ? ldu(rec + 1) : r0;
 #pragma unroll
           for (int c = 0; c < 4; ++c) point_body<MODE>(w, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
         } else {
-          const Win r1 = ldu(frec + 2 * f + 1);
+          const Win r1 = ldu(rec + 1);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int t = i4c(Tq, c);
@@ -1052,24 +1095,42 @@ __global__ __launch_bounds__(kBlock) void k_trange_init(int2* tr, int32_t F) {
   const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (f < F) tr[f] = make_int2(INT_MAX, INT_MIN);
 }
-__global__ __launch_bounds__(kBlock) void k_trange(const LayoutArgs a, int2* tr) {
+// ... and per sub-tile (kBlock float4 groups), feeding k_prep's sub-tile windows
+__global__ __launch_bounds__(kBlock) void k_trange(const LayoutArgs a, int2* tr, int2* str) {
+  __shared__ int s_lo[kSub][kBlock / 64], s_hi[kSub][kBlock / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = a.tiles[tile];
-    int lo = INT_MAX, hi = INT_MIN;
-    for (int e = threadIdx.x; e < 4 * tl.ngroups; e += kBlock) {
-      const int64_t p = tl.pstart + e;
-      if (local_index(a, tl, p) >= 0) {
-        const int t = a.tns(p);
-        lo = min(lo, t);
-        hi = max(hi, t);
+    int flo = INT_MAX, fhi = INT_MIN;
+#pragma unroll
+    for (int j = 0; j < kSub; ++j) {
+      int lo = INT_MAX, hi = INT_MIN;
+      const int e_end = min(4 * tl.ngroups, (j + 1) * 4 * kBlock);
+      for (int e = j * 4 * kBlock + threadIdx.x; e < e_end; e += kBlock) {
+        const int64_t p = tl.pstart + e;
+        if (local_index(a, tl, p) >= 0) {
+          const int t = a.tns(p);
+          lo = min(lo, t);
+          hi = max(hi, t);
+        }
       }
+      lo = wave_min(lo);
+      hi = wave_max(hi);
+      if (lane == 0) { s_lo[j][wid] = lo; s_hi[j][wid] = hi; }
+      flo = min(flo, lo);
+      fhi = max(fhi, hi);
     }
-    lo = wave_min(lo);
-    hi = wave_max(hi);
-    if ((threadIdx.x & 63) == 0 && lo <= hi) {
-      atomicMin(&tr[tl.frame].x, lo);
-      atomicMax(&tr[tl.frame].y, hi);
+    if (lane == 0 && flo <= fhi) {
+      atomicMin(&tr[tl.frame].x, flo);
+      atomicMax(&tr[tl.frame].y, fhi);
     }
+    __syncthreads();
+    if (threadIdx.x < kSub) {
+      int lo = INT_MAX, hi = INT_MIN;
+      for (int w = 0; w < kBlock / 64; ++w) { lo = min(lo, s_lo[threadIdx.x][w]); hi = max(hi, s_hi[threadIdx.x][w]); }
+      str[tile * kSub + threadIdx.x] = make_int2(lo, hi);
+    }
+    __syncthreads();
   }
 }
 

@@ -83,7 +83,7 @@ static int compute_trange(mc_batch* b) {
   hipLaunchKernelGGL(k_trange_init, dim3((b->F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, b->d_trange, b->F);
   if (b->n_tiles > 0)
     hipLaunchKernelGGL(k_trange, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
-                       b->d_trange);
+                       b->d_trange, b->d_strange);
   HIPCHK(hipGetLastError());
   b->trange_valid = true;
   return MC_OK;
@@ -235,7 +235,9 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
   b->doff.resize(F + 1);
   b->poff[0] = b->doff[0] = 0;
   std::vector<Tile> tiles;
+  std::vector<int32_t> ftile(F + 1, 0);
   for (int32_t f = 0; f < F; ++f) {
+    ftile[f] = (int32_t)std::min<size_t>(tiles.size(), INT32_MAX);
     if (b->counts[f] < 0) { delete b; return fail(MC_ERR_INVALID, "frame %d has a negative count", f); }
     const int64_t groups = (b->counts[f] + 3) / 4;
     b->doff[f + 1] = b->doff[f] + b->counts[f];
@@ -248,7 +250,8 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
       tiles.push_back(t);
     }
   }
-  if (tiles.size() > (size_t)INT32_MAX) { delete b; return fail(MC_ERR_INVALID, "too many tiles"); }
+  if (tiles.size() * kSub > (size_t)INT32_MAX) { delete b; return fail(MC_ERR_INVALID, "too many tiles"); }
+  ftile[F] = (int32_t)tiles.size();
   b->N = b->doff[F];
   b->P = b->poff[F];
   b->C = (flags & MC_BATCH_WITH_TIME) ? 5 : 4;
@@ -270,6 +273,14 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
   if ((r = dev_alloc(&b->d_fwin, 2 * (size_t)F))) return bail(r);
   b->frec_half = 2 * (size_t)std::max<int>(F, 1) * std::max(sizeof(PoseWin), sizeof(ImuSeg));
   if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_frec), 2 * b->frec_half))) return bail(r);
+  const size_t n_sub = std::max<size_t>(tiles.size(), 1) * kSub;
+  if (b->has_t()) {
+    if ((r = dev_alloc(&b->d_ftile, F + 1))) return bail(r);
+    if ((r = dev_alloc(&b->d_strange, n_sub))) return bail(r);
+    if ((r = dev_alloc(&b->d_swin, 2 * n_sub))) return bail(r);
+    b->srec_half = 2 * n_sub * std::max(sizeof(PoseWin), sizeof(ImuSeg));
+    if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_srec), 2 * b->srec_half))) return bail(r);
+  }
   if ((r = dev_alloc(&b->d_partial, 5 * (size_t)b->n_tiles))) return bail(r);
   hipStream_t s = c->stream;
   auto cpy = [&](void* d, const void* h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s); };
@@ -280,6 +291,8 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
       return bail(fail(MC_ERR_HIP, "batch metadata upload failed"));
     if (!tiles.empty() && cpy(b->d_tiles, tiles.data(), tiles.size() * sizeof(Tile)) != hipSuccess)
       return bail(fail(MC_ERR_HIP, "tile table upload failed"));
+    if (b->d_ftile && cpy(b->d_ftile, ftile.data(), (F + 1) * sizeof(int32_t)) != hipSuccess)
+      return bail(fail(MC_ERR_HIP, "frame tile table upload failed"));
   }
   // zero the columns so padding slots are defined even before the first upload
   if (hipMemsetAsync(b->d_cols, 0, col_vals * sizeof(float), s) != hipSuccess)
@@ -298,6 +311,9 @@ int mc_batch_destroy(mc_batch* b) {
   dev_free(b->d_trange); dev_free(b->d_fwin); dev_free(b->d_partial);
   if (b->d_frec) (void)hipFree(b->d_frec);
   b->d_frec = nullptr;
+  dev_free(b->d_ftile); dev_free(b->d_strange); dev_free(b->d_swin);
+  if (b->d_srec) (void)hipFree(b->d_srec);
+  b->d_srec = nullptr;
   delete b;
   return MC_OK;
 }
@@ -576,6 +592,9 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   pa.frame_time = pb->d_frame_time; pa.frame_start = pb->d_frame_start; pa.trange = pb->d_trange;
   pa.frame_tbl = frame_tbl; pa.pose_seg = pose_seg; pa.imu_seg = imu_seg;
   pa.fwin = fwin; pa.frec = frec;
+  FrameWin* swin = pb->d_swin ? pb->d_swin + (size_t)in->n_tiles * kSub * h : nullptr;
+  void* srec = pb->d_srec ? static_cast<char*>(pb->d_srec) + pb->srec_half * h : nullptr;
+  pa.ftile = pb->d_ftile; pa.strange = pb->d_strange; pa.swin = swin; pa.srec = srec;
   // one wave per frame, then one lane per pose segment / IMU sample
   int64_t table = 0;
   if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); table = pa.nseg; }
@@ -603,6 +622,7 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   da.frame_tbl = frame_tbl;
   da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start;
   da.fwin = fwin; da.frec = frec;
+  da.swin = swin; da.srec = srec;
   da.pose_time = c->d_time; da.pose_seg = pose_seg;
   da.imu_ts = c->d_imu_ts; da.imu_seg = imu_seg;
   if (mode == MC_MODE_POSE_SLERP) { da.nseg = pa.nseg; da.ntab = c->T; }

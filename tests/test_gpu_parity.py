@@ -315,6 +315,46 @@ def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
 
 
 @pytest.mark.parametrize("mode", ["pose_slerp", "imu"])
+def test_wide_frames_take_subtile_windows(mc, gpu_ctx, mode):
+    """Frames spanning many pose / IMU segments (100 Hz poses, 1 kHz IMU): time-ordered frames use
+    per-sub-tile windows of 1-2 segments (SGPR path, incl. sub-tiles straddling a boundary), a
+    shuffled frame the sub-tile LDS window, a 3-s frame the out-of-line search; all vs the oracle."""
+    rng = np.random.default_rng(12)
+    T = 4000
+    time = np.linspace(0, 40, T)
+    tr = {"time": time, "position_gps": np.cumsum(rng.normal(0, 0.2, (T, 3)), axis=0),
+          "orientation_imu": np.cumsum(rng.normal(0, 0.05, (T, 3)), axis=0)}
+    counts = [50_000, 50_000, 20_000, 4096, 7]
+    t_ns = [np.sort(rng.integers(0, 100_000_000, counts[0])),
+            np.arange(counts[1]) * 2000,                                     # exact 2 us spacing
+            rng.permutation(np.arange(counts[2]) * 5000),                     # shuffled
+            rng.integers(-1_500_000_000, 1_500_000_000, counts[3]),           # 3 s span
+            np.array([0, 1, 2, 99_999_999, 50_000_000, 3, 4])]
+    frames = [np.column_stack([rng.uniform(-90, 90, (n, 3)), rng.uniform(0, 1, n)]) for n in counts]
+    times = np.array([2.0, 10.005, 20.0, 30.0, 35.0])
+    sim = mc.LiDARMotionSimulator(context=gpu_ctx)
+    if mode == "pose_slerp":
+        out = sim.deskew_frames(frames, t_ns, tr, times)
+        for f in range(len(counts)):
+            ref = R.deskew_pose_slerp(frames[f][:, :3], t_ns[f], times[f], tr)
+            _, p = R.slerp_pose(time, tr["position_gps"], tr["orientation_imu"], times[f] + np.asarray(t_ns[f]) * 1e-9)
+            assert_scaled_close(out[f][:, :3], ref, scale_of(frames[f][:, :3], p), what=f"frame {f}")
+    else:
+        ts = np.arange(0, 40_000_000_000, 1_000_000, dtype=np.int64)            # 1 kHz
+        gyro = rng.normal(0, 0.5, (len(ts), 3))
+        starts = (times * 1e9).astype(np.int64)
+        b = gpu_ctx.batch(np.array(counts), with_time=True)
+        b.upload_aos(np.concatenate(frames))
+        b.upload_time(np.concatenate(t_ns).astype(np.int32))
+        b.set_frame_starts(starts)
+        gpu_ctx.set_imu(ts, gyro)
+        got = b.split(gpu_ctx.deskew(b, mode="imu").download_aos())
+        for f in range(len(counts)):
+            ref = R.compensate_arrays(frames[f][:, :3], starts[f] + np.asarray(t_ns[f], np.int64), starts[f], ts, gyro)
+            assert_scaled_close(got[f][:, :3], ref, scale_of(frames[f][:, :3]), what=f"imu frame {f}")
+
+
+@pytest.mark.parametrize("mode", ["pose_slerp", "imu"])
 def test_per_point_modes_pass_t_ns_through(mc, gpu_ctx, mode):
     """CSIM:1472 keeps each point's timestamp: out-of-place deskew into a batch with t_ns copies
     the column from inside the kernel (fast and out-of-line paths); in place leaves it as is; the
