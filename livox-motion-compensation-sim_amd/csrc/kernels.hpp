@@ -149,6 +149,29 @@ __device__ __forceinline__ T ldu(const T* p) {
   return __builtin_bit_cast(T, r);
 }
 
+// XCD-contiguous sub-tile order per kernel (tools/ab.py, profiles/r13/ab_xcd*.log): frame -7 %,
+// IMU -4 %; SLERP +3 % slower with it under every store policy, so it keeps the dealt order
+#ifndef MC_XCD_FRAME
+#define MC_XCD_FRAME 1
+#endif
+#ifndef MC_XCD_IMU
+#define MC_XCD_IMU 1
+#endif
+#ifndef MC_XCD_SLERP
+#define MC_XCD_SLERP 0
+#endif
+// XCD-aware unit order.  Workgroups are dealt round-robin over the 8 XCDs (observed; speed only,
+// never correctness): unit order b -> contiguous runs per XCD, so the 16-byte per-unit records
+// (tiles, sub-tile windows) of neighbouring units share 128-byte lines inside one XCD's L2
+// instead of each workgroup fetching its own line.  A bijection on [0, n) for any n.
+constexpr int kXcds = 8;
+template <bool ON>
+__device__ __forceinline__ int64_t xcd_unit(int64_t b, int64_t n) {
+  if (!ON) return b;
+  const int64_t x = b % kXcds, i = b / kXcds, per = n / kXcds, rem = n % kXcds;
+  return x * per + (x < rem ? x : rem) + i;
+}
+
 // 16-byte non-temporal store (output is written once and never re-read by this kernel)
 typedef float v4f __attribute__((ext_vector_type(4)));
 // Output store cache policy (measured with tools/ab.py, interleaved in one process):
@@ -517,7 +540,8 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
 // the per-point kernels' decomposition applied to frame mode (MC_FRAME_SUB=1)
 __device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a) {
   const int64_t n_sub = (int64_t)a.n_tiles * kSub;
-  for (int64_t st = blockIdx.x; st < n_sub; st += gridDim.x) {
+  for (int64_t it = blockIdx.x; it < n_sub; it += gridDim.x) {
+    const int64_t st = gridDim.x >= n_sub ? xcd_unit<MC_XCD_FRAME>(it, n_sub) : it;
     const Tile tl = ldu(a.tiles + st / kSub);
     const int g = (int)(st % kSub) * kBlock + threadIdx.x;
     if (g >= tl.ngroups) continue;
@@ -816,15 +840,21 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
   const Win* frec = reinterpret_cast<const Win*>(a.frec);
   const Win* srec = reinterpret_cast<const Win*>(a.srec);
 
-  for (int64_t st = blockIdx.x; st < n_sub; st += gridDim.x) {
+  for (int64_t it = blockIdx.x; it < n_sub; it += gridDim.x) {
+    const int64_t st = gridDim.x >= n_sub ? xcd_unit<(MODE == 2 ? MC_XCD_IMU : MC_XCD_SLERP)>(it, n_sub) : it;
     const Tile tl = ldu(a.tiles + st / kSub);
-    const FrameWin sw = ldu(a.swin + st);   // independent of the tile: issued with it
+    // IMU frames always span several samples: fetch the sub-tile window with the tile record
+    FrameWin sw;
+    if constexpr (MODE == 2) sw = ldu(a.swin + st);
     const int g0 = (int)(st % kSub) * kBlock;
     if (g0 >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
     const int f = tl.frame;
     const FrameWin ff = ldu(a.fwin + f);
     // frames wider than the SGPR path take their sub-tile's own window (k_prep)
     const bool sub = MC_SUBTILE_WIN && ff.W > MC_FASTPATH_MAXW;
+    if constexpr (MODE != 2) {
+      if (sub) sw = ldu(a.swin + st);
+    }
     const FrameWin fw = sub ? sw : ff;
     const Win* rec = sub ? srec + 2 * st : frec + 2 * f;
     if (fw.W > kWinMax) {
