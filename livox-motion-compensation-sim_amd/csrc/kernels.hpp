@@ -160,6 +160,9 @@ __device__ __forceinline__ T ldu(const T* p) {
 #ifndef MC_XCD_SLERP
 #define MC_XCD_SLERP 0
 #endif
+#ifndef MC_XCD_STAGE
+#define MC_XCD_STAGE 1       // the LDS stager pair's tile order
+#endif
 // XCD-aware unit order.  Workgroups are dealt round-robin over the 8 XCDs (observed; speed only,
 // never correctness): unit order b -> contiguous runs per XCD, so the 16-byte per-unit records
 // (tiles, sub-tile windows) of neighbouring units share 128-byte lines inside one XCD's L2
@@ -1016,8 +1019,8 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
 #if MC_STAGE_LDS
   __shared__ float s_t[4][kStageRow];
   if (ld == 4) {
-    for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-      const Tile tl = ldu(a.tiles + tile);
+    for (int64_t it = blockIdx.x; it < a.n_tiles; it += gridDim.x) {
+      const Tile tl = ldu(a.tiles + (gridDim.x >= a.n_tiles ? xcd_unit<MC_XCD_STAGE>(it, a.n_tiles) : it));
       const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
       const int64_t loc0 = tl.pstart - poff;
       const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
@@ -1068,8 +1071,8 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
 __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, double* __restrict__ aos) {
 #if MC_STAGE_LDS
   __shared__ float s_t[4][kStageRow];
-  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-    const Tile tl = ldu(a.tiles + tile);
+  for (int64_t it = blockIdx.x; it < a.n_tiles; it += gridDim.x) {
+    const Tile tl = ldu(a.tiles + (gridDim.x >= a.n_tiles ? xcd_unit<MC_XCD_STAGE>(it, a.n_tiles) : it));
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
     const int64_t loc0 = tl.pstart - poff;
     const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
