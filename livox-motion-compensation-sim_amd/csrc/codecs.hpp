@@ -14,6 +14,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "layout.hpp"
+
+#ifndef MC_XCD_CODEC
+#define MC_XCD_CODEC 1       // LVX / PCD unit order (XCD-contiguous, layout.hpp)
+#endif
+
 namespace mc {
 
 constexpr int kCodecBlock = 256;
@@ -93,7 +99,7 @@ __device__ __forceinline__ int32_t lvx_fixed(double v, double scale, double lo, 
 __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
-  const int64_t u = blockIdx.x;
+  const int64_t u = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x);   // grid = units exactly
   const int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u);
   const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
   const int64_t frow = a.src.doff[f];
@@ -381,7 +387,7 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
 
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
-  const int64_t u0 = (int64_t)blockIdx.x * kPcdTilesPerWG;
+  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
   for (int j = 0; j < kPcdTilesPerWG; ++j) {
     const int64_t u = u0 + j;
@@ -408,7 +414,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
   char* const s_text = reinterpret_cast<char*>(s_text4);
-  const int64_t u0 = (int64_t)blockIdx.x * kPcdTilesPerWG;
+  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
   for (int j = 0; j < kPcdTilesPerWG; ++j) {
     const int64_t u = u0 + j;

@@ -23,6 +23,8 @@
 #include <limits.h>
 #include <type_traits>
 
+#include "layout.hpp"
+
 namespace mc {
 
 // Build-time knobs (tools/ab.py builds variants of these and times them in one process):
@@ -64,11 +66,7 @@ constexpr int kWinMax = 64;                    // LDS window capacity (segments 
 // columns (x, y, z, intensity [, t_ns]) of 256 values back to back.  A wave's float4 access to
 // one column is 1 KB contiguous, and a workgroup's whole working set is one contiguous stretch
 // of HBM instead of C streams a batch apart (+4-5 % on a 5-in / 4-out pass, tools/layout_probe.hip).
-// Frames start at multiples of kBlkPts, so tiles and frame ranges are whole blocks.
-constexpr int kBlkPts = 256;
-__host__ __device__ __forceinline__ int64_t bidx(int C, int c, int64_t p) {
-  return ((p >> 8) * C + c) * kBlkPts + (p & (kBlkPts - 1));
-}
+// kBlkPts and the index bidx(C, c, p) live in layout.hpp (shared with the codecs).
 
 struct Tile {
   int64_t pstart;   // padded point index of the first group (multiple of kBlkPts)
@@ -163,18 +161,6 @@ __device__ __forceinline__ T ldu(const T* p) {
 #ifndef MC_XCD_STAGE
 #define MC_XCD_STAGE 1       // the LDS stager pair's tile order
 #endif
-// XCD-aware unit order.  Workgroups are dealt round-robin over the 8 XCDs (observed; speed only,
-// never correctness): unit order b -> contiguous runs per XCD, so the 16-byte per-unit records
-// (tiles, sub-tile windows) of neighbouring units share 128-byte lines inside one XCD's L2
-// instead of each workgroup fetching its own line.  A bijection on [0, n) for any n.
-constexpr int kXcds = 8;
-template <bool ON>
-__device__ __forceinline__ int64_t xcd_unit(int64_t b, int64_t n) {
-  if (!ON) return b;
-  const int64_t x = b % kXcds, i = b / kXcds, per = n / kXcds, rem = n % kXcds;
-  return x * per + (x < rem ? x : rem) + i;
-}
-
 // 16-byte non-temporal store (output is written once and never re-read by this kernel)
 typedef float v4f __attribute__((ext_vector_type(4)));
 // Output store cache policy (measured with tools/ab.py, interleaved in one process):

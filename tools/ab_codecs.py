@@ -1,0 +1,102 @@
+"""Interleaved, order-shuffled A/B of the LVX and ASCII-PCD encoders across library variants, one
+process, one device (GPU box only).  Each arm encodes the same device (N,4) f64 cloud; outputs of
+every arm are checked byte-identical to the first arm's.
+
+    make -C livox-motion-compensation-sim_amd/csrc variants VARIANTS="a:-DMC_KITERS=2 b:-DMC_XCD_CODEC=0"
+    python tools/ab_codecs.py --libs build/variants/lib_a.so,build/variants/lib_b.so
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+from ctypes import c_int64, c_uint64
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import mcamd as mc  # noqa: E402
+
+
+def setup(lib, counts):
+    ctx = mc.Context(0, lib_path=lib)
+    b = ctx.batch(counts)
+    b.synth(seed=0, frame_id_base=1000)
+    src = ctx.device_buffer(int(counts.sum()) * 32)
+    b.fetch_aos_device(src)
+    b.close()
+    F = len(counts)
+    pos = mc.codecs.lvx_layout(counts)
+    lvx_out = ctx.device_buffer(int(pos[-1]))
+    cap = int(counts.sum()) * 48
+    pcd_out = ctx.device_buffer(cap)
+    ids = np.arange(F, dtype=np.uint64)
+    ts = (np.arange(F) * 100_000_000).astype(np.uint64)
+    bpos = np.zeros(F + 1, np.int64)
+    ptr = mc._lib.ptr
+
+    def lvx():
+        mc._lib.check(ctx.lib.mc_lvx_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), ptr(ids, c_uint64),
+                                            ptr(ts, c_uint64), None, lvx_out.ptr, int(pos[-1])), "lvx_encode")
+
+    def pcd():
+        mc._lib.check(ctx.lib.mc_pcd_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), pcd_out.ptr, cap,
+                                            ptr(bpos, c_int64)), "pcd_encode")
+
+    return {"ctx": ctx, "lvx": lvx, "pcd": pcd, "lvx_out": lvx_out, "pcd_out": pcd_out, "bpos": bpos,
+            "lvx_bytes": int(pos[-1])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--frames", type=int, default=600)
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    libs = [l for l in args.libs.split(",") if l]
+    counts = np.full(args.frames, args.points, np.int64)
+    arms = {lib: setup(lib, counts) for lib in libs}
+    times = {lib: {"lvx": [], "pcd": []} for lib in libs}
+    order = list(libs)
+    rng = random.Random(1)
+    for _ in range(args.rounds):
+        rng.shuffle(order)
+        for lib in order:
+            a = arms[lib]
+            for name in ("lvx", "pcd"):
+                a[name]()
+                a["ctx"].read_timing()
+                a["ctx"].timing(True)
+                for _ in range(args.reps):
+                    a[name]()
+                a["ctx"].timing(False)
+                times[lib][name].append(a["ctx"].read_timing()["codec_ms"] / args.reps * 1e3)
+    # byte-identical outputs across arms (sampled: first and last 64 MB)
+    ref = arms[libs[0]]
+    for lib in libs[1:]:
+        a = arms[lib]
+        for key, nbytes in (("lvx_out", ref["lvx_bytes"]), ("pcd_out", int(ref["bpos"][-1]))):
+            for lo in (0, max(0, nbytes - (64 << 20))):
+                n = min(64 << 20, nbytes - lo)
+                x = np.empty(n, np.uint8)
+                y = np.empty(n, np.uint8)
+                mc._lib.check(ref["ctx"].lib.mc_memcpy_d2h(ref["ctx"].handle, x.ctypes.data, ref[key].ptr.value + lo, n))
+                mc._lib.check(a["ctx"].lib.mc_memcpy_d2h(a["ctx"].handle, y.ctypes.data, a[key].ptr.value + lo, n))
+                assert np.array_equal(x, y), (lib, key, lo)
+    out = {}
+    for lib in libs:
+        name = os.path.basename(lib)
+        out[name] = {k: {"median_us": statistics.median(v), "min_us": min(v)} for k, v in times[lib].items()}
+        print(f"{name:22s} lvx median {out[name]['lvx']['median_us']:8.1f} us   pcd (measure+write) median "
+              f"{out[name]['pcd']['median_us']:8.1f} us", flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
