@@ -238,72 +238,68 @@ def measure_scan(ctx, cfg, tr, reps, cpu_budget):
 
 def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     """SURVEY §8f row 3, reported beside the hot path: the byte-exact writers (LVX v1.1 LMC:24-272,
-    ASCII PCD LMC:932-948) encoding the rank's whole deskewed batch from a device (N,4) f64 cloud.
-    Kernel time only (HIP events); HBM bytes = 32 B/pt read + the encoded bytes written."""
+    ASCII PCD LMC:932-948) encoding the rank's whole deskewed batch straight from its float32
+    columns in HBM (mc_*_encode_batch).  Kernel time only (HIP events); HBM bytes = 16 B/pt read +
+    the encoded bytes written."""
     from ctypes import c_int64, c_uint64
     counts = np.ascontiguousarray(b_out.counts, np.int64)
     F = len(counts)
-    src = ctx.device_buffer(n_rank * 32)
-    b_out.fetch_aos_device(src)
     rep = {}
-    try:
-        pos = mc.codecs.lvx_layout(counts)
-        ids = np.arange(F, dtype=np.uint64)
-        ts = (np.arange(F) * 100_000_000).astype(np.uint64)
-        out = ctx.device_buffer(int(pos[-1]))
-        ptr = mc._lib.ptr
+    pos = mc.codecs.lvx_layout(counts)
+    ids = np.arange(F, dtype=np.uint64)
+    ts = (np.arange(F) * 100_000_000).astype(np.uint64)
+    out = ctx.device_buffer(int(pos[-1]))
+    ptr = mc._lib.ptr
 
-        def lvx():
-            mc._lib.check(ctx.lib.mc_lvx_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), ptr(ids, c_uint64),
-                                                ptr(ts, c_uint64), None, out.ptr, int(pos[-1])), "lvx_encode")
+    def lvx():
+        mc._lib.check(ctx.lib.mc_lvx_encode_batch(ctx.handle, b_out.handle, ptr(ids, c_uint64), ptr(ts, c_uint64),
+                                                  out.ptr, int(pos[-1])), "lvx_encode_batch")
+    lvx()
+    ctx.read_timing()
+    ctx.timing(True)
+    for _ in range(reps):
         lvx()
-        ctx.read_timing()
-        ctx.timing(True)
-        for _ in range(reps):
-            lvx()
-        ctx.timing(False)
-        ms = ctx.read_timing()["codec_ms"] / reps
-        out.close()
-        alg = 32 * n_rank + int(pos[-1])
-        rep["lvx"] = {"file_bytes": int(pos[-1]), "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
-                      "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
-                      "bytes_per_point": alg / n_rank, "traffic_over_algorithmic": aux_traffic("k_lvx_packages")}
-        bpos = np.zeros(F + 1, np.int64)
-        cap = n_rank * 48
-        out = ctx.device_buffer(cap)
+    ctx.timing(False)
+    ms = ctx.read_timing()["codec_ms"] / reps
+    out.close()
+    alg = 16 * n_rank + int(pos[-1])
+    rep["lvx"] = {"file_bytes": int(pos[-1]), "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
+                  "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
+                  "bytes_per_point": alg / n_rank, "traffic_over_algorithmic": aux_traffic("k_lvx_packages")}
+    bpos = np.zeros(F + 1, np.int64)
+    cap = n_rank * 48
+    out = ctx.device_buffer(cap)
 
-        def pcd():
-            mc._lib.check(ctx.lib.mc_pcd_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), out.ptr, cap,
-                                                ptr(bpos, c_int64)), "pcd_encode")
+    def pcd():
+        mc._lib.check(ctx.lib.mc_pcd_encode_batch(ctx.handle, b_out.handle, out.ptr, cap, ptr(bpos, c_int64)),
+                      "pcd_encode_batch")
+    pcd()
+    ctx.read_timing()
+    ctx.timing(True)
+    for _ in range(reps):
         pcd()
-        ctx.read_timing()
-        ctx.timing(True)
-        for _ in range(reps):
-            pcd()
-        ctx.timing(False)
-        ms = ctx.read_timing()["codec_ms"] / reps
-        out.close()
-        text = int(bpos[-1])
-        alg = 32 * n_rank + text
-        rep["pcd_ascii"] = {"text_bytes": text, "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
-                            "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
-                            "bytes_per_point": alg / n_rank, "note": "measure + write passes",
-                            "traffic_over_algorithmic": aux_traffic("k_pcd_measure", "k_pcd_write")}
-        if cpu_budget > 0:
-            from oracle import codecs as C
-            host = b_out.download_aos()[:int(counts[0])]
-            t0 = time.perf_counter()
-            C.lvx_bytes([{"frame_id": 0, "timestamp": 0.0, "points": host}])
-            t1 = time.perf_counter()
-            k = min(len(host), 20_000)
-            C.pcd_ascii_bytes(host[:k])
-            t2 = time.perf_counter()
-            rep["cpu_baseline"] = {"lvx_Mpoints_s": len(host) / (t1 - t0) / 1e6,
-                                   "pcd_Mpoints_s": k / (t2 - t1) / 1e6, "cores": 1, "kind": "port",
-                                   "sample": f"LVX 1 frame x {len(host)} pts (vectorised numpy oracle), "
-                                             f"PCD {k} pts (Python float formatting, as the reference)"}
-    finally:
-        src.close()
+    ctx.timing(False)
+    ms = ctx.read_timing()["codec_ms"] / reps
+    out.close()
+    text = int(bpos[-1])
+    alg = 16 * n_rank + text
+    rep["pcd_ascii"] = {"text_bytes": text, "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
+                        "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
+                        "bytes_per_point": alg / n_rank, "note": "measure + write passes",
+                        "traffic_over_algorithmic": aux_traffic("k_pcd_measure", "k_pcd_write")}
+    if cpu_budget > 0:
+        from oracle import codecs as C
+        host = b_out.download_aos()[:int(counts[0])]
+        t0 = time.perf_counter()
+        C.lvx_bytes([{"frame_id": 0, "timestamp": 0.0, "points": host}])
+        t1 = time.perf_counter()
+        k = min(len(host), 20_000)
+        C.pcd_ascii_bytes(host[:k])
+        t2 = time.perf_counter()
+        rep["cpu_baseline"] = {"lvx_Mpoints_s": len(host) / (t1 - t0) / 1e6,
+                               "pcd_Mpoints_s": k / (t2 - t1) / 1e6, "cores": 1, "kind": "port",
+                               "sample": f"LVX 1 frame x {len(host)} pts (vectorised numpy oracle), "
+                                         f"PCD {k} pts (Python float formatting, as the reference)"}
     return rep
 
 

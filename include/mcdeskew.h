@@ -172,6 +172,14 @@ int mc_lvx_encode(mc_ctx* ctx, const double* d_aos, int64_t ld, int32_t n_frames
  * written.  |value| >= 2^107 -> MC_ERR_INVALID (beyond the device formatter). */
 int mc_pcd_encode(mc_ctx* ctx, const double* d_aos, int64_t ld, int32_t n_frames, const int64_t* counts,
                   void* d_out, int64_t out_bytes, int64_t* body_pos);
+/* The same two encoders reading a batch's own float32 columns in HBM (frames = the batch's frames,
+ * 4 columns, intensity present): the bytes mc_lvx_encode / mc_pcd_encode produce from the batch's
+ * values widened to float64 (mc_batch_fetch_aos_f64_device), without that 48 B/point pass and
+ * with 16 instead of 32 B/point read.  The writers behind save_results (LMC:887-921) and the
+ * LVX export (LMC:24-272) on a device-resident, deskewed batch. */
+int mc_lvx_encode_batch(mc_ctx* ctx, const mc_batch* b, const uint64_t* frame_ids, const uint64_t* timestamp_ns,
+                        void* d_out, int64_t out_bytes);
+int mc_pcd_encode_batch(mc_ctx* ctx, const mc_batch* b, void* d_out, int64_t out_bytes, int64_t* body_pos);
 int mc_timing_read_codec(mc_ctx* ctx, double* ms_total, int64_t* launches);
 
 /* Synthetic Mid-70 frames generated on the device (counter-hash RNG, bit-identical to

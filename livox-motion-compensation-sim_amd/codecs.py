@@ -102,18 +102,21 @@ def encode_lvx(frames_data: List[dict], context: Context | None = None) -> bytes
 
 
 def encode_lvx_batch(batch: Batch, frame_ids, timestamps) -> bytes:
-    """LVX file of a device batch's frames (f32 columns widened to f64 on the device by the stager,
-    so records are those of the reference writer applied to ``batch.download_aos()``)."""
+    """LVX file of a device batch's frames, encoded from the batch's float32 columns in HBM
+    (mc_lvx_encode_batch): the records of the reference writer applied to ``batch.download_aos()``."""
     ctx = batch.ctx
-    buf = ctx.device_buffer(max(batch.n_points * 32, 8))
+    if len(frame_ids) != batch.n_frames or len(timestamps) != batch.n_frames:
+        raise ValueError("one frame id and one timestamp per frame expected")
+    ids = np.array([_u64(i, "frame_id") for i in frame_ids], np.uint64)
+    ts = np.array([_u64(int(t * 1e9), "timestamp_ns") for t in timestamps], np.uint64)
+    size = int(lvx_layout(batch.counts)[-1])
+    out = ctx.device_buffer(size)
     try:
-        if batch.n_points:
-            batch.fetch_aos_device(buf)
-        ids = [_u64(i, "frame_id") for i in frame_ids]
-        ts = [_u64(int(t * 1e9), "timestamp_ns") for t in timestamps]
-        return _lvx_encode_device(ctx, buf.ptr, 4, batch.counts, ids, ts, None).tobytes()
+        check(ctx.lib.mc_lvx_encode_batch(ctx.handle, batch.handle, ptr(ids, c_uint64), ptr(ts, c_uint64), out.ptr,
+                                          size), "lvx_encode_batch")
+        return out.to_host(np.uint8).tobytes()
     finally:
-        buf.close()
+        out.close()
 
 
 class LivoxLVXWriter:
@@ -205,16 +208,26 @@ def encode_pcd(points, context: Context | None = None) -> bytes:
 
 
 def encode_pcd_batch(batch: Batch) -> List[bytes]:
-    """PCD bytes of every frame of a device batch (the reference writer applied to the batch's
-    values widened to float64)."""
+    """PCD bytes of every frame of a device batch, formatted from the batch's float32 columns in HBM
+    (mc_pcd_encode_batch): the reference writer applied to the values widened to float64."""
     ctx = batch.ctx
-    buf = ctx.device_buffer(max(batch.n_points * 32, 8))
-    try:
-        if batch.n_points:
-            batch.fetch_aos_device(buf)
-        return _pcd_encode_device(ctx, buf.ptr, 4, batch.counts)
-    finally:
-        buf.close()
+    counts = np.ascontiguousarray(batch.counts, np.int64)
+    F = len(counts)
+    pos = np.zeros(F + 1, np.int64)
+    cap = max(int(counts.sum()) * 48, 64)
+    for _ in range(2):
+        out = ctx.device_buffer(cap)
+        try:
+            rc = ctx.lib.mc_pcd_encode_batch(ctx.handle, batch.handle, out.ptr, cap, ptr(pos, c_int64))
+            if rc == _lib.MC_ERR_SPACE:
+                cap = int(pos[-1])
+                continue
+            check(rc, "pcd_encode_batch")
+            text = out.to_host(np.uint8, count=int(pos[-1])).tobytes() if pos[-1] else b""
+        finally:
+            out.close()
+        return [pcd_header(c) + text[pos[f]:pos[f + 1]] for f, c in enumerate(counts)]
+    raise _lib.McError("pcd_encode_batch: output size changed between passes")
 
 
 def save_pcd(points, filename: str, context: Context | None = None) -> None:

@@ -59,6 +59,32 @@ size_t put(std::vector<uint8_t>& blob, const T* src, size_t n) {
   return at;
 }
 
+// where the points come from: a device (N, ld) float64 AoS array or a batch's blocked columns
+struct Source {
+  const double* aos = nullptr;
+  int64_t ld = 4;
+  const mc_batch* batch = nullptr;
+};
+
+CodecFrames frames_of(const Source& src, const int64_t* d_doff, const int64_t* d_units, int32_t F, int64_t n_units) {
+  CodecFrames cf;
+  cf.aos = src.aos;
+  cf.ld = src.batch ? 4 : src.ld;
+  cf.cols = src.batch ? src.batch->d_cols : nullptr;
+  cf.C = src.batch ? src.batch->C : 0;
+  cf.poff = src.batch ? src.batch->d_poff : nullptr;
+  cf.doff = d_doff;
+  cf.unit_off = d_units;
+  cf.F = F;
+  cf.n_units = n_units;
+  return cf;
+}
+
+int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, const uint64_t* frame_ids,
+               const uint64_t* ts_ns, const uint8_t* has_int, void* d_out, int64_t out_bytes);
+int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, void* d_out, int64_t out_bytes,
+               int64_t* body_pos);
+
 }  // namespace
 
 extern "C" {
@@ -78,10 +104,31 @@ int mc_lvx_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
                   int64_t out_bytes) {
   CHECK_ARG(c && d_out, "NULL argument");
   if (ld < 3) return fail(MC_ERR_INDEX, "LVX points need at least 3 columns; got %lld", (long long)ld);
+  Source src;
+  src.aos = d_aos;
+  src.ld = ld;
+  return lvx_encode(c, src, F, counts, frame_ids, ts_ns, has_int, d_out, out_bytes);
+}
+
+int mc_lvx_encode_batch(mc_ctx* c, const mc_batch* b, const uint64_t* frame_ids, const uint64_t* ts_ns, void* d_out,
+                        int64_t out_bytes) {
+  CHECK_ARG(c && b && d_out, "NULL argument");
+  CHECK_ARG(b->ctx == c, "batch belongs to another context");
+  Source src;
+  src.batch = b;
+  return lvx_encode(c, src, b->F, b->counts.data(), frame_ids, ts_ns, nullptr, d_out, out_bytes);
+}
+
+}  // extern "C"
+
+namespace {
+
+int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, const uint64_t* frame_ids,
+               const uint64_t* ts_ns, const uint8_t* has_int, void* d_out, int64_t out_bytes) {
   std::vector<int64_t> doff;
   if (int r = check_frames(F, counts, doff)) return r;
   CHECK_ARG(F == 0 || (frame_ids && ts_ns), "frame_ids / timestamp_ns are NULL");
-  CHECK_ARG(doff[F] == 0 || d_aos, "points pointer is NULL");
+  CHECK_ARG(doff[F] == 0 || src.aos || src.batch, "points pointer is NULL");
   CHECK_ARG(((uintptr_t)d_out & 1) == 0, "d_out must be 2-byte aligned");
   std::vector<int64_t> pos((size_t)F + 1), units((size_t)F + 1, 0);
   mc_lvx_layout(F, counts, pos.data());
@@ -108,8 +155,8 @@ int mc_lvx_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
   HIPCHK(hipMemsetAsync(c->d_codec_err, 0, sizeof(int), c->stream));
 
   LvxArgs a;
-  a.src = CodecFrames{d_aos, ld, reinterpret_cast<const int64_t*>(d + o_doff),
-                      reinterpret_cast<const int64_t*>(d + o_unit), F, n_pkg};
+  a.src = frames_of(src, reinterpret_cast<const int64_t*>(d + o_doff), reinterpret_cast<const int64_t*>(d + o_unit),
+                    F, n_pkg);
   a.frame_pos = reinterpret_cast<const int64_t*>(d + o_pos);
   a.frame_id = reinterpret_cast<const uint64_t*>(d + o_ids);
   a.ts_ns = reinterpret_cast<const uint64_t*>(d + o_ts);
@@ -132,13 +179,37 @@ int mc_lvx_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
   return MC_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
 int mc_pcd_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const int64_t* counts, void* d_out,
                   int64_t out_bytes, int64_t* body_pos) {
   CHECK_ARG(c && body_pos, "NULL argument");
   if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 0 with size %lld", (long long)ld);
+  Source src;
+  src.aos = d_aos;
+  src.ld = ld;
+  return pcd_encode(c, src, F, counts, d_out, out_bytes, body_pos);
+}
+
+int mc_pcd_encode_batch(mc_ctx* c, const mc_batch* b, void* d_out, int64_t out_bytes, int64_t* body_pos) {
+  CHECK_ARG(c && b && body_pos, "NULL argument");
+  CHECK_ARG(b->ctx == c, "batch belongs to another context");
+  Source src;
+  src.batch = b;
+  return pcd_encode(c, src, b->F, b->counts.data(), d_out, out_bytes, body_pos);
+}
+
+}  // extern "C"
+
+namespace {
+
+int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, void* d_out, int64_t out_bytes,
+               int64_t* body_pos) {
   std::vector<int64_t> doff;
   if (int r = check_frames(F, counts, doff)) return r;
-  CHECK_ARG(doff[F] == 0 || d_aos, "points pointer is NULL");
+  CHECK_ARG(doff[F] == 0 || src.aos || src.batch, "points pointer is NULL");
   std::vector<int64_t> units((size_t)F + 1, 0);
   for (int32_t f = 0; f < F; ++f) units[f + 1] = units[f] + (counts[f] + kCodecBlock - 1) / kCodecBlock;
   const int64_t n_tiles = units[F];
@@ -160,8 +231,8 @@ int mc_pcd_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
   HIPCHK(hipMemcpyAsync(d, blob.data(), o_tb, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemsetAsync(c->d_codec_err, 0, sizeof(int), c->stream));
   PcdArgs a;
-  a.src = CodecFrames{d_aos, ld, reinterpret_cast<const int64_t*>(d + o_doff),
-                      reinterpret_cast<const int64_t*>(d + o_unit), F, n_tiles};
+  a.src = frames_of(src, reinterpret_cast<const int64_t*>(d + o_doff), reinterpret_cast<const int64_t*>(d + o_unit),
+                    F, n_tiles);
   a.tile_bytes = reinterpret_cast<int32_t*>(d + o_tb);
   a.tile_pos = reinterpret_cast<const int64_t*>(d + o_tp);
   a.out = static_cast<char*>(d_out);
@@ -196,6 +267,10 @@ int mc_pcd_encode(mc_ctx* c, const double* d_aos, int64_t ld, int32_t F, const i
   HIPCHK(hipStreamSynchronize(c->stream));
   return MC_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int mc_timing_read_codec(mc_ctx* c, double* ms, int64_t* n) {
   CHECK_ARG(c, "ctx is NULL");

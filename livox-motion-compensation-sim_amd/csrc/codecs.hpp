@@ -36,7 +36,9 @@ constexpr int kPcdTilesPerWG = 4;                               // PCD tiles of 
 constexpr int kPcdTileText = 16384;                             // LDS text buffer per tile
 
 struct CodecFrames {
-  const double* aos; int64_t ld;
+  const double* aos; int64_t ld;   // (N, ld) float64 AoS source, or
+  const float* cols; int32_t C;    // a batch's blocked float32 columns (cols != null; ld = 4)
+  const int64_t* poff;             // [F+1] the batch's padded frame offsets
   const int64_t* doff;       // [F+1] dense row offset of each frame
   const int64_t* unit_off;   // [F+1] prefix of per-frame units
   int32_t F;
@@ -51,6 +53,26 @@ __device__ __forceinline__ int32_t codec_frame_of(const int64_t* __restrict__ un
     if (unit_off[mid] <= u) lo = mid + 1; else hi = mid;
   }
   return lo - 1;
+}
+
+// columns 0..3 of dense row `row` (frame f) as float64; ld == 3 leaves c[3] = 0.  A batch source
+// widens its float32 values exactly, so both sources give the bytes of the reference writer applied
+// to the same (N,4) float64 array (Batch.download_aos()).
+__device__ __forceinline__ void codec_point(const CodecFrames& s, int32_t f, int64_t row, double c[4]) {
+  if (s.cols) {
+    const float* q = s.cols + bidx(s.C, 0, s.poff[f] + (row - s.doff[f]));
+    c[0] = q[0]; c[1] = q[kBlkPts]; c[2] = q[2 * kBlkPts]; c[3] = q[3 * kBlkPts];
+    return;
+  }
+  const double* q = s.aos + row * s.ld;
+  if (s.ld == 4) {
+    const double2 p01 = *reinterpret_cast<const double2*>(q);
+    const double2 p23 = *reinterpret_cast<const double2*>(q + 2);
+    c[0] = p01.x; c[1] = p01.y; c[2] = p23.x; c[3] = p23.y;
+  } else {
+    c[0] = q[0]; c[1] = q[1]; c[2] = q[2];
+    c[3] = s.ld > 3 ? q[3] : 0.0;
+  }
 }
 
 // advance a workgroup-uniform frame cursor to unit u (units of a workgroup are consecutive)
@@ -112,28 +134,19 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   const int shift = (int)(S & 15);
   const uint64_t ts = a.ts_ns[f];
   const bool hi = a.has_int ? a.has_int[f] != 0 : a.src.ld > 3;
-  const int64_t ld = a.src.ld;
-  const double* __restrict__ base = a.src.aos + (frow + pkg0 * kLvxPkgPoints) * ld;
+  const int64_t row0 = frow + pkg0 * kLvxPkgPoints;
 
   for (int i = threadIdx.x; i < k * kLvxPkgPoints; i += kCodecBlock) {
     const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
     uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
     uint32_t x = 0, y = 0, z = 0, refl = 0;
     if (i < n) {
-      const double* q = base + (int64_t)i * ld;
-      double v0, v1, v2, v3 = 0.0;
-      if (ld == 4) {
-        const double2 p01 = *reinterpret_cast<const double2*>(q);
-        const double2 p23 = *reinterpret_cast<const double2*>(q + 2);
-        v0 = p01.x; v1 = p01.y; v2 = p23.x; v3 = p23.y;
-      } else {
-        v0 = q[0]; v1 = q[1]; v2 = q[2];
-        if (ld > 3) v3 = q[3];
-      }
-      x = (uint32_t)lvx_fixed(v0, 1000.0, -2147483648.0, 2147483647.0, a.err);
-      y = (uint32_t)lvx_fixed(v1, 1000.0, -2147483648.0, 2147483647.0, a.err);
-      z = (uint32_t)lvx_fixed(v2, 1000.0, -2147483648.0, 2147483647.0, a.err);
-      refl = hi ? (uint32_t)lvx_fixed(v3, 255.0, 0.0, 255.0, a.err) : 128u;   // tag byte 0
+      double v[4];
+      codec_point(a.src, f, row0 + i, v);
+      x = (uint32_t)lvx_fixed(v[0], 1000.0, -2147483648.0, 2147483647.0, a.err);
+      y = (uint32_t)lvx_fixed(v[1], 1000.0, -2147483648.0, 2147483647.0, a.err);
+      z = (uint32_t)lvx_fixed(v[2], 1000.0, -2147483648.0, 2147483647.0, a.err);
+      refl = hi ? (uint32_t)lvx_fixed(v[3], 255.0, 0.0, 255.0, a.err) : 128u;   // tag byte 0
     }
     r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
     r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
@@ -330,15 +343,9 @@ struct PcdLine {
   int len;
 };
 
-__device__ __forceinline__ void pcd_line(const double* __restrict__ q, int64_t ld, PcdLine& L, int* err) {
+__device__ __forceinline__ void pcd_line(const CodecFrames& s, int32_t f, int64_t row, PcdLine& L, int* err) {
   double c[4];
-  if (ld == 4) {
-    const double2 p01 = *reinterpret_cast<const double2*>(q);
-    const double2 p23 = *reinterpret_cast<const double2*>(q + 2);
-    c[0] = p01.x; c[1] = p01.y; c[2] = p23.x; c[3] = p23.y;
-  } else {
-    c[0] = q[0]; c[1] = q[1]; c[2] = q[2]; c[3] = q[3];
-  }
+  codec_point(s, f, row, c);
   L.len = 4;                                       // 3 separators + newline
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -397,7 +404,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
     int len = 0;
     if (valid) {
       PcdLine L;
-      pcd_line(a.src.aos + row * a.src.ld, a.src.ld, L, a.err);
+      pcd_line(a.src, f, row, L, a.err);
       len = L.len;
     }
     int total;
@@ -423,7 +430,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
     const int64_t row = pcd_row(a.src, u, f, valid);
     PcdLine L;
     L.len = 0;
-    if (valid) pcd_line(a.src.aos + row * a.src.ld, a.src.ld, L, a.err);
+    if (valid) pcd_line(a.src, f, row, L, a.err);
     int total;
     const int incl = block_scan(L.len, s_wave, total);
     const int excl = incl - L.len;

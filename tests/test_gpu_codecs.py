@@ -94,6 +94,39 @@ def test_codecs_from_device_batch(mc, gpu_ctx):
     assert lvx == ref
 
 
+@pytest.mark.parametrize("with_time", [False, True])
+def test_batch_source_encoders_match_f64_source(mc, gpu_ctx, with_time):
+    """mc_*_encode_batch read the batch's blocked float32 columns (4 or 5 per block); their bytes
+    must equal the f64-AoS encoders' on the same values: ragged frames across block boundaries,
+    half-way ties, inf, large magnitudes."""
+    rng = np.random.default_rng(8)
+    counts = np.array([255, 256, 257, 0, 1, 70_001], np.int64)
+    n = int(counts.sum())
+    pts = rng.normal(0, 50, (n, 4))
+    pts[:300] = rng.integers(-2 ** 20, 2 ** 20, (300, 4)) / 128.0          # exact f32 ties at 1e-6
+    pts[300:310] = np.array([np.inf, -np.inf, 1e30, -3.4e30])[rng.integers(0, 4, (10, 4))]
+    fin = np.isfinite(pts[:, 3])
+    pts[fin, 3] = np.abs(pts[fin, 3]) % 1.0                                 # inf stays inf
+    b = gpu_ctx.batch(counts, with_time=with_time)
+    b.upload_aos(pts)
+    host = b.split(b.download_aos())
+    assert [len(h) for h in host] == list(counts)
+    assert mc.codecs.encode_pcd_batch(b) == mc.codecs.encode_pcd_frames(host, gpu_ctx)
+    assert mc.codecs.encode_pcd_batch(b)[1] == C.pcd_ascii_bytes(host[1])
+    ok = np.isfinite(pts).all(axis=1) & (np.abs(pts) < 2e6).all(axis=1)
+    b2 = gpu_ctx.batch(counts, with_time=with_time)
+    b2.upload_aos(np.where(ok[:, None], pts, 1.5))
+    h2 = b2.split(b2.download_aos())
+    ids, ts = np.arange(6) + 40, np.arange(6) * 0.05
+    lvx = mc.codecs.encode_lvx_batch(b2, ids, ts)
+    assert lvx == mc.codecs.encode_lvx([{"frame_id": i, "timestamp": t, "points": h}
+                                        for i, t, h in zip(ids, ts, h2)], gpu_ctx)
+    nan = gpu_ctx.batch([3])
+    nan.upload_aos(np.array([[1.0, np.nan, 0, 0.5], [0, 0, 0, 0], [1, 1, 1, 1]]))
+    with pytest.raises(ValueError):                 # the reference's int(nan) (LMC:259)
+        mc.codecs.encode_lvx_batch(nan, [0], [0.0])
+
+
 def test_simulator_save_lvx_and_pcd(mc, gpu_ctx, tmp_path):
     sim = mc.LiDARMotionSimulator(context=gpu_ctx)
     rng = np.random.default_rng(1)

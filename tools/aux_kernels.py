@@ -40,16 +40,15 @@ def main():
     ids = np.arange(args.frames, dtype=np.uint64)
     ts = (np.arange(args.frames) * 100_000_000).astype(np.uint64)
     out = ctx.device_buffer(int(pos[-1]))
-    for _ in range(args.reps):
-        mc._lib.check(ctx.lib.mc_lvx_encode(ctx.handle, src.ptr, 4, args.frames, ptr(counts, c_int64),
-                                            ptr(ids, c_uint64), ptr(ts, c_uint64), None, out.ptr, int(pos[-1])))
+    for _ in range(args.reps):                 # from the batch's float32 columns (16 B / point read)
+        mc._lib.check(ctx.lib.mc_lvx_encode_batch(ctx.handle, b.handle, ptr(ids, c_uint64), ptr(ts, c_uint64),
+                                                  out.ptr, int(pos[-1])))
     out.close()
     cap = n * 48
     out = ctx.device_buffer(cap)
     bpos = np.zeros(args.frames + 1, np.int64)
     for _ in range(args.reps):
-        mc._lib.check(ctx.lib.mc_pcd_encode(ctx.handle, src.ptr, 4, args.frames, ptr(counts, c_int64), out.ptr,
-                                            cap, ptr(bpos, c_int64)))
+        mc._lib.check(ctx.lib.mc_pcd_encode_batch(ctx.handle, b.handle, out.ptr, cap, ptr(bpos, c_int64)))
     out.close()
     rng = np.random.default_rng(7)
     E = 29_000
@@ -69,8 +68,8 @@ def main():
     bits = ((E + 1023) // 1024) * ((F + 7) // 8) * 256 * 4      # pass-1 visibility words
     alg = {
         "k_soa_to_aos": 48 * n, "k_aos_to_soa": 48 * n,
-        "k_lvx_packages": 32 * n + int(pos[-1]) - 88 - 24 * args.frames,
-        "k_pcd_measure": 32 * n, "k_pcd_write": 32 * n + int(bpos[-1]),
+        "k_lvx_packages": 16 * n + int(pos[-1]) - 88 - 24 * args.frames,
+        "k_pcd_measure": 16 * n, "k_pcd_write": 16 * n + int(bpos[-1]),
         "k_scan_count": 24 * E + bits, "k_scan_emit": 24 * E + bits + 16 * int(scans.n_points),
     }
     print(json.dumps({"algorithmic_bytes_per_launch": alg, "points": n, "scene": E, "frames_scanned": len(times),
