@@ -17,6 +17,7 @@ import json
 import os
 import socket
 import struct
+import sys
 import time
 from ctypes import c_char, c_double, c_void_p
 
@@ -173,7 +174,17 @@ class RcclComm:
         data = rdv.broadcast_bytes(bytes(uid) if rdv.rank == 0 else None)
         uid = (c_char * 128).from_buffer_copy(data)
         h = c_void_p()
-        check(self.lib.mc_comm_init(ctx.handle, rdv.world_size, rdv.rank, uid, ctypes.byref(h)), "comm_init")
+        # librccl prints its version banner on stdout during init; keep stdout for the caller's
+        # output (bench.py's one JSON line) by pointing fd 1 at stderr meanwhile
+        sys.stdout.flush()
+        saved = os.dup(1)
+        try:
+            os.dup2(2, 1)
+            rc = self.lib.mc_comm_init(ctx.handle, rdv.world_size, rdv.rank, uid, ctypes.byref(h))
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+        check(rc, "comm_init")
         self.handle = h
 
     def gather_batch(self, local, merged=None, root: int = 0):
