@@ -248,20 +248,42 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   HIPCHK(hipMemcpyAsync(&err, c->d_codec_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (err) return fail(MC_ERR_INVALID, "a value has |v| >= 2^107, beyond the device %%.6f formatter");
+  // tiles holding a line outside the packed path (kPcdSlowTile) go to the byte-path kernel
   std::vector<int64_t> tpos((size_t)n_tiles);
+  std::vector<int32_t> slow;
   int64_t run = 0;
   for (int32_t f = 0; f < F; ++f) {
     body_pos[f] = run;
-    for (int64_t t = units[f]; t < units[f + 1]; ++t) { tpos[t] = run; run += tb[t]; }
+    for (int64_t t = units[f]; t < units[f + 1]; ++t) {
+      if (tb[t] & kPcdSlowTile) slow.push_back((int32_t)t);
+      tpos[t] = run;
+      run += tb[t] & ~kPcdSlowTile;
+    }
   }
   body_pos[F] = run;
   if (out_bytes < run)
     return fail(MC_ERR_SPACE, "PCD text needs %lld bytes, buffer has %lld", (long long)run, (long long)out_bytes);
   CHECK_ARG(d_out, "d_out is NULL");
   HIPCHK(hipMemcpyAsync(d + o_tp, tpos.data(), tpos.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-  {
+  const dim3 grid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
+  if (!MC_PCD_PACKED) {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    hipLaunchKernelGGL(k_pcd_write, dim3((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG)), dim3(kCodecBlock), 0, c->stream, a);
+    hipLaunchKernelGGL(k_pcd_write_bytes, grid, dim3(kCodecBlock), 0, c->stream, a, (const int32_t*)nullptr);
+  } else {
+    {
+      TimedRegion tr(c, &c->codec_ev, c->stream);
+      hipLaunchKernelGGL(k_pcd_write, grid, dim3(kCodecBlock), 0, c->stream, a);
+    }
+    HIPCHK(hipGetLastError());
+    if (!slow.empty()) {
+      // the list rides in the scratch blob's tile-byte slots, which k_pcd_write has finished reading
+      // (same stream); the byte path reads no tile bytes
+      HIPCHK(hipMemcpyAsync(a.tile_bytes, slow.data(), slow.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                            c->stream));
+      TimedRegion tr(c, &c->codec_ev, c->stream);
+      hipLaunchKernelGGL(k_pcd_write_bytes, dim3((uint32_t)slow.size()), dim3(kCodecBlock), 0, c->stream, a,
+                         (const int32_t*)a.tile_bytes);
+    }
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

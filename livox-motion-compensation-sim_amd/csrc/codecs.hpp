@@ -392,6 +392,145 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   return x + before;
 }
 
+// ---- packed line path (every value of the line |v| < 4294 and not within 1e-6 of a tie) -------
+// The common LiDAR line is formatted from four 32-bit integers N = round(|v| * 10^6): its text is
+// assembled in registers (digits packed four to a dword with multiply-shift division) and written to
+// LDS as dwords (ds_write2_b32), instead of ~40 single-byte LDS stores per line.  Lines share
+// their first and last dwords with their neighbours: those go through ds_or_b32 into a zeroed
+// buffer.  Lines with any other value take the byte path (fmt6_prepare / pcd_emit).
+#ifndef MC_PCD_PACKED
+#define MC_PCD_PACKED 1
+#endif
+#ifndef MC_PCD_FORCE_SLOW
+#define MC_PCD_FORCE_SLOW 0  // diagnostic: every tile through the byte path (slow-tile list)
+#endif
+
+struct PcdFast {
+  uint32_t n[4];   // round-half-even(|v| * 10^6)
+  uint32_t neg;    // bit k: value k is negative (signbit)
+  int len;         // line length in bytes
+  bool ok;         // all four values took the fast path
+};
+
+__device__ __forceinline__ int fast_nd(uint32_t n) {
+  const uint32_t ip = n / 1000000u;
+  return 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
+}
+
+// N = round-half-even(|v| * 10^6) exactly, for |v| < 4294 (NaN / larger values fail the test).
+// y = fl(a * 10^6) and e = fma(a, 10^6, -y) represent the exact product as y + e; fr = y - floor(y)
+// and fr - 0.5 are exact, so d = (fr - 0.5) + e has the sign of the exact fraction minus one half
+// (rounding preserves signs) and is zero only on an exact tie, which rounds to even.  Exact ties are
+// common in float32-valued clouds (any odd multiple of 1/128).
+__device__ __forceinline__ bool fmt6_fast(double v, uint32_t& n) {
+  const double a = fmin(fabs(v), 4294.0);
+  const double y = a * 1000000.0;
+  const double e = fma(a, 1000000.0, -y);
+  const double fl = floor(y);
+  const double d = ((y - fl) - 0.5) + e;
+  const uint32_t m = (uint32_t)fl;
+  n = m + ((d > 0.0 || (d == 0.0 && (m & 1u))) ? 1u : 0u);
+  return fabs(v) < 4294.0;
+}
+
+__device__ __forceinline__ void pcd_fast(const CodecFrames& s, int32_t f, int64_t row, PcdFast& P) {
+  double c[4];
+  codec_point(s, f, row, c);
+  P.ok = true;
+  P.neg = 0;
+  P.len = 4 + 4 * 7;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    P.ok &= fmt6_fast(c[k], P.n[k]);
+    const uint32_t ng = signbit(c[k]) ? 1u : 0u;
+    P.neg |= ng << k;
+    P.len += (int)ng + fast_nd(P.n[k]);
+  }
+}
+
+// three decimal digits of x < 1000 as characters in bytes 0..2 (most significant first)
+__device__ __forceinline__ uint32_t pack3(uint32_t x) {
+  const uint32_t h = __umul24(x, 41u) >> 12;
+  const uint32_t r = x - h * 100u;
+  const uint32_t t = __umul24(r, 103u) >> 10;
+  return (h | (t << 8) | ((r - t * 10u) << 16)) + 0x303030u;
+}
+
+// byte stream into LDS dwords, 32-bit operations only: `w` holds the n < 4 pending bytes that start
+// at dword `pos`; every completed dword is stored at once.  (A first version kept up to 7 pending
+// bytes in a 64-bit register and shifted by up to 56 bits: whole waves then wrote some fields at the
+// wrong place on gfx950, tools/pcd_check.py — so no 64-bit variable shifts here.)
+struct LdsLine {
+  uint32_t* base;
+  uint32_t w;
+  int n, pos;
+  bool first;
+  // append the k <= 4 bytes of x (bytes above k are zero)
+  __device__ __forceinline__ void put(uint32_t x, int k) {
+    const int sh = 8 * n;
+    w |= x << sh;
+    const uint32_t spill = (x >> 1) >> (31 - sh);   // the bytes beyond the dword (0 when sh == 0)
+    n += k;
+    if (n >= 4) {
+      if (first) {   // shared with the previous line
+        __hip_atomic_fetch_or(base + pos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        first = false;
+      } else {
+        base[pos] = w;
+      }
+      ++pos;
+      w = spill;
+      n -= 4;
+    }
+  }
+  // a partial last dword is shared with the next line
+  __device__ __forceinline__ void finish() {
+    if (n > 0) __hip_atomic_fetch_or(base + pos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+};
+
+// "%.6f" of one fast value plus its separator, appended to the line
+__device__ __forceinline__ void fast_value(LdsLine& w, uint32_t n, bool neg, uint32_t sep) {
+  const uint32_t ip = n / 1000000u, fp = n - ip * 1000000u;
+  const int nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
+  // integer digits (ip < 10^4): thousands | hundreds | tens | units, keep the last nd
+  const uint32_t th = __umul24(ip, 8389u) >> 23;
+  const uint32_t d4 = ((th + 0x30u) | (pack3(ip - th * 1000u) << 8)) >> (8 * (4 - nd));
+  // [-] digits '.': nd + 1 (+1) <= 6 bytes, as a 4-byte and a 0..2-byte piece
+  uint32_t h0, h1;
+  if (neg) {
+    h0 = '-' | (d4 << 8);
+    h1 = nd == 4 ? (d4 >> 24) | ('.' << 8) : (nd == 3 ? '.' : 0u);
+    if (nd < 3) h0 |= (uint32_t)'.' << (8 * (nd + 1));
+  } else {
+    h0 = nd == 4 ? d4 : d4 | ((uint32_t)'.' << (8 * nd));
+    h1 = nd == 4 ? '.' : 0u;
+  }
+  const int hl = nd + 1 + (neg ? 1 : 0);
+  w.put(h0, hl < 4 ? hl : 4);
+  w.put(h1, hl - 4 > 0 ? hl - 4 : 0);
+  const uint32_t fh = fp / 1000u;
+  const uint32_t f0 = pack3(fh), f1 = pack3(fp - fh * 1000u);
+  w.put(f0 | (f1 << 24), 4);                    // 3 digits + first of the next 3
+  w.put((f1 >> 8) | (sep << 16), 3);            // 2 digits + separator
+}
+
+__device__ __forceinline__ void pcd_emit_fast(const PcdFast& P, uint32_t* base, int off) {
+  LdsLine w;
+  w.base = base;
+  w.n = off & 3;
+  w.pos = off >> 2;
+  w.w = 0;
+  w.first = true;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fast_value(w, P.n[k], (P.neg >> k) & 1u, k < 3 ? ' ' : '\n');
+  w.finish();
+}
+
+// Tile flag: k_pcd_measure marks a tile holding any line outside the packed path by this bit of its
+// byte count; the host sends those tiles to k_pcd_write_bytes and the rest to k_pcd_write.
+constexpr int32_t kPcdSlowTile = 1 << 30;
+
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
@@ -402,28 +541,71 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
     bool valid;
     const int64_t row = pcd_row(a.src, u, f, valid);
     int len = 0;
+    bool slow = false;
     if (valid) {
-      PcdLine L;
-      pcd_line(a.src, f, row, L, a.err);
-      len = L.len;
+      PcdFast P;
+      pcd_fast(a.src, f, row, P);
+      len = P.len;
+      if (!P.ok) {
+        PcdLine L;
+        pcd_line(a.src, f, row, L, a.err);
+        len = L.len;
+        slow = true;
+      }
     }
+    const bool any_slow = __syncthreads_or(slow);
     int total;
     block_scan(len, s_wave, total);
-    if (threadIdx.x == 0) a.tile_bytes[u] = total;
+    if (threadIdx.x == 0) a.tile_bytes[u] = total | (any_slow || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
     __syncthreads();   // s_wave is reused by the next tile
   }
 }
 
-// every tile formats its lines into LDS (at the tile's HBM offset modulo 16) and stores the text
-// with codec_store_piece; a tile larger than the LDS buffer — only possible with extreme
-// magnitudes — is written line by line straight to HBM instead
+// Packed tiles: every line is formatted in registers and written to LDS as dwords (the tile's text
+// sits at its HBM offset modulo 16), then stored with codec_store_piece.  Tiles flagged slow are
+// skipped (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text
+// always fits the LDS buffer.
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
-  char* const s_text = reinterpret_cast<char*>(s_text4);
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
   for (int j = 0; j < kPcdTilesPerWG; ++j) {
+    const int64_t u = u0 + j;
+    if (u >= a.src.n_units) break;
+    if (a.tile_bytes[u] & kPcdSlowTile) continue;   // workgroup-uniform
+    bool valid;
+    const int64_t row = pcd_row(a.src, u, f, valid);
+    // zero the text buffer (lines OR the dwords they share), ordered before the line writes by
+    // block_scan's barrier
+    for (int i = threadIdx.x; i < kPcdTileText / 16 + 1; i += kCodecBlock) s_text4[i] = make_uint4(0, 0, 0, 0);
+    PcdFast P;
+    P.len = 0;
+    if (valid) pcd_fast(a.src, f, row, P);
+    int total;
+    const int excl = block_scan(P.len, s_wave, total) - P.len;
+    const int64_t G = a.tile_pos[u];
+    const int shift = (int)(G & 15);
+    if (valid) pcd_emit_fast(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
+    __syncthreads();
+    codec_store_piece(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
+    __syncthreads();   // s_wave / s_text are reused by the next tile
+  }
+}
+
+// Byte path (any %.6f value): every tile formats its lines byte by byte into LDS and stores the
+// text with codec_store_piece; a tile larger than the LDS buffer — only possible with extreme
+// magnitudes — is written line by line straight to HBM instead.  Tiles: list[blockIdx.x], or, with
+// list == nullptr, kPcdTilesPerWG consecutive tiles per workgroup (MC_PCD_PACKED=0: every tile).
+__global__ __launch_bounds__(kCodecBlock) void k_pcd_write_bytes(const PcdArgs a, const int32_t* list) {
+  __shared__ int s_wave[kCodecBlock / 64];
+  __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
+  char* const s_text = reinterpret_cast<char*>(s_text4);
+  const int64_t u0 = list ? (int64_t)list[blockIdx.x]
+                          : xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;
+  const int per = list ? 1 : kPcdTilesPerWG;
+  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  for (int j = 0; j < per; ++j) {
     const int64_t u = u0 + j;
     if (u >= a.src.n_units) break;
     bool valid;

@@ -80,6 +80,29 @@ def test_pcd_batched_frames_long_lines_and_limits(mc, gpu_ctx):
         mc.codecs.encode_pcd(np.zeros((2, 3)), gpu_ctx)
 
 
+def test_pcd_packed_path_digit_boundaries_and_mixed_tiles(mc, gpu_ctx):
+    """The packed line path (|v| < 4294, not within 1e-6 of a %.6f tie) against the oracle: every
+    integer-digit count and sign, values that round across a digit boundary, -0.0, near-ties on
+    either side of the 1e-6 guard, and 256-line tiles holding one byte-path line (first, middle,
+    last line of the tile) beside packed-only tiles."""
+    rng = np.random.default_rng(21)
+    edges = np.array([0.0, -0.0, 1e-7, 4.9e-7, 5e-7, 5.1e-7, 9.9999994, 9.9999995, 9.9999996, 99.9999996,
+                      999.9999996, 999.9999994, 1000.0, 4293.999999, 4293.9999996, 4294.0, 4294.5,
+                      0.1234565, 0.12345650001, 1.0000005, 1.00000049, 12.3456785])
+    edges = np.concatenate([edges, -edges])
+    mags = 10.0 ** rng.uniform(-8, np.log10(4293.9), (40_000, 4))
+    vals = rng.choice([-1.0, 1.0], mags.shape) * mags
+    vals[:len(edges), 0] = edges
+    vals[:len(edges), 1] = edges[::-1]
+    vals[:, 3] = np.where(np.arange(len(vals)) % 3 == 0, rng.uniform(0, 1, len(vals)), vals[:, 3])
+    for pos in (0, 1000, 1279, 256 * 10 + 128, 256 * 20 + 255, 39_999):
+        vals[pos, pos % 4] = 1e7 * (1 + pos)                  # one byte-path line in this tile
+    clouds = [vals[:1], vals[1:256], vals[256:512], vals[512:769], vals[769:], vals[:300] * 0.001]
+    got = mc.codecs.encode_pcd_frames(clouds, gpu_ctx)
+    for c, b in zip(clouds, got):
+        assert b == C.pcd_ascii_bytes(c)
+
+
 def test_codecs_from_device_batch(mc, gpu_ctx):
     counts = np.array([1000, 0, 2500, 96], np.int64)
     b = gpu_ctx.batch(counts, with_time=True)
