@@ -442,6 +442,26 @@ def test_compensator_disabled_and_driver(mc, gpu_ctx):
         assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case)
 
 
+@pytest.mark.parametrize("rate", [2.0, 7.7, 8.5, 30.0])
+def test_imu_small_angle_f32_path_and_threshold(mc, gpu_ctx, rate):
+    """Waves whose angles stay within 0.78 rad take the float32 path, the others the f64 one:
+    constant rates that put theta = rate * dt on either side of the threshold within one 0.1 s
+    frame (time-sorted points, so whole waves land on each side), plus points before the frame
+    start and a rate change between IMU samples; all within the parity bar of the oracle."""
+    rng = np.random.default_rng(int(rate * 10))
+    ts = np.arange(0, 2_000_000_000, 5_000_000, dtype=np.int64)
+    gyro = np.tile(np.array([rate, -0.6 * rate, 0.9 * rate]), (len(ts), 1))
+    gyro[len(ts) // 2 + 3:] *= -1.0                      # rate flip inside the frame window
+    n = 50_000
+    xyz = rng.uniform(-90, 90, (n, 3))
+    start = 1_000_000_000
+    t_abs = np.sort(start + rng.integers(-2_000_000, 100_000_000, n))
+    comp = mc.MotionCompensator({}, context=gpu_ctx)
+    got = comp.compensate_arrays(xyz, t_abs, start, ts, gyro)
+    ref = R.compensate_arrays(xyz, t_abs, start, ts, gyro)
+    assert_scaled_close(got, ref, scale_of(xyz), what=f"rate {rate}")
+
+
 def test_imu_slow_path_wide_subtile(mc, gpu_ctx):
     """1024 points spread over 1.5 s at 200 Hz IMU -> ~300 segments in one sub-tile."""
     rng = np.random.default_rng(4)
