@@ -527,6 +527,26 @@ __device__ __forceinline__ void pcd_emit_fast(const PcdFast& P, uint32_t* base, 
   w.finish();
 }
 
+// The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
+// characters with the separator, nd = 1 + [N >= 10^7] + [N >= 10^8] + [N >= 10^9] for
+// N = round-half-even(|v| 10^6).  N >= T (T even) <=> |v| 10^6 >= T - 1/2 exactly; y = fl(|v| 10^6)
+// decides that except when y lands on T - 1/2, where the product's error e does.  -1: a value
+// outside the packed path.
+__device__ __forceinline__ int pcd_fast_len(const double c[4]) {
+  int len = 4 + 4 * 8;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double a = fabs(c[k]);
+    ok = ok && a < 4294.0;
+    const double y = a * 1000000.0;
+    const bool tie_up = fma(a, 1000000.0, -y) >= 0.0;
+    len += (signbit(c[k]) ? 1 : 0) + (y > 9999999.5 || (y == 9999999.5 && tie_up)) +
+           (y > 99999999.5 || (y == 99999999.5 && tie_up)) + (y > 999999999.5 || (y == 999999999.5 && tie_up));
+  }
+  return ok ? len : -1;
+}
+
 // Tile flag: k_pcd_measure marks a tile holding any line outside the packed path by this bit of its
 // byte count; the host sends those tiles to k_pcd_write_bytes and the rest to k_pcd_write.
 constexpr int32_t kPcdSlowTile = 1 << 30;
@@ -540,23 +560,23 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
     if (u >= a.src.n_units) break;
     bool valid;
     const int64_t row = pcd_row(a.src, u, f, valid);
-    int len = 0;
-    bool slow = false;
+    // scanned value: line bytes + (byte-path line ? 1 << 20 : 0); a tile's bytes stay < 2^20 and
+    // its byte-path line count < 2^11, so one scan yields both (no extra barrier)
+    int v = 0;
     if (valid) {
-      PcdFast P;
-      pcd_fast(a.src, f, row, P);
-      len = P.len;
-      if (!P.ok) {
+      double c[4];
+      codec_point(a.src, f, row, c);
+      v = pcd_fast_len(c);
+      if (v < 0) {
         PcdLine L;
         pcd_line(a.src, f, row, L, a.err);
-        len = L.len;
-        slow = true;
+        v = L.len + (1 << 20);
       }
     }
-    const bool any_slow = __syncthreads_or(slow);
     int total;
-    block_scan(len, s_wave, total);
-    if (threadIdx.x == 0) a.tile_bytes[u] = total | (any_slow || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
+    block_scan(v, s_wave, total);
+    if (threadIdx.x == 0)
+      a.tile_bytes[u] = (total & ((1 << 20) - 1)) | ((total >> 20) || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
     __syncthreads();   // s_wave is reused by the next tile
   }
 }

@@ -22,13 +22,12 @@ sys.path.insert(0, ROOT)
 import mcamd as mc  # noqa: E402
 
 
-def setup(lib, counts):
+def setup(lib, counts, source="aos"):
     ctx = mc.Context(0, lib_path=lib)
     b = ctx.batch(counts)
     b.synth(seed=0, frame_id_base=1000)
     src = ctx.device_buffer(int(counts.sum()) * 32)
     b.fetch_aos_device(src)
-    b.close()
     F = len(counts)
     pos = mc.codecs.lvx_layout(counts)
     lvx_out = ctx.device_buffer(int(pos[-1]))
@@ -40,14 +39,22 @@ def setup(lib, counts):
     ptr = mc._lib.ptr
 
     def lvx():
+        if source == "batch":   # the batch's own float32 columns (mc_lvx_encode_batch)
+            mc._lib.check(ctx.lib.mc_lvx_encode_batch(ctx.handle, b.handle, ptr(ids, c_uint64), ptr(ts, c_uint64),
+                                                      lvx_out.ptr, int(pos[-1])), "lvx_encode_batch")
+            return
         mc._lib.check(ctx.lib.mc_lvx_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), ptr(ids, c_uint64),
                                             ptr(ts, c_uint64), None, lvx_out.ptr, int(pos[-1])), "lvx_encode")
 
     def pcd():
+        if source == "batch":
+            mc._lib.check(ctx.lib.mc_pcd_encode_batch(ctx.handle, b.handle, pcd_out.ptr, cap, ptr(bpos, c_int64)),
+                          "pcd_encode_batch")
+            return
         mc._lib.check(ctx.lib.mc_pcd_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), pcd_out.ptr, cap,
                                             ptr(bpos, c_int64)), "pcd_encode")
 
-    return {"ctx": ctx, "lvx": lvx, "pcd": pcd, "lvx_out": lvx_out, "pcd_out": pcd_out, "bpos": bpos,
+    return {"ctx": ctx, "batch": b, "lvx": lvx, "pcd": pcd, "lvx_out": lvx_out, "pcd_out": pcd_out, "bpos": bpos,
             "lvx_bytes": int(pos[-1])}
 
 
@@ -58,10 +65,12 @@ def main():
     ap.add_argument("--points", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--source", default="aos", choices=["aos", "batch"],
+                    help="encode from a device (N,4) float64 AoS array or from the batch's float32 columns")
     args = ap.parse_args()
     libs = [l for l in args.libs.split(",") if l]
     counts = np.full(args.frames, args.points, np.int64)
-    arms = {lib: setup(lib, counts) for lib in libs}
+    arms = {lib: setup(lib, counts, args.source) for lib in libs}
     times = {lib: {"lvx": [], "pcd": []} for lib in libs}
     order = list(libs)
     rng = random.Random(1)
