@@ -401,6 +401,9 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
 #ifndef MC_PCD_PACKED
 #define MC_PCD_PACKED 1
 #endif
+#ifndef MC_PCD_DIAG
+#define MC_PCD_DIAG 0        // diagnostic timing builds (wrong output): 1 no LDS text stores, 2 no digit math
+#endif
 #ifndef MC_PCD_FORCE_SLOW
 #define MC_PCD_FORCE_SLOW 0  // diagnostic: every tile through the byte path (slow-tile list)
 #endif
@@ -467,6 +470,10 @@ struct LdsLine {
   bool first;
   // append the k <= 4 bytes of x (bytes above k are zero)
   __device__ __forceinline__ void put(uint32_t x, int k) {
+#if MC_PCD_DIAG == 1   // diagnostic: no LDS stores (timing only)
+    w = (w ^ x) + (uint32_t)k;
+    return;
+#endif
     const int sh = 8 * n;
     w |= x << sh;
     const uint32_t spill = (x >> 1) >> (31 - sh);   // the bytes beyond the dword (0 when sh == 0)
@@ -491,6 +498,13 @@ struct LdsLine {
 
 // "%.6f" of one fast value plus its separator, appended to the line
 __device__ __forceinline__ void fast_value(LdsLine& w, uint32_t n, bool neg, uint32_t sep) {
+#if MC_PCD_DIAG == 2   // diagnostic: no digit arithmetic (timing only)
+  w.put(n | 0x30303030u, 4);
+  w.put(n ^ 0x2e2e2e2eu, 3 + (int)neg);
+  w.put(n + sep, 4);
+  w.put(sep, 2);
+  return;
+#endif
   const uint32_t ip = n / 1000000u, fp = n - ip * 1000000u;
   const int nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
   // integer digits (ip < 10^4): thousands | hundreds | tens | units, keep the last nd
@@ -525,6 +539,9 @@ __device__ __forceinline__ void pcd_emit_fast(const PcdFast& P, uint32_t* base, 
 #pragma unroll
   for (int k = 0; k < 4; ++k) fast_value(w, P.n[k], (P.neg >> k) & 1u, k < 3 ? ' ' : '\n');
   w.finish();
+#if MC_PCD_DIAG == 1
+  base[w.pos] = w.w;
+#endif
 }
 
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7

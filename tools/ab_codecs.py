@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--points", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-check", action="store_true", help="skip the byte-identity check (diagnostic builds)")
     ap.add_argument("--source", default="aos", choices=["aos", "batch"],
                     help="encode from a device (N,4) float64 AoS array or from the batch's float32 columns")
     args = ap.parse_args()
@@ -88,7 +89,7 @@ def main():
                 times[lib][name].append(a["ctx"].read_timing()["codec_ms"] / args.reps * 1e3)
     # byte-identical outputs across arms (sampled: first and last 64 MB)
     ref = arms[libs[0]]
-    for lib in libs[1:]:
+    for lib in ([] if args.no_check else libs[1:]):
         a = arms[lib]
         for key, nbytes in (("lvx_out", ref["lvx_bytes"]), ("pcd_out", int(ref["bpos"][-1]))):
             for lo in (0, max(0, nbytes - (64 << 20))):
