@@ -99,5 +99,26 @@ int main() {
   float ms = 0;
   hipEventElapsedTime(&ms, e0, e1);
   std::printf("{\"prep_alone_us\": %.1f}\n", ms * 1e3 / steps);
+  // the streaming kernel alone: per launch (an event pair around every launch, serialised by a
+  // host sync) vs back to back (one event pair around `steps` launches) -> the kernel-to-kernel gap
+  for (int round = 0; round < 3; ++round) {
+    double one = 0.0;
+    for (int it = 0; it < 20; ++it) {
+      hipEventRecord(e0, s);
+      hipLaunchKernelGGL(k_stream, dim3(grid), dim3(256), 0, s, in, out, n);
+      hipEventRecord(e1, s);
+      hipEventSynchronize(e1);
+      hipEventElapsedTime(&ms, e0, e1);
+      one += ms * 1e3 / 20;
+    }
+    hipEventRecord(e0, s);
+    for (int it = 0; it < steps; ++it) hipLaunchKernelGGL(k_stream, dim3(grid), dim3(256), 0, s, in, out, n);
+    hipEventRecord(e1, s);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&ms, e0, e1);
+    std::printf("{\"round\": %d, \"kernel_alone_us\": %.1f, \"back_to_back_step_us\": %.1f}\n", round, one,
+                ms * 1e3 / steps);
+    std::fflush(stdout);
+  }
   return 0;
 }
