@@ -544,6 +544,84 @@ __device__ __forceinline__ void pcd_emit_fast(const PcdFast& P, uint32_t* base, 
 #endif
 }
 
+// ---- SWAR line writer (MC_PCD_SWAR) ----------------------------------------------------------
+// The same bytes as pcd_emit_fast with about half the VALU work: the six fraction digits of all
+// values come out of one 32-bit word holding two 3-digit halves (multiply-shift division on both
+// 16-bit halves at once), the integer digits likewise from two 2-digit halves, and bytes are
+// placed with v_perm_b32; each value's text ([-]digits, then the fixed 8 bytes ".dddddd" + separator)
+// sits right-aligned in four dwords and is moved to the line's byte position with v_alignbyte_b32,
+// so the line writer stores whole dwords with no per-field bookkeeping.
+#ifndef MC_PCD_SWAR
+#define MC_PCD_SWAR 1
+#endif
+
+// one value of the line: pending n (< 4) bytes in w start at dword pos; FIRST: the pending bytes
+// belong to the previous line, so the first dword is ORed
+template <bool FIRST>
+__device__ __forceinline__ void swar_value(uint32_t* base, int& pos, int& n, uint32_t& w, uint32_t N, bool neg,
+                                           uint32_t sep) {
+  const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
+  const int nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
+  // fraction: halves fh = fp / 1000 (low) and fl (high) -> hundreds / tens / units of both
+  const uint32_t fh = fp / 1000u;
+  const uint32_t y = fh | ((fp - fh * 1000u) << 16);
+  const uint32_t h = ((y * 41u) >> 12) & 0x000F000Fu;            // y*41 < 2^32: halves < 1000
+  const uint32_t r = y - h * 100u;
+  const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;    // r halves < 100
+  const uint32_t ht = h | (t << 8);                               // [h_lo t_lo h_hi t_hi]
+  const uint32_t u = r - t * 10u;                                 // [u_lo 0 u_hi 0]
+  const uint32_t A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;             // . d1 d2 d3
+  const uint32_t B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);  // d4 d5 d6 sep
+  // integer part ip < 10^4: halves ip / 100 (low) and ip % 100 (high) -> tens / units
+  const uint32_t hi2 = __umul24(ip, 5243u) >> 19;
+  const uint32_t y2 = hi2 | ((ip - hi2 * 100u) << 16);
+  const uint32_t t2 = (__umul24(y2, 103u) >> 10) & 0x000F000Fu;
+  const uint32_t u2 = y2 - t2 * 10u;
+  uint32_t D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;   // 4 digits, leading zeros
+  uint32_t T0 = 0u;
+  if (neg) {   // the sign goes in front of the nd digits: byte 3 - nd of D, or byte 3 of T0
+    if (nd == 4) T0 = 0x2D000000u;
+    else {
+      const int sh = 8 * (3 - nd);
+      D = (D & ~(0xFFu << sh)) | (0x2Du << sh);
+    }
+  }
+  // text = bytes [s, 16) of T0 D A B, s = 8 - (neg + nd); move byte s to byte n
+  const int L = (neg ? 1 : 0) + nd + 8;
+  const int rs = 16 - L - n;                  // 0 .. 7
+  const bool q = rs >= 4;
+  const uint32_t m = (uint32_t)(rs & 3);
+  const uint32_t S0 = q ? D : T0, S1 = q ? A : D, S2 = q ? B : A, S3 = q ? 0u : B;
+  uint32_t U0 = __builtin_amdgcn_alignbyte(S1, S0, m);
+  const uint32_t U1 = __builtin_amdgcn_alignbyte(S2, S1, m);
+  const uint32_t U2 = __builtin_amdgcn_alignbyte(S3, S2, m);
+  const uint32_t U3 = __builtin_amdgcn_alignbyte(0u, S3, m);
+  U0 = (U0 & (0xFFFFFFFFu << (8 * n))) | w;  // n <= 3
+  const int M = n + L;                        // 9 .. 16 bytes from dword pos
+  if (FIRST) {
+    __hip_atomic_fetch_or(base + pos, U0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base[pos + 1] = U1;
+  } else {
+    base[pos] = U0;
+    base[pos + 1] = U1;
+  }
+  if (M >= 12) base[pos + 2] = U2;
+  if (M >= 16) base[pos + 3] = U3;
+  w = M >= 12 ? (M >= 16 ? 0u : U3) : U2;
+  pos += M >> 2;
+  n = M & 3;
+}
+
+__device__ __forceinline__ void pcd_emit_swar(const PcdFast& P, uint32_t* base, int off) {
+  int pos = off >> 2, n = off & 3;
+  uint32_t w = 0u;
+  swar_value<true>(base, pos, n, w, P.n[0], P.neg & 1u, ' ');
+  swar_value<false>(base, pos, n, w, P.n[1], (P.neg >> 1) & 1u, ' ');
+  swar_value<false>(base, pos, n, w, P.n[2], (P.neg >> 2) & 1u, ' ');
+  swar_value<false>(base, pos, n, w, P.n[3], (P.neg >> 3) & 1u, '\n');
+  if (n > 0) __hip_atomic_fetch_or(base + pos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
 // characters with the separator, nd = 1 + [N >= 10^7] + [N >= 10^8] + [N >= 10^9] for
 // N = round-half-even(|v| 10^6).  N >= T (T even) <=> |v| 10^6 >= T - 1/2 exactly; y = fl(|v| 10^6)
@@ -623,7 +701,11 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
     const int excl = block_scan(P.len, s_wave, total) - P.len;
     const int64_t G = a.tile_pos[u];
     const int shift = (int)(G & 15);
+#if MC_PCD_SWAR
+    if (valid) pcd_emit_swar(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
+#else
     if (valid) pcd_emit_fast(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
+#endif
     __syncthreads();
     codec_store_piece(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
     __syncthreads();   // s_wave / s_text are reused by the next tile
