@@ -1,0 +1,117 @@
+// Host build of the device "%.6f" line writers in livox-motion-compensation-sim_amd/csrc/codecs.hpp
+// (the section from `struct PcdFast` to `kPcdSlowTile`, spliced in by tests/test_pcd_formatter_host.py
+// at FORMATTER_SECTION) with host stand-ins for the gfx950 intrinsics it uses.  Every line of a
+// 256-line tile is written in reverse lane order into a zeroed buffer at a tile offset modulo 16,
+// as the kernel's lanes may interleave, and the text is compared with the C library's correctly
+// rounded "%.6f" (the same digits as Python's formatting).  Exit status = number of bad tiles.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#define __device__
+#define __forceinline__ inline
+#define __noinline__
+#define __ATOMIC_RELAXED 0
+#define __HIP_MEMORY_SCOPE_WORKGROUP 0
+static inline uint32_t __umul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
+static inline uint32_t __hip_atomic_fetch_or(uint32_t* p, uint32_t v, int, int) { const uint32_t o = *p; *p |= v; return o; }
+// v_perm_b32: byte i of the result = byte sel[i] of {s0:s1} (0-3 = s1, 4-7 = s0), 12 -> 0x00
+static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t v = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t c = (sel >> (8 * i)) & 0xffu;
+    const uint32_t b = c < 8 ? (uint32_t)(v >> (8 * c)) & 0xffu : (c == 12 ? 0u : 0xffu);
+    r |= b << (8 * i);
+  }
+  return r;
+}
+// v_alignbyte_b32: ({hi:lo} >> 8 * (k & 3))[31:0]
+static inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t k) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (k & 3)));
+}
+using std::fma;
+using std::signbit;
+struct CodecFrames { const double* aos; };
+static inline void codec_point(const CodecFrames& s, int32_t, int64_t row, double c[4]) {
+  for (int k = 0; k < 4; ++k) c[k] = s.aos[4 * row + k];
+}
+
+namespace mc {
+// FORMATTER_SECTION
+}  // namespace mc
+using namespace mc;
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? std::atoi(argv[1]) : 300000;
+  std::mt19937_64 g(1);
+  std::uniform_real_distribution<double> U(-90, 90);
+  std::vector<double> pts(4 * (size_t)N);
+  for (size_t i = 0; i < pts.size(); ++i) {
+    double x = (double)(float)(U(g) * std::pow(10.0, (double)(g() % 9) - 5));   // float32 values, 1e-5..1e3
+    if (i % 5 == 0) x = (double)(int64_t)(U(g) * 1000) / 128.0;                   // exact %.6f ties
+    if (i % 7 == 0) x = (double)(int64_t)(U(g) * 1e8) / 64.0 / 1e6;
+    if (i % 11 == 0) x = U(g) * (1 + 1e-15 * (double)(g() % 5));                 // full float64 values
+    if (i % 13 == 0) x = (g() % 2 ? -1 : 1) * (9.9999995 + 1e-9 * ((int)(g() % 200) - 100));   // digit carry
+    if (i % 17 == 0) x = 99.9999995 * (1 + 1e-16 * ((int)(g() % 9) - 4));
+    if (i % 19 == 0) x = (g() % 2 ? -1 : 1) * (4293.9999994 + 1e-7 * (double)(g() % 20));      // near 4294
+    if (i % 23 == 0) x = -0.0;
+    pts[i] = x;
+  }
+  const CodecFrames s{pts.data()};
+  std::vector<uint32_t> buf(16400 / 4 + 4);
+  int bad = 0;
+  long lines = 0, fast = 0;
+  for (int t = 0; t < N / 256; ++t) {
+    std::memset(buf.data(), 0, buf.size() * 4);
+    const int shift = t % 16;
+    int off = shift;
+    std::string want;
+    std::vector<PcdFast> P(256);
+    std::vector<int> offs(256);
+    for (int l = 0; l < 256; ++l) {
+      const double* c = &pts[4 * ((size_t)t * 256 + l)];
+      pcd_fast(s, 0, (int64_t)t * 256 + l, P[l]);
+      char line[160];
+      std::snprintf(line, sizeof line, "%.6f %.6f %.6f %.6f\n", c[0], c[1], c[2], c[3]);
+      const double cc[4] = {c[0], c[1], c[2], c[3]};
+      const int lf = pcd_fast_len(cc);
+      ++lines;
+      if (!P[l].ok) {
+        if (lf != -1) { ++bad; std::printf("pcd_fast_len accepted a byte-path line: %s", line); }
+        continue;
+      }
+      ++fast;
+      if ((int)std::strlen(line) != P[l].len || lf != P[l].len) {
+        ++bad;
+        std::printf("length %d / %d for %s", P[l].len, lf, line);
+      }
+      offs[l] = off;
+      off += P[l].len;
+      want += line;
+    }
+    for (int l = 255; l >= 0; --l)
+      if (P[l].ok) {
+#if MC_PCD_SWAR
+        pcd_emit_swar(P[l], buf.data(), offs[l]);
+#else
+        pcd_emit_fast(P[l], buf.data(), offs[l]);
+#endif
+      }
+    const std::string got(reinterpret_cast<const char*>(buf.data()) + shift, off - shift);
+    if (got != want) {
+      ++bad;
+      size_t i = 0;
+      while (i < got.size() && got[i] == want[i]) ++i;
+      std::printf("tile %d: byte %zu differs: got [%s] want [%s]\n", t, i, got.substr(i > 20 ? i - 20 : 0, 60).c_str(),
+                  want.substr(i > 20 ? i - 20 : 0, 60).c_str());
+    }
+  }
+  std::printf("lines %ld packed %ld bad %d\n", lines, fast, bad);
+  return bad > 255 ? 255 : bad;
+}
