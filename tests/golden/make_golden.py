@@ -19,6 +19,13 @@ Fixtures:
   slerp.npz           build-added SLERP mode: scipy Slerp + LERP over a parking interval that
                       straddles the yaw wrap (not a reference function: anchored on scipy).
   synth.npz           first 4096 points and f64 column sums of a synthetic 100k frame.
+  lmc_env_<cfg>.npz   scan_environment (LMC:701-770): the scenario's scene and numpy's RNG state
+                      right before the frame loop, plus every frame's point count.
+  codecs.npz          LVX v1.1 files (write_compatible_lvx, LMC:57-272) and ASCII PCD files
+                      (save_pcd, LMC:932-948) written by the reference, with their inputs.
+  coords.npz          CoordinateTransformer matrices / transforms and _transform_coordinates
+                      (CSIM:153-233, 2107-2163).
+  save_results.npz    the whole output directory of LMC's save_results (LMC:860-931).
 """
 from __future__ import annotations
 
