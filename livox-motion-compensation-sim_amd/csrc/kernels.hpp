@@ -739,6 +739,9 @@ __device__ __forceinline__ void imu_point(const ImuSeg& w, int t, float& x, floa
 #ifndef MC_IMU_F32
 #define MC_IMU_F32 1
 #endif
+#ifndef MC_IMU_DIAG
+#define MC_IMU_DIAG 0        // diagnostic timing build: 1 = no per-point angle vote (assumes small angles)
+#endif
 struct ImuF {
   float g[3], dg[3], inv_dt;
   int32_t ts;
@@ -933,6 +936,7 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
         const ImuF f0 = imu_f32(r0);
         const ImuF f1 = imu_f32(fw.W == 2 ? ldu(rec + 1) : r0);
         bool ok = true;
+#if MC_IMU_DIAG != 1
         if (act) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
@@ -941,6 +945,7 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
             ok = imu_angles_f32((mixed ? (int64_t)t >= fw.bnd1 : use1) ? f1 : f0, t, th) && ok;
           }
         }
+#endif
         if (__all(ok)) {
           if (act) {
 #pragma unroll
