@@ -392,12 +392,13 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   return x + before;
 }
 
-// ---- packed line path (every value of the line |v| < 4294 and not within 1e-6 of a tie) -------
+// ---- packed line path (every value of the line |v| < 4294, ties included) ----------------------
 // The common LiDAR line is formatted from four 32-bit integers N = round(|v| * 10^6): its text is
 // assembled in registers (digits packed four to a dword with multiply-shift division) and written to
-// LDS as dwords (ds_write2_b32), instead of ~40 single-byte LDS stores per line.  Lines share
-// their first and last dwords with their neighbours: those go through ds_or_b32 into a zeroed
-// buffer.  Lines with any other value take the byte path (fmt6_prepare / pcd_emit).
+// LDS as dwords, instead of ~40 single-byte LDS stores per line.  Lines share their first and last
+// dwords with their neighbours: those go through ds_or_b32 into a zeroed buffer.  Tiles holding a
+// line with any other value (NaN, inf, |v| >= 4294) take the byte path (fmt6_prepare / pcd_emit,
+// k_pcd_write_bytes).  Two writers: the SWAR one (default, below) and the per-field LdsLine one.
 #ifndef MC_PCD_PACKED
 #define MC_PCD_PACKED 1
 #endif
