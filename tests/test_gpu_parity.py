@@ -3,6 +3,8 @@
 Tolerance (north_star: <= 1e-5 relative per coordinate): per coordinate
 |gpu - ref| <= 1e-5 * (|p| + |t|), p the input point, t the translation applied.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -148,8 +150,14 @@ def test_full_size_c2_frame_mode_all_points(mc, gpu_ctx):
 
 
 @pytest.mark.parametrize("mode", ["pose_slerp", "imu"])
-def test_full_size_c2_per_point_modes_sampled(mc, gpu_ctx, mode):
+def test_full_size_c2_per_point_modes_all_points(mc, gpu_ctx, mode):
+    """BASELINE config 2 (600 x 100k) in the per-point modes, every point checked against the
+    oracle (frames in chunks on a thread pool: numpy releases the GIL), plus the rotation-norm
+    invariant of Path B over all 60M points."""
+    from concurrent.futures import ThreadPoolExecutor
+
     b, tr, times = _c2_batch(mc, gpu_ctx)
+    ts = gyro = starts = None
     if mode == "imu":
         ts, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
         gpu_ctx.set_imu(ts, gyro)
@@ -159,21 +167,29 @@ def test_full_size_c2_per_point_modes_sampled(mc, gpu_ctx, mode):
     ox, oy, oz, oi = out.download_columns()
     hx, hy, hz, hi, ht = synth.synth_batch(b.counts, seed=0, frame_id_base=1000)
     assert np.array_equal(oi, hi)
-    n = 100_000
-    for f in [0, 1, 2, 57, 123, 299, 300, 451, 598, 599]:
-        s = slice(f * n, (f + 1) * n)
+    n, F, per = 100_000, 600, 10
+
+    def chunk(f0):
+        s = slice(f0 * n, (f0 + per) * n)
         p = np.stack([hx[s], hy[s], hz[s]], axis=1).astype(np.float64)
         got = np.stack([ox[s], oy[s], oz[s]], axis=1)
+        fr = np.repeat(np.arange(f0, f0 + per), n)
+        t = ht[s].astype(np.int64)
         if mode == "pose_slerp":
-            ref = R.deskew_pose_slerp(p, ht[s], times[f], tr)
-            _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[f] + ht[s] * 1e-9)
+            Rm, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[fr] + t * 1e-9)
+            ref = np.einsum("nij,nj->ni", Rm, p) + pos
             sc = scale_of(p, pos)
-        else:
-            ref = R.compensate_arrays(p, starts[f] + ht[s].astype(np.int64), starts[f], ts, gyro)
+        else:   # R.compensate_arrays with a per-point frame start
+            w = R.imu_interpolate_gyro(ts, gyro, starts[fr] + t)
+            Rm = R.euler_xyz_matrix(w * (t * 1e-9)[:, None])
+            ref = np.einsum("nji,nj->ni", Rm, p)
             sc = scale_of(p)
-        assert_scaled_close(got, ref, sc, what=f"{mode} frame {f}")
-    # rigid motion: norms preserved (imu: rotation only) over the full 60M points
-    if mode == "imu":
+        return assert_scaled_close(got, ref, sc, what=f"{mode} frames {f0}..{f0 + per - 1}")
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as pool:
+        worst = max(pool.map(chunk, range(0, F, per)))
+    assert worst <= 1e-5
+    if mode == "imu":   # rotation only: norms preserved over the full 60M points
         nin = np.sqrt(hx.astype(np.float64) ** 2 + hy.astype(np.float64) ** 2 + hz.astype(np.float64) ** 2)
         nout = np.sqrt(ox.astype(np.float64) ** 2 + oy.astype(np.float64) ** 2 + oz.astype(np.float64) ** 2)
         assert np.max(np.abs(nout - nin) / nin) < 1e-5
@@ -237,7 +253,8 @@ def _check_frames(mc, ctx, b, tr, times, ts, gyro, mode, frames_to_check, n, see
     hx, hy, hz, hi, ht = synth.synth_batch(b.counts, seed=seed, frame_id_base=1000)
     assert np.array_equal(oi, hi)
     idx = R.select_pose_index(tr["time"], times)
-    for f in frames_to_check:
+
+    def check(f):
         s = slice(f * n, (f + 1) * n)
         p = np.stack([hx[s], hy[s], hz[s]], axis=1).astype(np.float64)
         got = np.stack([ox[s], oy[s], oz[s]], axis=1)
@@ -254,7 +271,11 @@ def _check_frames(mc, ctx, b, tr, times, ts, gyro, mode, frames_to_check, n, see
             st = int(times[f] * 1e9)
             ref = R.compensate_arrays(p, st + ht[s].astype(np.int64), st, ts, gyro)
             sc = scale_of(p)
-        assert_scaled_close(got, ref, sc, what=f"{mode} frame {f}")
+        return assert_scaled_close(got, ref, sc, what=f"{mode} frame {f}")
+
+    from concurrent.futures import ThreadPoolExecutor   # numpy releases the GIL
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as pool:
+        return max(pool.map(check, frames_to_check))
 
 
 @pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
@@ -264,12 +285,12 @@ def test_config1_highway_10x20k_all_points(mc, gpu_ctx, mode):
     _check_frames(mc, gpu_ctx, b, tr, times, ts, gyro, mode, range(10), 20_000, seed=5)
 
 
-@pytest.mark.parametrize("mode", ["pose_slerp", "frame"])
-def test_config3_parking_600x100k_sampled(mc, gpu_ctx, mode):
+@pytest.mark.parametrize("mode", ["pose_slerp", "frame", "imu"])
+def test_config3_parking_600x100k_all_points(mc, gpu_ctx, mode):
     """BASELINE config 3 (parking_detailed, circular, IMU/GPS noise on, SLERP-heavy): 600 x 100k,
-    frames sampled across the run including the yaw wrap region."""
+    every point of every frame (the run crosses the yaw wrap) in every mode."""
     b, tr, times, ts, gyro = _scenario_batch(mc, gpu_ctx, "parking_detailed", 600, 100_000, seed=9)
-    _check_frames(mc, gpu_ctx, b, tr, times, ts, gyro, mode, [0, 1, 150, 299, 300, 301, 450, 599], 100_000, seed=9)
+    _check_frames(mc, gpu_ctx, b, tr, times, ts, gyro, mode, range(600), 100_000, seed=9)
 
 
 # ---------------------------------------------------------------------------------------------
