@@ -195,6 +195,31 @@ def test_full_size_c2_per_point_modes_all_points(mc, gpu_ctx, mode):
         assert np.max(np.abs(nout - nin) / nin) < 1e-5
 
 
+def test_config5_shape_1m_point_frames_all_points(mc, gpu_ctx):
+    """BASELINE config 5's per-GPU shape (dense 1M-point frames; 150 of them = 1200 frames / 8 GPUs)
+    in the headline SLERP mode: every one of the 150M points against the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    F, n = 150, 1_000_000
+    b, tr, times = _c2_batch(mc, gpu_ctx, frames=F, n=n)
+    out = gpu_ctx.deskew(b, mode="pose_slerp")
+    ox, oy, oz, oi = out.download_columns()
+    out.close()
+    b.close()
+    hx, hy, hz, hi, ht = synth.synth_batch(np.full(F, n), seed=0, frame_id_base=1000)
+    assert np.array_equal(oi, hi)
+
+    def check(f):
+        s = slice(f * n, (f + 1) * n)
+        p = np.stack([hx[s], hy[s], hz[s]], axis=1).astype(np.float64)
+        Rm, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[f] + ht[s] * 1e-9)
+        ref = np.einsum("nij,nj->ni", Rm, p) + pos
+        return assert_scaled_close(np.stack([ox[s], oy[s], oz[s]], axis=1), ref, scale_of(p, pos), what=f"frame {f}")
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as pool:
+        assert max(pool.map(check, range(F))) <= 1e-5
+
+
 def test_max_size_c4_on_one_gpu_past_int32_indices(mc, gpu_ctx):
     """BASELINE config 4's whole job (6000 x 100k, urban poses over 600 s) on ONE device: 600 M
     points, 3.0 G values in the 5-column input (past 2^31), 12 GB in + 9.6 GB out.  SLERP into a
