@@ -2,6 +2,7 @@
 # One GPU-box session: gpu tests -> smoke -> bench -> rocprofv3 kernel trace.
 # Stops at the first fault / abort / timeout (exit codes other than 0 and pytest's 1).
 # Usage (from the repo root, on the GPU box):  bash tools/gpu_round.sh [tag] [steps]
+# CONFIGS=1 adds the other BASELINE configs (tools/bench_configs.py) at the end.
 set -u
 TAG=${1:-r01}
 STEPS=${2:-100}
@@ -45,3 +46,9 @@ tail -5 "$OUT/pmc_$TAG.log"
 timeout -k 10 900 python tools/pmc_traffic.py --aux --tag "$TAG" > "$OUT/pmc_aux_$TAG.log" 2>&1
 stop_if_fault $? pmc_aux
 tail -8 "$OUT/pmc_aux_$TAG.log"
+
+if [ "${CONFIGS:-0}" = "1" ]; then
+  timeout -k 10 900 python tools/bench_configs.py --out "$OUT/configs_$TAG.json" > "$OUT/configs_$TAG.log" 2>&1
+  stop_if_fault $? configs
+  cat "$OUT/configs_$TAG.log"
+fi
