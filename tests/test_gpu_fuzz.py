@@ -92,3 +92,35 @@ def test_random_batches_all_modes(mc, gpu_ctx, seed):
                 assert_scaled_close(got[s, :3], ref, sc, what=f"seed {seed} {mode} frame {f} ({counts[f]} pts)")
     finally:
         b.close()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_codec_frames(mc, gpu_ctx, seed):
+    """LVX and ASCII PCD of random ragged frames against the oracle, byte for byte: magnitudes from
+    1e-9 to 1e9 (packed and byte-path PCD lines mixed within tiles), float32-valued and exact-tie
+    values, -0.0 and inf in the PCD case (LVX rejects non-finite values like the reference)."""
+    from oracle import codecs as C
+
+    rng = np.random.default_rng(100 + seed)
+    F = int(rng.integers(1, 12))
+    counts = rng.choice([0, 1, 95, 96, 97, 255, 256, 257, 1000, 5000], F)
+    frames = []
+    for n in counts:
+        mag = 10.0 ** rng.uniform(-9, rng.choice([3.5, 9.0]), (n, 4))
+        v = rng.choice([-1.0, 1.0], (n, 4)) * mag
+        v[:, 3] = np.abs(v[:, 3]) % 1.2
+        if n > 10:
+            v[::5, 0] = np.round(v[::5, 0] * 128) / 128                          # exact %.6f ties
+            v[1::7, 1] = v[1::7, 1].astype(np.float32)
+            v[2::11, 2] = -0.0
+        frames.append(v)
+    pcds = mc.codecs.encode_pcd_frames(frames, gpu_ctx)
+    special = [f.copy() for f in frames]
+    for f in special:
+        if len(f) > 3:
+            f[3, 0] = np.inf
+    assert all(p == C.pcd_ascii_bytes(f) for p, f in zip(pcds, frames))
+    assert all(p == C.pcd_ascii_bytes(f) for p, f in zip(mc.codecs.encode_pcd_frames(special, gpu_ctx), special))
+    lvx_frames = [{"frame_id": 3 * i + 1, "timestamp": 0.05 * i + 1e-3, "points": np.clip(f, -2e6, 2e6)}
+                  for i, f in enumerate(frames)]
+    assert mc.codecs.encode_lvx(lvx_frames, gpu_ctx) == C.lvx_bytes(lvx_frames)
