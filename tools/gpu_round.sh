@@ -34,7 +34,7 @@ cat "$OUT/bench_$TAG.json"
 
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run \
-  -- python3 "$ROOT/bench.py" --steps 50 --no-cpu > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err"
+  -- python3 "$ROOT/bench.py" --steps "$STEPS" --no-cpu > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err"
 stop_if_fault $? rocprof
 find "$OUT/prof_$TAG" -name "*kernel_stats*" -exec cat {} \; | head -20
 
