@@ -58,14 +58,22 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--grids", default="0", help="comma list of max-grid caps tried with every lib (0: one "
                                                   "workgroup per (sub-)tile)")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="independent allocations (contexts) per library: where a batch's pages land moves a "
+                         "kernel by up to ~10 %% (DESIGN.md section 8), so a variant is judged by the median "
+                         "over its replicas")
     args = ap.parse_args()
-    libs = [l for l in args.libs.split(",") if l]
-    runs = {lib: setup(lib, args) for lib in libs}
+    base_libs = [l for l in args.libs.split(",") if l]
+    # replicas alternate across libraries so that no variant gets all the early (or late) allocations
+    arms = [(lib, r) for r in range(args.replicas) for lib in base_libs]
+    runs = {(f"{lib}#{r}" if args.replicas > 1 else lib): setup(lib, args) for lib, r in arms}
+    libs = list(runs)
     grids = [int(g) for g in args.grids.split(",")]
     if grids != [0]:   # each (lib, grid) pair becomes its own arm, sharing the lib's workload
         runs = {f"{lib}@{g}": (*runs[lib], g) for lib in libs for g in grids}
     else:
         runs = {lib: (*runs[lib], 0) for lib in libs}
+    variant = {arm: arm.split("#")[0] for arm in runs}   # arm -> library (replicas share one)
     libs = list(runs)
     n = args.frames * args.points
     out = {}
@@ -106,6 +114,13 @@ def main():
             print(f"{mode:10s} {name:22s} kernel median {med:7.1f} us  min {min(v):7.1f} us  "
                   f"{BYTES[mode] * n / (med * 1e-6) / 1e9:6.0f} GB/s | step wall {wmed:7.1f} us "
                   f"(+{wmed - med:5.1f})", flush=True)
+        if args.replicas > 1:   # per variant: median over its replicas' medians
+            for var in dict.fromkeys(variant.values()):
+                meds = [statistics.median(per[a]) for a in libs if variant[a] == var]
+                name = os.path.basename(var)
+                out[f"{mode}/{name}/replicas"] = {"median_us": statistics.median(meds), "replica_medians_us": meds}
+                print(f"{mode:10s} {name:22s} over {len(meds)} replicas: median {statistics.median(meds):7.1f} us "
+                      f"(replicas {', '.join(f'{m:.1f}' for m in meds)})", flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "ab.json"), "w") as f:
         json.dump(out, f, indent=1)
