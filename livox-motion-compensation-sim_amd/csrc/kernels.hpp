@@ -1044,6 +1044,11 @@ constexpr int kStageUnroll = 4;
 #ifndef MC_STAGE_ST
 #define MC_STAGE_ST 1        // LDS stager output stores (st_pol policy)
 #endif
+#ifndef MC_STAGE_BATCH
+#define MC_STAGE_BATCH 8     // LDS stager: 16-byte HBM loads per lane batched ahead of its LDS
+                             // writes (0: one at a time)
+#endif
+constexpr int kStageBatch = MC_STAGE_BATCH > 0 ? MC_STAGE_BATCH : 1;
 constexpr int kTilePts = 4 * kTileGroups;
 constexpr int kStageRow = kTilePts + 16;   // LDS row pad: the 4 rows start in different banks
 
@@ -1052,12 +1057,34 @@ constexpr int kStageRow = kTilePts + 16;   // LDS row pad: the 4 rows start in d
 __device__ __forceinline__ void stage_tile_lds_in(const LayoutArgs& a, const Tile& tl, const v2d* __restrict__ s2,
                                                   int nv, float (*s)[kStageRow]) {
   const int np = 4 * tl.ngroups;
+#if MC_STAGE_BATCH
+  // kStageBatch 16-byte loads in flight per lane before the first LDS write (one at a time, the
+  // lane waits out a full HBM latency per load)
+  for (int q0 = 0; q0 < 2 * np; q0 += kStageBatch * kBlock) {
+    v2d v[kStageBatch];
+#pragma unroll
+    for (int u = 0; u < kStageBatch; ++u) {
+      const int q = q0 + u * kBlock + threadIdx.x;
+      v[u] = q < 2 * nv ? __builtin_nontemporal_load(s2 + q) : v2d{0.0, 0.0};
+    }
+#pragma unroll
+    for (int u = 0; u < kStageBatch; ++u) {
+      const int q = q0 + u * kBlock + threadIdx.x;
+      if (q < 2 * np) {
+        const int j = q >> 1, h = q & 1;
+        s[2 * h][j] = (float)v[u].x;
+        s[2 * h + 1][j] = (float)v[u].y;
+      }
+    }
+  }
+#else
   for (int q = threadIdx.x; q < 2 * np; q += kBlock) {
     const v2d v = q < 2 * nv ? __builtin_nontemporal_load(s2 + q) : v2d{0.0, 0.0};
     const int j = q >> 1, h = q & 1;
     s[2 * h][j] = (float)v.x;
     s[2 * h + 1][j] = (float)v.y;
   }
+#endif
   __syncthreads();
   float* cx = a.cols + bidx(a.C, 0, tl.pstart);
   for (int g = threadIdx.x; g < tl.ngroups; g += kBlock)
@@ -1071,10 +1098,30 @@ __device__ __forceinline__ void stage_tile_lds_in(const LayoutArgs& a, const Til
 __device__ __forceinline__ void stage_tile_lds_out(const LayoutArgs& a, const Tile& tl, v2d* __restrict__ d2, int nv,
                                                    float (*s)[kStageRow]) {
   const float* cx = a.cols + bidx(a.C, 0, tl.pstart);
+#if MC_STAGE_BATCH
+  for (int g0 = 0; g0 < (nv + 3) / 4; g0 += 2 * kBlock) {
+    float4 t[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int g = g0 + u * kBlock + threadIdx.x;
+      if (g < (nv + 3) / 4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[u][c] = ld4(cx + ((g >> 6) * a.C + c) * kBlkPts + 4 * (g & 63));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int g = g0 + u * kBlock + threadIdx.x;
+      if (g < (nv + 3) / 4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) *reinterpret_cast<float4*>(&s[c][4 * g]) = t[u][c];
+    }
+  }
+#else
   for (int g = threadIdx.x; g < (nv + 3) / 4; g += kBlock)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       *reinterpret_cast<float4*>(&s[c][4 * g]) = ld4(cx + ((g >> 6) * a.C + c) * kBlkPts + 4 * (g & 63));
+#endif
   __syncthreads();
   for (int q = threadIdx.x; q < 2 * nv; q += kBlock) {
     const int j = q >> 1, h = q & 1;

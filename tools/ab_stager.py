@@ -26,28 +26,34 @@ def main():
     ap.add_argument("--points", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="independent buffer sets per library, allocated alternately (page placement "
+                         "moves streaming kernels by several percent, DESIGN.md section 8)")
     args = ap.parse_args()
     libs = [l for l in args.libs.split(",") if l]
     counts = np.full(args.frames, args.points, np.int64)
     counts[::7] -= 3                                    # ragged frames: partial groups and tiles
     n = int(counts.sum())
     runs = {}
-    for lib in libs:
-        ctx = mc.Context(0, lib_path=lib)
-        b = ctx.batch(counts)
-        b.synth(seed=1, frame_id_base=1000)
-        back = ctx.batch(counts)
-        buf = ctx.device_buffer(n * 32)
-        runs[lib] = (ctx, b, back, buf)
+    ctxs = {lib: mc.Context(0, lib_path=lib) for lib in libs}
+    for r in range(args.replicas):
+        for lib in libs:
+            ctx = ctxs[lib]
+            b = ctx.batch(counts)
+            b.synth(seed=1, frame_id_base=1000)
+            back = ctx.batch(counts)
+            buf = ctx.device_buffer(n * 32)
+            runs[(lib, r)] = (ctx, b, back, buf)
     ref = None
-    for lib, (ctx, b, back, buf) in runs.items():
+    for key, (ctx, b, back, buf) in runs.items():
+        lib = key
         b.fetch_aos_device(buf)
         back.stage_aos_device(buf)
         ck = (b.checksum().tolist(), back.checksum().tolist())
         assert ck[0][:4] == ck[1][:4], (lib, ck)
         ref = ref or ck
         assert ck == ref, (lib, ck, ref)
-    res = {lib: {"soa_to_aos": [], "aos_to_soa": []} for lib in libs}
+    res = {key: {"soa_to_aos": [], "aos_to_soa": []} for key in runs}
     for _ in range(args.rounds):
         for lib, (ctx, b, back, buf) in runs.items():
             for name, fn in (("soa_to_aos", lambda: b.fetch_aos_device(buf)),
@@ -63,10 +69,14 @@ def main():
                 t = ctx.read_timing()
                 res[lib][name].append(t["layout_ms"] / t["layout_launches"] * 1e3)
     out = {}
-    for lib, d in res.items():
-        out[os.path.basename(lib)] = {k: {"median_us": statistics.median(v), "min_us": min(v),
-                                          "frac_median": 48 * n / (statistics.median(v) * 1e-6) / 8e12}
-                                      for k, v in d.items()}
+    for lib in libs:
+        out[os.path.basename(lib)] = {}
+        for k in ("soa_to_aos", "aos_to_soa"):
+            reps = [statistics.median(res[(lib, r)][k]) for r in range(args.replicas)]
+            med = statistics.median(reps)
+            out[os.path.basename(lib)][k] = {"median_us": med, "replica_medians_us": reps,
+                                             "min_us": min(min(res[(lib, r)][k]) for r in range(args.replicas)),
+                                             "frac_median": 48 * n / (med * 1e-6) / 8e12}
     print(json.dumps(out, indent=1))
 
 
