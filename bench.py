@@ -141,28 +141,35 @@ def load_traffic(mode, frames, points):
     return None if e is None else e.get("hbm_bytes_per_launch")
 
 
-def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True):
+def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, graph=False):
     """Timed region: wall clock around ``steps`` steps.  ``live``: HIP events (no system-scope
     fence) around the kernels of every ``every``-th timed step themselves — on the stream each
     kernel is launched on — give the roofline's per-launch kernel time; events around every launch
     would cost ~2 % of the step rate (measured), sampling one step in ten ~0.2 %.  Otherwise a
-    second, untimed pass carries events around every launch."""
+    second, untimed pass carries events around every launch.  ``graph``: the ``steps`` steps are
+    one replay of a HIP graph of ``steps`` deskew steps (``Context.deskew_steps``: every step runs
+    its prep and kernel; the graph is captured before the timed region), else ``steps`` calls."""
     every = 10 if steps >= 50 else 5
     ctx.timing(live)           # warmup steps fill the context's event pool for the sampled steps
     for _ in range(warmup):
         ctx.deskew(b_in, b_out, mode=mode)
+    if graph:                  # capture + instantiate only (host work, untimed)
+        ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0, prepare=True)
     ctx.sync()
     ctx.timing(False)
     ctx.read_timing()          # drop the warmup events (back to the pool)
     rdv.barrier()
     t0 = time.perf_counter()
-    for i in range(steps):
-        sample = live and i % every == every // 2
-        if sample:
-            ctx.timing(True)
-        ctx.deskew(b_in, b_out, mode=mode)
-        if sample:
-            ctx.timing(False)
+    if graph:
+        ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0)
+    else:
+        for i in range(steps):
+            sample = live and i % every == every // 2
+            if sample:
+                ctx.timing(True)
+            ctx.deskew(b_in, b_out, mode=mode)
+            if sample:
+                ctx.timing(False)
     ctx.sync()
     t1 = time.perf_counter()
     rdv.barrier()
@@ -365,6 +372,9 @@ def main():
     ap.add_argument("--events-after", action="store_true",
                     help="per-launch HIP events in a second, untimed pass instead of the timed steps")
     ap.add_argument("--gather-timeout", type=float, default=120.0)
+    ap.add_argument("--graph", action="store_true",
+                    help="issue the timed steps as one HIP-graph replay (Context.deskew_steps; kernel time from "
+                         "wall-clock stamp nodes, not HIP events) instead of separate calls")
     ap.add_argument("--scenario", default="urban_complex", choices=list(SCENARIOS),
                     help="pose table of this LMC scenario (BASELINE config 3 = parking_detailed)")
     args = ap.parse_args()
@@ -402,7 +412,7 @@ def main():
     for mode in modes:
         steps = args.steps if mode == args.mode else max(10, args.steps // 4)
         wall, tm = run_mode(ctx, rdv, mode, b_xyz if mode == "frame" else b_in, b_out, steps, args.warmup,
-                            live=not args.events_after)
+                            live=not args.events_after, graph=args.graph)
         wall_max = rdv.max(wall)
         main_avg_s = tm["main_ms"] / max(tm["main_launches"], 1) / 1e3
         prep_avg_s = tm["prep_ms"] / max(tm["prep_launches"], 1) / 1e3
@@ -455,11 +465,16 @@ def main():
                          "kernel": {"pose_slerp": "k_deskew_points<1>", "imu": "k_deskew_points<2>",
                                     "frame": "k_deskew_frame"}[args.mode],
                          "kernel_avg_us": r["main_avg_us"], "bytes_per_point": BYTES_PER_POINT[args.mode],
-                         "kernel_time": (f"HIP events around the kernels of {r['timed_launches']} of the "
-                                         f"{r['steps']} timed steps (every 10th), on the kernel's stream"
-                                         if not args.events_after else
-                                         "HIP events around every launch of a second, untimed pass")},
+                         "kernel_time": ("HIP events around every launch of a second, untimed pass"
+                                         if args.events_after else
+                                         f"wall-clock stamp nodes around the kernels of {r['timed_launches']} of the "
+                                         f"{r['steps']} steps of the step graph (every 10th)"
+                                         if args.graph else
+                                         f"HIP events around the kernels of {r['timed_launches']} of the "
+                                         f"{r['steps']} timed steps (every 10th), on the kernel's stream")},
             "prep_avg_us": r["prep_avg_us"],
+            "step_issue": "per-call launches" if not args.graph else
+                          f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
             "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
                           "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"]}
                       for m, v in results.items()},

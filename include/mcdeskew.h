@@ -192,6 +192,16 @@ int mc_batch_checksum(mc_batch* b, double* sums5);
 /* out must have the same frame counts as in (it may be the same batch: in-place). */
 int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select);
 
+/* n_steps consecutive mc_deskew calls (same arguments) as one HIP graph: each step's pose prep and
+ * deskew kernel run exactly as in mc_deskew (prep one step ahead on a second queue), the graph's
+ * edges replacing the per-call cross-queue events.  The graph is captured on first use and
+ * replayed while the launch arguments (batches, tables, sizes) are unchanged.  sample_every > 0
+ * puts timing events around the kernels of every sample_every-th step (read by mc_timing_read).
+ * flags = MC_STEPS_PREPARE: capture / instantiate only, launch nothing.  Asynchronous. */
+#define MC_STEPS_PREPARE 1
+int mc_deskew_steps(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t n_steps,
+                    int32_t sample_every, int flags);
+
 /* One call of transform_pointcloud (LMC:772-776) on host arrays: points (n, ld>=4) float64 rows,
  * rpy / translation (3,) float64 -> out (n, 4) float64 = [R_xyz(rpy) p + t, intensity], computed in
  * float64 by a kernel that reads and writes pinned, device-mapped host memory (no DMA round trips:

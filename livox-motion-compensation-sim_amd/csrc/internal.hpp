@@ -71,6 +71,27 @@ class HostPool {
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
+// n deskew steps captured as one HIP graph (mc_deskew_steps), cached by its launch arguments
+struct StepGraph {
+  std::vector<char> key;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  // sampled steps: wall-clock stamps {prep start, prep end, kernel start, kernel end} per sample,
+  // written by one-lane stamp kernels inside the graph (captured event records are not timable)
+  int32_t samples = 0;
+  unsigned long long* d_stamps = nullptr;
+  int64_t pending = 0;   // sampled replays not yet read by mc_timing_read
+};
+inline void step_graph_destroy(StepGraph* g) {
+  if (!g) return;
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  if (g->graph) (void)hipGraphDestroy(g->graph);
+  if (g->d_stamps) (void)hipFree(g->d_stamps);
+  if (g->fork) (void)hipEventDestroy(g->fork);
+  if (g->join) (void)hipEventDestroy(g->join);
+  delete g;
+}
 }  // namespace mcimpl
 
 struct mc_ctx {
@@ -126,8 +147,10 @@ struct mc_ctx {
   // launch knobs / timing
   int32_t max_grid = 0;
   bool timing = false;
+  double wall_khz = 0.0;   // wall_clock64() rate
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> main_ev, prep_ev, layout_ev;
+  mcimpl::StepGraph* step_graph = nullptr;
 };
 
 struct mc_batch {

@@ -369,6 +369,12 @@ __device__ __forceinline__ int64_t wave_count(const T* a, int64_t n, T x) {
   return lo + __popcll(__ballot(in));
 }
 
+// Timestamp node of a graph-captured step (mc_deskew_steps): the constant-rate wall clock
+// (s_memrealtime, hipDeviceAttributeWallClockRate) when the stream reaches it.
+__global__ __launch_bounds__(64) void k_stamp(unsigned long long* dst) {
+  if (threadIdx.x == 0) *dst = (unsigned long long)wall_clock64();
+}
+
 // One wave per frame (frame work), then one lane per pose segment / IMU sample (table work).
 __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
   const int lane = threadIdx.x & 63;

@@ -150,6 +150,8 @@ int mc_destroy(mc_ctx* c) {
   for (auto& p : c->scan_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->prep_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->layout_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
+  mcimpl::step_graph_destroy(c->step_graph);
+  c->step_graph = nullptr;
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) { (void)hipEventDestroy(c->ev_main_done[i]); (void)hipEventDestroy(c->ev_prep_done[i]); }
   (void)hipEventDestroy(c->ev_order);
@@ -536,7 +538,8 @@ int mc_batch_checksum(mc_batch* b, double* sums) {
 }
 
 // ---- the hot path ---------------------------------------------------------------------------
-int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select) {
+namespace {
+int deskew_check(mc_ctx* c, const mc_batch* in, const mc_batch* out, int mode, int pose_select) {
   CHECK_ARG(c && in && out, "NULL argument");
   CHECK_ARG(in->ctx == c && out->ctx == c, "batches belong to another context");
   CHECK_ARG(mode >= MC_MODE_FRAME && mode <= MC_MODE_IMU, "unknown mode %d", mode);
@@ -559,31 +562,30 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
     if (!in->has_starts) return fail(MC_ERR_STATE, "frame start times not set (mc_batch_set_frame_start_ns)");
     if (!in->has_t()) return fail(MC_ERR_STATE, "input batch has no t_ns column");
   }
-  if (in->F == 0) return MC_OK;
-  DeviceGuard g(c->device);
-  hipStream_t s = c->stream, sd = c->side;
-  if (mode != MC_MODE_FRAME && !in->trange_valid) {
-    // lazily derived frame time spans are queued on the main stream: order the prep after them
-    if (int r = compute_trange(const_cast<mc_batch*>(in))) return r;
-    HIPCHK(hipEventRecord(c->ev_order, s));
-    HIPCHK(hipStreamWaitEvent(sd, c->ev_order, 0));
-  }
-  const mc_batch* pb = in;  // per-frame tables live with the input batch
+  return MC_OK;
+}
 
-  // Pipelining: the per-step tables come in two halves.  This step's prep runs on the side
-  // stream as soon as the deskew kernel that last read half `h` (two calls back) has finished,
-  // i.e. concurrently with the previous call's kernel; the kernel waits for its own prep.
-  const int h = c->buf;
-  c->buf ^= 1;
-  HIPCHK(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
+// Everything one step launches, for table half h: k_prep's and the deskew kernel's arguments and
+// grids.  Plain old data, zero-filled first, so two plans compare bytewise (the graph cache key).
+struct StepPlan {
+  PrepArgs pa;
+  DeskewArgs da;
+  uint32_t prep_blocks;
+  uint32_t grid;
+  int32_t kernel;   // -1: no deskew launch (no tiles); else the mode
+  int32_t pad;
+};
+
+void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int h, StepPlan* sp) {
+  std::memset(sp, 0, sizeof(*sp));
+  const mc_batch* pb = in;  // per-frame tables live with the input batch
   float4* frame_tbl = pb->d_frame_tbl + 3 * (size_t)in->F * h;
   FrameWin* fwin = pb->d_fwin + (size_t)in->F * h;
   void* frec = static_cast<char*>(pb->d_frec) + pb->frec_half * h;
   PoseSeg* pose_seg = c->d_pose_seg ? c->d_pose_seg + (size_t)c->T_cap * h : nullptr;
   ImuSeg* imu_seg = c->d_imu_seg ? c->d_imu_seg + (size_t)c->M_cap * h : nullptr;
 
-  PrepArgs pa;
-  std::memset(&pa, 0, sizeof(pa));
+  PrepArgs& pa = sp->pa;
   pa.mode = mode;
   pa.pose_select = pose_select;
   pa.n_frames = in->F;
@@ -600,20 +602,11 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); table = pa.nseg; }
   if (mode == MC_MODE_IMU) { pa.nseg = c->M; table = c->M; }
   const int64_t waves = in->F + (table + 63) / 64;
-  {
-    TimedRegion tr(c, &c->prep_ev, sd);
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, sd, pa);
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev_prep_done[h], sd));
-  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
-  if (in->n_tiles == 0) {
-    HIPCHK(hipEventRecord(c->ev_main_done[h], s));
-    return MC_OK;
-  }
+  sp->prep_blocks = (uint32_t)((waves + 3) / 4);
+  sp->kernel = -1;
+  if (in->n_tiles == 0) return;
 
-  DeskewArgs da;
-  std::memset(&da, 0, sizeof(da));
+  DeskewArgs& da = sp->da;
   da.in = in->d_cols; da.in_C = in->C;
   da.out = out->d_cols; da.out_C = out->C;
   // per-point modes pass the timestamps through (CSIM:1472) when out is another batch with t_ns
@@ -630,16 +623,167 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
   const int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
-  const dim3 grid(launch_grid(c, units)), block(kBlock);
+  sp->grid = (uint32_t)launch_grid(c, units);
+  sp->kernel = mode;
+}
+
+void launch_prep(const StepPlan& sp, hipStream_t sd) {
+  hipLaunchKernelGGL(k_prep, dim3(sp.prep_blocks), dim3(kBlock), 0, sd, sp.pa);
+}
+
+void launch_main(const StepPlan& sp, hipStream_t s) {
+  const dim3 grid(sp.grid), block(kBlock);
+  if (sp.kernel == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, sp.da);
+  else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, sp.da);
+  else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, sp.da);
+}
+
+// frame time spans derived lazily from t_ns (queued on the main stream)
+int ensure_trange(mc_batch* in, int mode) {
+  if (mode != MC_MODE_FRAME && !in->trange_valid) return compute_trange(in);
+  return MC_OK;
+}
+}  // namespace
+
+int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select) {
+  if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
+  if (in->F == 0) return MC_OK;
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream, sd = c->side;
+  if (mode != MC_MODE_FRAME && !in->trange_valid) {
+    // the spans are queued on the main stream: order the prep after them
+    if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
+    HIPCHK(hipEventRecord(c->ev_order, s));
+    HIPCHK(hipStreamWaitEvent(sd, c->ev_order, 0));
+  }
+
+  // Pipelining: the per-step tables come in two halves.  This step's prep runs on the side
+  // stream as soon as the deskew kernel that last read half `h` (two calls back) has finished,
+  // i.e. concurrently with the previous call's kernel; the kernel waits for its own prep.
+  const int h = c->buf;
+  c->buf ^= 1;
+  HIPCHK(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
+  StepPlan sp;
+  deskew_plan(c, in, out, mode, pose_select, h, &sp);
   {
+    TimedRegion tr(c, &c->prep_ev, sd);
+    launch_prep(sp, sd);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_prep_done[h], sd));
+  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
+  if (sp.kernel >= 0) {
     TimedRegion tr(c, &c->main_ev, s);
-    if (mode == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, da);
-    else if (mode == MC_MODE_POSE_SLERP)
-      hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, da);
-    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, da);
+    launch_main(sp, s);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_main_done[h], s));
+  return MC_OK;
+}
+
+// ---- n steps as one HIP graph ---------------------------------------------------------------
+// The step sequence of n mc_deskew calls (prep on the side stream one step ahead, kernel on the
+// main stream) captured once and replayed: the graph's edges replace the per-step cross-queue
+// event protocol (~6.5 us per step, tools/gap_probe.hip patterns 1 vs 4).  Every replay runs all
+// n preps and n kernels.  The graph is cached by its launch arguments (device pointers, sizes,
+// grids), which are all a launch bakes in: table and point contents are read when it runs.
+namespace {
+int build_step_graph(mc_ctx* c, const StepPlan* plan, int32_t n_steps, int32_t every, std::vector<char>&& key) {
+  mcimpl::step_graph_destroy(c->step_graph);
+  c->step_graph = nullptr;
+  auto* g = new mcimpl::StepGraph();
+  g->key = std::move(key);
+  auto bail = [&](hipError_t e, const char* what) {
+    mcimpl::step_graph_destroy(g);
+    return fail(MC_ERR_HIP, "step graph %s: %s", what, hipGetErrorString(e));
+  };
+  hipError_t e = hipEventCreateWithFlags(&g->fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g->join, hipEventDisableTiming);
+  auto sampled = [&](int32_t i) { return every > 0 && i % every == every / 2; };
+  for (int32_t i = 0; i < n_steps; ++i) g->samples += sampled(i) ? 1 : 0;
+  if (e == hipSuccess && g->samples > 0)
+    e = hipMalloc(&g->d_stamps, 4 * sizeof(unsigned long long) * (size_t)g->samples);
+  if (e != hipSuccess) return bail(e, "events");
+  if (c->wall_khz <= 0.0) {
+    int khz = 0;
+    e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device);
+    if (e != hipSuccess || khz <= 0) return bail(e, "wall clock rate");
+    c->wall_khz = khz;
+  }
+  unsigned long long* st = g->d_stamps;
+  hipStream_t s = c->stream, sd = c->side;
+  e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) return bail(e, "begin capture");
+  // capture: any error is remembered and the capture still ended, so the stream leaves capture mode
+  auto rec = [&](hipError_t r) { if (e == hipSuccess) e = r; };
+  rec(hipEventRecord(g->fork, s));
+  rec(hipStreamWaitEvent(sd, g->fork, 0));
+  size_t k = 0;
+  for (int32_t i = 0; i < n_steps && e == hipSuccess; ++i) {
+    const int h = i & 1;
+    const StepPlan& sp = plan[h];
+    const bool smp = sampled(i);
+    if (i >= 2) rec(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
+    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, sd, st + 4 * k + 0);
+    launch_prep(sp, sd);
+    rec(hipGetLastError());
+    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, sd, st + 4 * k + 1);
+    rec(hipEventRecord(c->ev_prep_done[h], sd));
+    rec(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
+    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, st + 4 * k + 2);
+    launch_main(sp, s);
+    rec(hipGetLastError());
+    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, st + 4 * k++ + 3);
+    rec(hipEventRecord(c->ev_main_done[h], s));
+  }
+  rec(hipEventRecord(g->join, sd));
+  rec(hipStreamWaitEvent(s, g->join, 0));
+  const hipError_t ec = hipStreamEndCapture(s, &g->graph);
+  if (e != hipSuccess) return bail(e, "capture");
+  if (ec != hipSuccess) return bail(ec, "end capture");
+  e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) return bail(e, "instantiate");
+  c->step_graph = g;
+  return MC_OK;
+}
+}  // namespace
+
+int mc_deskew_steps(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t n_steps,
+                    int32_t sample_every, int flags) {
+  if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
+  CHECK_ARG(n_steps >= 1 && n_steps <= (1 << 16), "n_steps %d outside [1, 65536]", n_steps);
+  CHECK_ARG(sample_every >= 0, "sample_every %d < 0", sample_every);
+  CHECK_ARG((flags & ~MC_STEPS_PREPARE) == 0, "unknown flags 0x%x", flags);
+  if (in->F == 0 || in->n_tiles == 0) {
+    // nothing for a graph to carry (no points): the plain calls
+    if (flags & MC_STEPS_PREPARE) return MC_OK;
+    for (int32_t i = 0; i < n_steps; ++i)
+      if (int r = mc_deskew(c, in, out, mode, pose_select)) return r;
+    return MC_OK;
+  }
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  // queued on the main stream, ahead of the graph (whose prep branch forks from it)
+  if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
+  // the graph starts on half 0 whatever c->buf is: everything that last used either half precedes
+  // it on the main stream (a plain call's kernel waits for its own prep)
+  StepPlan plan[2];
+  deskew_plan(c, in, out, mode, pose_select, 0, &plan[0]);
+  deskew_plan(c, in, out, mode, pose_select, 1, &plan[1]);
+  std::vector<char> key(sizeof(plan) + 2 * sizeof(int32_t));
+  std::memcpy(key.data(), plan, sizeof(plan));
+  std::memcpy(key.data() + sizeof(plan), &n_steps, sizeof(int32_t));
+  std::memcpy(key.data() + sizeof(plan) + sizeof(int32_t), &sample_every, sizeof(int32_t));
+  if (!c->step_graph || c->step_graph->key != key) {
+    if (int r = build_step_graph(c, plan, n_steps, sample_every, std::move(key))) return r;
+  }
+  if (flags & MC_STEPS_PREPARE) return MC_OK;
+  HIPCHK(hipGraphLaunch(c->step_graph->exec, s));
+  // later plain calls order their side-stream prep after the whole graph
+  HIPCHK(hipEventRecord(c->ev_main_done[0], s));
+  HIPCHK(hipEventRecord(c->ev_main_done[1], s));
+  c->buf = 0;
+  if (sample_every > 0) c->step_graph->pending += 1;
   return MC_OK;
 }
 
@@ -902,7 +1046,26 @@ int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms,
   DeviceGuard g(c->device);
   if (int r = sync_all(c)) return r;
   if (int r = sum_events(c, c->main_ev, main_ms, main_n)) return r;
-  return sum_events(c, c->prep_ev, prep_ms, prep_n);
+  if (int r = sum_events(c, c->prep_ev, prep_ms, prep_n)) return r;
+  // graph-captured steps: their sampled events hold the last replay; each replay since the last
+  // read counts with those times
+  if (mcimpl::StepGraph* g = c->step_graph) {
+    if (g->pending > 0 && g->samples > 0) {
+      std::vector<unsigned long long> h(4 * (size_t)g->samples);
+      HIPCHK(hipMemcpy(h.data(), g->d_stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      double m = 0.0, p = 0.0;
+      for (int32_t k = 0; k < g->samples; ++k) {
+        p += (double)(h[4 * k + 1] - h[4 * k + 0]) / c->wall_khz;   // ticks / kHz = ms
+        m += (double)(h[4 * k + 3] - h[4 * k + 2]) / c->wall_khz;
+      }
+      if (main_ms) *main_ms += m * g->pending;
+      if (main_n) *main_n += (int64_t)g->samples * g->pending;
+      if (prep_ms) *prep_ms += p * g->pending;
+      if (prep_n) *prep_n += (int64_t)g->samples * g->pending;
+    }
+    g->pending = 0;
+  }
+  return MC_OK;
 }
 
 // ---- scan_environment (LMC:701-770) --------------------------------------------------------

@@ -84,6 +84,16 @@ class Context:
                                  _lib.POSE_SELECT[pose_select]), f"deskew[{mode}]")
         return out
 
+    def deskew_steps(self, inp: "Batch", out: "Batch", n_steps: int, mode: str = "frame",
+                     pose_select: str = "searchsorted", sample_every: int = 0, prepare: bool = False) -> "Batch":
+        """``n_steps`` calls of :meth:`deskew` replayed as one HIP graph (asynchronous); every step
+        runs its prep and kernel.  ``prepare``: capture the graph only.  ``sample_every``: timing
+        events around every n-th step's kernels (:meth:`read_timing`)."""
+        check(self.lib.mc_deskew_steps(self.handle, inp.handle, out.handle, _lib.MODES[mode],
+                                       _lib.POSE_SELECT[pose_select], int(n_steps), int(sample_every),
+                                       1 if prepare else 0), f"deskew_steps[{mode}]")
+        return out
+
     def transform_affine(self, inp: "Batch", out: "Batch | None" = None, mats=None, w_column: bool = False) -> "Batch":
         """p' = A p + b (CSIM:214-233) with one 3x4 [A | b] for all frames or one per frame;
         ``w_column``: the 4th column is the homogeneous w (p' = A p + b w).  Synchronous."""

@@ -91,6 +91,59 @@ int main() {
       }
     }
   }
+  // P4 / P5: the P1 / P2 step sequence captured once as a hipGraph of `steps` steps and replayed
+  // (the prep of step i+1 is a graph branch parallel to step i's streaming kernel in P4)
+  for (int pat : {4, 5}) {
+    for (int round = 0; round < 3; ++round) {
+      hipGraph_t graph;
+      hipGraphExec_t exec;
+      hipEvent_t fork, join;
+      hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+      hipEventCreateWithFlags(&join, hipEventDisableTiming);
+      hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+      if (pat == 4) {
+        hipEventRecord(fork, s);
+        hipStreamWaitEvent(sd, fork, 0);
+      }
+      for (int it = 0; it < steps; ++it) {
+        const int h = it & 1;
+        if (pat == 4) {
+          if (it >= 2) hipStreamWaitEvent(sd, main_done[h], 0);
+          hipLaunchKernelGGL(k_prep, dim3(pn / 256), dim3(256), 0, sd, tbl, pout, pn, 16);
+          hipEventRecord(prep_done[h], sd);
+          hipStreamWaitEvent(s, prep_done[h], 0);
+        } else {
+          hipLaunchKernelGGL(k_prep, dim3(pn / 256), dim3(256), 0, s, tbl, pout, pn, 16);
+        }
+        hipLaunchKernelGGL(k_stream, dim3(grid), dim3(256), 0, s, in, out, n);
+        if (pat == 4) hipEventRecord(main_done[h], s);
+      }
+      if (pat == 4) {
+        hipEventRecord(join, sd);
+        hipStreamWaitEvent(s, join, 0);
+      }
+      if (hipStreamEndCapture(s, &graph) != hipSuccess ||
+          hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) {
+        std::printf("{\"pattern\": %d, \"error\": \"capture/instantiate failed\"}\n", pat);
+        return 2;
+      }
+      hipGraphLaunch(exec, s);   // warm
+      hipStreamSynchronize(s);
+      hipEventRecord(e0, s);
+      hipGraphLaunch(exec, s);
+      hipEventRecord(e1, s);
+      hipEventSynchronize(e1);
+      float gms = 0;
+      hipEventElapsedTime(&gms, e0, e1);
+      std::printf("{\"pattern\": %d, \"graph\": true, \"prep_chain\": 16, \"round\": %d, \"step_us\": %.1f}\n", pat,
+                  round, gms * 1e3 / steps);
+      std::fflush(stdout);
+      hipGraphExecDestroy(exec);
+      hipGraphDestroy(graph);
+      hipEventDestroy(fork);
+      hipEventDestroy(join);
+    }
+  }
   // the prep kernel alone
   hipEventRecord(e0, s);
   for (int it = 0; it < steps; ++it) hipLaunchKernelGGL(k_prep, dim3(pn / 256), dim3(256), 0, s, tbl, pout, pn, 16);
