@@ -52,6 +52,9 @@ namespace mc {
 #ifndef MC_NT_LOAD
 #define MC_NT_LOAD 1         // non-temporal input loads (streamed once): +5-8% measured (tools/ab.py)
 #endif
+#ifndef MC_EARLY_LOADS
+#define MC_EARLY_LOADS 0     // 1: point loads before the window records (rejected: SLERP 322 -> 338 us, IMU -0.3 %)
+#endif
 #ifndef MC_POINTS_WAVES
 #define MC_POINTS_WAVES 0    // min waves/SIMD requested for the per-point kernels (0: compiler's choice)
 #endif
@@ -896,6 +899,24 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
     const int g0 = (int)(st % kSub) * kBlock;
     if (g0 >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
     const int f = tl.frame;
+    const int g = g0 + tid;
+    const bool act = g < tl.ngroups;
+    const int64_t p = tl.pstart + 4 * (int64_t)g;
+    float4 X, Y, Z, I;
+    int4 Tq;
+    const float* q = a.in + bidx((int)a.in_C, 0, p);   // the float4 group never straddles a block
+#define MC_POINT_LOADS                                          \
+    if (act) {                                                  \
+      Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts)); \
+      X = ld4(q);                                               \
+      Y = ld4(q + kBlkPts);                                     \
+      Z = ld4(q + 2 * kBlkPts);                                 \
+      I = ld4(q + 3 * kBlkPts);                                 \
+    }
+#if MC_EARLY_LOADS
+    // the point loads depend on the tile record only: in flight while the window record arrives
+    MC_POINT_LOADS
+#endif
     const FrameWin ff = ldu(a.fwin + f);
     // frames wider than the SGPR path take their sub-tile's own window (k_prep)
     const bool sub = MC_SUBTILE_WIN && ff.W > MC_FASTPATH_MAXW;
@@ -908,20 +929,10 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
       deskew_subtile_slow<MODE>(a, tl, g0);
       continue;
     }
-    const int g = g0 + tid;
-    const bool act = g < tl.ngroups;
-    const int64_t p = tl.pstart + 4 * (int64_t)g;
-
-    float4 X, Y, Z, I;
-    int4 Tq;
-    const float* q = a.in + bidx((int)a.in_C, 0, p);   // the float4 group never straddles a block
-    if (act) {
-      Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts));
-      X = ld4(q);
-      Y = ld4(q + kBlkPts);
-      Z = ld4(q + 2 * kBlkPts);
-      I = ld4(q + 3 * kBlkPts);
-    }
+#if !MC_EARLY_LOADS
+    MC_POINT_LOADS
+#endif
+#undef MC_POINT_LOADS
 
     if (fw.W <= MC_FASTPATH_MAXW) {
       const Win r0 = ldu(rec);
