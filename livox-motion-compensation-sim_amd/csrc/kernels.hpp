@@ -52,6 +52,9 @@ namespace mc {
 #ifndef MC_NT_LOAD
 #define MC_NT_LOAD 1         // non-temporal input loads (streamed once): +5-8% measured (tools/ab.py)
 #endif
+#ifndef MC_IMU_PK
+#define MC_IMU_PK 0          // 1: IMU f32 path on float2 pairs (-3 % instructions; rejected: 327.1 vs 325.6 us)
+#endif
 #ifndef MC_EARLY_LOADS
 #define MC_EARLY_LOADS 0     // 1: point loads before the window records (rejected: SLERP 322 -> 338 us, IMU -0.3 %)
 #endif
@@ -792,6 +795,45 @@ __device__ __forceinline__ void imu_rotate_f32(const float th[3], float& x, floa
   x = x2; y = y3; z = z3;
 }
 
+// The same f32 small-angle path for two points at once: every operation of imu_angles_f32 /
+// sincos_quadrant(q = 0) / imu_rotate_f32 on a float2, in the same order (so the same bits), which
+// the compiler issues as packed v_pk_fma_f32 / v_pk_mul_f32 — half the VALU instructions.
+typedef float mcf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ mcf2 fma2(mcf2 a, mcf2 b, mcf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ bool imu_angles2_f32(const ImuF wa, const ImuF wb, int ta, int tb, mcf2 th[3]) {
+  const mcf2 al = {fmaxf((float)(ta - wa.ts) * wa.inv_dt, 0.f), fmaxf((float)(tb - wb.ts) * wb.inv_dt, 0.f)};
+  const mcf2 dt = mcf2{(float)ta, (float)tb} * 1e-9f;
+  bool ok = wa.ok && wb.ok && ta > -(1 << 30) && ta < (1 << 30) && tb > -(1 << 30) && tb < (1 << 30);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    th[c] = fma2(al, mcf2{wa.dg[c], wb.dg[c]}, mcf2{wa.g[c], wb.g[c]}) * dt;
+    ok = ok && fabsf(th[c].x) <= kImuF32MaxAngle && fabsf(th[c].y) <= kImuF32MaxAngle;
+  }
+  return ok;
+}
+__device__ __forceinline__ void sincos2_small(mcf2 r, mcf2& s, mcf2& c) {
+  const mcf2 z = r * r;
+  mcf2 ps = fma2(z, mcf2(-1.9515295891e-4f), mcf2(8.3321608736e-3f));
+  ps = fma2(z, ps, mcf2(-1.6666654611e-1f));
+  s = fma2(z * r, ps, r);
+  mcf2 pc = fma2(z, mcf2(2.443315711809948e-5f), mcf2(-1.388731625493765e-3f));
+  pc = fma2(z, pc, mcf2(4.166664568298827e-2f));
+  c = fma2(z * z, pc, fma2(mcf2(-0.5f), z, mcf2(1.0f)));
+}
+__device__ __forceinline__ void imu_rotate2_f32(const mcf2 th[3], mcf2& x, mcf2& y, mcf2& z) {
+  mcf2 sa, ca, sb, cb, sc, cc;
+  sincos2_small(th[0], sa, ca);
+  sincos2_small(th[1], sb, cb);
+  sincos2_small(th[2], sc, cc);
+  const mcf2 x1 = fma2(cc, x, sc * y);
+  const mcf2 y1 = fma2(-sc, x, cc * y);
+  const mcf2 x2 = fma2(cb, x1, -sb * z);
+  const mcf2 z2 = fma2(sb, x1, cb * z);
+  const mcf2 y3 = fma2(ca, y1, sa * z2);
+  const mcf2 z3 = fma2(-sa, y1, ca * z2);
+  x = x2; y = y3; z = z3;
+}
+
 __device__ __forceinline__ float& f4c(float4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
@@ -953,28 +995,53 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
         const ImuF f0 = imu_f32(r0);
         const ImuF f1 = imu_f32(fw.W == 2 ? ldu(rec + 1) : r0);
         bool ok = true;
+#define MC_PICK(t) ((mixed ? (int64_t)(t) >= fw.bnd1 : use1) ? f1 : f0)
 #if MC_IMU_DIAG != 1
         if (act) {
+#if MC_IMU_PK
+#pragma unroll
+          for (int c = 0; c < 4; c += 2) {
+            const int ta = i4c(Tq, c), tb = i4c(Tq, c + 1);
+            mcf2 th[3];
+            ok = imu_angles2_f32(MC_PICK(ta), MC_PICK(tb), ta, tb, th) && ok;
+          }
+#else
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int t = i4c(Tq, c);
             float th[3];
-            ok = imu_angles_f32((mixed ? (int64_t)t >= fw.bnd1 : use1) ? f1 : f0, t, th) && ok;
+            ok = imu_angles_f32(MC_PICK(t), t, th) && ok;
           }
+#endif
         }
 #endif
         if (__all(ok)) {
           if (act) {
+#if MC_IMU_PK
+#pragma unroll
+            for (int c = 0; c < 4; c += 2) {
+              const int ta = i4c(Tq, c), tb = i4c(Tq, c + 1);
+              mcf2 th[3];
+              imu_angles2_f32(MC_PICK(ta), MC_PICK(tb), ta, tb, th);
+              mcf2 x = {f4c(X, c), f4c(X, c + 1)}, y = {f4c(Y, c), f4c(Y, c + 1)}, z = {f4c(Z, c), f4c(Z, c + 1)};
+              imu_rotate2_f32(th, x, y, z);
+              f4c(X, c) = x.x; f4c(X, c + 1) = x.y;
+              f4c(Y, c) = y.x; f4c(Y, c + 1) = y.y;
+              f4c(Z, c) = z.x; f4c(Z, c + 1) = z.y;
+            }
+#else
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const int t = i4c(Tq, c);
               float th[3];
-              imu_angles_f32((mixed ? (int64_t)t >= fw.bnd1 : use1) ? f1 : f0, t, th);
+              imu_angles_f32(MC_PICK(t), t, th);
               imu_rotate_f32(th, f4c(X, c), f4c(Y, c), f4c(Z, c));
             }
+#endif
           }
           done = true;
         }
+#undef MC_PICK
       }
 #endif
       if (act && !done) {
