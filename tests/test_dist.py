@@ -52,11 +52,13 @@ def _rdv_worker(rank, world, port, q):
     q.put((rank, got, mx, blob))
 
 
-def test_rendezvous_two_processes():
+@pytest.mark.parametrize("world", [3, 8])
+def test_rendezvous_processes(world):
+    """The control plane at 3 ranks and at the 8 of one MI355X node (bench.py --gpus 8)."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rdv_worker, args=(r, 3, port, q)) for r in range(3)]
+    ps = [ctx.Process(target=_rdv_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=120) for _ in ps)
@@ -64,8 +66,8 @@ def test_rendezvous_two_processes():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, got, mx, blob in res:
-        assert got == [{"rank": r, "n": r * 10} for r in range(3)]
-        assert mx == 3.0
+        assert got == [{"rank": r, "n": r * 10} for r in range(world)]
+        assert mx == (world - 1) * 1.5
         assert blob == b"uid-" + bytes(range(124))
 
 
