@@ -42,7 +42,8 @@ SCENARIOS = {   # LMC:1182-1204 (BASELINE configs 2 / 4 / 5: urban; 3: parking; 
 def config_label(scenario, frames, points):
     if scenario == "urban_complex" and points >= 1_000_000:
         return "BASELINE config 5 shape: 1M-pt dense frames"
-    return {"urban_complex": "BASELINE config 2 (config 4 at 8 GPUs)", "parking_detailed": "BASELINE config 3",
+    return {"urban_complex": "BASELINE config 2 per GPU; config 4's frame shape at N GPUs (config 4 itself is "
+                             "6000 frames = 750 per GPU at 8)", "parking_detailed": "BASELINE config 3",
             "highway_simple": "BASELINE config 1 scenario"}[scenario]
 
 
