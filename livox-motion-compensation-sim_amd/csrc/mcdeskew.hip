@@ -538,6 +538,9 @@ int mc_batch_checksum(mc_batch* b, double* sums) {
 }
 
 // ---- the hot path ---------------------------------------------------------------------------
+#ifndef MC_PREP_SERIAL
+#define MC_PREP_SERIAL 0   // 1: per-step prep on the main stream (rejected: step wall +2 to +6 us)
+#endif
 namespace {
 int deskew_check(mc_ctx* c, const mc_batch* in, const mc_batch* out, int mode, int pose_select) {
   CHECK_ARG(c && in && out, "NULL argument");
@@ -657,6 +660,25 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
     HIPCHK(hipStreamWaitEvent(sd, c->ev_order, 0));
   }
 
+#if MC_PREP_SERIAL
+  // variant: the prep on the main stream right before its kernel (no cross-queue events)
+  {
+    StepPlan sp;
+    deskew_plan(c, in, out, mode, pose_select, c->buf, &sp);
+    HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[c->buf], 0));   // a pipelined prep of an earlier call
+    {
+      TimedRegion tr(c, &c->prep_ev, s);
+      launch_prep(sp, s);
+    }
+    if (sp.kernel >= 0) {
+      TimedRegion tr(c, &c->main_ev, s);
+      launch_main(sp, s);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_main_done[c->buf], s));
+    return MC_OK;
+  }
+#endif
   // Pipelining: the per-step tables come in two halves.  This step's prep runs on the side
   // stream as soon as the deskew kernel that last read half `h` (two calls back) has finished,
   // i.e. concurrently with the previous call's kernel; the kernel waits for its own prep.
