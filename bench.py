@@ -1,19 +1,33 @@
-"""Benchmark: Mpoints/s deskewed + % of HBM roofline on synthetic Mid-70 100k-point frames.
+"""Benchmark: Mpoints/s deskewed + % of HBM roofline on synthetic Mid-70 frames, BASELINE configs.
 
-One step = one pass of the hot path over one batch: the per-step pose prep (pose selection /
-segment tables) + the deskew kernel over every point of the rank's 600 frames x 100k points
-(BASELINE config 2: urban_complex, figure_eight).  Inputs are generated on the device and are
-resident in HBM before the timed region.  Weak scaling: each rank owns 600 frames of a
-600*N-frame urban_complex run (frames shard by index, no collective on the data path); the
-RCCL gather of the merged cloud to rank 0 is timed separately after the steps.
+One step = one pass of the hot path over the rank's batch: the per-step pose prep (pose selection /
+segment tables, LMC:804-812) + the deskew kernel over every point of the rank's frames.  Inputs are
+generated on the device and are resident in HBM before the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode pose_slerp|frame|imu]
+Workload = a BASELINE config (BASELINE.json "configs"), whose frames shard by index across the ranks
+as contiguous point-balanced ranges (dist.plan_shards) — no collective on the data path:
+    --config 2  urban_complex figure_eight, 600 frames x 100k        (default at 1 GPU)
+    --config 3  parking_detailed circular, 600 x 100k, noise on
+    --config 4  urban_complex figure_eight, 6000 x 100k (duration 600 s; 750 per GPU at 8)
+                                                                      (default at N > 1 GPUs)
+    --config 5  urban_complex poses, 1200 x 1M-point dense frames (150 per GPU at 8)
+    --config 1  highway_simple linear, 10 x 20k (the reference's CPU case; launch-bound)
+The total job is fixed per config ("scaling": "strong").  --frames F [--points n] instead runs F
+frames per GPU of a longer run (weak scaling, the round-1 default).
+
+After the timed steps (outside the timed region): the rank's output is spot-checked against the
+oracle (N = 1), or, at N > 1, the merged cloud is gathered to rank 0 over RCCL (LMC:887-889), timed,
+and sampled frames of every rank's shard are checked against the oracle (``gather.parity``).  A
+failed or hung gather or a parity miss exits non-zero after the JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode pose_slerp|frame|imu] [--config C]
     torchrun --nproc-per-node N ... bench.py --gpus N   (one process per GPU, RCCL over xGMI)
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -24,42 +38,130 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import mcamd as mc  # noqa: E402
 
-URBAN = {"duration": 120.0, "trajectory_type": "figure_eight", "environment_complexity": "complex",
-         "max_speed": 12.0, "lidar_fps": 10}   # LMC:1183-1189
 BYTES_PER_POINT = {"pose_slerp": 36, "imu": 36, "frame": 32}   # SURVEY §8d algorithmic bytes
 HBM_PEAK_GBS = 8000.0                                          # MI355X_MICROARCH.md chip table
+KERNEL = {"pose_slerp": "k_deskew_points<1>", "imu": "k_deskew_points<2>", "frame": "k_deskew_frame"}
+REL_TOL = 1e-5                                                 # north_star, scaled per point
 
-
-SCENARIOS = {   # LMC:1182-1204 (BASELINE configs 2 / 4 / 5: urban; 3: parking; 1: highway)
-    "urban_complex": URBAN,
+SCENARIOS = {   # LMC:1182-1204
+    "urban_complex": {"duration": 120.0, "trajectory_type": "figure_eight", "environment_complexity": "complex",
+                      "max_speed": 12.0, "lidar_fps": 10},
     "parking_detailed": {"duration": 30.0, "trajectory_type": "circular", "environment_complexity": "medium",
                          "max_speed": 5.0, "lidar_fps": 20},
     "highway_simple": {"duration": 60.0, "trajectory_type": "linear", "environment_complexity": "simple",
                        "max_speed": 25.0, "lidar_fps": 15},
 }
+CONFIGS = {    # BASELINE.json "configs" (index = position + 1)
+    1: {"scenario": "highway_simple", "frames": 10, "points": 20_000,
+        "label": "BASELINE config 1: highway_simple linear, 10 frames x 20k pts"},
+    2: {"scenario": "urban_complex", "frames": 600, "points": 100_000,
+        "label": "BASELINE config 2: urban_complex figure_eight, 600 frames x 100k pts"},
+    3: {"scenario": "parking_detailed", "frames": 600, "points": 100_000,
+        "label": "BASELINE config 3: parking_detailed circular, 600 frames x 100k pts, IMU/GPS noise on"},
+    4: {"scenario": "urban_complex", "frames": 6000, "points": 100_000, "duration": 600.0,
+        "label": "BASELINE config 4: urban_complex figure_eight, 6000 frames x 100k pts sharded over the GPUs, "
+                 "RCCL gather of merged_aligned"},
+    5: {"scenario": "urban_complex", "frames": 1200, "points": 1_000_000,
+        "label": "BASELINE config 5: 1200 x 1M-pt dense frames (urban_complex poses), HBM-roofline stress"},
+}
 
 
-def config_label(scenario, frames, points):
-    if scenario == "urban_complex" and points >= 1_000_000:
-        return "BASELINE config 5 shape: 1M-pt dense frames"
-    return {"urban_complex": "BASELINE config 2 per GPU; config 4's frame shape at N GPUs (config 4 itself is "
-                             "6000 frames = 750 per GPU at 8)", "parking_detailed": "BASELINE config 3",
-            "highway_simple": "BASELINE config 1 scenario"}[scenario]
+def cpu_cores() -> dict:
+    """Host cores this process may use: the affinity mask, bounded by a cgroup CPU quota if any."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, math.ceil(quota)))
+    return {"affinity": aff, "cgroup_quota_cpus": quota, "usable": usable}
 
 
-def workload(rank, world, frames, points, scenario="urban_complex"):
-    base = SCENARIOS[scenario]
-    cfg = dict(base, duration=max(base["duration"], frames * world / base["lidar_fps"]))
-    sim = mc.LiDARMotionSimulator(cfg)
+def workload(args, rank, world):
+    """(config id or None, label, scenario cfg, pose table, global frame times, global counts,
+    this rank's frame range [lo, hi))."""
+    if args.frames is not None:      # custom weak-scaling job: args.frames per GPU
+        cid, scen, F, n = None, args.scenario, args.frames * world, args.points
+        base = SCENARIOS[scen]
+        cfg = dict(base, duration=max(base["duration"], F / base["lidar_fps"]))
+        label = f"custom: {scen}, {args.frames} frames x {n} pts per GPU (weak scaling)"
+    else:
+        cid = args.config if args.config != "auto" else (2 if world == 1 else 4)
+        cid = int(cid)
+        c = CONFIGS[cid]
+        scen, F, n = c["scenario"], c["frames"], c["points"]
+        cfg = dict(SCENARIOS[scen])
+        if "duration" in c:
+            cfg["duration"] = c["duration"]
+        label = c["label"]
+    sim = mc.LiDARMotionSimulator(cfg)       # seeds numpy's global RNG (LMC:288), seed 42
     tr = sim.add_sensor_noise(sim.generate_trajectory())
-    times = sim.lidar_times()
-    lo = rank * frames
-    return cfg, tr, times[lo:lo + frames], lo
+    times = sim.lidar_times()[:F]
+    assert len(times) == F, (len(times), F)
+    counts = np.full(F, n, dtype=np.int64)
+    b = mc.dist.plan_shards(counts, world)
+    return cid, label, scen, cfg, tr, times, counts, int(b[rank]), int(b[rank + 1])
 
 
+# ---------------------------------------------------------------------------------------------
+# oracle checks (outside the timed region)
+# ---------------------------------------------------------------------------------------------
+def oracle_frame(mode, tr, t_frame, start_ns, imu, n, frame_id):
+    """The oracle's output for one synthetic frame (global frame id) and its per-point scale."""
+    from oracle import restatement as R
+    from oracle import synth
+    x, y, z, i, t = synth.synth_frame(n, 0, 1000 + frame_id)
+    p = np.stack([x, y, z], 1).astype(np.float64)
+    if mode == "pose_slerp":
+        ref = R.deskew_pose_slerp(p, t, t_frame, tr)
+        _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], t_frame + t * 1e-9)
+        scale = np.linalg.norm(p, axis=1) + np.linalg.norm(pos, axis=1)
+    elif mode == "frame":
+        k = int(R.select_pose_index(tr["time"], t_frame))
+        ref = p @ R.euler_xyz_matrix(tr["orientation_imu"][k]).T + tr["position_gps"][k]
+        scale = np.linalg.norm(p, axis=1) + np.linalg.norm(tr["position_gps"][k])
+    else:
+        ref = R.compensate_arrays(p, start_ns + t.astype(np.int64), start_ns, imu[0], imu[1])
+        scale = np.linalg.norm(p, axis=1)
+    return ref, scale, i
+
+
+def check_frames(batch, mode, tr, times, imu, counts, local_frames, global_ids):
+    """Frames of ``batch`` (local indices) against the oracle (global frame ids): the scaled
+    per-coordinate error |a-b| / (|p|+|t|) that gates parity and the naive |a-b|/|b| beside it."""
+    worst, naive = 0.0, []
+    bad_int = 0
+    for lf, gf in zip(local_frames, global_ids):
+        got = batch.download_frames(lf, lf + 1)
+        ref, scale, inten = oracle_frame(mode, tr, float(times[gf]), int(times[gf] * 1e9), imu, int(counts[gf]), gf)
+        err = np.abs(got[:, :3] - ref)
+        worst = max(worst, float((err.max(axis=1) / scale).max()) if len(ref) else 0.0)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            naive.append((err / np.abs(ref)).ravel())
+        bad_int += int(np.count_nonzero(got[:, 3] != inten.astype(np.float64)))
+    nv = np.concatenate(naive) if naive else np.zeros(0)
+    nv = nv[np.isfinite(nv)]
+    return {"frames_checked": [int(g) for g in global_ids], "worst_scaled_err": worst, "tol": REL_TOL,
+            "ok": bool(worst <= REL_TOL and bad_int == 0), "intensity_mismatches": bad_int,
+            "naive_rel_err": {"max": float(nv.max()) if nv.size else 0.0,
+                              "p99_9": float(np.quantile(nv, 0.999)) if nv.size else 0.0,
+                              "median": float(np.median(nv)) if nv.size else 0.0,
+                              "coords_above_1e-5": int(np.count_nonzero(nv > 1e-5)), "coords": int(nv.size),
+                              "note": "|a-b|/|b| per coordinate, no scale floor: large on coordinates that "
+                                      "rotate to ~0 (SURVEY §8c); the gate is worst_scaled_err"}}
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU baseline (before the GPU is touched; the all-cores legs spawn worker processes)
+# ---------------------------------------------------------------------------------------------
 def _cpu_frames(mode, tr, times, counts, frame_lo, budget_s, f_first=0, f_step=1):
-    """The oracle on frames f_first, f_first+f_step, ... until budget_s of compute; 1 BLAS thread.
-    Returns (points, seconds, frames)."""
+    """The oracle on frames f_first, f_first+f_step, ... until budget_s of compute, one BLAS
+    thread.  Returns (points, seconds, frames).  frame mode = the reference's own op sequence
+    (scipy from_euler, R @ P.T, + t, column_stack; LMC:772-776) after the pose selection (804-812)."""
     from threadpoolctl import threadpool_limits
     from oracle import restatement as R
     from oracle import synth
@@ -78,7 +180,8 @@ def _cpu_frames(mode, tr, times, counts, frame_lo, budget_s, f_first=0, f_step=1
             t0 = time.perf_counter()
             if mode == "frame":
                 k = int(R.select_pose_index(tr["time"], times[f]))
-                R.transform_pointcloud(pts, {"translation": tr["position_gps"][k], "rotation": tr["orientation_imu"][k]})
+                R.transform_pointcloud_ref_ops(pts, {"translation": tr["position_gps"][k],
+                                                     "rotation": tr["orientation_imu"][k]})
             elif mode == "pose_slerp":
                 out = R.deskew_pose_slerp(pts[:, :3], t, times[f], tr)
                 np.column_stack([out, pts[:, 3]])
@@ -96,60 +199,89 @@ def _cpu_worker(job):
     return _cpu_frames(*job)
 
 
-def cpu_baselines(mode, tr, times, counts, frame_lo, budget_s, procs):
-    """The oracle (numpy restatement of the reference's op sequence) on the same synthetic frames,
-    generation excluded: one core, then `procs` processes (one BLAS thread each) splitting the
-    frames round-robin.  Runs before the GPU is touched (the pool is spawned)."""
-    import multiprocessing as mp
-    done, secs, nf = _cpu_frames(mode, tr, times, counts, frame_lo, budget_s)
-    single = {"value": done / secs / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
-              "sample": f"{nf} of {len(counts)} frames x {int(counts[0])} pts (oracle numpy restatement, "
-                        f"same synthetic frames, generation excluded, {secs:.1f} s)"}
+def cpu_leg(mode, tr, times, counts, frame_lo, budget_s, procs, pool):
+    n0 = int(counts[0]) if len(counts) else 0
     if procs <= 1:
-        return single
+        done, secs, nf = _cpu_frames(mode, tr, times, counts, frame_lo, budget_s)
+        return {"value": done / secs / 1e6, "unit": "Mpoints/s", "cores": 1, "blas_threads": 1,
+                "sample": f"{nf} of {len(counts)} frames x {n0} pts, {secs:.1f} s of compute"}
     jobs = [(mode, tr, times, counts, frame_lo, budget_s, p, procs) for p in range(procs)]
-    with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.map(_cpu_worker, jobs)
+    res = pool.map(_cpu_worker, jobs)
     pts = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     frames = sum(r[2] for r in res)
-    multi = {"value": pts / wall / 1e6, "unit": "Mpoints/s", "cores": procs, "kind": "port",
-             "sample": f"{frames} of {len(counts)} frames x {int(counts[0])} pts over {procs} processes "
-                       f"(1 BLAS thread each, round-robin frames), rate = points / slowest worker's compute time",
-             "single_core": single}
-    return multi
+    return {"value": pts / wall / 1e6, "unit": "Mpoints/s", "cores": procs, "blas_threads": 1,
+            "sample": f"{frames} of {len(counts)} frames x {n0} pts over {procs} processes (round-robin frames), "
+                      f"rate = points / slowest worker's compute time"}
 
+
+def cpu_baselines(mode, tr, times, counts, frame_lo, budget_s, procs):
+    """The oracle (numpy restatement of the reference's op sequence) on the same synthetic frames,
+    generation excluded: the headline mode and the reference's own frame-mode op sequence
+    (LMC:772-776), each on one core and on ``procs`` processes (OPENBLAS threads = 1 everywhere)."""
+    import multiprocessing as mp
+    legs = [mode] + (["frame"] if mode != "frame" else [])
+    out = {}
+    with mp.get_context("spawn").Pool(procs) if procs > 1 else _NullPool() as pool:
+        for m in legs:
+            single = cpu_leg(m, tr, times, counts, frame_lo, budget_s, 1, None)
+            multi = cpu_leg(m, tr, times, counts, frame_lo, budget_s, procs, pool) if procs > 1 else None
+            out[m] = {"single_core": single, "all_cores": multi}
+    head = out[mode]["all_cores"] or out[mode]["single_core"]
+    line = {"value": head["value"], "unit": "Mpoints/s", "cores": head["cores"], "kind": "port",
+            "sample": f"{mode} mode: " + head["sample"],
+            "legs": out,
+            "note": "oracle = numpy restatement of the reference's op sequence (oracle/restatement.py), same "
+                    "synthetic frames as the GPU, generation excluded; frame leg = scipy from_euler -> R @ P.T -> "
+                    "+ t -> column_stack per frame (LMC:772-776, the reference's own per-frame sequence)"}
+    return line
+
+
+class _NullPool:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+# ---------------------------------------------------------------------------------------------
+# side measurements (SURVEY §8f rows), unchanged contracts
+# ---------------------------------------------------------------------------------------------
+def traffic_file():
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        return json.load(f)
 
 
 def aux_traffic(*kernels):
     """PMC traffic / algorithmic bytes of the kernels around the path (tools/pmc_traffic.py --aux)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        d = json.load(f)
+    d = traffic_file()
     got = {k: d[f"aux:{k}"]["traffic_over_algorithmic"] for k in kernels if f"aux:{k}" in d}
     return got or None
 
 
 def load_traffic(mode, frames, points):
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        d = json.load(f)
-    e = d.get(f"{mode}:{frames}x{points}")
-    return None if e is None else e.get("hbm_bytes_per_launch")
+    """HBM bytes per launch of this mode at this per-GPU shape from profiles/pmc_traffic.json, with
+    where it came from (a separate rocprofv3 --pmc session, not this run)."""
+    e = traffic_file().get(f"{mode}:{frames}x{points}")
+    if e is None:
+        return None, None
+    src = {"file": "profiles/pmc_traffic.json", "key": f"{mode}:{frames}x{points}", "session": e.get("tag"),
+           "traffic_over_algorithmic": e.get("traffic_over_algorithmic"),
+           "how": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes of bench.py (tools/pmc_traffic.py; "
+                  "FETCH_SIZE x2 gfx950 correction), measured in that session, not in this run"}
+    return e.get("hbm_bytes_per_launch"), src
 
 
 def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, graph=False):
-    """Timed region: wall clock around ``steps`` steps.  ``live``: HIP events (no system-scope
-    fence) around the kernels of every ``every``-th timed step themselves — on the stream each
-    kernel is launched on — give the roofline's per-launch kernel time; events around every launch
-    would cost ~2 % of the step rate (measured), sampling one step in ten ~0.2 %.  Otherwise a
-    second, untimed pass carries events around every launch.  ``graph``: the ``steps`` steps are
-    one replay of a HIP graph of ``steps`` deskew steps (``Context.deskew_steps``: every step runs
-    its prep and kernel; the graph is captured before the timed region), else ``steps`` calls."""
+    """Timed region: wall clock around ``steps`` steps.  ``live``: HIP events on the sampled steps'
+    kernels themselves (hipExtLaunchKernel start/stop events: the dispatch's own timestamps, no
+    marker packets between the steps) give the roofline's per-launch kernel time.  Otherwise a
+    second, untimed pass carries events on every launch.  ``graph``: the ``steps`` steps are one
+    replay of a HIP graph (Context.deskew_steps), else ``steps`` calls."""
     every = 10 if steps >= 50 else 5
     ctx.timing(live)           # warmup steps fill the context's event pool for the sampled steps
     for _ in range(warmup):
@@ -181,7 +313,7 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, graph=False)
         ctx.sync()
         ctx.timing(False)
     tm = ctx.read_timing()
-    return t1 - t0, tm
+    return t1 - t0, tm, every
 
 
 def measure_stager(ctx, b_in, b_out, n_rank, reps):
@@ -219,9 +351,10 @@ def measure_scan(ctx, cfg, tr, reps, cpu_budget):
     E = 29_000
     env = np.column_stack([rng.uniform(-200, 200, E), rng.uniform(-200, 200, E), rng.uniform(-25, 70, E),
                            rng.uniform(0, 1, E)])
-    times = mc.trajectory.lidar_times(cfg)[:1200]
+    urban = SCENARIOS["urban_complex"]
+    times = mc.trajectory.lidar_times(dict(cfg, **urban))[:1200]
     F = len(times)
-    scfg = dict(mc.default_config(), **URBAN)
+    scfg = dict(mc.default_config(), **urban)
     ctx.set_environment(env)
     ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
     out = ctx.scan(times, scfg)
@@ -309,7 +442,7 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
                         "traffic_over_algorithmic": aux_traffic("k_pcd_measure", "k_pcd_write")}
     if cpu_budget > 0:
         from oracle import codecs as C
-        host = b_out.download_aos()[:int(counts[0])]
+        host = b_out.download_frames(0, 1)
         t0 = time.perf_counter()
         C.lvx_bytes([{"frame_id": 0, "timestamp": 0.0, "points": host}])
         t1 = time.perf_counter()
@@ -323,10 +456,13 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     return rep
 
 
-def timed_gather(ctx, rdv, b_in, b_out, mode, n_rank, world, timeout_s):
+# ---------------------------------------------------------------------------------------------
+# the merged-cloud gather (N > 1)
+# ---------------------------------------------------------------------------------------------
+def timed_gather(ctx, rdv, b_in, b_out, mode, n_rank, world, timeout_s, check):
     """The merged-cloud gather to rank 0 (LMC:887-889 over RCCL), after and outside the timed
-    steps, under a watchdog so that a stuck collective can never cost the throughput line.
-    Returns (report, hung).  The root's wall time is the gather time (it receives every shard)."""
+    steps, under a watchdog.  ``check(merged)`` runs on the root afterwards (the parity of sampled
+    frames).  Returns (report, hung).  The root's wall time is the gather time."""
     import threading
     res = {}
 
@@ -335,18 +471,21 @@ def timed_gather(ctx, rdv, b_in, b_out, mode, n_rank, world, timeout_s):
             comm = mc.dist.RcclComm(ctx, rdv)
             ctx.deskew(b_in, b_out, mode=mode)
             ctx.sync()
+            sizes = rdv.allgather(int(b_out.n_points))
             rdv.barrier()
             t0 = time.perf_counter()
             merged = mc.dist.gather_merged(ctx, comm, rdv, b_out, root=0)
             dt = time.perf_counter() - t0
-            moved = 16 * n_rank * (world - 1)
-            res["report"] = {"seconds": dt, "bytes_into_root": moved, "GBs": moved / dt / 1e9,
-                             "merged_points": int(n_rank * world), "timed_on": "root wall clock"}
+            moved = 16 * (sum(sizes) - sizes[0])
+            rep = {"seconds": dt, "bytes_into_root": moved, "GBs": moved / dt / 1e9,
+                   "merged_points": int(sum(sizes)), "timed_on": "root wall clock"}
             if merged is not None:
+                rep["parity"] = check(merged)
                 merged.close()
+            res["report"] = rep
             comm.close()
-        except Exception as e:  # report, never fail the throughput line
-            res["report"] = {"error": str(e)}
+        except Exception as e:  # reported; the process exits non-zero after the line
+            res["report"] = {"error": f"{type(e).__name__}: {e}"}
 
     th = threading.Thread(target=work, daemon=True)
     th.start()
@@ -362,37 +501,43 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", default="pose_slerp", choices=list(BYTES_PER_POINT))
-    ap.add_argument("--frames", type=int, default=600)
-    ap.add_argument("--points", type=int, default=100_000)
-    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work (per process)")
-    ap.add_argument("--cpu-procs", type=int, default=16, help="processes for the all-cores CPU baseline "
-                    "(the box's CPU share per GPU)")
+    ap.add_argument("--config", default="auto", choices=["auto", "1", "2", "3", "4", "5"],
+                    help="BASELINE config (auto: 2 at one GPU, 4 at N > 1)")
+    ap.add_argument("--frames", type=int, default=None, help="custom job: frames per GPU (weak scaling)")
+    ap.add_argument("--points", type=int, default=100_000, help="custom job: points per frame")
+    ap.add_argument("--scenario", default="urban_complex", choices=list(SCENARIOS), help="custom job: pose table")
+    ap.add_argument("--cpu-budget", type=float, default=6.0, help="seconds of CPU work per baseline leg")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="processes for the all-cores CPU legs (0: every core this process may use)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra-modes", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL merged-cloud gather (N>1)")
+    ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check (N=1)")
     ap.add_argument("--events-after", action="store_true",
                     help="per-launch HIP events in a second, untimed pass instead of the timed steps")
-    ap.add_argument("--gather-timeout", type=float, default=120.0)
+    ap.add_argument("--gather-timeout", type=float, default=300.0)
     ap.add_argument("--graph", action="store_true",
                     help="issue the timed steps as one HIP-graph replay (Context.deskew_steps; kernel time from "
                          "wall-clock stamp nodes, not HIP events) instead of separate calls")
-    ap.add_argument("--scenario", default="urban_complex", choices=list(SCENARIOS),
-                    help="pose table of this LMC scenario (BASELINE config 3 = parking_detailed)")
     args = ap.parse_args()
 
     rank, local_rank, world = mc.dist.env_rank()
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     rdv = mc.dist.Rendezvous(rank, world)
-    cfg, tr, times, lo = workload(rank, world, args.frames, args.points, args.scenario)
-    counts = np.full(args.frames, args.points, dtype=np.int64)
+    cid, label, scen, cfg, tr, times_all, counts_all, lo, hi = workload(args, rank, world)
+    times = times_all[lo:hi]
+    counts = counts_all[lo:hi]
+    cores = cpu_cores()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        # before the GPU is initialised: the all-cores leg spawns worker processes
-        cpu = cpu_baselines(args.mode, tr, times, counts, lo, args.cpu_budget,
-                            min(args.cpu_procs, len(os.sched_getaffinity(0))))
-        cpu["cores_available"] = len(os.sched_getaffinity(0))
+        # before the GPU is initialised: the all-cores legs spawn worker processes
+        procs = args.cpu_procs or cores["usable"]
+        cpu = cpu_baselines(args.mode, tr, times, counts, lo, args.cpu_budget, procs)
+        cpu["cores_visible"] = cores
     ctx = mc.Context()   # $MCDESKEW_DEVICE, else $LOCAL_RANK
+    devices = rdv.allgather(ctx.pci_bus_id())
+    n_devices = len(set(devices))
 
     b_in = ctx.batch(counts, with_time=True)
     b_out = ctx.batch(counts)
@@ -407,93 +552,124 @@ def main():
     ts_imu, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
     ctx.set_imu(ts_imu, gyro)
     n_rank = int(counts.sum())
+    n_total = int(counts_all.sum())
+    src_of = {m: (b_xyz if m == "frame" else b_in) for m in BYTES_PER_POINT}
 
     modes = [args.mode] + ([] if args.no_extra_modes else [m for m in BYTES_PER_POINT if m != args.mode])
     results = {}
+    every = 10
     for mode in modes:
         steps = args.steps if mode == args.mode else max(10, args.steps // 4)
-        wall, tm = run_mode(ctx, rdv, mode, b_xyz if mode == "frame" else b_in, b_out, steps, args.warmup,
-                            live=not args.events_after, graph=args.graph)
+        wall, tm, ev = run_mode(ctx, rdv, mode, src_of[mode], b_out, steps, args.warmup,
+                                live=not args.events_after, graph=args.graph)
+        if mode == args.mode:
+            every = ev
         wall_max = rdv.max(wall)
         main_avg_s = tm["main_ms"] / max(tm["main_launches"], 1) / 1e3
         prep_avg_s = tm["prep_ms"] / max(tm["prep_launches"], 1) / 1e3
-        achieved = BYTES_PER_POINT[mode] * n_rank / main_avg_s / 1e9
+        achieved = BYTES_PER_POINT[mode] * n_rank / main_avg_s / 1e9 if main_avg_s > 0 else 0.0
         results[mode] = {"wall_s": wall_max, "steps": steps, "main_avg_us": main_avg_s * 1e6,
                          "timed_launches": int(tm["main_launches"]),
                          "prep_avg_us": prep_avg_s * 1e6, "achieved_GBs": achieved,
-                         "value": n_rank * world * steps / wall_max / 1e6}
+                         "value": n_total * steps / wall_max / 1e6}
 
-    stager = measure_stager(ctx, b_xyz, b_out, n_rank, min(args.steps, 50))
+    stager = measure_stager(ctx, b_xyz, b_out, n_rank, min(args.steps, 50)) if n_rank else None
     scan = codecs = None
-    if not args.no_extra_modes:
+    if not args.no_extra_modes and n_rank:
         scan = measure_scan(ctx, cfg, tr, 10, 0.0 if (args.no_cpu or world > 1) else 3.0)
         ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
         ctx.deskew(b_in, b_out, mode=args.mode)
         codecs = measure_codecs(ctx, b_out, n_rank, 5, 0.0 if (args.no_cpu or world > 1) else 1.0)
 
-    gather = None
+    imu = (ts_imu, gyro)
+    F_all = len(counts_all)
+    gather = parity = None
     hung = False
     if world > 1 and not args.no_gather:
-        gather, hung = timed_gather(ctx, rdv, b_xyz if args.mode == "frame" else b_in, b_out, args.mode, n_rank,
-                                    world, args.gather_timeout)
+        bounds = mc.dist.plan_shards(counts_all, world)
+        sample = sorted({int(g) for r in range(world) if bounds[r + 1] > bounds[r]
+                         for g in (bounds[r], (bounds[r] + bounds[r + 1]) // 2, bounds[r + 1] - 1)})
 
+        def check(merged):
+            return check_frames(merged, args.mode, tr, times_all, imu, counts_all, sample, sample)
+        gather, hung = timed_gather(ctx, rdv, src_of[args.mode], b_out, args.mode, n_rank, world,
+                                    args.gather_timeout, check)
+    elif world == 1 and not args.no_check and F_all:
+        ctx.deskew(src_of[args.mode], b_out, mode=args.mode)
+        ctx.sync()
+        loc = sorted({0, F_all // 2, F_all - 1})
+        parity = check_frames(b_out, args.mode, tr, times_all, imu, counts_all, loc, loc)
+
+    ok = True
     if rank == 0:
         r = results[args.mode]
-        traffic = load_traffic(args.mode, args.frames, args.points)
+        per_gpu_frames = hi - lo
+        traffic, traffic_src = load_traffic(args.mode, per_gpu_frames, int(counts_all[0]) if F_all else 0)
+        shared = n_devices < world
+        scaling = "weak" if cid is None else "strong"
+        gather_ok = None if gather is None else bool("error" not in gather and gather.get("parity", {}).get("ok"))
+        ok = (gather_ok is not False) and (parity is None or parity["ok"]) and not hung
         line = {
             "metric": "Mpoints/s deskewed (100k-pt Mid-70 frames) + % HBM roofline",
             "value": r["value"],
             "unit": "Mpoints/s",
-            "n_gpus": world,
+            "n_gpus": n_devices,
             "steps": r["steps"],
             "warmup": args.warmup,
             "ms_per_step": r["wall_s"] / r["steps"] * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling if not shared else f"{scaling} (NOT a scaling result: {world} ranks share "
+                                                  f"{n_devices} device(s))",
             "vs_baseline": None,
             "dtype": "f32 (f64 pose/angle setup)",
-            "data": f"synthetic Mid-70 frames (counter-hash generator, on device); reference {args.scenario} "
-                    "pose table, seed 42",
-            "config": {"workload": f"{args.scenario} {cfg['trajectory_type']}, {args.frames} frames x {args.points} "
-                                   f"pts per GPU ({config_label(args.scenario, args.frames, args.points)}; "
-                                   f"weak scaling over {world} GPU)",
-                       "scenario": args.scenario,
-                       "mode": args.mode, "frames_per_gpu": args.frames, "points_per_frame": args.points,
-                       "global_frames": args.frames * world, "parallelism": f"frame-shard x{world}"},
+            "data": f"synthetic Mid-70 frames (counter-hash generator, on device); reference {scen} pose table, "
+                    "seed 42, GPS/IMU noise on",
+            "config": {"workload": f"{label}; {world} rank(s), frames {lo}..{hi - 1} on rank 0",
+                       "baseline_config": cid, "scenario": scen, "mode": args.mode,
+                       "global_frames": F_all, "points_per_frame": int(counts_all[0]) if F_all else 0,
+                       "total_points": n_total, "rank0_frames": per_gpu_frames,
+                       "parallelism": f"frame-shard x{world} (dist.plan_shards)", "ranks": world,
+                       "devices": n_devices},
             "roofline": {"bound": "hbm", "achieved": r["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": r["achieved_GBs"] / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "kernel": {"pose_slerp": "k_deskew_points<1>", "imu": "k_deskew_points<2>",
-                                    "frame": "k_deskew_frame"}[args.mode],
-                         "kernel_avg_us": r["main_avg_us"], "bytes_per_point": BYTES_PER_POINT[args.mode],
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": KERNEL[args.mode], "kernel_avg_us": r["main_avg_us"],
+                         "bytes_per_point": BYTES_PER_POINT[args.mode], "points_per_launch": n_rank,
                          "kernel_time": ("HIP events around every launch of a second, untimed pass"
                                          if args.events_after else
                                          f"wall-clock stamp nodes around the kernels of {r['timed_launches']} of the "
-                                         f"{r['steps']} steps of the step graph (every 10th)"
+                                         f"{r['steps']} steps of the step graph (every {every}th)"
                                          if args.graph else
-                                         f"HIP events around the kernels of {r['timed_launches']} of the "
-                                         f"{r['steps']} timed steps (every 10th), on the kernel's stream")},
+                                         f"HIP events (hipExtLaunchKernel start/stop, the dispatch's own timestamps) "
+                                         f"on the kernels of {r['timed_launches']} of the {r['steps']} timed steps "
+                                         f"(every {every}th), on the kernel's stream")},
+            "step_over_kernel": (r["wall_s"] / r["steps"] * 1e6) / r["main_avg_us"] if r["main_avg_us"] else None,
             "prep_avg_us": r["prep_avg_us"],
-            "step_issue": "per-call launches" if not args.graph else
-                          f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
+            "step_issue": ("per-call launches; prep as an any-order packet on the kernel's queue"
+                           if not args.graph else f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)"),
             "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
-                          "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"]}
+                          "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"],
+                          "ms_per_step": v["wall_s"] / v["steps"] * 1e3}
                       for m, v in results.items()},
             "stager": stager,
             "scan_environment": scan,
             "codecs": codecs,
+            "parity": parity,
             "gather": gather,
+            "gather_ok": gather_ok,
+            "ok": ok,
         }
         if cpu is not None:
             line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     if hung:
-        # a collective is stuck inside RCCL: finalisers would block on its stream; the result
-        # line is out, so leave without running them
+        # a collective is stuck inside RCCL: finalisers would block on its stream; the line is out
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(3)
     rdv.close()
+    if not ok:
+        sys.exit(4)
 
 
 if __name__ == "__main__":

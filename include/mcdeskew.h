@@ -87,6 +87,9 @@ typedef struct mc_comm mc_comm;
 int mc_abi_version(void);
 const char* mc_last_error(void);
 int mc_device_count(int* count);
+/* PCI bus id ("dddd:bb:dd.f") of a visible device: tells ranks that share one GPU apart from
+ * ranks on distinct GPUs (bench.py counts devices, not ranks) */
+int mc_device_pci_bus_id(int device, char* out, int len);
 int mc_create(int device, mc_ctx** out);
 int mc_destroy(mc_ctx* ctx);
 int mc_sync(mc_ctx* ctx);
@@ -122,6 +125,9 @@ int mc_batch_upload_columns_f32(mc_batch* b, const float* x, const float* y, con
 int mc_batch_upload_time_ns(mc_batch* b, const int32_t* t_ns);
 /* device SoA float32 -> host dense AoS (N,4) float64 (the (N,4) f64 layout LMC:776 returns) */
 int mc_batch_download_aos_f64(mc_batch* b, double* aos_out);
+/* frames [f0, f1) only: (doff[f1] - doff[f0], 4) float64 rows (spot checks of batches too large
+ * to bring back whole, e.g. BASELINE config 5's 1.2 G points) */
+int mc_batch_download_frames_aos_f64(mc_batch* b, int32_t f0, int32_t f1, double* aos_out);
 int mc_batch_download_columns_f32(mc_batch* b, float* x, float* y, float* z, float* intensity);
 int mc_batch_download_time_ns(mc_batch* b, int32_t* t_ns);
 
@@ -240,6 +246,18 @@ int mc_comm_destroy(mc_comm* comm);
  * non-root ranks and on root must have been created with the concatenated frame counts. */
 int mc_comm_gather_batch(mc_comm* comm, const mc_batch* local, int root, mc_batch* merged);
 int mc_comm_allreduce_max_f64(mc_comm* comm, double* values, int64_t n);
+/* Host only (no device work): the plan mc_comm_gather_batch follows for n ranks whose shards hold
+ * padded[q] points of columns[q] (4 or 5) values per block into a merged batch of merged_padded
+ * points and merged_columns columns: offset_out[q] = the shard's first padded point in the merged
+ * batch (rank order == np.vstack order, LMC:887-889), stage_offset_out[q] = its value offset in the
+ * root's staging area (-1: received in place), *stage_values_out = staging size.  Invalid plans
+ * (sizes that do not add up, a shard with fewer columns than the merged batch) -> MC_ERR_INVALID. */
+int mc_gather_plan(int32_t nranks, int32_t root, const int64_t* padded, const int64_t* columns, int64_t merged_padded,
+                   int32_t merged_columns, int64_t* offset_out, int64_t* stage_offset_out, int64_t* stage_values_out);
+/* The same merge inside one process: n shard batches of one context into `merged` (created with the
+ * concatenated frame counts), shard `root` playing the root's own batch and device copies standing
+ * in for the RCCL receives — the plan, staging and re-pitch of mc_comm_gather_batch.  Synchronous. */
+int mc_gather_batches(mc_ctx* ctx, int32_t n, const mc_batch* const* shards, int32_t root, mc_batch* merged);
 
 #ifdef __cplusplus
 }

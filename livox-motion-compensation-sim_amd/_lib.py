@@ -50,6 +50,7 @@ _SIGS = {
     "mc_abi_version": (c_int, []),
     "mc_last_error": (c_char_p, []),
     "mc_device_count": (c_int, [POINTER(c_int)]),
+    "mc_device_pci_bus_id": (c_int, [c_int, POINTER(c_char), c_int]),
     "mc_create": (c_int, [c_int, POINTER(c_void_p)]),
     "mc_destroy": (c_int, [c_void_p]),
     "mc_sync": (c_int, [c_void_p]),
@@ -65,6 +66,7 @@ _SIGS = {
     "mc_batch_upload_columns_f32": (c_int, [c_void_p, _pf, _pf, _pf, _pf]),
     "mc_batch_upload_time_ns": (c_int, [c_void_p, _pi32]),
     "mc_batch_download_aos_f64": (c_int, [c_void_p, _pd]),
+    "mc_batch_download_frames_aos_f64": (c_int, [c_void_p, c_int32, c_int32, _pd]),
     "mc_batch_download_columns_f32": (c_int, [c_void_p, _pf, _pf, _pf, _pf]),
     "mc_batch_download_time_ns": (c_int, [c_void_p, _pi32]),
     "mc_device_alloc": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
@@ -101,6 +103,8 @@ _SIGS = {
     "mc_comm_destroy": (c_int, [c_void_p]),
     "mc_comm_gather_batch": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "mc_comm_allreduce_max_f64": (c_int, [c_void_p, _pd, c_int64]),
+    "mc_gather_plan": (c_int, [c_int32, c_int32, _pi64, _pi64, c_int64, c_int32, _pi64, _pi64, _pi64]),
+    "mc_gather_batches": (c_int, [c_void_p, c_int32, c_void_p, c_int32, c_void_p]),
 }
 EXPORTED = tuple(_SIGS)
 

@@ -10,6 +10,7 @@
 // librccl is dlopen'ed on first use so the core library loads without it.
 #include "../../include/mcdeskew.h"
 #include "internal.hpp"
+#include "plan.hpp"
 
 #include <dlfcn.h>
 #include <rccl/rccl.h>
@@ -72,12 +73,42 @@ struct mc_comm {
   mc_ctx* ctx = nullptr;
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
-  int64_t* d_scratch = nullptr;  // 2 (nranks + 1) int64 for the (padded size, columns) allgather
+  int64_t* d_scratch = nullptr;  // 4 (nranks + 1) int64: the (sizes, columns, merged sizes) allgather
   float* d_stage = nullptr;      // root: shards whose column count differs from the merged batch
   int64_t stage_cap = 0;
   double* d_red = nullptr;       // reduction buffer
   int64_t red_cap = 0;
 };
+
+namespace {
+// grow-only device staging area for shards re-pitched on arrival
+int ensure_stage(float** d, int64_t* cap, int64_t values) {
+  if (values <= *cap) return MC_OK;
+  if (*d) (void)hipFree(*d);
+  *d = nullptr;
+  *cap = 0;
+  const hipError_t e = hipMalloc(d, (size_t)values * sizeof(float));
+  if (e != hipSuccess) return fail(MC_ERR_NOMEM, "gather staging (%lld values): %s", (long long)values, hipGetErrorString(e));
+  *cap = values;
+  return MC_OK;
+}
+// plan.hpp's gather_finish with device copies on stream s (HIP status of the first failure)
+hipError_t finish_on_device(const mcplan::GatherPlan& G, int nranks, int root, const int64_t* P, const int64_t* C,
+                            mc_batch* merged, const float* root_src, const float* stage, hipStream_t s) {
+  hipError_t err = hipSuccess;
+  auto copy = [&](float* d, const float* src, int64_t n) {
+    err = hipMemcpyAsync(d, src, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s);
+    return err == hipSuccess ? 0 : 1;
+  };
+  auto copy2d = [&](float* d, int64_t dp, const float* src, int64_t sp, int64_t w, int64_t rows) {
+    err = hipMemcpy2DAsync(d, (size_t)dp * sizeof(float), src, (size_t)sp * sizeof(float), (size_t)w * sizeof(float),
+                           (size_t)rows, hipMemcpyDeviceToDevice, s);
+    return err == hipSuccess ? 0 : 1;
+  };
+  mcplan::gather_finish(G, nranks, root, P, C, merged->d_cols, merged->C, root_src, stage, copy, copy2d);
+  return err;
+}
+}  // namespace
 
 #define NCCLCHK(expr)                                                                     \
   do {                                                                                    \
@@ -115,7 +146,7 @@ int mc_comm_init(mc_ctx* ctx, int nranks, int rank, const char id_in[128], mc_co
   c->rank = rank;
   ncclResult_t r = g_rccl.CommInitRank(&c->comm, nranks, id, rank);
   if (r != ncclSuccess) { delete c; return fail(MC_ERR_COMM, "ncclCommInitRank: %s", g_rccl.GetErrorString(r)); }
-  if (hipMalloc(&c->d_scratch, sizeof(int64_t) * 2 * (nranks + 1)) != hipSuccess) {
+  if (hipMalloc(&c->d_scratch, sizeof(int64_t) * 4 * (nranks + 1)) != hipSuccess) {
     g_rccl.CommDestroy(c->comm);
     delete c;
     return fail(MC_ERR_NOMEM, "hipMalloc failed");
@@ -140,18 +171,27 @@ int mc_comm_gather_batch(mc_comm* c, const mc_batch* local, int root, mc_batch* 
   if (!c || !local) return fail(MC_ERR_INVALID, "NULL argument");
   if (root < 0 || root >= c->nranks) return fail(MC_ERR_INVALID, "bad root %d", root);
   if (local->ctx != c->ctx) return fail(MC_ERR_INVALID, "batch belongs to another context");
+  const bool is_root = c->rank == root;
+  if (is_root && !merged) return fail(MC_ERR_INVALID, "root needs a merged batch");
+  if (is_root && merged->ctx != c->ctx) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
   HIPCHK(hipSetDevice(c->ctx->device));
   hipStream_t s = c->ctx->stream;
-  // every rank's padded length and column count (the merged layout is the rank-ordered concatenation)
-  const int64_t mine[2] = {local->P, local->C};
-  HIPCHK(hipMemcpyAsync(c->d_scratch + 2 * c->nranks, mine, sizeof(mine), hipMemcpyHostToDevice, s));
-  NCCLCHK(g_rccl.AllGather(c->d_scratch + 2 * c->nranks, c->d_scratch, 2, ncclInt64, c->comm, s));
-  std::vector<int64_t> PC(2 * c->nranks);
-  HIPCHK(hipMemcpyAsync(PC.data(), c->d_scratch, sizeof(int64_t) * 2 * c->nranks, hipMemcpyDeviceToHost, s));
+  // every rank's (padded length, column count) and the root's merged (padded length, column
+  // count): all ranks then hold the whole plan and reject a bad one together, before any send
+  const int64_t mine[4] = {local->P, local->C, is_root ? merged->P : -1, is_root ? merged->C : -1};
+  const int nr = c->nranks;
+  HIPCHK(hipMemcpyAsync(c->d_scratch + 4 * nr, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+  NCCLCHK(g_rccl.AllGather(c->d_scratch + 4 * nr, c->d_scratch, 4, ncclInt64, c->comm, s));
+  std::vector<int64_t> all(4 * (size_t)nr);
+  HIPCHK(hipMemcpyAsync(all.data(), c->d_scratch, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  auto P = [&](int q) { return PC[2 * q]; };
-  auto C = [&](int q) { return PC[2 * q + 1]; };
-  if (c->rank != root) {
+  std::vector<int64_t> P(nr), C(nr);
+  for (int q = 0; q < nr; ++q) { P[q] = all[4 * (size_t)q]; C[q] = all[4 * (size_t)q + 1]; }
+  mcplan::GatherPlan G;
+  const std::string perr =
+      mcplan::plan_gather(nr, root, P.data(), C.data(), all[4 * (size_t)root + 2], all[4 * (size_t)root + 3], &G);
+  if (!perr.empty()) return fail(MC_ERR_INVALID, "%s", perr.c_str());
+  if (!is_root) {
     if (local->P > 0) {
       NCCLCHK(g_rccl.GroupStart());
       NCCLCHK(g_rccl.Send(local->d_cols, (size_t)(local->C * local->P), ncclFloat32, root, c->comm, s));
@@ -160,53 +200,17 @@ int mc_comm_gather_batch(mc_comm* c, const mc_batch* local, int root, mc_batch* 
     HIPCHK(hipStreamSynchronize(s));
     return MC_OK;
   }
-  if (!merged) return fail(MC_ERR_INVALID, "root needs a merged batch");
-  int64_t tot = 0, staged = 0;
-  for (int q = 0; q < c->nranks; ++q) {
-    tot += P(q);
-    if (q != root && C(q) != merged->C) staged += C(q) * P(q);
-  }
-  if (tot != merged->P)
-    return fail(MC_ERR_INVALID, "merged batch holds %lld padded points, ranks sent %lld", (long long)merged->P,
-                (long long)tot);
-  if (staged > c->stage_cap) {
-    if (c->d_stage) (void)hipFree(c->d_stage);
-    c->d_stage = nullptr;
-    c->stage_cap = 0;
-    HIPCHK(hipMalloc(&c->d_stage, staged * sizeof(float)));
-    c->stage_cap = staged;
-  }
-  // copy the first min(C) columns of every block of a shard into the merged batch at `off`
-  auto repitch = [&](const float* src, int64_t cs, int64_t np, int64_t off) {
-    const int64_t cm = merged->C, w = std::min(cs, cm);
-    return hipMemcpy2DAsync(merged->d_cols + off * cm, (size_t)(cm * mcimpl::kBatchBlock * sizeof(float)), src,
-                            (size_t)(cs * mcimpl::kBatchBlock * sizeof(float)), (size_t)(w * mcimpl::kBatchBlock * sizeof(float)),
-                            (size_t)(np / mcimpl::kBatchBlock), hipMemcpyDeviceToDevice, s);
-  };
-  std::vector<int64_t> off(c->nranks), soff(c->nranks, -1);
+  if (int r = ensure_stage(&c->d_stage, &c->stage_cap, G.stage_values)) return r;
   NCCLCHK(g_rccl.GroupStart());
-  for (int64_t q = 0, o = 0, so = 0; q < c->nranks; o += P(q), ++q) {
-    off[q] = o;
-    if (q == root || P(q) == 0) continue;
-    float* dst = merged->d_cols + o * merged->C;   // o is a multiple of kBatchBlock
-    if (C(q) != merged->C) {
-      dst = c->d_stage + so;
-      soff[q] = so;
-      so += C(q) * P(q);
-    }
-    NCCLCHK(g_rccl.Recv(dst, (size_t)(C(q) * P(q)), ncclFloat32, (int)q, c->comm, s));
+  for (int q = 0; q < nr; ++q) {
+    if (q == root || P[q] == 0) continue;
+    float* dst = mcplan::gather_dst(G, q, merged->d_cols, merged->C, c->d_stage);
+    NCCLCHK(g_rccl.Recv(dst, (size_t)(C[q] * P[q]), ncclFloat32, q, c->comm, s));
   }
   NCCLCHK(g_rccl.GroupEnd());
-  if (P(root) > 0) {
-    if (local->C == merged->C)
-      HIPCHK(hipMemcpyAsync(merged->d_cols + off[root] * merged->C, local->d_cols,
-                            (size_t)(local->C * local->P) * sizeof(float), hipMemcpyDeviceToDevice, s));
-    else
-      HIPCHK(repitch(local->d_cols, local->C, local->P, off[root]));
-  }
-  for (int q = 0; q < c->nranks; ++q)
-    if (soff[q] >= 0) HIPCHK(repitch(c->d_stage + soff[q], C(q), P(q), off[q]));
+  HIPCHK(finish_on_device(G, nr, root, P.data(), C.data(), merged, local->d_cols, c->d_stage, s));
   HIPCHK(hipStreamSynchronize(s));
+  merged->trange_valid = false;   // column 4 (t_ns) was written: its cached spans are stale
   return MC_OK;
 }
 
@@ -226,6 +230,54 @@ int mc_comm_allreduce_max_f64(mc_comm* c, double* v, int64_t n) {
   NCCLCHK(g_rccl.AllReduce(c->d_red, c->d_red, (size_t)n, ncclFloat64, ncclMax, c->comm, s));
   HIPCHK(hipMemcpyAsync(v, c->d_red, sizeof(double) * n, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  return MC_OK;
+}
+
+// Host-only: the plan of a merged-cloud gather (plan.hpp), for callers and tests to inspect.
+int mc_gather_plan(int32_t nranks, int32_t root, const int64_t* padded, const int64_t* columns, int64_t merged_padded,
+                   int32_t merged_columns, int64_t* offset_out, int64_t* stage_offset_out, int64_t* stage_values_out) {
+  if (!padded || !columns) return fail(MC_ERR_INVALID, "NULL argument");
+  mcplan::GatherPlan G;
+  const std::string perr = mcplan::plan_gather(nranks, root, padded, columns, merged_padded, merged_columns, &G);
+  if (!perr.empty()) return fail(MC_ERR_INVALID, "%s", perr.c_str());
+  for (int32_t q = 0; q < nranks; ++q) {
+    if (offset_out) offset_out[q] = G.off[q];
+    if (stage_offset_out) stage_offset_out[q] = G.stage_off[q];
+  }
+  if (stage_values_out) *stage_values_out = G.stage_values;
+  return MC_OK;
+}
+
+// One process, n shard batches of one context merged exactly as mc_comm_gather_batch merges n
+// ranks' shards: the same plan, staging and re-pitch; device copies stand in for the RCCL
+// receives (shard `root` is the root's own batch).
+int mc_gather_batches(mc_ctx* ctx, int32_t n, const mc_batch* const* shards, int32_t root, mc_batch* merged) {
+  if (!ctx || !shards || !merged || n < 1) return fail(MC_ERR_INVALID, "NULL argument");
+  if (merged->ctx != ctx) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
+  std::vector<int64_t> P(n), C(n);
+  for (int32_t q = 0; q < n; ++q) {
+    if (!shards[q] || shards[q]->ctx != ctx) return fail(MC_ERR_INVALID, "shard %d is NULL or of another context", q);
+    P[q] = shards[q]->P;
+    C[q] = shards[q]->C;
+  }
+  mcplan::GatherPlan G;
+  const std::string perr = mcplan::plan_gather(n, root, P.data(), C.data(), merged->P, merged->C, &G);
+  if (!perr.empty()) return fail(MC_ERR_INVALID, "%s", perr.c_str());
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  float* stage = nullptr;
+  if (G.stage_values > 0) HIPCHK(hipMalloc(&stage, (size_t)G.stage_values * sizeof(float)));
+  hipError_t e = hipSuccess;
+  for (int32_t q = 0; q < n && e == hipSuccess; ++q) {
+    if (q == root || P[q] == 0) continue;
+    e = hipMemcpyAsync(mcplan::gather_dst(G, q, merged->d_cols, merged->C, stage), shards[q]->d_cols,
+                       (size_t)(C[q] * P[q]) * sizeof(float), hipMemcpyDeviceToDevice, s);
+  }
+  if (e == hipSuccess) e = finish_on_device(G, n, root, P.data(), C.data(), merged, shards[root]->d_cols, stage, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (stage) (void)hipFree(stage);
+  if (e != hipSuccess) return fail(MC_ERR_HIP, "gather_batches: %s", hipGetErrorString(e));
+  merged->trange_valid = false;
   return MC_OK;
 }
 

@@ -77,6 +77,22 @@ struct TimedRegion {
   }
 };
 
+// A pair of timing events for one kernel launched with hipExtLaunchKernel: the runtime stamps
+// them from the dispatch itself, so timing adds no marker packets between the step's kernels.
+struct LaunchEvents {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  explicit LaunchEvents(mc_ctx* c) {
+    if (!c->timing) return;
+    e0 = ev_take(c);
+    e1 = e0 ? ev_take(c) : nullptr;
+    if (e0 && !e1) { c->ev_pool.push_back(e0); e0 = nullptr; }
+  }
+  void keep(std::vector<std::pair<hipEvent_t, hipEvent_t>>* v) {
+    if (e0) v->emplace_back(e0, e1);
+    e0 = e1 = nullptr;
+  }
+};
+
 // both streams idle (before reallocating tables a pipelined prep may still read or write)
 static inline int sync_all(mc_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->side));

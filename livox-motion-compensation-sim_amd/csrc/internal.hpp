@@ -100,6 +100,10 @@ struct mc_ctx {
   hipStream_t side = nullptr;     // per-step pose prep, pipelined one step ahead of `stream`
   // per-step tables are double-buffered: prep of step i+1 (side) overlaps the kernel of step i
   int buf = 0;
+  // true until the next k_prep must wait for everything queued before it (an ordinary, barrier
+  // launch): set by async writers of the prep's inputs (t_ns spans) and by step-graph replays;
+  // cleared by mc_deskew, whose deskew kernel then ends the queue (see mc_deskew)
+  bool prep_fence = true;
   hipEvent_t ev_main_done[2] = {nullptr, nullptr};
   hipEvent_t ev_prep_done[2] = {nullptr, nullptr};
   hipEvent_t ev_order = nullptr;  // orders side-stream prep after async main-stream staging
@@ -160,6 +164,7 @@ struct mc_batch {
   int64_t P = 0;    // padded points (poff[F]; every frame starts on a kBlkPts boundary)
   int32_t C = 4;    // columns per block: x | y | z | intensity [| t_ns]
   std::vector<int64_t> counts, poff, doff;
+  std::vector<int32_t> ftile;      // first tile of each frame (F+1), host copy
   int32_t n_tiles = 0;
   // blocked columns: block k (points 256k .. 256k+255) holds its C columns of 256 values back to
   // back, C * P values in all (mc::bidx); t_ns, when present, is column 4 (int32 bits)

@@ -1101,6 +1101,7 @@ struct LayoutArgs {
   const Tile* tiles; int32_t n_tiles;
   const int64_t* poff; const int64_t* doff; const int64_t* counts;
   float* cols; int32_t C;   // blocked columns x|y|z|i[|t_ns]; C == 5 carries the t_ns column
+  int64_t dbase;            // AoS row of the first frame covered (a frame range's fetch: doff[f0]; else 0)
   __device__ __forceinline__ float& col(int c, int64_t p) const { return cols[bidx(C, c, p)]; }
   __device__ __forceinline__ int32_t& tns(int64_t p) const {
     return reinterpret_cast<int32_t*>(cols)[bidx(C, 4, p)];
@@ -1277,7 +1278,7 @@ __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, doubl
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
     const int64_t loc0 = tl.pstart - poff;
     const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
-    stage_tile_lds_out(a, tl, reinterpret_cast<v2d*>(aos + (doff + loc0) * 4), nv, s_t);
+    stage_tile_lds_out(a, tl, reinterpret_cast<v2d*>(aos + (doff - a.dbase + loc0) * 4), nv, s_t);
   }
   return;
 #endif
@@ -1286,7 +1287,7 @@ __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, doubl
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
     const int64_t loc0 = tl.pstart - poff;
     const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
-    v2d* d2 = reinterpret_cast<v2d*>(aos + (doff + loc0) * 4);
+    v2d* d2 = reinterpret_cast<v2d*>(aos + (doff - a.dbase + loc0) * 4);
     for (int q0 = 0; q0 < 2 * nv; q0 += kStageUnroll * kBlock) {
       v2d v[kStageUnroll];
 #pragma unroll

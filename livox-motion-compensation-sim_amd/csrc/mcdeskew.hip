@@ -5,9 +5,11 @@
 // plain pointers and sizes in, status codes out (thread-local message in mc_last_error()).
 #include "../../include/mcdeskew.h"
 #include "kernels.hpp"
+#include <hip/hip_ext.h>
 #include "scan.hpp"
 #include "internal.hpp"
 #include "hostutil.hpp"
+#include "plan.hpp"
 
 #include <algorithm>
 #include <array>
@@ -41,13 +43,17 @@ static int launch_grid(const mc_ctx* c, int32_t n_tiles) {
   return g < 1 ? 1 : g;
 }
 
-static_assert(mcimpl::kBatchBlock == kBlkPts, "batch block size");
+static_assert(mcimpl::kBatchBlock == kBlkPts && mcplan::kBlk == kBlkPts, "batch block size");
+static_assert(sizeof(mcplan::TileRec) == sizeof(Tile) && offsetof(mcplan::TileRec, frame) == offsetof(Tile, frame) &&
+                  offsetof(mcplan::TileRec, ngroups) == offsetof(Tile, ngroups),
+              "host tile records are uploaded as mc::Tile");
 
 static LayoutArgs layout_of(const mc_batch* b) {
   LayoutArgs a;
   a.tiles = b->d_tiles; a.n_tiles = b->n_tiles;
   a.poff = b->d_poff; a.doff = b->d_doff; a.counts = b->d_counts;
   a.cols = b->d_cols; a.C = b->C;
+  a.dbase = 0;
   return a;
 }
 
@@ -100,6 +106,12 @@ int mc_device_count(int* count) {
   CHECK_ARG(count, "count is NULL");
   *count = 0;
   HIPCHK(hipGetDeviceCount(count));
+  return MC_OK;
+}
+
+int mc_device_pci_bus_id(int device, char* out, int len) {
+  CHECK_ARG(out && len >= 16, "output buffer needs >= 16 bytes");
+  HIPCHK(hipDeviceGetPCIBusId(out, len, device));
   return MC_OK;
 }
 
@@ -229,31 +241,19 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
   *out = nullptr;
   CHECK_ARG(F >= 0, "n_frames must be >= 0");
   CHECK_ARG(F == 0 || counts, "counts is NULL");
+  // host-side layout planning (plan.cpp; sanitizer-tested on the CPU, tests/test_sanitizers.py)
+  mcplan::BatchLayout L;
+  const std::string perr = mcplan::plan_batch(counts, F, kTileGroups, kSub, &L);
+  if (!perr.empty()) return fail(MC_ERR_INVALID, "%s", perr.c_str());
   mc_batch* b = new mc_batch();
   b->ctx = c;
   b->F = F;
   b->counts.assign(counts, counts + F);
-  b->poff.resize(F + 1);
-  b->doff.resize(F + 1);
-  b->poff[0] = b->doff[0] = 0;
-  std::vector<Tile> tiles;
-  std::vector<int32_t> ftile(F + 1, 0);
-  for (int32_t f = 0; f < F; ++f) {
-    ftile[f] = (int32_t)std::min<size_t>(tiles.size(), INT32_MAX);
-    if (b->counts[f] < 0) { delete b; return fail(MC_ERR_INVALID, "frame %d has a negative count", f); }
-    const int64_t groups = (b->counts[f] + 3) / 4;
-    b->doff[f + 1] = b->doff[f] + b->counts[f];
-    b->poff[f + 1] = b->poff[f] + (b->counts[f] + kBlkPts - 1) / kBlkPts * kBlkPts;
-    for (int64_t g0 = 0; g0 < groups; g0 += kTileGroups) {
-      Tile t;
-      t.pstart = b->poff[f] + 4 * g0;
-      t.frame = f;
-      t.ngroups = (int32_t)std::min<int64_t>(kTileGroups, groups - g0);
-      tiles.push_back(t);
-    }
-  }
-  if (tiles.size() * kSub > (size_t)INT32_MAX) { delete b; return fail(MC_ERR_INVALID, "too many tiles"); }
-  ftile[F] = (int32_t)tiles.size();
+  b->poff = std::move(L.poff);
+  b->doff = std::move(L.doff);
+  b->ftile = std::move(L.ftile);
+  const std::vector<mcplan::TileRec>& tiles = L.tiles;
+  const std::vector<int32_t>& ftile = b->ftile;
   b->N = b->doff[F];
   b->P = b->poff[F];
   b->C = (flags & MC_BATCH_WITH_TIME) ? 5 : 4;
@@ -487,6 +487,30 @@ int mc_batch_download_aos_f64(mc_batch* b, double* aos) {
   return MC_OK;
 }
 
+int mc_batch_download_frames_aos_f64(mc_batch* b, int32_t f0, int32_t f1, double* aos) {
+  CHECK_ARG(b, "batch is NULL");
+  CHECK_ARG(0 <= f0 && f0 <= f1 && f1 <= b->F, "frame range [%d, %d) outside [0, %d)", f0, f1, b->F);
+  const int64_t rows = b->doff[f1] - b->doff[f0];
+  if (rows == 0) return MC_OK;
+  CHECK_ARG(aos, "output pointer is NULL");
+  mc_ctx* c = b->ctx;
+  DeviceGuard g(c->device);
+  void* st = nullptr;
+  if (int r = ctx_stage(c, (size_t)rows * 4 * sizeof(double), &st)) return r;
+  // the stager over the tiles of frames [f0, f1) only, writing rows from doff[f0] on
+  LayoutArgs a = layout_of(b);
+  a.tiles = b->d_tiles + b->ftile[f0];
+  a.n_tiles = b->ftile[f1] - b->ftile[f0];
+  a.dbase = b->doff[f0];
+  if (a.n_tiles > 0)
+    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, a.n_tiles)), dim3(kBlock), 0, c->stream, a,
+                       static_cast<double*>(st));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(aos, st, (size_t)rows * 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
 int mc_batch_download_columns_f32(mc_batch* b, float* x, float* y, float* z, float* in) {
   CHECK_ARG(b, "batch is NULL");
   if (b->N == 0) return MC_OK;
@@ -538,8 +562,14 @@ int mc_batch_checksum(mc_batch* b, double* sums) {
 }
 
 // ---- the hot path ---------------------------------------------------------------------------
-#ifndef MC_PREP_SERIAL
-#define MC_PREP_SERIAL 0   // 1: per-step prep on the main stream (rejected: step wall +2 to +6 us)
+// How mc_deskew issues a step's k_prep (tools/anyorder_probe.hip, tools/ab.py):
+//   0  on the side stream one step ahead, ordered by cross-queue events (round 1: ~7-10 us per step)
+//   1  on the main stream right before its kernel (serial; rejected in round 1: step wall +2 to +6 us)
+//   2  on the main stream as an any-order packet (hipExtAnyOrderLaunch: AQL barrier bit clear) right
+//      behind the previous step's deskew kernel, so it runs beside that kernel's tail without a
+//      second queue; the deskew kernel after it is an ordinary packet and waits for both
+#ifndef MC_PREP_ISSUE
+#define MC_PREP_ISSUE 2
 #endif
 namespace {
 int deskew_check(mc_ctx* c, const mc_batch* in, const mc_batch* out, int mode, int pose_select) {
@@ -630,15 +660,26 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   sp->kernel = mode;
 }
 
-void launch_prep(const StepPlan& sp, hipStream_t sd) {
-  hipLaunchKernelGGL(k_prep, dim3(sp.prep_blocks), dim3(kBlock), 0, sd, sp.pa);
+// Launches with optional hipExtLaunchKernel timing events (e0/e1 null: untimed) and AQL flags.
+// Inside a graph capture (build_step_graph) both events are null and flags 0.
+void launch_prep(const StepPlan& sp, hipStream_t sd, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
+                 unsigned flags = 0) {
+  if (!e0 && !flags) hipLaunchKernelGGL(k_prep, dim3(sp.prep_blocks), dim3(kBlock), 0, sd, sp.pa);
+  else hipExtLaunchKernelGGL(k_prep, dim3(sp.prep_blocks), dim3(kBlock), 0, sd, e0, e1, flags, sp.pa);
 }
 
-void launch_main(const StepPlan& sp, hipStream_t s) {
+void launch_main(const StepPlan& sp, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
   const dim3 grid(sp.grid), block(kBlock);
-  if (sp.kernel == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, sp.da);
-  else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, sp.da);
-  else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, sp.da);
+  if (!e0) {
+    if (sp.kernel == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, sp.da);
+    else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, sp.da);
+    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, sp.da);
+    return;
+  }
+  if (sp.kernel == MC_MODE_FRAME) hipExtLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, e0, e1, 0u, sp.da);
+  else if (sp.kernel == MC_MODE_POSE_SLERP)
+    hipExtLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, e0, e1, 0u, sp.da);
+  else hipExtLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, e0, e1, 0u, sp.da);
 }
 
 // frame time spans derived lazily from t_ns (queued on the main stream)
@@ -653,40 +694,29 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   if (in->F == 0) return MC_OK;
   DeviceGuard g(c->device);
   hipStream_t s = c->stream, sd = c->side;
+  (void)sd;
   if (mode != MC_MODE_FRAME && !in->trange_valid) {
     // the spans are queued on the main stream: order the prep after them
     if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
+#if MC_PREP_ISSUE == 0
     HIPCHK(hipEventRecord(c->ev_order, s));
     HIPCHK(hipStreamWaitEvent(sd, c->ev_order, 0));
-  }
-
-#if MC_PREP_SERIAL
-  // variant: the prep on the main stream right before its kernel (no cross-queue events)
-  {
-    StepPlan sp;
-    deskew_plan(c, in, out, mode, pose_select, c->buf, &sp);
-    HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[c->buf], 0));   // a pipelined prep of an earlier call
-    {
-      TimedRegion tr(c, &c->prep_ev, s);
-      launch_prep(sp, s);
-    }
-    if (sp.kernel >= 0) {
-      TimedRegion tr(c, &c->main_ev, s);
-      launch_main(sp, s);
-    }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev_main_done[c->buf], s));
-    return MC_OK;
-  }
 #endif
-  // Pipelining: the per-step tables come in two halves.  This step's prep runs on the side
-  // stream as soon as the deskew kernel that last read half `h` (two calls back) has finished,
-  // i.e. concurrently with the previous call's kernel; the kernel waits for its own prep.
+    c->prep_fence = true;
+  }
+  // Per-step tables come in two halves: this step's prep writes half h, which the deskew kernel
+  // two calls back read; the previous call's kernel reads the other half.
   const int h = c->buf;
   c->buf ^= 1;
-  HIPCHK(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
   StepPlan sp;
   deskew_plan(c, in, out, mode, pose_select, h, &sp);
+  // a per-point deskew that carries t_ns into another batch rewrites that batch's time column:
+  // its cached [min, max] spans no longer describe it
+  if (sp.kernel >= 0 && sp.da.copy_t) out->trange_valid = false;
+#if MC_PREP_ISSUE == 0
+  // the prep on the side stream as soon as the kernel that last read half h has finished, i.e.
+  // concurrently with the previous call's kernel; the kernel waits for its own prep
+  HIPCHK(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
   {
     TimedRegion tr(c, &c->prep_ev, sd);
     launch_prep(sp, sd);
@@ -700,6 +730,34 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_main_done[h], s));
+#else
+  // One queue.  Any-order prep (MC_PREP_ISSUE 2) only right behind this context's own deskew
+  // kernel (prep_fence clear): the packets before it are then that kernel — still reading the
+  // other half — and, before it, work the kernel's barrier already waited for.  Everything else
+  // that could precede it either finished before its API call returned (trajectory / IMU / frame
+  // tables are uploaded synchronously) or set the fence (t_ns spans queued above, graph replays).
+  // The deskew kernel's own packet keeps the barrier bit, so it waits for this prep, and anything
+  // queued after it waits for both.  With no kernel to follow (no tiles) the prep is ordinary.
+  const unsigned fl = (MC_PREP_ISSUE == 2 && !c->prep_fence && sp.kernel >= 0) ? hipExtAnyOrderLaunch : 0u;
+  {
+    LaunchEvents ev(c);
+    launch_prep(sp, s, ev.e0, ev.e1, fl);
+    ev.keep(&c->prep_ev);
+  }
+  HIPCHK(hipGetLastError());
+  if (sp.kernel >= 0) {
+    LaunchEvents ev(c);
+    launch_main(sp, s, ev.e0, ev.e1);
+    ev.keep(&c->main_ev);
+    HIPCHK(hipGetLastError());
+    c->prep_fence = false;
+  } else {
+    c->prep_fence = true;
+  }
+  // No event records here: a marker packet between this kernel and the next step's any-order prep
+  // would hold that prep until this kernel completes.  Everything is on one queue, so the stream
+  // order is the only ordering the halves need (a graph replay forks its prep branch from s).
+#endif
   return MC_OK;
 }
 
@@ -801,6 +859,7 @@ int mc_deskew_steps(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int 
   }
   if (flags & MC_STEPS_PREPARE) return MC_OK;
   HIPCHK(hipGraphLaunch(c->step_graph->exec, s));
+  c->prep_fence = true;   // the graph's last kernel reads a half the next any-order prep may write
   // later plain calls order their side-stream prep after the whole graph
   HIPCHK(hipEventRecord(c->ev_main_done[0], s));
   HIPCHK(hipEventRecord(c->ev_main_done[1], s));

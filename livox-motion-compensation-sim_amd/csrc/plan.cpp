@@ -1,0 +1,84 @@
+// plan.cpp — host-only batch layout and gather planning (see plan.hpp).
+#include "plan.hpp"
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+
+namespace mcplan {
+
+static std::string msg(const char* fmt, long long a, long long b = 0, long long c = 0) {
+  char buf[256];
+  std::snprintf(buf, sizeof(buf), fmt, a, b, c);
+  return buf;
+}
+
+std::string plan_batch(const int64_t* counts, int32_t F, int32_t tile_groups, int32_t sub_per_tile,
+                       BatchLayout* out) {
+  if (F < 0) return "n_frames must be >= 0";
+  if (F > 0 && !counts) return "counts is NULL";
+  if (tile_groups < 1 || sub_per_tile < 1) return "bad tile geometry";
+  BatchLayout& L = *out;
+  L.poff.assign((size_t)F + 1, 0);
+  L.doff.assign((size_t)F + 1, 0);
+  L.ftile.assign((size_t)F + 1, 0);
+  L.tiles.clear();
+  // every frame's tile count first: one allocation, and the int32 bound is checked before any
+  // tile is built (a huge count must fail cleanly, not exhaust host memory)
+  int64_t n_tiles = 0;
+  for (int32_t f = 0; f < F; ++f) {
+    if (counts[f] < 0) return msg("frame %lld has a negative count", f);
+    if (counts[f] > (INT64_MAX / 8)) return msg("frame %lld count %lld is too large", f, counts[f]);
+    const int64_t groups = (counts[f] + 3) / 4;
+    n_tiles += (groups + tile_groups - 1) / tile_groups;
+    if (n_tiles > (int64_t)INT32_MAX / sub_per_tile) return "too many tiles";
+  }
+  L.tiles.reserve((size_t)n_tiles);
+  for (int32_t f = 0; f < F; ++f) {
+    L.ftile[f] = (int32_t)L.tiles.size();
+    const int64_t groups = (counts[f] + 3) / 4;
+    L.doff[f + 1] = L.doff[f] + counts[f];
+    L.poff[f + 1] = L.poff[f] + (counts[f] + kBlk - 1) / kBlk * kBlk;
+    for (int64_t g0 = 0; g0 < groups; g0 += tile_groups) {
+      TileRec t;
+      t.pstart = L.poff[f] + 4 * g0;
+      t.frame = f;
+      t.ngroups = (int32_t)std::min<int64_t>(tile_groups, groups - g0);
+      L.tiles.push_back(t);
+    }
+  }
+  L.ftile[F] = (int32_t)L.tiles.size();
+  return "";
+}
+
+std::string plan_gather(int32_t nranks, int32_t root, const int64_t* P, const int64_t* C, int64_t merged_P,
+                        int64_t merged_C, GatherPlan* out) {
+  if (nranks < 1) return msg("bad rank count %lld", nranks);
+  if (root < 0 || root >= nranks) return msg("bad root %lld of %lld ranks", root, nranks);
+  if (!P || !C) return "shard sizes are NULL";
+  if (merged_C != 4 && merged_C != 5) return msg("merged batch has %lld columns (4 or 5 expected)", merged_C);
+  GatherPlan& G = *out;
+  G.off.assign((size_t)nranks, 0);
+  G.stage_off.assign((size_t)nranks, -1);
+  G.stage_values = 0;
+  int64_t o = 0;
+  for (int32_t q = 0; q < nranks; ++q) {
+    if (P[q] < 0 || P[q] % kBlk != 0) return msg("rank %lld sent %lld padded points (not a block multiple)", q, P[q]);
+    if (C[q] != 4 && C[q] != 5) return msg("rank %lld sent %lld columns (4 or 5 expected)", q, C[q]);
+    if (P[q] > 0 && C[q] < merged_C)
+      return msg("rank %lld sent %lld columns into a %lld-column merged batch (t_ns would be undefined)", q, C[q],
+                 merged_C);
+    G.off[q] = o;
+    if (P[q] > INT64_MAX / 8 - o) return "merged size overflows";
+    o += P[q];
+    if (q != root && P[q] > 0 && C[q] != merged_C) {
+      G.stage_off[q] = G.stage_values;
+      G.stage_values += C[q] * P[q];
+    }
+  }
+  if (o != merged_P)
+    return msg("merged batch holds %lld padded points, ranks sent %lld", merged_P, o);
+  return "";
+}
+
+}  // namespace mcplan

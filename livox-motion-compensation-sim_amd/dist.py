@@ -204,6 +204,36 @@ class RcclComm:
             self.handle = None
 
 
+def gather_plan(padded, columns, merged_padded: int, merged_columns: int, root: int = 0) -> dict:
+    """The plan ``mc_comm_gather_batch`` follows (host only, csrc/plan.cpp): per rank the shard's
+    first padded point in the merged batch (rank order == np.vstack order, LMC:887-889) and its
+    value offset in the root's staging area (-1: received in place); raises ValueError for an
+    invalid plan (sizes that do not add up, a shard narrower than the merged batch)."""
+    lib = _lib.load()
+    P = np.ascontiguousarray(padded, dtype=np.int64)
+    C = np.ascontiguousarray(columns, dtype=np.int64)
+    if P.shape != C.shape or P.ndim != 1:
+        raise ValueError("padded / columns: one entry per rank")
+    off = np.zeros(len(P), np.int64)
+    soff = np.zeros(len(P), np.int64)
+    sv = np.zeros(1, np.int64)
+    check(lib.mc_gather_plan(len(P), int(root), ptr(P, ctypes.c_int64), ptr(C, ctypes.c_int64), int(merged_padded),
+                             int(merged_columns), ptr(off, ctypes.c_int64), ptr(soff, ctypes.c_int64),
+                             ptr(sv, ctypes.c_int64)), "gather_plan")
+    return {"offset": off, "stage_offset": soff, "stage_values": int(sv[0])}
+
+
+def gather_batches(ctx, shards, root: int = 0, merged=None):
+    """One process, several shard batches of ``ctx`` merged as ``gather_merged`` merges ranks'
+    shards (same plan, staging and re-pitch; device copies in place of the RCCL receives).
+    ``merged`` defaults to a 4-column batch of the concatenated frame counts."""
+    if merged is None:
+        merged = ctx.batch(np.concatenate([np.asarray(b.counts, np.int64) for b in shards]))
+    arr = (c_void_p * len(shards))(*[b.handle.value for b in shards])
+    check(ctx.lib.mc_gather_batches(ctx.handle, len(shards), arr, int(root), merged.handle), "gather_batches")
+    return merged
+
+
 def gather_merged(ctx, comm: RcclComm, rdv: Rendezvous, local, root: int = 0):
     """Merged aligned cloud of all ranks on ``root`` (None elsewhere) — the LMC:888 vstack."""
     all_counts = rdv.allgather([int(c) for c in local.counts])

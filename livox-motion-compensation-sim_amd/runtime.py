@@ -46,6 +46,11 @@ class Context:
         check(lib.mc_device_count(ctypes.byref(n)), "mc_device_count")
         return n.value
 
+    def pci_bus_id(self) -> str:
+        buf = (ctypes.c_char * 64)()
+        check(self.lib.mc_device_pci_bus_id(int(self.device), buf, 64), "pci_bus_id")
+        return buf.value.decode()
+
     def close(self):
         self._fin()
 
@@ -284,6 +289,16 @@ class Batch:
     def download_aos(self) -> np.ndarray:
         out = np.empty((self.n_points, 4), np.float64)
         check(self.lib.mc_batch_download_aos_f64(self.handle, ptr(out, c_double)), "download_aos")
+        return out
+
+    def download_frames(self, f0: int, f1: int) -> np.ndarray:
+        """Frames [f0, f1) as dense (n, 4) float64 rows (a spot check of a batch too large to
+        bring back whole)."""
+        f0, f1 = int(f0), int(f1)
+        if not 0 <= f0 <= f1 <= self.n_frames:
+            raise ValueError(f"frame range [{f0}, {f1}) outside [0, {self.n_frames})")
+        out = np.empty((int(self.offsets[f1] - self.offsets[f0]), 4), np.float64)
+        check(self.lib.mc_batch_download_frames_aos_f64(self.handle, f0, f1, ptr(out, c_double)), "download_frames")
         return out
 
     def download_columns(self):

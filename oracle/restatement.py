@@ -22,7 +22,7 @@ from __future__ import annotations
 import numpy as np
 
 __all__ = [
-    "euler_xyz_matrix", "euler_xyz_quat", "select_pose_index", "transform_pointcloud",
+    "euler_xyz_matrix", "euler_xyz_quat", "select_pose_index", "transform_pointcloud", "transform_pointcloud_ref_ops",
     "align_frames", "merge_aligned", "scan_environment", "imu_interpolate_gyro", "compensate_arrays",
     "compensate_point_cloud_loop", "slerp_pose", "deskew_pose_slerp",
 ]
@@ -80,6 +80,17 @@ def transform_pointcloud(points, transformation) -> np.ndarray:
     points = np.asarray(points)
     R = euler_xyz_matrix(np.asarray(transformation["rotation"], dtype=np.float64))
     transformed = (R @ points[:, :3].T).T + np.asarray(transformation["translation"], dtype=np.float64)
+    return np.column_stack([transformed, points[:, 3]])
+
+
+def transform_pointcloud_ref_ops(points, transformation) -> np.ndarray:
+    """LMC:772-776 as the reference executes it, op for op: scipy ``Rotation.from_euler('xyz',
+    rotation).as_matrix()`` (LMC:774), ``R @ points[:, :3].T`` (775), ``.T + translation`` (775),
+    ``np.column_stack`` with the intensity column (776).  Used as bench.py's frame-mode CPU
+    baseline (the reference's own per-frame cost); numerically equal to transform_pointcloud."""
+    from scipy.spatial.transform import Rotation
+    R = Rotation.from_euler("xyz", transformation["rotation"]).as_matrix()
+    transformed = (R @ points[:, :3].T).T + transformation["translation"]
     return np.column_stack([transformed, points[:, 3]])
 
 

@@ -118,3 +118,86 @@ def test_gloo_world2_shard_and_gather_equals_vstack():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(res)
+
+
+def _blocked(rows, counts, C):
+    """Dense (N, C) rows of ragged frames -> the batch's blocked column layout."""
+    counts = np.asarray(counts, np.int64)
+    pad = (counts + 255) // 256 * 256
+    poff = np.concatenate([[0], np.cumsum(pad)])
+    doff = np.concatenate([[0], np.cumsum(counts)])
+    flat = np.zeros(int(poff[-1]) * C, np.float32)
+    for f in range(len(counts)):
+        p = poff[f] + np.arange(counts[f])
+        for c in range(C):
+            flat[((p >> 8) * C + c) * 256 + (p & 255)] = rows[doff[f]:doff[f + 1], c]
+    return flat, int(poff[-1])
+
+
+def _unblocked(flat, counts, C):
+    counts = np.asarray(counts, np.int64)
+    pad = (counts + 255) // 256 * 256
+    poff = np.concatenate([[0], np.cumsum(pad)])
+    out = []
+    for f in range(len(counts)):
+        p = poff[f] + np.arange(counts[f])
+        out.append(np.stack([flat[((p >> 8) * C + c) * 256 + (p & 255)] for c in range(C)], 1))
+    return np.concatenate(out) if out else np.zeros((0, C), np.float32)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
+def test_gather_plan_of_sharded_run_equals_vstack(world):
+    """The library's gather plan (mc_gather_plan, the host half of mc_comm_gather_batch) applied to
+    plan_shards' point-balanced frame shards with numpy copies in place of the RCCL receives: the
+    merged batch, read back in frame order, is np.vstack of the ranks' aligned clouds (LMC:887-889).
+    Every root, 4- and 5-column shards (t_ns carried or not), empty shards, ragged frames."""
+    d = pkg().dist
+    rng = np.random.default_rng(world)
+    for trial in range(6):
+        F = int(rng.integers(0, 30))
+        counts = rng.choice([0, 1, 7, 255, 256, 257, 3000, 10_001], F)
+        b = d.plan_shards(counts, world)
+        shard_counts = [counts[b[r]:b[r + 1]] for r in range(world)]
+        merged_C = int(rng.choice([4, 5]))
+        Cs = [5 if merged_C == 5 else int(rng.choice([4, 5])) for _ in range(world)]
+        rows = [rng.standard_normal((int(sc.sum()), 5)).astype(np.float32) for sc in shard_counts]
+        shards, P = [], []
+        for r in range(world):
+            flat, pr = _blocked(rows[r], shard_counts[r], Cs[r])
+            shards.append(flat)
+            P.append(pr)
+        root = int(rng.integers(0, world))
+        plan = d.gather_plan(P, Cs, sum(P), merged_C, root=root)
+        merged = np.full(sum(P) * merged_C, np.nan, np.float32)
+        stage = np.full(plan["stage_values"], np.nan, np.float32)
+        for q in range(world):          # the receives
+            if q == root or P[q] == 0:
+                continue
+            n = Cs[q] * P[q]
+            if plan["stage_offset"][q] >= 0:
+                stage[plan["stage_offset"][q]:plan["stage_offset"][q] + n] = shards[q]
+            else:
+                merged[plan["offset"][q] * merged_C:plan["offset"][q] * merged_C + n] = shards[q]
+        for q in range(world):          # the root's own shard and the re-pitches
+            if P[q] == 0 or (q != root and plan["stage_offset"][q] < 0):
+                continue
+            src = shards[q] if q == root else stage[plan["stage_offset"][q]:plan["stage_offset"][q] + Cs[q] * P[q]]
+            blocks = src.reshape(P[q] // 256, Cs[q], 256)[:, :merged_C]
+            o = plan["offset"][q] * merged_C
+            merged[o:o + P[q] * merged_C] = blocks.reshape(-1)
+        got = _unblocked(merged, counts, merged_C)
+        want = np.vstack([rw[:, :merged_C] for rw in rows]) if rows else np.zeros((0, merged_C))
+        assert np.array_equal(got, want), (world, trial, root, Cs, merged_C)
+
+
+def test_gather_plan_rejects_narrow_shards_and_bad_totals():
+    d = pkg().dist
+    with pytest.raises(ValueError, match="columns"):
+        d.gather_plan([256, 512], [4, 5], 768, 5)          # t_ns would be left undefined
+    with pytest.raises(ValueError, match="padded points"):
+        d.gather_plan([256, 512], [5, 5], 1024, 4)
+    with pytest.raises(ValueError, match="block"):
+        d.gather_plan([100], [4], 100, 4)
+    with pytest.raises(ValueError, match="root"):
+        d.gather_plan([256], [4], 256, 4, root=1)
+    assert d.gather_plan([0, 256], [4, 4], 256, 4)["offset"].tolist() == [0, 0]

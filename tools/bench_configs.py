@@ -2,7 +2,9 @@
 
   config 1  highway_simple, 10 frames x 20k points
   config 3  parking_detailed, 600 x 100k (noise on; the SLERP-heavy pose table)
-  config 5  the per-GPU shape of 1200 x 1M-point frames over 8 GPUs: 150 x 1M
+  config 4  the whole 6000 x 100k job on ONE GPU (600 M points; 8 GPUs shard it 750 per GPU)
+  config 5  the whole 1200 x 1M-point job on ONE GPU (1.2 G points, 6.0 G input values > 2^32)
+  config 5 shape  its per-GPU shape at 8 GPUs: 150 x 1M
 
 Each run is a child process under its own time limit; the first failure ends the sweep.
 Usage (GPU box):  python tools/bench_configs.py --out gpurun_out/configs.json
@@ -15,8 +17,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = {
-    "config1_highway_10x20k": ["--scenario", "highway_simple", "--frames", "10", "--points", "20000"],
-    "config3_parking_600x100k": ["--scenario", "parking_detailed", "--frames", "600", "--points", "100000"],
+    "config1_highway_10x20k": ["--config", "1"],
+    "config3_parking_600x100k": ["--config", "3"],
+    "config4_whole_6000x100k_1gpu": ["--config", "4", "--no-extra-modes"],
+    "config5_whole_1200x1M_1gpu": ["--config", "5", "--no-extra-modes"],
     "config5_shape_150x1M": ["--frames", "150", "--points", "1000000"],
 }
 
@@ -36,7 +40,8 @@ def main():
             break
         line = json.loads(p.stdout.strip().splitlines()[-1])
         res[name] = {"config": line["config"], "value_Mpoints_s": line["value"], "ms_per_step": line["ms_per_step"],
-                     "modes": line["modes"]}
+                     "modes": line["modes"], "roofline": line["roofline"], "parity": line.get("parity"),
+                     "step_over_kernel": line.get("step_over_kernel")}
         print(name, {m: round(v["frac"], 4) for m, v in line["modes"].items()}, flush=True)
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
