@@ -256,12 +256,56 @@ __device__ __forceinline__ void euler_xyz_matrix(double r, double p, double y, d
   R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
 }
 
+// f64 sin/cos for the per-step prep (k_prep), whose latency is one wave's serial f64 chain: ocml's
+// sincos carries a Payne-Hanek branch (v_trig_preop) inlined at every call site (k_prep was 7.2 k
+// instructions).  Cody-Waite reduction by pi/2 in three 33-bit parts (fdlibm's pio2_1/2/3) with
+// fma, so every product n * pio2_k is exact: the reduced argument is good to ~1e-16 absolute for
+// |x| < 2^50 rad (n exact); then the fdlibm __kernel_sin / __kernel_cos minimax polynomials on
+// |r| <= pi/4 (<= 2.4 ulp measured against long double over 2e7 arguments).  A pose angle of
+// 2^50 rad or more (or non-finite) gives NaN.
+__device__ __forceinline__ void sincos_prep(double x, double* s, double* c) {
+  if (!(fabs(x) < 1125899906842624.0)) { *s = *c = __builtin_nan(""); return; }
+  const double n = rint(x * 6.36619772367581382433e-01);
+  double r = fma(-n, 1.57079632673412561417e+00, x);      // pio2_1: first 33 bits of pi/2
+  r = fma(-n, 6.07710050630396597660e-11, r);              // pio2_2
+  r = fma(-n, 2.02226624871116645580e-21, r);              // pio2_3
+  const double z = r * r;
+  double ps = fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+  ps = fma(z, ps, 2.75573137070700676789e-06);
+  ps = fma(z, ps, -1.98412698298579493134e-04);
+  ps = fma(z, ps, 8.33333333332248946124e-03);
+  ps = fma(z, ps, -1.66666666666666324348e-01);
+  const double sr = fma(r * z, ps, r);
+  double pc = fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+  pc = fma(z, pc, -2.75573143513906633035e-07);
+  pc = fma(z, pc, 2.48015872894767294178e-05);
+  pc = fma(z, pc, -1.38888888888741095749e-03);
+  pc = fma(z, pc, 4.16666666666666019037e-02);
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cr = w + (((1.0 - w) - hz) + z * z * pc);
+  const int q = (int)(int64_t)n;
+  const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+  *s = (q & 2) ? -s0 : s0;
+  *c = ((q + 1) & 2) ? -c0 : c0;
+}
+
+// euler_xyz_matrix with sincos_prep (k_prep's frame table; the f64 host-array kernels keep ocml)
+__device__ __forceinline__ void euler_xyz_matrix_prep(double r, double p, double y, double R[9]) {
+  double sr, cr, sp, cp, sy, cy;
+  sincos_prep(r, &sr, &cr);
+  sincos_prep(p, &sp, &cp);
+  sincos_prep(y, &sy, &cy);
+  R[0] = cy * cp; R[1] = cy * sp * sr - sy * cr; R[2] = cy * sp * cr + sy * sr;
+  R[3] = sy * cp; R[4] = sy * sp * sr + cy * cr; R[5] = sy * sp * cr - cy * sr;
+  R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
+}
+
 // unit quaternion (x,y,z,w) of the same rotation (q = qz * qy * qx)
 __device__ __forceinline__ void euler_xyz_quat(double r, double p, double y, double q[4]) {
   double sr, cr, sp, cp, sy, cy;
-  sincos(0.5 * r, &sr, &cr);
-  sincos(0.5 * p, &sp, &cp);
-  sincos(0.5 * y, &sy, &cy);
+  sincos_prep(0.5 * r, &sr, &cr);
+  sincos_prep(0.5 * p, &sp, &cp);
+  sincos_prep(0.5 * y, &sy, &cy);
   q[0] = sr * cp * cy - cr * sp * sy;
   q[1] = cr * sp * cy + sr * cp * sy;
   q[2] = cr * cp * sy - sr * sp * cy;
@@ -280,7 +324,8 @@ __device__ __forceinline__ PoseSeg make_pose_seg(const double* time, const doubl
   if (d > 1.0) d = 1.0;
   const double th = acos(d);
   const bool small = th < 1e-6;
-  const double inv_sin = small ? 0.0 : 1.0 / sin(th);
+  // sin(acos(d)) from the same d (no second transcendental on the prep's serial chain)
+  const double inv_sin = small ? 0.0 : 1.0 / sqrt((1.0 - d) * (1.0 + d));
   PoseSeg s;
   s.q0 = make_float4((float)q0[0], (float)q0[1], (float)q0[2], (float)q0[3]);
   s.q1 = make_float4((float)q1[0], (float)q1[1], (float)q1[2], (float)q1[3]);
@@ -375,6 +420,37 @@ __device__ __forceinline__ int64_t wave_count(const T* a, int64_t n, T x) {
   return lo + __popcll(__ballot(in));
 }
 
+// Two searches of the same sorted table in the same rounds (the prep's frame window needs the
+// segment of the frame's first and of its last point): round one's probes serve both, later rounds
+// issue their two loads together, so the wave waits out one memory latency per round, not two.
+template <bool STRICT, typename T>
+__device__ __forceinline__ void wave_count2(const T* a, int64_t n, T x0, T x1, int64_t* c0, int64_t* c1) {
+  const int lane = threadIdx.x & 63;
+  int64_t lo0 = 0, hi0 = n, lo1 = 0, hi1 = n;
+  bool done0 = false, done1 = false;
+  while (!(done0 && done1)) {
+    const bool fine0 = !done0 && hi0 - lo0 <= 64, fine1 = !done1 && hi1 - lo1 <= 64;
+    const int64_t st0 = fine0 ? 1 : (hi0 - lo0 + 63) / 64, st1 = fine1 ? 1 : (hi1 - lo1 + 63) / 64;
+    const int64_t i0 = lo0 + lane * st0, i1 = lo1 + lane * st1;
+    // both loads issued before either compare (the same entry when the two ranges still coincide)
+    const T v0 = (!done0 && i0 < hi0) ? a[i0] : T(0);
+    const T v1 = (!done1 && i1 < hi1) ? ((i1 == i0 && !done0) ? v0 : a[i1]) : T(0);
+    const bool in0 = !done0 && i0 < hi0 && (STRICT ? v0 < x0 : v0 <= x0);
+    const bool in1 = !done1 && i1 < hi1 && (STRICT ? v1 < x1 : v1 <= x1);
+    const int n0 = __popcll(__ballot(in0)), n1 = __popcll(__ballot(in1));
+    if (!done0) {
+      if (fine0 || n0 == 0) { *c0 = lo0 + n0 * (fine0 ? 1 : 0); done0 = true; }
+      else { const int64_t nlo = lo0 + (int64_t)(n0 - 1) * st0 + 1, nhi = lo0 + (int64_t)n0 * st0;
+             lo0 = nlo; hi0 = nhi < hi0 ? nhi : hi0; }
+    }
+    if (!done1) {
+      if (fine1 || n1 == 0) { *c1 = lo1 + n1 * (fine1 ? 1 : 0); done1 = true; }
+      else { const int64_t nlo = lo1 + (int64_t)(n1 - 1) * st1 + 1, nhi = lo1 + (int64_t)n1 * st1;
+             lo1 = nlo; hi1 = nhi < hi1 ? nhi : hi1; }
+    }
+  }
+}
+
 // Timestamp node of a graph-captured step (mc_deskew_steps): the constant-rate wall clock
 // (s_memrealtime, hipDeviceAttributeWallClockRate) when the stream reaches it.
 __global__ __launch_bounds__(64) void k_stamp(unsigned long long* dst) {
@@ -403,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
     }
     if (lane < 3) {   // lane i writes row i of R and t_i
       double R[9];
-      euler_xyz_matrix(a.rpy[3 * idx], a.rpy[3 * idx + 1], a.rpy[3 * idx + 2], R);
+      euler_xyz_matrix_prep(a.rpy[3 * idx], a.rpy[3 * idx + 1], a.rpy[3 * idx + 2], R);
       a.frame_tbl[3 * f + lane] = make_float4((float)R[3 * lane], (float)R[3 * lane + 1], (float)R[3 * lane + 2],
                                               (float)a.pos[3 * idx + lane]);
     }
@@ -415,14 +491,16 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
   if (tr.x <= tr.y) {
     if (a.mode == 1) {
       const double tf = a.frame_time[f];
-      klo = wave_count<false>(a.time, a.T, tf + (double)tr.x * 1e-9) - 1;
-      khi = wave_count<false>(a.time, a.T, tf + (double)tr.y * 1e-9) - 1;
+      wave_count2<false>(a.time, a.T, tf + (double)tr.x * 1e-9, tf + (double)tr.y * 1e-9, &klo, &khi);
+      klo -= 1;
+      khi -= 1;
       klo = klo < 0 ? 0 : (klo > a.nseg - 1 ? a.nseg - 1 : klo);
       khi = khi < 0 ? 0 : (khi > a.nseg - 1 ? a.nseg - 1 : khi);
     } else {
       const int64_t fs = a.frame_start[f];
-      klo = wave_count<false>(a.imu_ts, a.M, fs + (int64_t)tr.x) - 1;
-      khi = wave_count<false>(a.imu_ts, a.M, fs + (int64_t)tr.y) - 1;
+      wave_count2<false>(a.imu_ts, a.M, fs + (int64_t)tr.x, fs + (int64_t)tr.y, &klo, &khi);
+      klo -= 1;
+      khi -= 1;
       klo = klo < 0 ? 0 : klo;
       khi = khi < 0 ? 0 : khi;
     }
@@ -460,7 +538,17 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
   // frame spans ~1 ms, so its own window is 1-2 segments and takes the SGPR path (no LDS staging,
   // no barrier: -10 % kernel time on SLERP, tools/ab.py).  Lane per sub-tile; segment of t =
   // last k in [klo, khi] with bound(k) <= t (klo if none), as the kernel's window search.
+  // A window of <= 64 segments (every IMU frame): lane j holds bound(klo + j), loaded in one round,
+  // and a sub-tile's segment is a count over the lanes' bounds (no dependent loads); wider windows
+  // search the table.
+  const bool in_regs = W <= 64;
+  const int64_t my_bnd = (in_regs && lane < W) ? (lane == 0 ? INT64_MIN : bound(klo + lane)) : INT64_MAX;
   auto seg_of = [&](int64_t t) {
+    if (in_regs) {
+      int64_t k = klo - 1;
+      for (int j = 0; j < W; ++j) k += (__shfl(my_bnd, j, 64) <= t) ? 1 : 0;
+      return k < klo ? klo : k;
+    }
     int64_t lo = klo, hi = khi;   // invariant: answer in [lo, hi]
     while (lo < hi) {
       const int64_t mid = (lo + hi + 1) >> 1;
@@ -469,13 +557,14 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
     return lo;
   };
   const int64_t st0 = (int64_t)a.ftile[f] * kSub, st1 = (int64_t)a.ftile[f + 1] * kSub;
-  for (int64_t st = st0 + lane; st < st1; st += 64) {
-    const int2 r = a.strange[st];
-    int64_t k0 = klo, n = 1;
-    if (r.x <= r.y) {
-      k0 = seg_of(r.x);
-      n = seg_of(r.y) - k0 + 1;
-    }
+  for (int64_t base = st0; base < st1; base += 64) {   // a uniform trip count: the shuffles see every lane
+    const int64_t st = base + lane;
+    const bool valid = st < st1;
+    const int2 r = valid ? a.strange[st] : make_int2(1, 0);
+    const bool has = r.x <= r.y;
+    const int64_t s0 = seg_of(has ? (int64_t)r.x : INT64_MIN), s1 = seg_of(has ? (int64_t)r.y : INT64_MIN);
+    if (!valid) continue;
+    const int64_t k0 = has ? s0 : klo, n = has ? s1 - s0 + 1 : 1;
     a.swin[st] = window(k0, n);
     if (n <= MC_FASTPATH_MAXW) {
       record(k0, a.srec, 2 * st);

@@ -20,7 +20,7 @@ stop_if_fault() {  # $1 = rc, $2 = step
   fi
 }
 
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --durations=0 --timeout 300 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 stop_if_fault $? pytest
 tail -5 "$OUT/pytest_gpu_$TAG.log"
 
@@ -28,7 +28,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 stop_if_fault $? smoke
 cat "$OUT/smoke_$TAG.log"
 
-timeout -k 10 600 python bench.py --steps "$STEPS" > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
+timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 5 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
 stop_if_fault $? bench
 cat "$OUT/bench_$TAG.json"
 
