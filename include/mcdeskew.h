@@ -139,6 +139,7 @@ int mc_device_alloc(mc_ctx* ctx, int64_t bytes, void** dptr);
 int mc_device_free(mc_ctx* ctx, void* dptr);
 int mc_memcpy_h2d(mc_ctx* ctx, void* dptr, const void* host, int64_t bytes);
 int mc_memcpy_d2h(mc_ctx* ctx, void* host, const void* dptr, int64_t bytes);
+int mc_memcpy_d2d(mc_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int mc_batch_stage_aos_f64_device(mc_batch* b, const double* d_aos, int64_t ld);
 int mc_batch_fetch_aos_f64_device(mc_batch* b, double* d_aos);
 int mc_timing_read_layout(mc_ctx* ctx, double* ms_total, int64_t* launches);

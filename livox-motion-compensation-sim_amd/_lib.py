@@ -73,6 +73,7 @@ _SIGS = {
     "mc_device_free": (c_int, [c_void_p, c_void_p]),
     "mc_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "mc_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "mc_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "mc_batch_stage_aos_f64_device": (c_int, [c_void_p, c_void_p, c_int64]),
     "mc_batch_fetch_aos_f64_device": (c_int, [c_void_p, c_void_p]),
     "mc_timing_read_layout": (c_int, [c_void_p, _pd, _pi64]),

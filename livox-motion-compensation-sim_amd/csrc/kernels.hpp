@@ -312,13 +312,24 @@ __device__ __forceinline__ void euler_xyz_quat(double r, double p, double y, dou
   q[3] = cr * cp * cy + sr * sp * sy;
 }
 
-// segment k of the pose table: shortest-arc quaternion pair, Theta, position delta
-__device__ __forceinline__ PoseSeg make_pose_seg(const double* time, const double* pos, const double* rpy,
-                                                 int64_t T, int64_t k) {
-  const int64_t k1 = (k + 1 < T) ? k + 1 : k;
+// One pose sample (time, Euler angles, position) as the prep's registers hold it.
+struct PoseSample {
+  double t, r[3], p[3];
+};
+__device__ __forceinline__ PoseSample load_pose(const double* time, const double* pos, const double* rpy,
+                                                int64_t k) {
+  PoseSample s;
+  s.t = time[k];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) { s.r[c] = rpy[3 * k + c]; s.p[c] = pos[3 * k + c]; }
+  return s;
+}
+
+// segment [a, b] of the pose table: shortest-arc quaternion pair, Theta, position delta
+__device__ __forceinline__ PoseSeg pose_seg_of(const PoseSample& a, const PoseSample& b) {
   double q0[4], q1[4];
-  euler_xyz_quat(rpy[3 * k], rpy[3 * k + 1], rpy[3 * k + 2], q0);
-  euler_xyz_quat(rpy[3 * k1], rpy[3 * k1 + 1], rpy[3 * k1 + 2], q1);
+  euler_xyz_quat(a.r[0], a.r[1], a.r[2], q0);
+  euler_xyz_quat(b.r[0], b.r[1], b.r[2], q1);
   double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
   if (d < 0.0) { d = -d; q1[0] = -q1[0]; q1[1] = -q1[1]; q1[2] = -q1[2]; q1[3] = -q1[3]; }
   if (d > 1.0) d = 1.0;
@@ -329,33 +340,55 @@ __device__ __forceinline__ PoseSeg make_pose_seg(const double* time, const doubl
   PoseSeg s;
   s.q0 = make_float4((float)q0[0], (float)q0[1], (float)q0[2], (float)q0[3]);
   s.q1 = make_float4((float)q1[0], (float)q1[1], (float)q1[2], (float)q1[3]);
-  const double* p0 = pos + 3 * k;
-  const double* p1 = pos + 3 * k1;
-  s.p0c = make_float4((float)p0[0], (float)p0[1], (float)p0[2], (float)d);
-  s.dpt = make_float4((float)(p1[0] - p0[0]), (float)(p1[1] - p0[1]), (float)(p1[2] - p0[2]), (float)th);
+  s.p0c = make_float4((float)a.p[0], (float)a.p[1], (float)a.p[2], (float)d);
+  s.dpt = make_float4((float)(b.p[0] - a.p[0]), (float)(b.p[1] - a.p[1]), (float)(b.p[2] - a.p[2]), (float)th);
   s.misc = make_float4((float)inv_sin, small ? 1.f : 0.f, 0.f, 0.f);
-  s.t0 = time[k];
-  const double dt = time[k1] - time[k];
+  s.t0 = a.t;
+  const double dt = b.t - a.t;
   s.inv_dt = dt > 0.0 ? 1.0 / dt : 0.0;
   return s;
 }
 
-// IMU record k (CSIM:1482-1516): the bracketing pair (k, k+1), or the last sample alone
-__device__ __forceinline__ ImuSeg make_imu_seg(const int64_t* ts, const double* gyro, int64_t M, int64_t k) {
+// segment k of the pose table (k + 1 clamped to the last sample)
+__device__ __forceinline__ PoseSeg make_pose_seg(const double* time, const double* pos, const double* rpy,
+                                                 int64_t T, int64_t k) {
+  const int64_t k1 = (k + 1 < T) ? k + 1 : k;
+  return pose_seg_of(load_pose(time, pos, rpy, k), load_pose(time, pos, rpy, k1));
+}
+
+// One IMU sample (ns timestamp, gyro).
+struct ImuSample {
+  int64_t ts;
+  double g[3];
+};
+__device__ __forceinline__ ImuSample load_imu(const int64_t* ts, const double* gyro, int64_t k) {
+  ImuSample s;
+  s.ts = ts[k];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) s.g[c] = gyro[3 * k + c];
+  return s;
+}
+
+// IMU record (CSIM:1482-1516): the bracketing pair (a, b), or a alone (last = a is the last sample)
+__device__ __forceinline__ ImuSeg imu_seg_of(const ImuSample& a, const ImuSample& b, bool last) {
   ImuSeg s;
-  const double* g = gyro + 3 * k;
-  s.g[0] = g[0]; s.g[1] = g[1]; s.g[2] = g[2];
-  if (k + 1 < M) {
-    const double* g1 = gyro + 3 * (k + 1);
-    s.dg[0] = g1[0] - g[0]; s.dg[1] = g1[1] - g[1]; s.dg[2] = g1[2] - g[2];
-    const int64_t dtn = ts[k + 1] - ts[k];
+  s.g[0] = a.g[0]; s.g[1] = a.g[1]; s.g[2] = a.g[2];
+  if (!last) {
+    s.dg[0] = b.g[0] - a.g[0]; s.dg[1] = b.g[1] - a.g[1]; s.dg[2] = b.g[2] - a.g[2];
+    const int64_t dtn = b.ts - a.ts;
     s.inv_dt = dtn > 0 ? 1.0 / (double)dtn : 0.0;
   } else {
     s.dg[0] = s.dg[1] = s.dg[2] = 0.0;
     s.inv_dt = 0.0;
   }
-  s.ts = ts[k];
+  s.ts = a.ts;
   return s;
+}
+
+// IMU record k: the pair (k, k+1), or the last sample alone
+__device__ __forceinline__ ImuSeg make_imu_seg(const int64_t* ts, const double* gyro, int64_t M, int64_t k) {
+  const bool last = k + 1 >= M;
+  return imu_seg_of(load_imu(ts, gyro, k), load_imu(ts, gyro, last ? k : k + 1), last);
 }
 
 __device__ __forceinline__ PoseWin make_pose_win(const PoseSeg& s, double tf) {
@@ -457,92 +490,200 @@ __global__ __launch_bounds__(64) void k_stamp(unsigned long long* dst) {
   if (threadIdx.x == 0) *dst = (unsigned long long)wall_clock64();
 }
 
-// One wave per frame (frame work), then one lane per pose segment / IMU sample (table work).
-__global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
+// ---- k_prep's searches: one load round from an interpolation guess ----------------------------
+// The per-step prep is a chain of dependent memory round trips per frame wave (frame record ->
+// search rounds -> the records' samples -> math), and its latency is step time: the deskew kernel
+// waits for it.  Every table here is a uniform or near-uniform grid (pose samples at gps_rate, IMU
+// at its rate), so the wave loads the 64 consecutive entries around the interpolation guess for
+// the frame, together with each entry's pose / IMU sample, in ONE round: the search is a ballot
+// over the lanes (exact whenever the answer lies inside the window, checked; otherwise the full
+// wave-cooperative search), and the samples the records need are shuffled from the lanes that
+// hold them (a sample outside the window is loaded).  Frame: 2 memory round trips instead of 5-6.
+#ifndef MC_PREP_PROBE
+#define MC_PREP_PROBE 1
+#endif
+
+// first index of the 64-entry window [base, base + 64) around the guess for x in a[0..n)
+template <typename T>
+__device__ __forceinline__ int64_t probe_base(int64_t n, T a0, T a1, double x) {
+  if (n <= 64) return 0;
+  const double span = (double)a1 - (double)a0;
+  double g = span > 0.0 ? (x - (double)a0) / span * (double)(n - 1) : 0.0;
+  g = fmin(fmax(g, 0.0), (double)(n - 1));   // fmax(NaN, 0) = 0
+  const int64_t b = (int64_t)g - 31;
+  return b < 0 ? 0 : (b > n - 64 ? n - 64 : b);
+}
+
+// entries of the sorted a[0..n) that are <= x (STRICT: < x) from the window (lane j holds
+// v = a[base + j] when base + j < n); -1 when the answer is not decided inside the window
+template <bool STRICT, typename T>
+__device__ __forceinline__ int64_t probe_count(T v, int64_t base, int64_t n, T x) {
   const int lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);   // global wave id
+  const bool in = base + lane < n && (STRICT ? v < x : v <= x);
+  const uint64_t m = __ballot(in);
+  const bool lo_ok = base == 0 || (m & 1ull);            // everything before the window counts
+  const bool hi_ok = base + 64 >= n || !(m >> 63);       // nothing after it does
+  return (lo_ok && hi_ok) ? base + (int64_t)__popcll(m) : -1;
+}
+
+// entry k of a table whose entries [base, base + 64) the lanes hold (v), else p[stride * k].
+// Every lane of the wave must call it (a cross-lane read).
+template <typename T>
+__device__ __forceinline__ T fetch(T v, int64_t base, int64_t k, const T* p, int stride) {
+  const int64_t j = k - base;
+  const bool in = j >= 0 && j < 64;
+  const T s = __shfl(v, in ? (int)j : 0, 64);
+  return in ? s : p[stride * k];
+}
+__device__ __forceinline__ PoseSample fetch_pose(const PoseSample& v, int64_t base, int64_t k, const PrepArgs& a) {
+  PoseSample s;
+  s.t = fetch(v.t, base, k, a.time, 1);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    s.r[c] = fetch(v.r[c], base, k, a.rpy + c, 3);
+    s.p[c] = fetch(v.p[c], base, k, a.pos + c, 3);
+  }
+  return s;
+}
+__device__ __forceinline__ ImuSample fetch_imu(const ImuSample& v, int64_t base, int64_t k, const PrepArgs& a) {
+  ImuSample s;
+  s.ts = fetch(v.ts, base, k, a.imu_ts, 1);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) s.g[c] = fetch(v.g[c], base, k, a.gyro + c, 3);
+  return s;
+}
+
+// One wave per frame (frame work), then one lane per pose segment / IMU sample (table work).
+// MODE = the deskew mode (k_prep dispatches on a.mode).
+template <int MODE>
+__device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = block * (kBlock / 64) + (threadIdx.x >> 6);   // global wave id
   if (gw >= a.n_frames) {
     const int64_t k = (gw - a.n_frames) * 64 + lane;
-    if (a.mode == 1 && k < a.nseg) a.pose_seg[k] = make_pose_seg(a.time, a.pos, a.rpy, a.T, k);
-    if (a.mode == 2 && k < a.M) a.imu_seg[k] = make_imu_seg(a.imu_ts, a.gyro, a.M, k);
+    if (MODE == 1 && k < a.nseg) a.pose_seg[k] = make_pose_seg(a.time, a.pos, a.rpy, a.T, k);
+    if (MODE == 2 && k < a.M) a.imu_seg[k] = make_imu_seg(a.imu_ts, a.gyro, a.M, k);
     return;
   }
   const int64_t f = gw;
-  if (a.mode == 0) {
+  if (MODE == 0) {
     // Path A pose selection (LMC:804-812) + Euler->R (LMC:774)
-    int64_t idx;
+    PoseSample ps;
     if (a.pose_select == 1) {
-      idx = f;  // explicit per-frame transformation (host checks T == n_frames)
+      ps = load_pose(a.time, a.pos, a.rpy, f);   // explicit per-frame transformation (host checks T == n_frames)
     } else {
-      idx = wave_count<true>(a.time, a.T, a.frame_time[f]);   // searchsorted 'left'
+      const double tf = a.frame_time[f];
+      const int64_t base = MC_PREP_PROBE ? probe_base<double>(a.T, a.time[0], a.time[a.T - 1], tf) : 0;
+      const int64_t pi = base + lane;
+      PoseSample pv{};
+      if (MC_PREP_PROBE && pi < a.T) pv = load_pose(a.time, a.pos, a.rpy, pi);
+      int64_t idx = MC_PREP_PROBE ? probe_count<true>(pv.t, base, a.T, tf) : -1;
+      if (idx < 0) idx = wave_count<true>(a.time, a.T, tf);   // searchsorted 'left'
       if (idx > a.T - 1) idx = a.T - 1;
+      ps = fetch_pose(pv, MC_PREP_PROBE ? base : INT64_MIN / 2, idx, a);
     }
     if (lane < 3) {   // lane i writes row i of R and t_i
       double R[9];
-      euler_xyz_matrix_prep(a.rpy[3 * idx], a.rpy[3 * idx + 1], a.rpy[3 * idx + 2], R);
+      euler_xyz_matrix_prep(ps.r[0], ps.r[1], ps.r[2], R);
+      const double t = lane == 0 ? ps.p[0] : (lane == 1 ? ps.p[1] : ps.p[2]);   // no dynamic index (no alloca)
       a.frame_tbl[3 * f + lane] = make_float4((float)R[3 * lane], (float)R[3 * lane + 1], (float)R[3 * lane + 2],
-                                              (float)a.pos[3 * idx + lane]);
+                                              (float)t);
     }
     return;
   }
   // per-frame window from the frame's time span (recorded when t_ns was staged)
   const int2 tr = a.trange[f];
+  const bool has = tr.x <= tr.y;
+  const int64_t n_tab = MODE == 1 ? a.T : a.M;
+  const double tf = MODE == 1 ? a.frame_time[f] : 0.0;
+  const int64_t fs = MODE == 2 ? a.frame_start[f] : 0;
+  // the probe window and its samples (one round)
+  int64_t base = INT64_MIN / 2;   // no window: every fetch loads
+  PoseSample pv{};
+  ImuSample iv{};
+  if (MC_PREP_PROBE) {
+    if (MODE == 1) {
+      const double xm = has ? tf + 0.5e-9 * ((double)tr.x + (double)tr.y) : tf;
+      base = probe_base<double>(a.T, a.time[0], a.time[a.T - 1], xm);
+      if (base + lane < a.T) pv = load_pose(a.time, a.pos, a.rpy, base + lane);
+    } else {
+      const double xm = (double)fs + (has ? 0.5 * ((double)tr.x + (double)tr.y) : 0.0);
+      base = probe_base<int64_t>(a.M, a.imu_ts[0], a.imu_ts[a.M - 1], xm);
+      if (base + lane < a.M) iv = load_imu(a.imu_ts, a.gyro, base + lane);
+    }
+  }
   int64_t klo = 0, khi = 0;
-  if (tr.x <= tr.y) {
-    if (a.mode == 1) {
-      const double tf = a.frame_time[f];
-      wave_count2<false>(a.time, a.T, tf + (double)tr.x * 1e-9, tf + (double)tr.y * 1e-9, &klo, &khi);
-      klo -= 1;
-      khi -= 1;
+  if (has) {
+    int64_t c0 = -1, c1 = -1;
+    if (MODE == 1) {
+      const double x0 = tf + (double)tr.x * 1e-9, x1 = tf + (double)tr.y * 1e-9;
+      if (MC_PREP_PROBE) { c0 = probe_count<false>(pv.t, base, a.T, x0); c1 = probe_count<false>(pv.t, base, a.T, x1); }
+      if (c0 < 0 || c1 < 0) wave_count2<false>(a.time, a.T, x0, x1, &c0, &c1);
+      klo = c0 - 1;
+      khi = c1 - 1;
       klo = klo < 0 ? 0 : (klo > a.nseg - 1 ? a.nseg - 1 : klo);
       khi = khi < 0 ? 0 : (khi > a.nseg - 1 ? a.nseg - 1 : khi);
     } else {
-      const int64_t fs = a.frame_start[f];
-      wave_count2<false>(a.imu_ts, a.M, fs + (int64_t)tr.x, fs + (int64_t)tr.y, &klo, &khi);
-      klo -= 1;
-      khi -= 1;
+      const int64_t x0 = fs + (int64_t)tr.x, x1 = fs + (int64_t)tr.y;
+      if (MC_PREP_PROBE) { c0 = probe_count<false>(iv.ts, base, a.M, x0); c1 = probe_count<false>(iv.ts, base, a.M, x1); }
+      if (c0 < 0 || c1 < 0) wave_count2<false>(a.imu_ts, a.M, x0, x1, &c0, &c1);
+      klo = c0 - 1;
+      khi = c1 - 1;
       klo = klo < 0 ? 0 : klo;
       khi = khi < 0 ? 0 : khi;
     }
   }
   const int64_t W = khi - klo + 1;
-  const double tf = a.mode == 1 ? a.frame_time[f] : 0.0;
-  const int64_t fs = a.mode == 2 ? a.frame_start[f] : 0;
-  // frame-relative ns where segment k starts (the LDS path's s_bnd, the SGPR path's bnd1)
-  auto bound = [&](int64_t k) -> int64_t {
-    return a.mode == 1 ? rel_ns_ceil(a.time[k], tf) : a.imu_ts[k] - fs;
+  auto clampk = [&](int64_t k) { return k < n_tab - 1 ? k : n_tab - 1; };
+  // frame-relative ns where the segment of sample s starts (the LDS path's s_bnd, the SGPR path's bnd1)
+  auto bound_pose = [&](const PoseSample& s) -> int64_t { return rel_ns_ceil(s.t, tf); };
+  auto bound_imu = [&](const ImuSample& s) -> int64_t { return s.ts - fs; };
+  auto bound_at = [&](int64_t k) -> int64_t { return MODE == 1 ? rel_ns_ceil(a.time[k], tf) : a.imu_ts[k] - fs; };
+  // record of segment k from samples k, k+1 (clamped) / IMU k, k+1 (or k alone at the end)
+  // s0, s1 come from fetch_pose / fetch_imu; write at dst[slot]
+  auto write_pose = [&](const PoseSample& s0, const PoseSample& s1, void* dst, int64_t slot) {
+    reinterpret_cast<PoseWin*>(dst)[slot] = make_pose_win(pose_seg_of(s0, s1), tf);
   };
-  auto record = [&](int64_t k, void* dst, int64_t slot) {
-    if (a.mode == 1) {
-      reinterpret_cast<PoseWin*>(dst)[slot] = make_pose_win(make_pose_seg(a.time, a.pos, a.rpy, a.T, k), tf);
-    } else {
-      ImuSeg sg = make_imu_seg(a.imu_ts, a.gyro, a.M, k);
-      sg.ts -= fs;
-      reinterpret_cast<ImuSeg*>(dst)[slot] = sg;
-    }
+  auto write_imu = [&](const ImuSample& s0, const ImuSample& s1, bool last, void* dst, int64_t slot) {
+    ImuSeg sg = imu_seg_of(s0, s1, last);
+    sg.ts -= fs;
+    reinterpret_cast<ImuSeg*>(dst)[slot] = sg;
   };
-  auto window = [&](int64_t k0, int64_t n) {
+  // the frame's two records (lane 0: segment klo + the window header, lane 1: klo + 1); every lane
+  // takes part in the fetches
+  {
+    const int64_t k = clampk(klo + (lane == 1 ? 1 : 0));
+    const int64_t k1 = clampk(k + 1);
+    const bool writes = lane < 2 && !(lane == 1 && W < 2);
     FrameWin w;
-    w.klo = (int32_t)k0;
-    w.W = n > kWinMax ? kWinMax + 1 : (int32_t)n;
-    w.bnd1 = n >= 2 ? bound(k0 + 1) : INT64_MAX;
-    return w;
-  };
-  // lane 0: record klo (+ the window header), lane 1: record klo+1
-  if (lane < 2 && !(lane == 1 && W < 2)) {
-    record(klo + lane, a.frec, 2 * f + lane);
-    if (lane == 0) a.fwin[f] = window(klo, W);
+    w.klo = (int32_t)klo;
+    w.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
+    if (MODE == 1) {
+      const PoseSample s0 = fetch_pose(pv, base, k, a), s1 = fetch_pose(pv, base, k1, a);
+      if (writes) write_pose(s0, s1, a.frec, 2 * f + lane);
+      w.bnd1 = W >= 2 ? bound_pose(s1) : INT64_MAX;   // lane 0: s1 = sample klo + 1
+    } else {
+      const ImuSample s0 = fetch_imu(iv, base, k, a), s1 = fetch_imu(iv, base, k1, a);
+      if (writes) write_imu(s0, s1, k + 1 >= a.M, a.frec, 2 * f + lane);
+      w.bnd1 = W >= 2 ? bound_imu(s1) : INT64_MAX;
+    }
+    if (lane == 0) a.fwin[f] = w;
   }
   if (!MC_SUBTILE_WIN || W <= MC_FASTPATH_MAXW || !a.swin) return;
   // A wide frame (IMU: ~20 samples per 0.1 s frame): each 1024-point sub-tile of a time-ordered
   // frame spans ~1 ms, so its own window is 1-2 segments and takes the SGPR path (no LDS staging,
   // no barrier: -10 % kernel time on SLERP, tools/ab.py).  Lane per sub-tile; segment of t =
   // last k in [klo, khi] with bound(k) <= t (klo if none), as the kernel's window search.
-  // A window of <= 64 segments (every IMU frame): lane j holds bound(klo + j), loaded in one round,
-  // and a sub-tile's segment is a count over the lanes' bounds (no dependent loads); wider windows
-  // search the table.
+  // A window of <= 64 segments (every IMU frame): lane j holds bound(klo + j) (from the probe
+  // window), and a sub-tile's segment is a count over the lanes' bounds; wider windows search the
+  // table.
   const bool in_regs = W <= 64;
-  const int64_t my_bnd = (in_regs && lane < W) ? (lane == 0 ? INT64_MIN : bound(klo + lane)) : INT64_MAX;
+  int64_t my_bnd = INT64_MAX;
+  if (in_regs) {
+    const int64_t kb = clampk(klo + lane);
+    const int64_t b = MODE == 1 ? bound_pose(fetch_pose(pv, base, kb, a)) : bound_imu(fetch_imu(iv, base, kb, a));
+    my_bnd = lane == 0 ? INT64_MIN : (lane < W ? b : INT64_MAX);
+  }
   auto seg_of = [&](int64_t t) {
     if (in_regs) {
       int64_t k = klo - 1;
@@ -552,25 +693,49 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
     int64_t lo = klo, hi = khi;   // invariant: answer in [lo, hi]
     while (lo < hi) {
       const int64_t mid = (lo + hi + 1) >> 1;
-      if (bound(mid) <= t) lo = mid; else hi = mid - 1;
+      if (bound_at(mid) <= t) lo = mid; else hi = mid - 1;
     }
     return lo;
   };
   const int64_t st0 = (int64_t)a.ftile[f] * kSub, st1 = (int64_t)a.ftile[f + 1] * kSub;
-  for (int64_t base = st0; base < st1; base += 64) {   // a uniform trip count: the shuffles see every lane
-    const int64_t st = base + lane;
+  for (int64_t sb = st0; sb < st1; sb += 64) {   // a uniform trip count: the shuffles see every lane
+    const int64_t st = sb + lane;
     const bool valid = st < st1;
     const int2 r = valid ? a.strange[st] : make_int2(1, 0);
-    const bool has = r.x <= r.y;
-    const int64_t s0 = seg_of(has ? (int64_t)r.x : INT64_MIN), s1 = seg_of(has ? (int64_t)r.y : INT64_MIN);
-    if (!valid) continue;
-    const int64_t k0 = has ? s0 : klo, n = has ? s1 - s0 + 1 : 1;
-    a.swin[st] = window(k0, n);
-    if (n <= MC_FASTPATH_MAXW) {
-      record(k0, a.srec, 2 * st);
-      if (n >= 2) record(k0 + 1, a.srec, 2 * st + 1);
+    const bool hs = r.x <= r.y;
+    const int64_t s0 = seg_of(hs ? (int64_t)r.x : INT64_MIN), s1 = seg_of(hs ? (int64_t)r.y : INT64_MIN);
+    const int64_t k0 = hs ? s0 : klo, n = hs ? s1 - s0 + 1 : 1;
+    FrameWin w;
+    w.klo = (int32_t)k0;
+    w.W = n > kWinMax ? kWinMax + 1 : (int32_t)n;
+    // samples k0, k0 + 1, k0 + 2 (clamped): records k0 and k0 + 1 and the boundary of k0 + 1
+    const int64_t ka = clampk(k0), kb = clampk(k0 + 1), kc = clampk(k0 + 2);
+    const bool rec = valid && n <= MC_FASTPATH_MAXW;
+    if (MODE == 1) {
+      const PoseSample sa = fetch_pose(pv, base, ka, a), sb_ = fetch_pose(pv, base, kb, a);
+      const PoseSample sc = fetch_pose(pv, base, kc, a);
+      w.bnd1 = n >= 2 ? bound_pose(sb_) : INT64_MAX;
+      if (rec) {
+        write_pose(sa, sb_, a.srec, 2 * st);
+        if (n >= 2) write_pose(sb_, sc, a.srec, 2 * st + 1);
+      }
+    } else {
+      const ImuSample sa = fetch_imu(iv, base, ka, a), sb_ = fetch_imu(iv, base, kb, a);
+      const ImuSample sc = fetch_imu(iv, base, kc, a);
+      w.bnd1 = n >= 2 ? bound_imu(sb_) : INT64_MAX;
+      if (rec) {
+        write_imu(sa, sb_, ka + 1 >= a.M, a.srec, 2 * st);
+        if (n >= 2) write_imu(sb_, sc, kb + 1 >= a.M, a.srec, 2 * st + 1);
+      }
     }
+    if (valid) a.swin[st] = w;
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
+  if (a.mode == 0) prep_body<0>(a, blockIdx.x);
+  else if (a.mode == 1) prep_body<1>(a, blockIdx.x);
+  else prep_body<2>(a, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------------

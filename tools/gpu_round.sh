@@ -2,7 +2,7 @@
 # One GPU-box session: gpu tests -> smoke -> bench -> rocprofv3 kernel trace.
 # Stops at the first fault / abort / timeout (exit codes other than 0 and pytest's 1).
 # Usage (from the repo root, on the GPU box):  bash tools/gpu_round.sh [tag] [steps]
-# CONFIGS=1 adds the other BASELINE configs (tools/bench_configs.py) at the end.
+# PMC=0 stops after the rocprof trace.  CONFIGS=1 adds the other BASELINE configs (tools/bench_configs.py) at the end.
 set -u
 TAG=${1:-r01}
 STEPS=${2:-100}
@@ -39,6 +39,7 @@ stop_if_fault $? rocprof
 find "$OUT/prof_$TAG" -name "*kernel_stats*" -exec cat {} \; | head -20
 
 cd "$ROOT"
+if [ "${PMC:-1}" = "0" ]; then exit 0; fi
 timeout -k 10 1200 python tools/pmc_traffic.py --tag "$TAG" > "$OUT/pmc_$TAG.log" 2>&1
 stop_if_fault $? pmc
 tail -5 "$OUT/pmc_$TAG.log"

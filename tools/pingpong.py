@@ -1,0 +1,108 @@
+"""Is the deskew kernels' HBM rate helped by the 256 MB Infinity Cache (MALL) re-serving the previous
+step's buffers?  One step reads 1.2 GB and writes 0.96 GB (600 x 100k, SLERP), so at most
+256 MB / 2.16 GB of a step could be re-served; this A/B measures it (GPU box only):
+
+  same      every step on buffer set A (the bench's pattern)
+  pp2       steps alternate between two independent sets A, B (4.3 GB working set)
+  pp4       four sets (8.6 GB)
+  flush     set A, but a 2 GB streaming copy of unrelated buffers runs before every step
+            (untimed; the kernel's events time the deskew kernel only)
+
+Each arm: HIP events on every deskew launch (hipExtLaunchKernel start/stop); arms interleave over
+rounds in one process.  Each set is a separate allocation, so placement differs per set: the
+per-set medians are reported too.
+
+    python tools/pingpong.py --modes pose_slerp,imu,frame --rounds 5 --steps 16
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import mcamd as mc  # noqa: E402
+
+BYTES = {"pose_slerp": 36, "imu": 36, "frame": 32}
+
+
+def make_set(ctx, counts, times, seed):
+    b_in = ctx.batch(counts, with_time=True)
+    b_in.synth(seed=seed, frame_id_base=1000)
+    b_in.set_frame_times(times)
+    b_in.set_frame_starts((times * 1e9).astype(np.int64))
+    b_xyz = ctx.batch(counts)
+    b_xyz.synth(seed=seed, frame_id_base=1000)
+    b_xyz.set_frame_times(times)
+    return {"in": b_in, "xyz": b_xyz, "out": ctx.batch(counts)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="pose_slerp,imu,frame")
+    ap.add_argument("--frames", type=int, default=600)
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pingpong.json"))
+    args = ap.parse_args()
+    ctx = mc.Context(0)
+    sim = mc.LiDARMotionSimulator({"duration": 120.0, "trajectory_type": "figure_eight", "max_speed": 12.0,
+                                   "lidar_fps": 10})
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:args.frames]
+    counts = np.full(args.frames, args.points, np.int64)
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    ts, g = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    ctx.set_imu(ts, g)
+    sets = [make_set(ctx, counts, times, s) for s in range(4)]
+    n = int(counts.sum())
+    flush_a = ctx.device_buffer(2 << 30)
+    flush_b = ctx.device_buffer(2 << 30)
+    arms = {"same": [0], "pp2": [0, 1], "pp4": [0, 1, 2, 3], "flush": [0]}
+    res = {}
+    for mode in args.modes.split(","):
+        key = "xyz" if mode == "frame" else "in"
+        per = {a: [] for a in arms}
+        per_set = {a: {s: [] for s in arms[a]} for a in arms}
+        for rnd in range(args.rounds):
+            for arm, use in arms.items():
+                for k in range(4):                       # warm every set of the arm
+                    s = sets[use[k % len(use)]]
+                    ctx.deskew(s[key], s["out"], mode=mode)
+                ctx.sync()
+                ctx.read_timing()
+                for i in range(args.steps):
+                    s_id = use[i % len(use)]
+                    s = sets[s_id]
+                    if arm == "flush":                  # evict the MALL: 2 GB D2D copy, untimed
+                        mc._lib.check(ctx.lib.mc_memcpy_d2d(ctx.handle, flush_b.ptr, flush_a.ptr, flush_a.nbytes),
+                                      "memcpy_d2d")
+                    ctx.timing(True)
+                    ctx.deskew(s[key], s["out"], mode=mode)
+                    ctx.timing(False)
+                    ctx.sync()
+                    t = ctx.read_timing()
+                    us = t["main_ms"] / max(t["main_launches"], 1) * 1e3
+                    per[arm].append(us)
+                    per_set[arm][s_id].append(us)
+        for arm in arms:
+            med = statistics.median(per[arm])
+            res[f"{mode}/{arm}"] = {"median_us": med, "min_us": min(per[arm]), "max_us": max(per[arm]),
+                                   "frac": BYTES[mode] * n / (med * 1e-6) / 8e12,
+                                   "per_set_median_us": {str(s): statistics.median(v) for s, v in per_set[arm].items()}}
+            print(f"{mode:10s} {arm:6s} median {med:7.1f} us  ({BYTES[mode] * n / (med * 1e-6) / 1e9:6.0f} GB/s)  "
+                  f"per set: {', '.join(f'{s}:{statistics.median(v):.1f}' for s, v in per_set[arm].items())}",
+                  flush=True)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
