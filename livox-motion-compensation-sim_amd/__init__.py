@@ -17,7 +17,7 @@ from . import _lib, codecs, config, coords, dist, runtime, trajectory  # noqa: F
 from .coords import CoordinateSystem, CoordinateTransformer, GPSData  # noqa: F401
 from .codecs import LivoxLVXWriter  # noqa: F401
 from ._lib import McError, McLibraryError  # noqa: F401
-from .compensator import IMUData, LiDARPoint, MotionCompensator  # noqa: F401
+from .compensator import IMUData, LiDARPoint, MotionCompensator, imu_to_arrays  # noqa: F401
 from .config import default_config, validate_config  # noqa: F401
 from .runtime import Batch, Context, default_context  # noqa: F401
 from .simulator import LiDARMotionSimulator  # noqa: F401

@@ -57,7 +57,6 @@ class MotionCompensator:
         self.config = config
         self.enable_compensation = config.get("enable_motion_compensation", True)
         self._context = context
-        self._imu_key = None
 
     @property
     def context(self) -> Context:
@@ -65,13 +64,13 @@ class MotionCompensator:
             self._context = default_context()
         return self._context
 
-    def _upload_imu(self, ts: np.ndarray, gyro: np.ndarray, key=None):
-        if key is not None and key == self._imu_key:
-            return
+    def _upload_imu(self, ts: np.ndarray, gyro: np.ndarray):
+        """Arrays are rebuilt from the caller's data on every call (the reference reads the list
+        each time, CSIM:1482-1516), so an in-place edit of any sample is always seen; the context
+        skips only the device upload, and only for byte-equal contents."""
         if len(ts) > 1 and np.any(np.diff(ts) < 0):
             raise ValueError("IMU timestamps must be non-decreasing")
         self.context.set_imu(ts, gyro)
-        self._imu_key = key
 
     # ---- reference signature (CSIM:1435) ---------------------------------------------------
     def compensate_point_cloud(self, points: List[LiDARPoint], imu_data: List[IMUData],
@@ -81,27 +80,22 @@ class MotionCompensator:
             return points
         if not points:
             return []
-        ts, g = self._imu_cached(imu_data)
+        ts, g = self._imu_arrays(imu_data)
         xyz = np.array([(p.x, p.y, p.z) for p in points], dtype=np.float64).reshape(-1, 3)
         t = np.fromiter((p.timestamp for p in points), dtype=np.int64, count=len(points))
-        out = self.compensate_arrays(xyz, t, frame_start_time, ts, g, _imu_key=self._imu_key)
+        out = self.compensate_arrays(xyz, t, frame_start_time, ts, g)
         cls = type(points[0])
         return [cls(x=float(o[0]), y=float(o[1]), z=float(o[2]), intensity=p.intensity,
                     timestamp=p.timestamp, ring=p.ring, tag=p.tag) for o, p in zip(out, points)]
 
-    def _imu_cached(self, imu_data):
-        key = (id(imu_data), len(imu_data), imu_data[0].timestamp, imu_data[-1].timestamp)
-        if key != getattr(self, "_imu_arrays_key", None):
-            self._imu_arrays = imu_to_arrays(imu_data)
-            self._imu_arrays_key = key
-            self._imu_key = None
-        ts, g = self._imu_arrays
-        self._upload_imu(ts, g, key)
+    def _imu_arrays(self, imu_data):
+        ts, g = imu_to_arrays(imu_data)
+        self._upload_imu(ts, g)
         return ts, g
 
     # ---- array fast path ------------------------------------------------------------------
     def compensate_arrays(self, xyz, timestamp_ns, frame_start_ns: int, imu_ts, gyro, *,
-                          intensity=None, _imu_key=None) -> np.ndarray:
+                          intensity=None) -> np.ndarray:
         """(N,3) points with absolute int64 ns timestamps -> compensated (N,3) float64."""
         xyz = np.asarray(xyz, dtype=np.float64).reshape(-1, 3)
         if not self.enable_compensation or len(imu_ts) == 0:
@@ -110,7 +104,7 @@ class MotionCompensator:
         if n == 0:
             return np.zeros((0, 3))
         imu_ts = np.ascontiguousarray(imu_ts, dtype=np.int64)
-        self._upload_imu(imu_ts, np.ascontiguousarray(gyro, dtype=np.float64).reshape(-1, 3), _imu_key)
+        self._upload_imu(imu_ts, np.ascontiguousarray(gyro, dtype=np.float64).reshape(-1, 3))
         t_rel = np.asarray(timestamp_ns, dtype=np.int64) - int(frame_start_ns)
         ctx = self.context
         b = ctx.batch([n], with_time=True)
@@ -136,7 +130,7 @@ class MotionCompensator:
                 c["motion_compensated"] = True
                 out.append(c)
             return out
-        ts, g = self._imu_cached(imu_data)
+        ts, g = self._imu_arrays(imu_data)
         counts = np.array([len(fr["points"]) for fr in frames_data], np.int64)
         ctx = self.context
         pts_all = [p for fr in frames_data for p in fr["points"]]

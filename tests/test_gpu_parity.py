@@ -488,6 +488,32 @@ def test_compensator_disabled_and_driver(mc, gpu_ctx):
         assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case)
 
 
+def test_compensator_sees_in_place_imu_edits(mc, gpu_ctx):
+    """The reference reads the IMU list on every call (CSIM:1482-1516): editing interior samples of
+    the same list object between calls (same length, same first / last timestamps) must change
+    the result; a second compensator on the same context must not inherit a stale table."""
+    g = golden("csim_pathb.npz")
+    xyz, ts0 = g["mid/xyz"], g["mid/ts"]
+    start = int(g["mid/frame_start"])
+    imu = [mc.IMUData(int(t), *map(float, gy), 0.0, 0.0, 0.0) for t, gy in zip(g["mid/imu_ts"], g["mid/imu_gyro"])]
+    pts = [mc.LiDARPoint(*map(float, p), 0, int(t), 0, 0) for p, t in zip(xyz, ts0)]
+    comp = mc.MotionCompensator({}, context=gpu_ctx)
+    for k in range(3):
+        if k:
+            for s in imu[1:-1]:
+                s.gyro_x, s.gyro_z = s.gyro_x + 0.3 * k, s.gyro_z - 0.5 * k
+        ts, gyro = mc.imu_to_arrays(imu)
+        got = np.array([[p.x, p.y, p.z] for p in comp.compensate_point_cloud(pts, imu, start, 100_000_000)])
+        ref = R.compensate_arrays(xyz, ts0, start, ts, gyro)
+        assert_scaled_close(got, ref, scale_of(xyz), what=f"edit {k}")
+    other = mc.MotionCompensator({}, context=gpu_ctx)
+    imu2 = [mc.IMUData(int(t), *map(float, gy), 0.0, 0.0, 0.0) for t, gy in zip(g["mid/imu_ts"], g["mid/imu_gyro"])]
+    got = np.array([[p.x, p.y, p.z] for p in other.compensate_point_cloud(pts, imu2, start, 100_000_000)])
+    assert_scaled_close(got, R.compensate_arrays(xyz, ts0, start, *mc.imu_to_arrays(imu2)), scale_of(xyz))
+    got = np.array([[p.x, p.y, p.z] for p in comp.compensate_point_cloud(pts, imu, start, 100_000_000)])
+    assert_scaled_close(got, R.compensate_arrays(xyz, ts0, start, *mc.imu_to_arrays(imu)), scale_of(xyz))
+
+
 @pytest.mark.parametrize("rate", [2.0, 7.7, 8.5, 30.0])
 def test_imu_small_angle_f32_path_and_threshold(mc, gpu_ctx, rate):
     """Waves whose angles stay within 0.78 rad take the float32 path, the others the f64 one:
