@@ -40,7 +40,14 @@ import mcamd as mc  # noqa: E402
 
 BYTES_PER_POINT = {"pose_slerp": 36, "imu": 36, "frame": 32}   # SURVEY §8d algorithmic bytes
 HBM_PEAK_GBS = 8000.0                                          # MI355X_MICROARCH.md chip table
-KERNEL = {"pose_slerp": "k_deskew_points<1>", "imu": "k_deskew_points<2>", "frame": "k_deskew_frame"}
+KERNEL = {"pose_slerp": "k_deskew_points<1", "imu": "k_deskew_points<2", "frame": "k_deskew_frame"}
+# the kernel each issue mode times (pipeline: the step's deskew with the next step's prep in its first
+# workgroups; the last step's launch is the plain kernel)
+KERNEL_OF = {"pipeline": {"pose_slerp": "k_deskew_points<1, true>", "imu": "k_deskew_points<2, true>",
+                          "frame": "k_deskew_frame_next"},
+             "calls": {"pose_slerp": "k_deskew_points<1, false>", "imu": "k_deskew_points<2, false>",
+                       "frame": "k_deskew_frame"}}
+KERNEL_OF["graph"] = KERNEL_OF["calls"]
 REL_TOL = 1e-5                                                 # north_star, scaled per point
 
 SCENARIOS = {   # LMC:1182-1204
@@ -276,16 +283,21 @@ def load_traffic(mode, frames, points):
     return e.get("hbm_bytes_per_launch"), src
 
 
-def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, graph=False):
+def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipeline"):
     """Timed region: wall clock around ``steps`` steps.  ``live``: HIP events on the sampled steps'
     kernels themselves (hipExtLaunchKernel start/stop events: the dispatch's own timestamps, no
     marker packets between the steps) give the roofline's per-launch kernel time.  Otherwise a
-    second, untimed pass carries events on every launch.  ``graph``: the ``steps`` steps are one
-    replay of a HIP graph (Context.deskew_steps), else ``steps`` calls."""
+    second, untimed pass carries events on every launch.  ``issue``: "pipeline" = one
+    Context.deskew_steps(pipeline=True) call, each step's launch also running the next step's prep
+    (the first step's prep is its own launch, inside the timed region); "graph" = one replay of a
+    HIP graph of the steps; "calls" = ``steps`` Context.deskew calls (prep + kernel each)."""
     every = 10 if steps >= 50 else 5
+    graph = issue == "graph"
     ctx.timing(live)           # warmup steps fill the context's event pool for the sampled steps
     for _ in range(warmup):
         ctx.deskew(b_in, b_out, mode=mode)
+    if issue == "pipeline" and warmup:
+        ctx.deskew_steps(b_in, b_out, warmup, mode=mode, sample_every=1 if live else 0, pipeline=True)
     if graph:                  # capture + instantiate only (host work, untimed)
         ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0, prepare=True)
     ctx.sync()
@@ -293,8 +305,9 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, graph=False)
     ctx.read_timing()          # drop the warmup events (back to the pool)
     rdv.barrier()
     t0 = time.perf_counter()
-    if graph:
-        ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0)
+    if graph or issue == "pipeline":
+        ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0,
+                         pipeline=issue == "pipeline")
     else:
         for i in range(steps):
             sample = live and i % every == every // 2
@@ -307,11 +320,14 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, graph=False)
     t1 = time.perf_counter()
     rdv.barrier()
     if not live:
-        ctx.timing(True)
-        for _ in range(min(steps, 50)):
-            ctx.deskew(b_in, b_out, mode=mode)
+        if issue == "pipeline":
+            ctx.deskew_steps(b_in, b_out, min(steps, 50), mode=mode, sample_every=1, pipeline=True)
+        else:
+            ctx.timing(True)
+            for _ in range(min(steps, 50)):
+                ctx.deskew(b_in, b_out, mode=mode)
+            ctx.timing(False)
         ctx.sync()
-        ctx.timing(False)
     tm = ctx.read_timing()
     return t1 - t0, tm, every
 
@@ -516,10 +532,14 @@ def main():
     ap.add_argument("--events-after", action="store_true",
                     help="per-launch HIP events in a second, untimed pass instead of the timed steps")
     ap.add_argument("--gather-timeout", type=float, default=300.0)
-    ap.add_argument("--graph", action="store_true",
-                    help="issue the timed steps as one HIP-graph replay (Context.deskew_steps; kernel time from "
-                         "wall-clock stamp nodes, not HIP events) instead of separate calls")
+    ap.add_argument("--issue", choices=["pipeline", "calls", "graph"], default="pipeline",
+                    help="how the timed steps are issued: pipeline = one Context.deskew_steps(pipeline=True), each "
+                         "step's launch also running the next step's prep; calls = one Context.deskew per step "
+                         "(prep + kernel); graph = one HIP-graph replay (kernel time from wall-clock stamp nodes)")
+    ap.add_argument("--graph", action="store_true", help="same as --issue graph")
     args = ap.parse_args()
+    if args.graph:
+        args.issue = "graph"
 
     rank, local_rank, world = mc.dist.env_rank()
     if world != args.gpus and "WORLD_SIZE" in os.environ:
@@ -561,16 +581,17 @@ def main():
     for mode in modes:
         steps = args.steps if mode == args.mode else max(10, args.steps // 4)
         wall, tm, ev = run_mode(ctx, rdv, mode, src_of[mode], b_out, steps, args.warmup,
-                                live=not args.events_after, graph=args.graph)
+                                live=not args.events_after, issue=args.issue)
         if mode == args.mode:
             every = ev
         wall_max = rdv.max(wall)
         main_avg_s = tm["main_ms"] / max(tm["main_launches"], 1) / 1e3
-        prep_avg_s = tm["prep_ms"] / max(tm["prep_launches"], 1) / 1e3
+        prep_avg_s = tm["prep_ms"] / tm["prep_launches"] / 1e3 if tm["prep_launches"] else None
         achieved = BYTES_PER_POINT[mode] * n_rank / main_avg_s / 1e9 if main_avg_s > 0 else 0.0
         results[mode] = {"wall_s": wall_max, "steps": steps, "main_avg_us": main_avg_s * 1e6,
                          "timed_launches": int(tm["main_launches"]),
-                         "prep_avg_us": prep_avg_s * 1e6, "achieved_GBs": achieved,
+                         "prep_avg_us": prep_avg_s * 1e6 if prep_avg_s is not None else None,
+                         "achieved_GBs": achieved,
                          "value": n_total * steps / wall_max / 1e6}
 
     stager = measure_stager(ctx, b_xyz, b_out, n_rank, min(args.steps, 50)) if n_rank else None
@@ -633,20 +654,23 @@ def main():
             "roofline": {"bound": "hbm", "achieved": r["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": r["achieved_GBs"] / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": KERNEL[args.mode], "kernel_avg_us": r["main_avg_us"],
+                         "kernel": KERNEL_OF[args.issue][args.mode], "kernel_avg_us": r["main_avg_us"],
                          "bytes_per_point": BYTES_PER_POINT[args.mode], "points_per_launch": n_rank,
                          "kernel_time": ("HIP events around every launch of a second, untimed pass"
                                          if args.events_after else
                                          f"wall-clock stamp nodes around the kernels of {r['timed_launches']} of the "
                                          f"{r['steps']} steps of the step graph (every {every}th)"
-                                         if args.graph else
+                                         if args.issue == "graph" else
                                          f"HIP events (hipExtLaunchKernel start/stop, the dispatch's own timestamps) "
                                          f"on the kernels of {r['timed_launches']} of the {r['steps']} timed steps "
                                          f"(every {every}th), on the kernel's stream")},
             "step_over_kernel": (r["wall_s"] / r["steps"] * 1e6) / r["main_avg_us"] if r["main_avg_us"] else None,
             "prep_avg_us": r["prep_avg_us"],
-            "step_issue": ("per-call launches; prep as an any-order packet on the kernel's queue"
-                           if not args.graph else f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)"),
+            "step_issue": {"calls": "per-call launches; prep as an any-order packet on the kernel's queue",
+                           "graph": f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
+                           "pipeline": f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
+                                       "k_prep, then each step's deskew kernel with the next step's prep in its "
+                                       "first workgroups (every step runs its own prep, one launch ahead)"}[args.issue],
             "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
                           "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"],
                           "ms_per_step": v["wall_s"] / v["steps"] * 1e3}

@@ -199,13 +199,18 @@ int mc_batch_checksum(mc_batch* b, double* sums5);
 /* out must have the same frame counts as in (it may be the same batch: in-place). */
 int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select);
 
-/* n_steps consecutive mc_deskew calls (same arguments) as one HIP graph: each step's pose prep and
- * deskew kernel run exactly as in mc_deskew (prep one step ahead on a second queue), the graph's
- * edges replacing the per-call cross-queue events.  The graph is captured on first use and
- * replayed while the launch arguments (batches, tables, sizes) are unchanged.  sample_every > 0
- * puts timing events around the kernels of every sample_every-th step (read by mc_timing_read).
- * flags = MC_STEPS_PREPARE: capture / instantiate only, launch nothing.  Asynchronous. */
+/* n_steps consecutive mc_deskew calls (same arguments), LMC:802-832 n times over one batch.
+ * Default: one HIP graph: each step's pose prep and deskew kernel run exactly as in mc_deskew
+ * (prep one step ahead on a second queue), the graph's edges replacing the per-call cross-queue
+ * events.  The graph is captured on first use and replayed while the launch arguments (batches,
+ * tables, sizes) are unchanged.
+ * MC_STEPS_PIPELINE: no graph; n + 1 launches: step 0's prep, then n deskew launches of which the
+ * first n - 1 also run the next step's prep in their first workgroups (every step still runs its
+ * own prep, one launch ahead, into the other table half).
+ * sample_every > 0 puts timing events around the kernels of every sample_every-th step (read by
+ * mc_timing_read).  MC_STEPS_PREPARE: capture / instantiate only, launch nothing.  Asynchronous. */
 #define MC_STEPS_PREPARE 1
+#define MC_STEPS_PIPELINE 2
 int mc_deskew_steps(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t n_steps,
                     int32_t sample_every, int flags);
 

@@ -27,6 +27,8 @@ MC_MODE_IMU = 2
 MC_POSE_SEARCHSORTED = 0
 MC_POSE_DIRECT = 1
 MC_BATCH_WITH_TIME = 1
+STEPS_PREPARE = 1    # MC_STEPS_PREPARE
+STEPS_PIPELINE = 2   # MC_STEPS_PIPELINE
 
 MODES = {"frame": MC_MODE_FRAME, "pose_slerp": MC_MODE_POSE_SLERP, "imu": MC_MODE_IMU}
 POSE_SELECT = {"searchsorted": MC_POSE_SEARCHSORTED, "direct": MC_POSE_DIRECT}

@@ -81,8 +81,9 @@ struct TimedRegion {
 // them from the dispatch itself, so timing adds no marker packets between the step's kernels.
 struct LaunchEvents {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  explicit LaunchEvents(mc_ctx* c) {
-    if (!c->timing) return;
+  explicit LaunchEvents(mc_ctx* c) : LaunchEvents(c, c->timing) {}
+  LaunchEvents(mc_ctx* c, bool on) {
+    if (!on) return;
     e0 = ev_take(c);
     e1 = e0 ? ev_take(c) : nullptr;
     if (e0 && !e1) { c->ev_pool.push_back(e0); e0 = nullptr; }

@@ -793,10 +793,12 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
 #define MC_FRAME_SUB 1       // frame kernel over kBlock-group sub-tiles, one group per thread (-3 %)
 #endif
 // the per-point kernels' decomposition applied to frame mode (MC_FRAME_SUB=1)
-__device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a) {
+// pre: workgroups ahead of the deskew part of the grid (0 unless fused with a prep)
+__device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a, const uint32_t pre) {
   const int64_t n_sub = (int64_t)a.n_tiles * kSub;
-  for (int64_t it = blockIdx.x; it < n_sub; it += gridDim.x) {
-    const int64_t st = gridDim.x >= n_sub ? xcd_unit<MC_XCD_FRAME>(it, n_sub) : it;
+  const uint32_t nb = gridDim.x - pre;
+  for (int64_t it = blockIdx.x - pre; it < n_sub; it += nb) {
+    const int64_t st = nb >= n_sub ? xcd_unit<MC_XCD_FRAME>(it, n_sub) : it;
     const Tile tl = ldu(a.tiles + st / kSub);
     const int g = (int)(st % kSub) * kBlock + threadIdx.x;
     if (g >= tl.ngroups) continue;
@@ -823,7 +825,7 @@ __device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a) {
 
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
 #if MC_FRAME_SUB
-  deskew_frame_sub(a);
+  deskew_frame_sub(a, 0u);
 #else
   deskew_frame_body<false>(a);
 #endif
@@ -1172,12 +1174,18 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
 //   W <= 64     the window's records are staged into LDS once (one barrier), each point picks its
 //               segment by searching the boundaries;
 //   W > 64      pathological span: per-point search of the global tables.
-template <int MODE>
-#if MC_POINTS_WAVES > 0
-__global__ __launch_bounds__(kBlock, MC_POINTS_WAVES) void k_deskew_points(const DeskewArgs a) {
-#else
-__global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
-#endif
+// NEXT: the launch also runs the next step's prep in its first `pre` workgroups (see the
+// k_deskew_frame_next comment)
+// (NEXT: at least 4 waves / SIMD like the plain kernel — the prep body alone would take 172 VGPRs)
+template <int MODE, bool NEXT = false>
+__global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS_WAVES : 1)) void k_deskew_points(
+    const DeskewArgs a, const PrepArgs pn, const uint32_t pre) {
+  if constexpr (NEXT) {
+    if (blockIdx.x < pre) {
+      prep_body<MODE>(pn, blockIdx.x);
+      return;
+    }
+  }
   using Win = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
   __shared__ Win s_win[kWinMax];
   __shared__ int64_t s_bnd[kWinMax];
@@ -1186,8 +1194,9 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
   const Win* frec = reinterpret_cast<const Win*>(a.frec);
   const Win* srec = reinterpret_cast<const Win*>(a.srec);
 
-  for (int64_t it = blockIdx.x; it < n_sub; it += gridDim.x) {
-    const int64_t st = gridDim.x >= n_sub ? xcd_unit<(MODE == 2 ? MC_XCD_IMU : MC_XCD_SLERP)>(it, n_sub) : it;
+  const uint32_t b0 = NEXT ? blockIdx.x - pre : blockIdx.x, nb = NEXT ? gridDim.x - pre : gridDim.x;
+  for (int64_t it = b0; it < n_sub; it += nb) {
+    const int64_t st = nb >= n_sub ? xcd_unit<(MODE == 2 ? MC_XCD_IMU : MC_XCD_SLERP)>(it, n_sub) : it;
     const Tile tl = ldu(a.tiles + st / kSub);
     // IMU frames always span several samples: fetch the sub-tile window with the tile record
     FrameWin sw;
@@ -1346,6 +1355,22 @@ __global__ __launch_bounds__(kBlock) void k_deskew_points(const DeskewArgs a) {
       if (a.copy_t) st_points<MODE>(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
     }
   }
+}
+
+// ---- the next step's prep inside this step's launch (mc_deskew_steps, MC_STEPS_PIPELINE) ---------
+// Workgroups [0, pre) run k_prep's body for the NEXT step (its table half), the rest this step's
+// deskew over the half the previous launch's prep wrote.  The two halves never alias, and the
+// kernel boundary orders the prep's stores before the next launch's reads, so no flag or fence
+// inside the launch; the prep workgroups are dispatched first and finish beside the first deskew
+// workgroups instead of as a dependent kernel on the queue (~5 us per step).  pre is a multiple of
+// the XCD count, so deskew workgroup b - pre sits on the XCD xcd_unit assumes.
+__global__ __launch_bounds__(kBlock, 4) void k_deskew_frame_next(const DeskewArgs a, const PrepArgs p,
+                                                                 const uint32_t pre) {
+  if (blockIdx.x < pre) {
+    prep_body<0>(p, blockIdx.x);
+    return;
+  }
+  deskew_frame_sub(a, pre);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -685,14 +685,27 @@ void launch_main(const StepPlan& sp, hipStream_t s, hipEvent_t e0 = nullptr, hip
   const dim3 grid(sp.grid), block(kBlock);
   if (!e0) {
     if (sp.kernel == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, sp.da);
-    else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, sp.da);
-    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, sp.da);
+    else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, sp.da, sp.pa, 0u);
+    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, sp.da, sp.pa, 0u);
     return;
   }
   if (sp.kernel == MC_MODE_FRAME) hipExtLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, e0, e1, 0u, sp.da);
   else if (sp.kernel == MC_MODE_POSE_SLERP)
-    hipExtLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, e0, e1, 0u, sp.da);
-  else hipExtLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, e0, e1, 0u, sp.da);
+    hipExtLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+  else hipExtLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+}
+
+// This step's deskew (sp) with the NEXT step's prep (nx) in the first workgroups of the same launch
+// (k_deskew_points<MODE, true> / k_deskew_frame_next): pre = nx's prep workgroups rounded up to the
+// XCD count.  sp reads one table half, nx writes the other.
+void launch_fused(const StepPlan& sp, const StepPlan& nx, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  const uint32_t pre = (nx.prep_blocks + kXcds - 1) / kXcds * kXcds;
+  const dim3 grid(sp.grid + pre), block(kBlock);
+  if (sp.kernel == MC_MODE_FRAME)
+    hipExtLaunchKernelGGL(k_deskew_frame_next, grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
+  else if (sp.kernel == MC_MODE_POSE_SLERP)
+    hipExtLaunchKernelGGL((k_deskew_points<1, true>), grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
+  else hipExtLaunchKernelGGL((k_deskew_points<2, true>), grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
 }
 
 // frame time spans derived lazily from t_ns (queued on the main stream)
@@ -845,12 +858,50 @@ int build_step_graph(mc_ctx* c, const StepPlan* plan, int32_t n_steps, int32_t e
 }
 }  // namespace
 
+namespace {
+// n steps as n launches, step i's launch carrying step i+1's prep (MC_STEPS_PIPELINE): one
+// standalone k_prep for step 0, then n deskew launches; the kernel boundaries order each prep
+// before the step that reads it, as in mc_deskew.  Step i reads half h0 ^ (i & 1).
+int deskew_steps_pipelined(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select,
+                           int32_t n_steps, int32_t every) {
+  hipStream_t s = c->stream;
+  if (mode != MC_MODE_FRAME && !in->trange_valid) {
+    if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
+    c->prep_fence = true;
+  }
+  const int h0 = c->buf;
+  StepPlan plan[2];
+  deskew_plan(c, in, out, mode, pose_select, h0, &plan[0]);
+  deskew_plan(c, in, out, mode, pose_select, h0 ^ 1, &plan[1]);
+  if (plan[0].da.copy_t) out->trange_valid = false;
+  auto sampled = [&](int32_t i) { return every > 0 && i % every == every / 2; };
+  {
+    // step 0's prep: any-order right behind this context's own deskew kernel, as in mc_deskew
+    const unsigned fl = (MC_PREP_ISSUE == 2 && !c->prep_fence) ? hipExtAnyOrderLaunch : 0u;
+    LaunchEvents ev(c, sampled(0));
+    launch_prep(plan[0], s, ev.e0, ev.e1, fl);
+    ev.keep(&c->prep_ev);
+    HIPCHK(hipGetLastError());
+  }
+  for (int32_t i = 0; i < n_steps; ++i) {
+    LaunchEvents ev(c, sampled(i));
+    if (i + 1 < n_steps) launch_fused(plan[i & 1], plan[(i + 1) & 1], s, ev.e0, ev.e1);
+    else launch_main(plan[i & 1], s, ev.e0, ev.e1);
+    ev.keep(&c->main_ev);
+    HIPCHK(hipGetLastError());
+  }
+  c->buf = h0 ^ (n_steps & 1);   // the half the last launch did not read
+  c->prep_fence = false;
+  return MC_OK;
+}
+}  // namespace
+
 int mc_deskew_steps(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t n_steps,
                     int32_t sample_every, int flags) {
   if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
   CHECK_ARG(n_steps >= 1 && n_steps <= (1 << 16), "n_steps %d outside [1, 65536]", n_steps);
   CHECK_ARG(sample_every >= 0, "sample_every %d < 0", sample_every);
-  CHECK_ARG((flags & ~MC_STEPS_PREPARE) == 0, "unknown flags 0x%x", flags);
+  CHECK_ARG((flags & ~(MC_STEPS_PREPARE | MC_STEPS_PIPELINE)) == 0, "unknown flags 0x%x", flags);
   if (in->F == 0 || in->n_tiles == 0) {
     // nothing for a graph to carry (no points): the plain calls
     if (flags & MC_STEPS_PREPARE) return MC_OK;
@@ -860,6 +911,10 @@ int mc_deskew_steps(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int 
   }
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  if (flags & MC_STEPS_PIPELINE) {
+    if (flags & MC_STEPS_PREPARE) return MC_OK;   // nothing to capture
+    return deskew_steps_pipelined(c, in, out, mode, pose_select, n_steps, sample_every);
+  }
   // queued on the main stream, ahead of the graph (whose prep branch forks from it)
   if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
   // the graph starts on half 0 whatever c->buf is: everything that last used either half precedes

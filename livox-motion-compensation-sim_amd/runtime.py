@@ -95,13 +95,16 @@ class Context:
         return out
 
     def deskew_steps(self, inp: "Batch", out: "Batch", n_steps: int, mode: str = "frame",
-                     pose_select: str = "searchsorted", sample_every: int = 0, prepare: bool = False) -> "Batch":
-        """``n_steps`` calls of :meth:`deskew` replayed as one HIP graph (asynchronous); every step
-        runs its prep and kernel.  ``prepare``: capture the graph only.  ``sample_every``: timing
-        events around every n-th step's kernels (:meth:`read_timing`)."""
+                     pose_select: str = "searchsorted", sample_every: int = 0, prepare: bool = False,
+                     pipeline: bool = False) -> "Batch":
+        """``n_steps`` calls of :meth:`deskew` (asynchronous); every step runs its prep and kernel.
+        Default: replayed as one HIP graph (``prepare``: capture the graph only).  ``pipeline``: no
+        graph; each step's launch also runs the next step's prep (MC_STEPS_PIPELINE).
+        ``sample_every``: timing events around every n-th step's kernels (:meth:`read_timing`)."""
+        flags = (_lib.STEPS_PREPARE if prepare else 0) | (_lib.STEPS_PIPELINE if pipeline else 0)
         check(self.lib.mc_deskew_steps(self.handle, inp.handle, out.handle, _lib.MODES[mode],
                                        _lib.POSE_SELECT[pose_select], int(n_steps), int(sample_every),
-                                       1 if prepare else 0), f"deskew_steps[{mode}]")
+                                       flags), f"deskew_steps[{mode}]")
         return out
 
     def transform_affine(self, inp: "Batch", out: "Batch | None" = None, mats=None, w_column: bool = False) -> "Batch":

@@ -1,4 +1,5 @@
-"""GPU: n deskew steps replayed as one HIP graph (mc_deskew_steps) give the plain calls' bytes.
+"""GPU: n deskew steps (mc_deskew_steps) give the plain calls' bytes, replayed as one HIP graph or
+pipelined (MC_STEPS_PIPELINE: each step's launch also runs the next step's prep).
 
 Every step of the graph recomputes its pose prep and reruns its kernel, so after any number of
 replays the output is bit-identical to one mc_deskew call on the same batch; the oracle check of
@@ -37,24 +38,25 @@ def _cols(b):
     return np.stack(b.download_columns())
 
 
+@pytest.mark.parametrize("pipeline", [False, True])
 @pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
 @pytest.mark.parametrize("n_steps", [1, 2, 7])
-def test_steps_match_plain_calls(mc, gpu_ctx, mode, n_steps):
+def test_steps_match_plain_calls(mc, gpu_ctx, mode, n_steps, pipeline):
     counts = [3000, 0, 1, 257, 20_000, 1023, 4097]
     b, tr, times = _setup(mc, gpu_ctx, counts)
     ref = gpu_ctx.batch(b.counts)
     gpu_ctx.deskew(b, ref, mode=mode)
     want = _cols(ref)
     out = gpu_ctx.batch(b.counts)
-    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode)
+    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode, pipeline=pipeline)
     gpu_ctx.sync()
     assert np.array_equal(_cols(out), want)
-    # replay of the cached graph, then interleaved with plain calls on the same tables
+    # again (graph: replay of the cached graph), then interleaved with plain calls on the same tables
     out2 = gpu_ctx.batch(b.counts)
     gpu_ctx.deskew(b, out2, mode=mode)
-    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode)
+    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode, pipeline=pipeline)
     gpu_ctx.deskew(b, out2, mode=mode)
-    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode)
+    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode, pipeline=pipeline)
     gpu_ctx.sync()
     assert np.array_equal(_cols(out), want)
     assert np.array_equal(_cols(out2), want)
@@ -62,14 +64,16 @@ def test_steps_match_plain_calls(mc, gpu_ctx, mode, n_steps):
         x.close()
 
 
-def test_steps_oracle_and_recapture_on_new_trajectory(mc, gpu_ctx):
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_steps_oracle_and_recapture_on_new_trajectory(mc, gpu_ctx, pipeline):
     """A graph replayed after the trajectory grows (new table pointers and sizes) must be re-captured:
-    the output follows the new table (checked against the oracle), not the old graph's."""
+    the output follows the new table (checked against the oracle), not the old graph's.  Pipelined:
+    every step's prep reads the tables current when it runs (nothing carried over from the last call)."""
     counts = [5000, 5000, 5000]
     b, tr, times = _setup(mc, gpu_ctx, counts, seed=11)
     out = gpu_ctx.batch(b.counts)
-    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp", prepare=True)   # capture only
-    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp")
+    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp", prepare=True, pipeline=pipeline)   # capture only
+    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp", pipeline=pipeline)
     gpu_ctx.sync()
     first = _cols(out)
     # a longer, shifted trajectory: every point's pose changes
@@ -79,7 +83,7 @@ def test_steps_oracle_and_recapture_on_new_trajectory(mc, gpu_ctx):
     rpy2 = np.column_stack([np.interp(t2, tr["time"], tr["orientation_imu"][:, i]) for i in range(3)])
     tr2 = {"time": t2, "position_gps": pos2, "orientation_imu": rpy2}
     gpu_ctx.set_trajectory(t2, pos2, rpy2)
-    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp")
+    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp", pipeline=pipeline)
     gpu_ctx.sync()
     got = _cols(out)
     assert not np.array_equal(got, first)
@@ -93,6 +97,49 @@ def test_steps_oracle_and_recapture_on_new_trajectory(mc, gpu_ctx):
         _, pos = R.slerp_pose(t2, pos2, rpy2, times[f] + ht[s] * 1e-9)
         assert_scaled_close(got[:3, s].T, ref, scale_of(p, pos), what=f"frame {f}")
     assert np.array_equal(got[3], hi)
+    out.close()
+    b.close()
+
+
+@pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
+def test_pipelined_steps_in_place_and_new_frame_times(mc, gpu_ctx, mode):
+    """In place (out = in), n pipelined steps compound exactly as n plain calls; new frame times
+    between two pipelined calls reach the next call's first step (its prep runs after the upload)."""
+    counts = [4000, 17, 0, 9000, 2048]
+    b, tr, times = _setup(mc, gpu_ctx, counts, seed=5)
+    c = gpu_ctx.batch(b.counts, with_time=True)
+    c.synth(seed=5, frame_id_base=1000)
+    c.set_frame_times(times)
+    c.set_frame_starts((times * 1e9).astype(np.int64))
+    for _ in range(3):
+        gpu_ctx.deskew(c, c, mode=mode)
+    gpu_ctx.deskew_steps(b, b, 3, mode=mode, pipeline=True)
+    gpu_ctx.sync()
+    assert np.array_equal(_cols(b), _cols(c))
+    t2 = times + 0.037
+    for x in (b, c):
+        x.synth(seed=5, frame_id_base=1000)
+    out, want = gpu_ctx.batch(b.counts), gpu_ctx.batch(b.counts)
+    gpu_ctx.deskew_steps(b, out, 2, mode=mode, pipeline=True)
+    b.set_frame_times(t2)
+    b.set_frame_starts((t2 * 1e9).astype(np.int64))
+    gpu_ctx.deskew_steps(b, out, 2, mode=mode, pipeline=True)
+    gpu_ctx.deskew(b, want, mode=mode)
+    gpu_ctx.sync()
+    assert np.array_equal(_cols(out), _cols(want))
+    for x in (out, want, c, b):
+        x.close()
+
+
+def test_pipelined_steps_sampled_timing(mc, gpu_ctx):
+    b, _, _ = _setup(mc, gpu_ctx, [20_000] * 8)
+    out = gpu_ctx.batch(b.counts)
+    gpu_ctx.read_timing()
+    gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp", sample_every=5, pipeline=True)   # steps 2, 7, 12, 17
+    t = gpu_ctx.read_timing()
+    assert t["main_launches"] == 4 and t["main_ms"] > 0
+    gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp", pipeline=True)
+    assert gpu_ctx.read_timing()["main_launches"] == 0
     out.close()
     b.close()
 

@@ -61,7 +61,7 @@ def run(args):
 
 
 def parse(args):
-    kern = {"frame": "k_deskew_frame", "pose_slerp": "k_deskew_points<1>", "imu": "k_deskew_points<2>"}[args.mode]
+    kern = {"frame": "k_deskew_frame", "pose_slerp": "k_deskew_points<1", "imu": "k_deskew_points<2"}[args.mode]
     rows = []
     for fn in glob.glob(os.path.join(args.parse, "**", "*counter_collection*.csv"), recursive=True):
         rows += [r for r in csv.DictReader(open(fn)) if kern in r["Kernel_Name"]]

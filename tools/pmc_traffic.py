@@ -22,7 +22,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = {"pose_slerp": "k_deskew_points<1>", "imu": "k_deskew_points<2>", "frame": "k_deskew_frame"}
+KERNEL = {"pose_slerp": "k_deskew_points<1", "imu": "k_deskew_points<2", "frame": "k_deskew_frame"}
 BYTES_PER_POINT = {"pose_slerp": 36, "imu": 36, "frame": 32}
 
 

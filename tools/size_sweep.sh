@@ -31,7 +31,7 @@ import csv, glob, sys, statistics, collections
 d = collections.defaultdict(list)
 for fn in glob.glob(sys.argv[1] + "/**/*counter_collection*.csv", recursive=True):
     for r in csv.DictReader(open(fn)):
-        if "k_deskew_points<1>" in r["Kernel_Name"]:
+        if "k_deskew_points<1" in r["Kernel_Name"]:
             d[r["Counter_Name"]].append(float(r["Counter_Value"]))
 print(sys.argv[2], {k: statistics.median(v) for k, v in d.items()})
 PY

@@ -27,7 +27,7 @@ def load(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--kernel", default="k_deskew_points<1>")
+    ap.add_argument("--kernel", default="k_deskew_points<1")
     ap.add_argument("--label", default="")
     args = ap.parse_args()
     rows = load(args.trace)
