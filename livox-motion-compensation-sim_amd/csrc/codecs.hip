@@ -239,7 +239,9 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   a.err = c->d_codec_err;
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    hipLaunchKernelGGL(k_pcd_measure, dim3((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG)), dim3(kCodecBlock), 0, c->stream, a);
+    const dim3 mgrid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
+    if (a.src.cols) hipLaunchKernelGGL(k_pcd_measure<true>, mgrid, dim3(kCodecBlock), 0, c->stream, a);
+    else hipLaunchKernelGGL(k_pcd_measure<false>, mgrid, dim3(kCodecBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());
   std::vector<int32_t> tb((size_t)n_tiles);
@@ -272,7 +274,8 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   } else {
     {
       TimedRegion tr(c, &c->codec_ev, c->stream);
-      hipLaunchKernelGGL(k_pcd_write, grid, dim3(kCodecBlock), 0, c->stream, a);
+      if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kCodecBlock), 0, c->stream, a);
+      else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kCodecBlock), 0, c->stream, a);
     }
     HIPCHK(hipGetLastError());
     if (!slow.empty()) {

@@ -452,6 +452,45 @@ __device__ __forceinline__ void pcd_fast(const CodecFrames& s, int32_t f, int64_
   }
 }
 
+// ---- float32 source (a batch's own columns) ----------------------------------------------------
+// v = m 2^e with a 24-bit m: |v| 10^6 = m 10^6 2^e has a significand below 2^44, so the float64
+// product is exact and N = rint(|v| 10^6) (round half to even) is exact with no error term.  The
+// digit count needs no arithmetic at all: N >= 10^k <=> |v| >= (10^k - 1/2) / 10^6, and the
+// smallest float32 at or above 9.9999995 / 99.9999995 / 999.9999995 is 10 / 100 / 1000 exactly
+// (the float32 below each is 1 ulp ~ 1e-6 .. 6e-5 under it, outside the half-unit band).
+__device__ __forceinline__ bool fmt6_fast_f32(float v, uint32_t& n) {
+  const float a = fminf(fabsf(v), 4294.0f);   // NaN -> 4294 (the line fails the test below)
+  n = (uint32_t)rint((double)a * 1000000.0);
+  return fabsf(v) < 4294.0f;
+}
+
+__device__ __forceinline__ void pcd_fast_vals_f32(const float c[4], PcdFast& P) {
+  P.ok = true;
+  P.neg = 0;
+  P.len = 4 + 4 * 7;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    P.ok &= fmt6_fast_f32(c[k], P.n[k]);
+    const float a = fabsf(c[k]);
+    const uint32_t ng = signbit(c[k]) ? 1u : 0u;
+    P.neg |= ng << k;
+    P.len += (int)ng + 1 + (a >= 10.0f) + (a >= 100.0f) + (a >= 1000.0f);
+  }
+}
+
+// pcd_fast_len for float32 values: line length, or -1 outside the packed path
+__device__ __forceinline__ int pcd_fast_len_f32(const float c[4]) {
+  int len = 4 + 4 * 8;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = fabsf(c[k]);
+    ok = ok && a < 4294.0f;
+    len += (signbit(c[k]) ? 1 : 0) + (a >= 10.0f) + (a >= 100.0f) + (a >= 1000.0f);
+  }
+  return ok ? len : -1;
+}
+
 // three decimal digits of x < 1000 as characters in bytes 0..2 (most significant first)
 __device__ __forceinline__ uint32_t pack3(uint32_t x) {
   const uint32_t h = __umul24(x, 41u) >> 12;
@@ -556,6 +595,19 @@ __device__ __forceinline__ void pcd_emit_fast(const PcdFast& P, uint32_t* base, 
 #define MC_PCD_SWAR 1
 #endif
 
+// y * 41 as two shift-adds (y*9, then + y*32): the compiler folds the plain product into a
+// quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t mul41(uint32_t y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t y9, r;
+  asm("v_lshl_add_u32 %0, %1, 3, %1" : "=v"(y9) : "v"(y));
+  asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(y), "v"(y9));
+  return r;
+#else
+  return y * 41u;
+#endif
+}
+
 // one value of the line: pending n (< 4) bytes in w start at dword pos; FIRST: the pending bytes
 // belong to the previous line, so the first dword is ORed
 template <bool FIRST>
@@ -563,10 +615,12 @@ __device__ __forceinline__ void swar_value(uint32_t* base, int& pos, int& n, uin
                                            uint32_t sep) {
   const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
   const int nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
-  // fraction: halves fh = fp / 1000 (low) and fl (high) -> hundreds / tens / units of both
-  const uint32_t fh = fp / 1000u;
+  // fraction: halves fh = fp / 1000 (low) and fl (high) -> hundreds / tens / units of both.
+  // fh = (fp * 4294968) >> 32 is exact for fp < 10^6 (error fp * 0.704 / 2^32 < 1.7e-4 < 1/1000)
+  // and both factors fit 24 bits: one full-rate v_mul_hi_u32_u24 instead of v_mul_hi_u32.
+  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32);
   const uint32_t y = fh | ((fp - fh * 1000u) << 16);
-  const uint32_t h = ((y * 41u) >> 12) & 0x000F000Fu;            // y*41 < 2^32: halves < 1000
+  const uint32_t h = ((mul41(y)) >> 12) & 0x000F000Fu;           // y*41 < 2^32: halves < 1000
   const uint32_t r = y - h * 100u;
   const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;    // r halves < 100
   const uint32_t ht = h | (t << 8);                               // [h_lo t_lo h_hi t_hi]
@@ -647,6 +701,14 @@ __device__ __forceinline__ int pcd_fast_len(const double c[4]) {
 // byte count; the host sends those tiles to k_pcd_write_bytes and the rest to k_pcd_write.
 constexpr int32_t kPcdSlowTile = 1 << 30;
 
+// columns 0..3 of dense row `row` of a batch source as float32 (codec_point widens them)
+__device__ __forceinline__ void codec_point_f32(const CodecFrames& s, int32_t f, int64_t row, float c[4]) {
+  const float* q = s.cols + bidx(s.C, 0, s.poff[f] + (row - s.doff[f]));
+  c[0] = q[0]; c[1] = q[kBlkPts]; c[2] = q[2 * kBlkPts]; c[3] = q[3 * kBlkPts];
+}
+
+// F32: the source is a batch's float32 columns (the packed path then works in float32, above)
+template <bool F32>
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
@@ -660,9 +722,15 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
     // its byte-path line count < 2^11, so one scan yields both (no extra barrier)
     int v = 0;
     if (valid) {
-      double c[4];
-      codec_point(a.src, f, row, c);
-      v = pcd_fast_len(c);
+      if constexpr (F32) {
+        float c[4];
+        codec_point_f32(a.src, f, row, c);
+        v = pcd_fast_len_f32(c);
+      } else {
+        double c[4];
+        codec_point(a.src, f, row, c);
+        v = pcd_fast_len(c);
+      }
       if (v < 0) {
         PcdLine L;
         pcd_line(a.src, f, row, L, a.err);
@@ -681,6 +749,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
 // sits at its HBM offset modulo 16), then stored with codec_store_piece.  Tiles flagged slow are
 // skipped (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text
 // always fits the LDS buffer.
+template <bool F32>
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
@@ -697,10 +766,18 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
     for (int i = threadIdx.x; i < kPcdTileText / 16 + 1; i += kCodecBlock) s_text4[i] = make_uint4(0, 0, 0, 0);
     PcdFast P;
     P.len = 0;
-    if (valid) pcd_fast(a.src, f, row, P);
+    if (valid) {
+      if constexpr (F32) {
+        float c[4];
+        codec_point_f32(a.src, f, row, c);
+        pcd_fast_vals_f32(c, P);
+      } else {
+        pcd_fast(a.src, f, row, P);
+      }
+    }
+    const int64_t G = a.tile_pos[u];   // issued before the scan's barrier
     int total;
     const int excl = block_scan(P.len, s_wave, total) - P.len;
-    const int64_t G = a.tile_pos[u];
     const int shift = (int)(G & 15);
 #if MC_PCD_SWAR
     if (valid) pcd_emit_swar(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);

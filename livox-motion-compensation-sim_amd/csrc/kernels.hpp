@@ -823,8 +823,60 @@ __device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a, const uint
   }
 }
 
+// Quad decomposition (MC_FRAME_QUAD): a workgroup covers 64 float4 groups of a sub-tile and each
+// lane ONE column of one group (lane & 3 = x, y, z, intensity): one 16-byte load and one 16-byte
+// store per lane, four times the lanes of deskew_frame_sub.  The quad's x / y / z float4s reach
+// every lane of the quad through DPP quad broadcasts (no LDS), lane c < 3 forms output column c of
+// the four points (R row c . p + t_c, the same fmaf chain as deskew_frame_sub), lane 3 passes the
+// intensities through.  A bare 16 B-in / 16 B-out stream runs at 6.61-6.68 TB/s with one load and
+// one store per lane vs 6.12 with four of each (tools/stage_probe.hip, profiles/round2/s07).
+#ifndef MC_FRAME_QUAD
+#define MC_FRAME_QUAD 1
+#endif
+constexpr int kQuadGroups = kBlock / 4;   // float4 groups per workgroup in the quad decomposition
+
+template <int K>   // quad_perm [K, K, K, K]: lane K of each quad to all four
+__device__ __forceinline__ float quad_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), K * 0x55, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uint32_t pre) {
+  const int64_t n_units = (int64_t)a.n_tiles * kSub * (kBlock / kQuadGroups);
+  const uint32_t nb = gridDim.x - pre;
+  const int c = threadIdx.x & 3;
+  for (int64_t it = blockIdx.x - pre; it < n_units; it += nb) {
+    const int64_t un = nb >= n_units ? xcd_unit<MC_XCD_FRAME>(it, n_units) : it;
+    const int64_t st = un / (kBlock / kQuadGroups);
+    const Tile tl = ldu(a.tiles + st / kSub);
+    const int g0 = (int)(st % kSub) * kBlock + (int)(un % (kBlock / kQuadGroups)) * kQuadGroups;
+    if (g0 >= tl.ngroups) continue;   // uniform: empty quarter of a short sub-tile
+    const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
+    const float4 r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
+    const float4 r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
+    const int g = g0 + (threadIdx.x >> 2);
+    const bool act = g < tl.ngroups;   // uniform over a quad
+    const int64_t p = tl.pstart + 4 * (int64_t)g;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (act) v = ld4(a.in + bidx((int)a.in_C, c, p));
+    // every lane takes part in the broadcasts (inactive quads carry zeros)
+    float4 X, Y, Z;
+    X.x = quad_bcast<0>(v.x); X.y = quad_bcast<0>(v.y); X.z = quad_bcast<0>(v.z); X.w = quad_bcast<0>(v.w);
+    Y.x = quad_bcast<1>(v.x); Y.y = quad_bcast<1>(v.y); Y.z = quad_bcast<1>(v.z); Y.w = quad_bcast<1>(v.w);
+    Z.x = quad_bcast<2>(v.x); Z.y = quad_bcast<2>(v.y); Z.z = quad_bcast<2>(v.z); Z.w = quad_bcast<2>(v.w);
+    const float4 r = c == 0 ? r0 : (c == 1 ? r1 : r2);
+    float4 o;
+    o.x = fmaf(r.x, X.x, fmaf(r.y, Y.x, fmaf(r.z, Z.x, r.w)));
+    o.y = fmaf(r.x, X.y, fmaf(r.y, Y.y, fmaf(r.z, Z.y, r.w)));
+    o.z = fmaf(r.x, X.z, fmaf(r.y, Y.z, fmaf(r.z, Z.z, r.w)));
+    o.w = fmaf(r.x, X.w, fmaf(r.y, Y.w, fmaf(r.z, Z.w, r.w)));
+    if (act) st_frame(a.out + bidx((int)a.out_C, c, p), c == 3 ? v : o);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
-#if MC_FRAME_SUB
+#if MC_FRAME_QUAD
+  deskew_frame_quad(a, 0u);
+#elif MC_FRAME_SUB
   deskew_frame_sub(a, 0u);
 #else
   deskew_frame_body<false>(a);
@@ -1370,7 +1422,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_deskew_frame_next(const DeskewArg
     prep_body<0>(p, blockIdx.x);
     return;
   }
+#if MC_FRAME_QUAD
+  deskew_frame_quad(a, pre);
+#else
   deskew_frame_sub(a, pre);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------

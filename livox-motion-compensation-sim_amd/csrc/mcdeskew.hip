@@ -668,7 +668,8 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (mode == MC_MODE_IMU) { da.nseg = c->M; da.ntab = c->M; }
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
-  const int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
+  int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
+  if (mode == MC_MODE_FRAME && MC_FRAME_QUAD) units = in->n_tiles * kSub * (kBlock / kQuadGroups);
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
 }

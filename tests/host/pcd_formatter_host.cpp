@@ -37,6 +37,7 @@ static inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint
 }
 using std::fma;
 using std::signbit;
+using std::rint;
 struct CodecFrames { const double* aos; };
 static inline void codec_point(const CodecFrames& s, int32_t, int64_t row, double c[4]) {
   for (int k = 0; k < 4; ++k) c[k] = s.aos[4 * row + k];
@@ -66,7 +67,33 @@ int main(int argc, char** argv) {
   const CodecFrames s{pts.data()};
   std::vector<uint32_t> buf(16400 / 4 + 4);
   int bad = 0;
-  long lines = 0, fast = 0;
+  long lines = 0, fast = 0, f32_lines = 0;
+  // every float32 in [0, 4294] at a stride, and every float32 within 4096 ulps of each digit-count
+  // threshold (10, 100, 1000) and of 4294: the float32 path's N and length equal the float64 path's
+  {
+    auto check = [&](float v) {
+      for (float w : {v, -v}) {
+        uint32_t n32 = 0, n64 = 0;
+        const bool k32 = fmt6_fast_f32(w, n32), k64 = fmt6_fast((double)w, n64);
+        const float c4[4] = {w, w, w, w};
+        const double d4[4] = {w, w, w, w};
+        if (k32 != k64 || (k64 && n32 != n64) || pcd_fast_len_f32(c4) != pcd_fast_len(d4)) {
+          if (++bad < 20) std::printf("float32 value %.9g: n %u/%u ok %d/%d\n", (double)w, n32, n64, k32, k64);
+        }
+      }
+    };
+    uint32_t top;
+    const float lim = 4294.5f;
+    std::memcpy(&top, &lim, 4);
+    for (uint32_t b = 0; b <= top; b += 97) { float v; std::memcpy(&v, &b, 4); check(v); }
+    for (float t : {10.0f, 100.0f, 1000.0f, 4294.0f}) {
+      float v = t;
+      for (int i = 0; i < 4096; ++i) v = std::nextafter(v, 0.0f);
+      for (int i = 0; i < 8192; ++i, v = std::nextafter(v, 1e9f)) check(v);
+    }
+    check(std::nanf(""));
+    check(INFINITY);
+  }
   for (int t = 0; t < N / 256; ++t) {
     std::memset(buf.data(), 0, buf.size() * 4);
     const int shift = t % 16;
@@ -82,6 +109,18 @@ int main(int argc, char** argv) {
       const double cc[4] = {c[0], c[1], c[2], c[3]};
       const int lf = pcd_fast_len(cc);
       ++lines;
+      // the float32-source path (k_pcd_*<true>) on float32-valued lines: same N, signs, lengths
+      const float cf[4] = {(float)c[0], (float)c[1], (float)c[2], (float)c[3]};
+      if ((double)cf[0] == c[0] && (double)cf[1] == c[1] && (double)cf[2] == c[2] && (double)cf[3] == c[3]) {
+        PcdFast Q;
+        pcd_fast_vals_f32(cf, Q);
+        ++f32_lines;
+        if (pcd_fast_len_f32(cf) != lf || Q.ok != P[l].ok ||
+            (Q.ok && (Q.len != P[l].len || Q.neg != P[l].neg || std::memcmp(Q.n, P[l].n, sizeof Q.n)))) {
+          ++bad;
+          std::printf("float32 path differs (len %d/%d ok %d/%d) for %s", Q.len, P[l].len, Q.ok, P[l].ok, line);
+        }
+      }
       if (!P[l].ok) {
         if (lf != -1) { ++bad; std::printf("pcd_fast_len accepted a byte-path line: %s", line); }
         continue;
@@ -112,6 +151,6 @@ int main(int argc, char** argv) {
                   want.substr(i > 20 ? i - 20 : 0, 60).c_str());
     }
   }
-  std::printf("lines %ld packed %ld bad %d\n", lines, fast, bad);
+  std::printf("lines %ld packed %ld float32 %ld bad %d\n", lines, fast, f32_lines, bad);
   return bad > 255 ? 255 : bad;
 }
