@@ -213,6 +213,14 @@ __device__ __forceinline__ int4 ld4(const int32_t* p) {
 #endif
 }
 
+__device__ __forceinline__ int ld1(const int32_t* p) {
+#if MC_NT_LOAD
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
@@ -1189,10 +1197,10 @@ __device__ __forceinline__ Win select_win(bool s, const Win& a, const Win& b) {
 }
 
 // per-point path for frames whose points span more than kWinMax segments
-template <int MODE>
+template <int MODE, int NG = kBlock>   // NG float4 groups from g0 (a sub-tile, or a quad quarter)
 __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const Tile tl, int g0) {
   const int f = tl.frame;
-  const int e_end = 4 * min(tl.ngroups, g0 + kBlock);
+  const int e_end = 4 * min(tl.ngroups, g0 + NG);
   for (int e = 4 * g0 + threadIdx.x; e < e_end; e += kBlock) {
     const int64_t p = tl.pstart + e;
     const float* q = a.in + bidx((int)a.in_C, 0, p);
@@ -1226,6 +1234,142 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
 //   W <= 64     the window's records are staged into LDS once (one barrier), each point picks its
 //               segment by searching the boundaries;
 //   W > 64      pathological span: per-point search of the global tables.
+// ---- quad decomposition of the per-point kernels (MC_POINTS_QUAD) -----------------------------
+// As deskew_frame_quad: a workgroup covers 64 float4 groups (a quarter of a 1024-point sub-tile,
+// same windows), lane c of a quad loads column c of its group (x, y, z, intensity) plus the group's
+// t_ns float4 (the quad's four lanes read the same 16 bytes: one request).  A 4x4 transpose through
+// DPP quad broadcasts gives lane k point k's x, y, z, t; the per-point math runs once per lane on
+// one point (the same slerp_point / imu_point / float32 small-angle code, the same window and vote
+// logic per wave), and a second transpose returns output column c to lane c for one 16-byte
+// store.  Bare 5-in / 4-out blocked streams: 6.41-6.47 TB/s with four lanes per group vs
+// 6.13-6.20 with one (tools/stage_probe.hip, profiles/round2/s09) — but the kernels are not bare
+// streams: with the per-point math once per lane (4x the lanes, each carrying the window / vote
+// logic and both transposes) they ran 50 % slower, so the default stays one lane per group.
+#ifndef MC_POINTS_QUAD
+#define MC_POINTS_QUAD 0     // rejected: SLERP 479.9 vs 320.5 us, IMU 520.9 vs 343.7 us (3 replicas, profiles/round2/s10)
+#endif
+
+// component k (= this lane's index in its quad) of lane L's float4
+template <int L>
+__device__ __forceinline__ float quad_pick(const float4& v, int k) {
+  const float a = quad_bcast<L>(v.x), b = quad_bcast<L>(v.y), c = quad_bcast<L>(v.z), d = quad_bcast<L>(v.w);
+  return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+}
+
+// output column k (this lane's index in its quad) of lane J's point: x, y or z (k = 3: unused)
+template <int J>
+__device__ __forceinline__ float quad_sel(float x, float y, float z, int k) {
+  const float bx = quad_bcast<J>(x), by = quad_bcast<J>(y), bz = quad_bcast<J>(z);
+  return k == 0 ? bx : (k == 1 ? by : bz);
+}
+
+template <int MODE>
+using WinOf = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
+
+template <int MODE>
+__device__ __forceinline__ void deskew_points_quad(const DeskewArgs& a, const uint32_t pre, WinOf<MODE>* s_win,
+                                                   int64_t* s_bnd) {
+  using Win = WinOf<MODE>;
+  constexpr int kQ = kBlock / kQuadGroups;
+  const int tid = threadIdx.x;
+  const int k = tid & 3;                 // lane in quad: loads / stores column k, computes point k
+  const int64_t n_sub = (int64_t)a.n_tiles * kSub;
+  const int64_t n_units = n_sub * kQ;
+  const uint32_t nb = gridDim.x - pre;
+  const Win* frec = reinterpret_cast<const Win*>(a.frec);
+  const Win* srec = reinterpret_cast<const Win*>(a.srec);
+  for (int64_t it = blockIdx.x - pre; it < n_units; it += nb) {
+    const int64_t un = nb >= n_units ? xcd_unit<(MODE == 2 ? MC_XCD_IMU : MC_XCD_SLERP)>(it, n_units) : it;
+    const int64_t st = un / kQ;
+    const Tile tl = ldu(a.tiles + st / kSub);
+    FrameWin sw;
+    if constexpr (MODE == 2) sw = ldu(a.swin + st);
+    const int g0 = (int)(st % kSub) * kBlock + (int)(un % kQ) * kQuadGroups;
+    if (g0 >= tl.ngroups) continue;      // uniform: empty quarter of a short sub-tile
+    const int f = tl.frame;
+    const int g = g0 + (tid >> 2);
+    const bool act = g < tl.ngroups;     // uniform over a quad
+    const int64_t p = tl.pstart + 4 * (int64_t)g;
+    const float* q = a.in + bidx((int)a.in_C, 0, p);
+    const FrameWin ff = ldu(a.fwin + f);
+    const bool sub = MC_SUBTILE_WIN && ff.W > MC_FASTPATH_MAXW;
+    if constexpr (MODE != 2) {
+      if (sub) sw = ldu(a.swin + st);
+    }
+    const FrameWin fw = sub ? sw : ff;
+    const Win* rec = sub ? srec + 2 * st : frec + 2 * f;
+    if (fw.W > kWinMax) {
+      deskew_subtile_slow<MODE, kQuadGroups>(a, tl, g0);
+      continue;
+    }
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    int t = 0;
+    if (act) {
+      v = ld4(q + k * kBlkPts);
+      t = ld1(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts) + k);   // point k's t_ns (a 16-byte run per quad)
+    }
+    // transpose in: point k's coordinates to lane k (every lane takes part in the broadcasts)
+    float x = quad_pick<0>(v, k), y = quad_pick<1>(v, k), z = quad_pick<2>(v, k);
+    if (fw.W <= MC_FASTPATH_MAXW) {
+      const Win r0 = ldu(rec);
+      bool use1 = false, mixed = false;
+      if (fw.W == 2) {
+        const int64_t b1 = fw.bnd1;
+        const bool w1 = __any(act && (int64_t)t >= b1), w0 = __any(act && (int64_t)t < b1);
+        use1 = w1 && !w0;
+        mixed = w1 && w0;
+      }
+      bool done = false;
+#if MC_IMU_F32 && !MC_NULL_COMPUTE
+      if constexpr (MODE == 2) {
+        const ImuF f0 = imu_f32(r0);
+        const ImuF f1 = imu_f32(fw.W == 2 ? ldu(rec + 1) : r0);
+        const ImuF fk = select_win((mixed ? (int64_t)t >= fw.bnd1 : use1), f0, f1);
+        float th[3];
+        const bool ok = !act || imu_angles_f32(fk, t, th);
+        if (__all(ok)) {
+          if (act) imu_rotate_f32(th, x, y, z);
+          done = true;
+        }
+      }
+#endif
+      if (act && !done) {
+        if (!mixed) {
+          point_body<MODE>(use1 ? ldu(rec + 1) : r0, t, x, y, z);
+        } else {
+          point_body<MODE>(select_win((int64_t)t >= fw.bnd1, r0, ldu(rec + 1)), t, x, y, z);
+        }
+      }
+    } else {
+      const int W = fw.W;
+      if (tid < W) {
+        const int64_t kk = fw.klo + tid;
+        if constexpr (MODE == 1) {
+          const double tf = a.frame_time[f];
+          s_win[tid] = make_pose_win(a.pose_seg[kk], tf);
+          s_bnd[tid] = rel_ns_ceil(a.pose_time[kk], tf);
+        } else {
+          ImuSeg sg = a.imu_seg[kk];
+          sg.ts -= a.frame_start[f];
+          s_win[tid] = sg;
+          s_bnd[tid] = sg.ts;
+        }
+      }
+      __syncthreads();
+      if (act) point_body<MODE>(s_win[win_index(s_bnd, W, (int64_t)t)], t, x, y, z);
+      __syncthreads();   // the LDS window is rewritten by the next unit
+    }
+    // transpose out: column k of the quad's four points to lane k (lane 3 keeps the intensities)
+    const float4 o = make_float4(quad_sel<0>(x, y, z, k), quad_sel<1>(x, y, z, k), quad_sel<2>(x, y, z, k),
+                                 quad_sel<3>(x, y, z, k));
+    if (act) {
+      float* ob = a.out + bidx((int)a.out_C, 0, p);
+      st_points<MODE>(ob + k * kBlkPts, k == 3 ? v : o);
+      if (a.copy_t && k == 3) st_points<MODE>(ob + 4 * kBlkPts, ld4(q + 4 * kBlkPts));
+    }
+  }
+}
+
 // NEXT: the launch also runs the next step's prep in its first `pre` workgroups (see the
 // k_deskew_frame_next comment)
 // (NEXT: at least 4 waves / SIMD like the plain kernel — the prep body alone would take 172 VGPRs)
@@ -1241,6 +1385,10 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
   using Win = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
   __shared__ Win s_win[kWinMax];
   __shared__ int64_t s_bnd[kWinMax];
+#if MC_POINTS_QUAD
+  deskew_points_quad<MODE>(a, NEXT ? pre : 0u, s_win, s_bnd);
+  return;
+#endif
   const int tid = threadIdx.x;
   const int64_t n_sub = (int64_t)a.n_tiles * kSub;
   const Win* frec = reinterpret_cast<const Win*>(a.frec);

@@ -670,6 +670,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
   int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
   if (mode == MC_MODE_FRAME && MC_FRAME_QUAD) units = in->n_tiles * kSub * (kBlock / kQuadGroups);
+  if (mode != MC_MODE_FRAME && MC_POINTS_QUAD) units = in->n_tiles * kSub * (kBlock / kQuadGroups);
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
 }
