@@ -1242,7 +1242,7 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
 // one point (the same slerp_point / imu_point / float32 small-angle code, the same window and vote
 // logic per wave), and a second transpose returns output column c to lane c for one 16-byte
 // store.  Bare 5-in / 4-out blocked streams: 6.41-6.47 TB/s with four lanes per group vs
-// 6.13-6.20 with one (tools/stage_probe.hip, profiles/round2/s09) — but the kernels are not bare
+// 6.13-6.20 with one (tools/stage_probe.hip, profiles/round2/s10/stage_probe_blocked.json) — but the kernels are not bare
 // streams: with the per-point math once per lane (4x the lanes, each carrying the window / vote
 // logic and both transposes) they ran 50 % slower, so the default stays one lane per group.
 #ifndef MC_POINTS_QUAD
@@ -1699,8 +1699,94 @@ __device__ __forceinline__ void stage_tile_lds_out(const LayoutArgs& a, const Ti
   __syncthreads();
 }
 
+// ---- 256-point stager units (MC_STAGE_QUAD) ---------------------------------------------------
+// A workgroup moves 256 points (64 float4 groups, one 256-point block of the batch) per unit, so
+// every lane issues ONE 16-byte load and two 16-byte stores (SoA -> AoS) or two loads and one store
+// (AoS -> SoA), each wave instruction covering 1 KB contiguous on both sides, transposed through a
+// 4 KB LDS tile.  Bare streams of these lane shapes: 6.11 TB/s (16 B in / 32 B out, 1 / 2 per
+// lane) vs 5.22-5.34 with the 2048-point tile's 8 / 16 per lane; 6.42 TB/s (32 B in / 16 B out,
+// 2 / 1) (tools/stage_probe.hip, profiles/round2/s07).  (A register-only version through DPP quad
+// transposes stored each row-side instruction with 16-byte holes: SoA -> AoS 721-777 vs 504 us,
+// profiles/round2/s11-s12.)
+#ifndef MC_STAGE_QUAD
+#define MC_STAGE_QUAD 1
+#endif
+constexpr int kStageQuarters = kTileGroups / kQuadGroups;   // 256-point units per tile
+constexpr int kUnitRow = kQuadGroups * 4 + 4;              // LDS floats per column (+4: banks)
+
+__device__ __forceinline__ void soa_to_aos_unit(const LayoutArgs& a, double* __restrict__ aos) {
+  __shared__ float s[4 * kUnitRow];
+  const int64_t n_units = (int64_t)a.n_tiles * kStageQuarters;
+  const int t = threadIdx.x;
+  for (int64_t it = blockIdx.x; it < n_units; it += gridDim.x) {
+    const int64_t un = gridDim.x >= n_units ? xcd_unit<MC_XCD_STAGE>(it, n_units) : it;
+    const Tile tl = ldu(a.tiles + un / kStageQuarters);
+    const int g0 = (int)(un % kStageQuarters) * kQuadGroups;
+    if (g0 >= tl.ngroups) continue;   // uniform
+    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+    const int64_t p0 = tl.pstart + 4 * (int64_t)g0;   // first point of the unit (a block boundary)
+    // column c = t >> 6 of group t & 63: one wave = one column's 1 KB run
+    const int c = t >> 6, gi = t & 63;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g0 + gi < tl.ngroups) v = ld4(a.cols + bidx(a.C, c, p0 + 4 * gi));
+    *reinterpret_cast<float4*>(&s[c * kUnitRow + 4 * gi]) = v;
+    __syncthreads();
+    // rows: chunk i = row i >> 1, half i & 1 (x, y | z, w); lane t stores chunks t and 256 + t
+    const int64_t loc0 = p0 - poff;
+    v2d* d = reinterpret_cast<v2d*>(aos + (doff - a.dbase + loc0) * 4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + u * kBlock, r = i >> 1, h = i & 1;
+      if (loc0 + r < cnt) {
+        const v2d w = {(double)s[(2 * h) * kUnitRow + r], (double)s[(2 * h + 1) * kUnitRow + r]};
+        st_pol<MC_STAGE_ST>(reinterpret_cast<float*>(d + i), __builtin_bit_cast(float4, w));
+      }
+    }
+    __syncthreads();   // s is rewritten by the next unit
+  }
+}
+
+__device__ __forceinline__ void aos_to_soa_unit(const LayoutArgs& a, const double* __restrict__ aos) {
+  __shared__ float s[4 * kUnitRow];
+  const int64_t n_units = (int64_t)a.n_tiles * kStageQuarters;
+  const int t = threadIdx.x;
+  for (int64_t it = blockIdx.x; it < n_units; it += gridDim.x) {
+    const int64_t un = gridDim.x >= n_units ? xcd_unit<MC_XCD_STAGE>(it, n_units) : it;
+    const Tile tl = ldu(a.tiles + un / kStageQuarters);
+    const int g0 = (int)(un % kStageQuarters) * kQuadGroups;
+    if (g0 >= tl.ngroups) continue;   // uniform
+    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+    const int64_t p0 = tl.pstart + 4 * (int64_t)g0;
+    const int64_t loc0 = p0 - poff;
+    const v2d* s2 = reinterpret_cast<const v2d*>(aos + (doff + loc0) * 4);
+    v2d w[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {   // both loads in flight before the LDS writes
+      const int i = t + u * kBlock;
+      w[u] = (loc0 + (i >> 1) < cnt) ? __builtin_nontemporal_load(s2 + i) : v2d{0.0, 0.0};   // padding: zeros
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + u * kBlock, r = i >> 1, h = i & 1;
+      s[(2 * h) * kUnitRow + r] = (float)w[u].x;
+      s[(2 * h + 1) * kUnitRow + r] = (float)w[u].y;
+    }
+    __syncthreads();
+    const int c = t >> 6, gi = t & 63;
+    if (g0 + gi < tl.ngroups)
+      st_pol<MC_STAGE_ST>(a.cols + bidx(a.C, c, p0 + 4 * gi), *reinterpret_cast<const float4*>(&s[c * kUnitRow + 4 * gi]));
+    __syncthreads();
+  }
+}
+
 // AoS f64 (dense, row stride ld) -> padded SoA f32 (padding slots zeroed)
 __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const double* __restrict__ aos, int64_t ld) {
+#if MC_STAGE_QUAD
+  if (ld == 4) {
+    aos_to_soa_unit(a, aos);
+    return;
+  }
+#endif
 #if MC_STAGE_LDS
   __shared__ float s_t[4][kStageRow];
   if (ld == 4) {
@@ -1754,6 +1840,10 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
 
 // padded SoA f32 -> dense AoS (N,4) f64  (the (N,4) float64 layout LMC:776 returns)
 __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, double* __restrict__ aos) {
+#if MC_STAGE_QUAD
+  soa_to_aos_unit(a, aos);
+  return;
+#endif
 #if MC_STAGE_LDS
   __shared__ float s_t[4][kStageRow];
   for (int64_t it = blockIdx.x; it < a.n_tiles; it += gridDim.x) {

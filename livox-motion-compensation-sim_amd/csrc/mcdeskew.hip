@@ -44,6 +44,11 @@ static int launch_grid(const mc_ctx* c, int32_t n_tiles) {
 }
 
 static_assert(mcimpl::kBatchBlock == kBlkPts && mcplan::kBlk == kBlkPts, "batch block size");
+
+// workgroups of a stager launch over n_tiles tiles (the quad stager: 64-group units; ld: AoS columns)
+static int32_t stage_units(int32_t n_tiles, int64_t ld) {
+  return (MC_STAGE_QUAD && ld == 4) ? n_tiles * kStageQuarters : n_tiles;
+}
 static_assert(sizeof(mcplan::TileRec) == sizeof(Tile) && offsetof(mcplan::TileRec, frame) == offsetof(Tile, frame) &&
                   offsetof(mcplan::TileRec, ngroups) == offsetof(Tile, ngroups),
               "host tile records are uploaded as mc::Tile");
@@ -365,8 +370,8 @@ static int launch_stage(mc_batch* b, const double* d_aos, int64_t ld) {
   if (b->n_tiles == 0) return MC_OK;
   {
     TimedRegion tr(c, &c->layout_ev, c->stream);
-    hipLaunchKernelGGL(k_aos_to_soa, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
-                       d_aos, ld);
+    hipLaunchKernelGGL(k_aos_to_soa, dim3(launch_grid(c, stage_units(b->n_tiles, ld))), dim3(kBlock), 0, c->stream,
+                       layout_of(b), d_aos, ld);
   }
   HIPCHK(hipGetLastError());
   return MC_OK;
@@ -377,8 +382,8 @@ static int launch_fetch(mc_batch* b, double* d_aos) {
   if (b->n_tiles == 0) return MC_OK;
   {
     TimedRegion tr(c, &c->layout_ev, c->stream);
-    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b),
-                       d_aos);
+    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, stage_units(b->n_tiles, 4))), dim3(kBlock), 0, c->stream,
+                       layout_of(b), d_aos);
   }
   HIPCHK(hipGetLastError());
   return MC_OK;
@@ -513,7 +518,7 @@ int mc_batch_download_frames_aos_f64(mc_batch* b, int32_t f0, int32_t f1, double
   a.n_tiles = b->ftile[f1] - b->ftile[f0];
   a.dbase = b->doff[f0];
   if (a.n_tiles > 0)
-    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, a.n_tiles)), dim3(kBlock), 0, c->stream, a,
+    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, stage_units(a.n_tiles, 4))), dim3(kBlock), 0, c->stream, a,
                        static_cast<double*>(st));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(aos, st, (size_t)rows * 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
