@@ -5,6 +5,7 @@
   config 4  the whole 6000 x 100k job on ONE GPU (600 M points; 8 GPUs shard it 750 per GPU)
   config 5  the whole 1200 x 1M-point job on ONE GPU (1.2 G points, 6.0 G input values > 2^32)
   config 5 shape  its per-GPU shape at 8 GPUs: 150 x 1M
+  (configs 4 / 5 whole jobs also in frame mode: the reference's own transform_pointcloud, LMC:772-776)
 
 Each run is a child process under its own time limit; the first failure ends the sweep.
 Usage (GPU box):  python tools/bench_configs.py --out gpurun_out/configs.json
@@ -20,7 +21,9 @@ CONFIGS = {
     "config1_highway_10x20k": ["--config", "1"],
     "config3_parking_600x100k": ["--config", "3"],
     "config4_whole_6000x100k_1gpu": ["--config", "4", "--no-extra-modes"],
+    "config4_whole_6000x100k_1gpu_frame": ["--config", "4", "--no-extra-modes", "--mode", "frame"],
     "config5_whole_1200x1M_1gpu": ["--config", "5", "--no-extra-modes"],
+    "config5_whole_1200x1M_1gpu_frame": ["--config", "5", "--no-extra-modes", "--mode", "frame"],
     "config5_shape_150x1M": ["--frames", "150", "--points", "1000000"],
 }
 
