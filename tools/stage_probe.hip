@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -106,14 +107,16 @@ static void run(const char* name, v4f* in, v4f* out, long units) {
   hipEventDestroy(e1);
 }
 
-int main() {
-  const long pts = 60000000;     // the bench batch: 60 M points
+int main(int argc, char** argv) {
+  const long pts = argc > 1 ? atol(argv[1]) : 60000000;   // default: the bench batch, 60 M points
+  const bool blocked_only = argc > 2;
   const long units = pts / 4;    // one float4 (4 f32 points of a column, or 2 f64 values) per lane per load
   v4f *in, *out;
   if (hipMalloc(&in, 32 * pts) != hipSuccess || hipMalloc(&out, 32 * pts) != hipSuccess) return 1;
   hipMemset(in, 0, 32 * pts);
   hipMemset(out, 0, 32 * pts);
   hipDeviceSynchronize();
+  if (blocked_only) goto blocked;
   // soa_to_aos shape: 16 B read, 32 B written per point (pts / 4 lanes x 4 loads + 8 stores)
   run<4, 8, 0>("r16w32 default", in, out, units);
   run<4, 8, 1>("r16w32 sc1", in, out, units);
@@ -137,7 +140,10 @@ int main() {
   run<0, 8, 2>("w32 nt (write only)", in, out, units);
   run<0, 8, 0>("w32 default (write only)", in, out, units);
   // 5-in / 4-out blocked (the per-point kernels' 20 B in / 16 B out per point)
+blocked:
   const long groups = pts / 4;
+  run<1, 1, 1>("r16w16 sc1 (1 load / 1 store)", in, out, pts);
+  run<4, 4, 2>("r16w16 nt", in, out, pts / 4);
   run_blocked<1, 0, 2>("blocked5x4 1 lane/group nt K0", in, out, groups);
   run_blocked<2, 0, 2>("blocked5x4 2 lanes/group nt K0", in, out, groups);
   run_blocked<4, 0, 2>("blocked5x4 4 lanes/group nt K0", in, out, groups);
