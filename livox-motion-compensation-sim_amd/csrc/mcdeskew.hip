@@ -16,6 +16,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -624,8 +625,18 @@ struct StepPlan {
   uint32_t prep_blocks;
   uint32_t grid;
   int32_t kernel;   // -1: no deskew launch (no tiles); else the mode
-  int32_t pad;
+  uint32_t lds;     // dynamic LDS reserved by the per-point launches (an occupancy cap; 0: none)
 };
+
+// Diagnostic occupancy cap for the per-point kernels: $MCDESKEW_POINTS_LDS bytes of dynamic LDS
+// per workgroup (160 KB per CU), read once.
+static uint32_t points_lds_reserve() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("MCDESKEW_POINTS_LDS");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+  }();
+  return v;
+}
 
 void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int h, StepPlan* sp) {
   std::memset(sp, 0, sizeof(*sp));
@@ -678,6 +689,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (mode != MC_MODE_FRAME && MC_POINTS_QUAD) units = in->n_tiles * kSub * (kBlock / kQuadGroups);
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
+  sp->lds = mode == MC_MODE_FRAME ? 0u : points_lds_reserve();
 }
 
 // Launches with optional hipExtLaunchKernel timing events (e0/e1 null: untimed) and AQL flags.
@@ -692,14 +704,14 @@ void launch_main(const StepPlan& sp, hipStream_t s, hipEvent_t e0 = nullptr, hip
   const dim3 grid(sp.grid), block(kBlock);
   if (!e0) {
     if (sp.kernel == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, sp.da);
-    else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, sp.da, sp.pa, 0u);
-    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, sp.da, sp.pa, 0u);
+    else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, sp.lds, s, sp.da, sp.pa, 0u);
+    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, sp.lds, s, sp.da, sp.pa, 0u);
     return;
   }
   if (sp.kernel == MC_MODE_FRAME) hipExtLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, e0, e1, 0u, sp.da);
   else if (sp.kernel == MC_MODE_POSE_SLERP)
-    hipExtLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
-  else hipExtLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+    hipExtLaunchKernelGGL((k_deskew_points<1>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+  else hipExtLaunchKernelGGL((k_deskew_points<2>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
 }
 
 // This step's deskew (sp) with the NEXT step's prep (nx) in the first workgroups of the same launch
@@ -711,8 +723,8 @@ void launch_fused(const StepPlan& sp, const StepPlan& nx, hipStream_t s, hipEven
   if (sp.kernel == MC_MODE_FRAME)
     hipExtLaunchKernelGGL(k_deskew_frame_next, grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
   else if (sp.kernel == MC_MODE_POSE_SLERP)
-    hipExtLaunchKernelGGL((k_deskew_points<1, true>), grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
-  else hipExtLaunchKernelGGL((k_deskew_points<2, true>), grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
+    hipExtLaunchKernelGGL((k_deskew_points<1, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, nx.pa, pre);
+  else hipExtLaunchKernelGGL((k_deskew_points<2, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, nx.pa, pre);
 }
 
 // frame time spans derived lazily from t_ns (queued on the main stream)

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_blocked(const v4f* __restrict__ in, v4f
 }
 
 template <int LPG, int K, int POL>
-static void run_blocked(const char* name, v4f* in, v4f* out, long groups) {
+static void run_blocked(const char* name, v4f* in, v4f* out, long groups, unsigned lds = 0) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -65,7 +65,7 @@ static void run_blocked(const char* name, v4f* in, v4f* out, long groups) {
   std::vector<float> ms;
   for (int i = 0; i < 25; ++i) {
     hipEventRecord(e0);
-    hipLaunchKernelGGL((k_blocked<LPG, K, POL>), dim3(grid), dim3(256), 0, 0, in, out, groups);
+    hipLaunchKernelGGL((k_blocked<LPG, K, POL>), dim3(grid), dim3(256), lds, 0, in, out, groups);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float t;
@@ -154,6 +154,11 @@ blocked:
   run_blocked<4, 16, 1>("blocked5x4 4 lanes/group sc1 K16", in, out, groups);
   run_blocked<1, 48, 1>("blocked5x4 1 lane/group sc1 K48", in, out, groups);
   run_blocked<4, 48, 1>("blocked5x4 4 lanes/group sc1 K48", in, out, groups);
+  // occupancy caps through reserved LDS (160 KB per CU; 4-wave workgroups): waves / SIMD = WGs / CU
+  run_blocked<1, 16, 1>("blocked5x4 1 lane/group sc1 K16 occ<=6", in, out, groups, 26 * 1024);
+  run_blocked<1, 16, 1>("blocked5x4 1 lane/group sc1 K16 occ<=4", in, out, groups, 40 * 1024);
+  run_blocked<1, 16, 1>("blocked5x4 1 lane/group sc1 K16 occ<=3", in, out, groups, 52 * 1024);
+  run_blocked<1, 16, 1>("blocked5x4 1 lane/group sc1 K16 occ<=2", in, out, groups, 64 * 1024);
   hipFree(in);
   hipFree(out);
   return 0;
