@@ -29,7 +29,10 @@ constexpr int kLvxPkgHdr = 22;
 constexpr int kLvxPkg = kLvxPkgHdr + kLvxPkgPoints * kLvxRec;   // 1366 bytes
 constexpr int kLvxFrameHdr = 24;
 constexpr int kLvxFileHdr = 88;
-constexpr int kLvxPkgPerWG = 8;                                 // one unit = up to 8 packages of a frame
+#ifndef MC_LVX_PKG_PER_WG
+#define MC_LVX_PKG_PER_WG 8
+#endif
+constexpr int kLvxPkgPerWG = MC_LVX_PKG_PER_WG;                 // one unit = up to this many packages of a frame
 constexpr int kLvxUnitPoints = kLvxPkgPerWG * kLvxPkgPoints;    // 768
 constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment shift
 constexpr int kPcdTilesPerWG = 4;                               // PCD tiles of kCodecBlock lines per workgroup
