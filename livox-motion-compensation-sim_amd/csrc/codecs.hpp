@@ -35,7 +35,10 @@ constexpr int kLvxFileHdr = 88;
 constexpr int kLvxPkgPerWG = MC_LVX_PKG_PER_WG;                 // one unit = up to this many packages of a frame
 constexpr int kLvxUnitPoints = kLvxPkgPerWG * kLvxPkgPoints;    // 768
 constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment shift
-constexpr int kPcdTilesPerWG = 4;                               // PCD tiles of kCodecBlock lines per workgroup
+#ifndef MC_PCD_TILES_PER_WG
+#define MC_PCD_TILES_PER_WG 8   // 4 / 8 / 16 / 32: 1048.0 / 1023.5 / 1029.2 / 1054.9 us (profiles/round2/s26)
+#endif
+constexpr int kPcdTilesPerWG = MC_PCD_TILES_PER_WG;             // PCD tiles of kCodecBlock lines per workgroup
 constexpr int kPcdTileText = 16384;                             // LDS text buffer per tile
 
 struct CodecFrames {
@@ -680,6 +683,82 @@ __device__ __forceinline__ void pcd_emit_swar(const PcdFast& P, uint32_t* base, 
   if (n > 0) __hip_atomic_fetch_or(base + pos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ---- byte-store line writer (MC_PCD_BYTES) ----------------------------------------------------
+// The same digits as swar_value, but the text goes to LDS with byte stores at its final offsets
+// instead of being aligned in registers and stored as dwords (which needed a zeroed buffer and
+// ds_or for the dwords two lines share): ".ddd" and "ddd" + separator are 8 bytes at a known
+// offset, the head ([-] and nd integer digits) sits right before them.  Values go in reverse
+// order, and every value but the line's first stores its 4-digit field and a '-' unconditionally
+// (at most 5 bytes before its '.'): bytes left of its own head fall inside the previous value of
+// the same line, which is written afterwards and overwrites them.  The line's first value stores
+// exactly its own bytes, so no lane ever writes another line's text: no zeroing, no atomics.
+#ifndef MC_PCD_BYTES
+#define MC_PCD_BYTES 1
+#endif
+#ifndef MC_PCD_PREFETCH
+#define MC_PCD_PREFETCH 1    // float32 source: each tile's values, flag and offset loaded one tile ahead
+#endif
+
+// digit fields of N = round(|v| 10^6) < 2^32: nd integer digits; D = 4 integer digits with leading
+// zeros (byte 0 = thousands); A = ". d1 d2 d3"; B = "d4 d5 d6 sep" (bytes in text order)
+__device__ __forceinline__ void fmt6_fields(uint32_t N, uint32_t sep, int& nd, uint32_t& D, uint32_t& A, uint32_t& B) {
+  const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
+  nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
+  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32);   // fp / 1000, exact
+  const uint32_t y = fh | ((fp - fh * 1000u) << 16);
+  const uint32_t h = ((mul41(y)) >> 12) & 0x000F000Fu;
+  const uint32_t r = y - h * 100u;
+  const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;
+  const uint32_t ht = h | (t << 8);
+  const uint32_t u = r - t * 10u;
+  A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;
+  B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);
+  const uint32_t hi2 = __umul24(ip, 5243u) >> 19;
+  const uint32_t y2 = hi2 | ((ip - hi2 * 100u) << 16);
+  const uint32_t t2 = (__umul24(y2, 103u) >> 10) & 0x000F000Fu;
+  const uint32_t u2 = y2 - t2 * 10u;
+  D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;
+}
+
+__device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+
+// one value whose text starts at byte o of the tile buffer; EXACT: the line's first value
+template <bool EXACT>
+__device__ __forceinline__ void bytes_value(uint8_t* base, int o, uint32_t N, bool neg, uint32_t sep) {
+  int nd;
+  uint32_t D, A, B;
+  fmt6_fields(N, sep, nd, D, A, B);
+  uint8_t* pa = base + o + nd + (neg ? 1 : 0);   // the '.'
+  put4(pa, A);
+  put4(pa + 4, B);
+  if (EXACT) {
+    pa[-1] = (uint8_t)(D >> 24);
+    if (nd >= 2) pa[-2] = (uint8_t)(D >> 16);
+    if (nd >= 3) pa[-3] = (uint8_t)(D >> 8);
+    if (nd >= 4) pa[-4] = (uint8_t)D;
+    if (neg) pa[-nd - 1] = '-';
+  } else {
+    put4(pa - 4, D);          // leading zeros land in the previous value (rewritten after)
+    pa[-nd - 1] = '-';        // the sign slot, or a byte of the previous value
+  }
+}
+
+__device__ __forceinline__ void pcd_emit_bytes(const PcdFast& P, uint8_t* base, int off) {
+  int len[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t ip = P.n[k] / 1000000u;
+    len[k] = 8 + (int)((P.neg >> k) & 1u) + 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
+  }
+  const int o1 = off + len[0], o2 = o1 + len[1], o3 = o2 + len[2];
+  bytes_value<false>(base, o3, P.n[3], (P.neg >> 3) & 1u, '\n');
+  bytes_value<false>(base, o2, P.n[2], (P.neg >> 2) & 1u, ' ');
+  bytes_value<false>(base, o1, P.n[1], (P.neg >> 1) & 1u, ' ');
+  bytes_value<true>(base, off, P.n[0], P.neg & 1u, ' ');
+}
+
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
 // characters with the separator, nd = 1 + [N >= 10^7] + [N >= 10^8] + [N >= 10^9] for
 // N = round-half-even(|v| 10^6).  N >= T (T even) <=> |v| 10^6 >= T - 1/2 exactly; y = fl(|v| 10^6)
@@ -716,6 +795,42 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  if constexpr (F32 && MC_PCD_PREFETCH) {
+    // as k_pcd_write: tile j + 1's values are loaded while tile j is measured
+    const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+    bool vn = false;
+    int64_t rn = 0;
+    int32_t fn = f;
+    auto fetch = [&](int64_t u) {
+      rn = pcd_row(a.src, u, f, vn);
+      fn = f;
+      if (vn) codec_point_f32(a.src, f, rn, cn);
+    };
+    if (u0 < u_end) fetch(u0);
+    for (int64_t u = u0; u < u_end; ++u) {
+      const float c[4] = {cn[0], cn[1], cn[2], cn[3]};
+      const bool valid = vn;
+      const int64_t row = rn;
+      const int32_t fr = fn;
+      if (u + 1 < u_end) fetch(u + 1);
+      int v = 0;
+      if (valid) {
+        v = pcd_fast_len_f32(c);
+        if (v < 0) {
+          PcdLine L;
+          pcd_line(a.src, fr, row, L, a.err);
+          v = L.len + (1 << 20);
+        }
+      }
+      int total;
+      block_scan(v, s_wave, total);
+      if (threadIdx.x == 0)
+        a.tile_bytes[u] = (total & ((1 << 20) - 1)) | ((total >> 20) || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
+      __syncthreads();   // s_wave is reused by the next tile
+    }
+    return;
+  }
   for (int j = 0; j < kPcdTilesPerWG; ++j) {
     const int64_t u = u0 + j;
     if (u >= a.src.n_units) break;
@@ -752,12 +867,59 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
 // sits at its HBM offset modulo 16), then stored with codec_store_piece.  Tiles flagged slow are
 // skipped (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text
 // always fits the LDS buffer.
+// One packed tile: scan the line lengths, write the lines into LDS, store the text.
+__device__ __forceinline__ void pcd_tile_out(const PcdArgs& a, const PcdFast& P, bool valid, int64_t G, int* s_wave,
+                                             uint4* s_text4) {
+  int total;
+  const int excl = block_scan(P.len, s_wave, total) - P.len;
+  const int shift = (int)(G & 15);
+#if MC_PCD_BYTES
+  if (valid) pcd_emit_bytes(P, reinterpret_cast<uint8_t*>(s_text4), shift + excl);
+#elif MC_PCD_SWAR
+  if (valid) pcd_emit_swar(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
+#else
+  if (valid) pcd_emit_fast(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
+#endif
+  __syncthreads();
+  codec_store_piece(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
+  __syncthreads();   // s_wave / s_text are reused by the next tile
+}
+
 template <bool F32>
 __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kCodecBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  if constexpr (F32 && MC_PCD_PREFETCH && MC_PCD_BYTES) {
+    // tile j + 1's loads are in flight while tile j is formatted and stored: one HBM round trip
+    // per workgroup instead of one per tile
+    const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+    bool vn = false;
+    int32_t flag_n = 0;
+    int64_t gn = 0;
+    auto fetch = [&](int64_t u) {
+      const int64_t row = pcd_row(a.src, u, f, vn);
+      if (vn) codec_point_f32(a.src, f, row, cn);
+      flag_n = a.tile_bytes[u];
+      gn = a.tile_pos[u];
+    };
+    if (u0 < u_end) fetch(u0);
+    for (int64_t u = u0; u < u_end; ++u) {
+      const float c[4] = {cn[0], cn[1], cn[2], cn[3]};
+      const bool valid = vn;
+      const int32_t flag = flag_n;
+      const int64_t G = gn;
+      if (u + 1 < u_end) fetch(u + 1);
+      if (flag & kPcdSlowTile) continue;   // workgroup-uniform
+      PcdFast P;
+      P.len = 0;
+      if (valid) pcd_fast_vals_f32(c, P);
+      pcd_tile_out(a, P, valid, G, s_wave, s_text4);
+    }
+    return;
+  }
   for (int j = 0; j < kPcdTilesPerWG; ++j) {
     const int64_t u = u0 + j;
     if (u >= a.src.n_units) break;
@@ -765,8 +927,9 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
     bool valid;
     const int64_t row = pcd_row(a.src, u, f, valid);
     // zero the text buffer (lines OR the dwords they share), ordered before the line writes by
-    // block_scan's barrier
-    for (int i = threadIdx.x; i < kPcdTileText / 16 + 1; i += kCodecBlock) s_text4[i] = make_uint4(0, 0, 0, 0);
+    // block_scan's barrier; the byte-store writer needs no zeroing
+    if (!MC_PCD_BYTES)
+      for (int i = threadIdx.x; i < kPcdTileText / 16 + 1; i += kCodecBlock) s_text4[i] = make_uint4(0, 0, 0, 0);
     PcdFast P;
     P.len = 0;
     if (valid) {
@@ -779,17 +942,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
       }
     }
     const int64_t G = a.tile_pos[u];   // issued before the scan's barrier
-    int total;
-    const int excl = block_scan(P.len, s_wave, total) - P.len;
-    const int shift = (int)(G & 15);
-#if MC_PCD_SWAR
-    if (valid) pcd_emit_swar(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
-#else
-    if (valid) pcd_emit_fast(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
-#endif
-    __syncthreads();
-    codec_store_piece(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
-    __syncthreads();   // s_wave / s_text are reused by the next tile
+    pcd_tile_out(a, P, valid, G, s_wave, s_text4);
   }
 }
 

@@ -95,7 +95,11 @@ int main(int argc, char** argv) {
     check(INFINITY);
   }
   for (int t = 0; t < N / 256; ++t) {
+#if MC_PCD_BYTES
+    std::memset(buf.data(), 0xA5, buf.size() * 4);   // the byte writer must not rely on zeros
+#else
     std::memset(buf.data(), 0, buf.size() * 4);
+#endif
     const int shift = t % 16;
     int off = shift;
     std::string want;
@@ -136,13 +140,25 @@ int main(int argc, char** argv) {
     }
     for (int l = 255; l >= 0; --l)
       if (P[l].ok) {
-#if MC_PCD_SWAR
+#if MC_PCD_BYTES
+        pcd_emit_bytes(P[l], reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
+#elif MC_PCD_SWAR
         pcd_emit_swar(P[l], buf.data(), offs[l]);
 #else
         pcd_emit_fast(P[l], buf.data(), offs[l]);
 #endif
       }
     const std::string got(reinterpret_cast<const char*>(buf.data()) + shift, off - shift);
+#if MC_PCD_BYTES
+    // nothing written outside the tile's text
+    const unsigned char* bb = reinterpret_cast<const unsigned char*>(buf.data());
+    for (size_t i = 0; i < buf.size() * 4; ++i)
+      if ((i < (size_t)shift || i >= (size_t)off) && bb[i] != 0xA5) {
+        ++bad;
+        std::printf("tile %d: byte %zu outside the text [%d, %d) was written\n", t, i, shift, off);
+        break;
+      }
+#endif
     if (got != want) {
       ++bad;
       size_t i = 0;

@@ -20,13 +20,15 @@ def formatter_section() -> str:
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
-@pytest.mark.parametrize("swar", [1, 0])
-def test_line_writers_match_printf(tmp_path, swar):
+@pytest.mark.parametrize("writer", ["bytes", "swar", "fields"])
+def test_line_writers_match_printf(tmp_path, writer):
+    swar = 0 if writer == "fields" else 1
+    nbytes = 1 if writer == "bytes" else 0
     code = open(HARNESS).read().replace("// FORMATTER_SECTION", formatter_section())
     cpp = tmp_path / "fmt.cpp"
     cpp.write_text(code)
     exe = tmp_path / "fmt"
-    subprocess.run(["g++", "-O2", "-std=c++17", f"-DMC_PCD_SWAR={swar}", "-DMC_PCD_DIAG=0", str(cpp), "-o", str(exe)],
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-DMC_PCD_SWAR={swar}", f"-DMC_PCD_BYTES={nbytes}", "-DMC_PCD_DIAG=0", str(cpp), "-o", str(exe)],
                    check=True, capture_output=True, text=True)
     r = subprocess.run([str(exe), "200000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]

@@ -8,6 +8,9 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU \
   --output-format csv -d "$OUT/sq" -o run -- python3 "$ROOT/tools/aux_kernels.py" --reps 2 > "$OUT/sq.log" 2>&1 || exit 1
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
+  -- python3 "$ROOT/tools/aux_kernels.py" --reps 2 > "$OUT/trace.log" 2>&1 || exit 1
+find "$OUT/trace" -name "*kernel_stats*" -exec cat {} \; | grep -E "pcd|lvx|soa" | cut -d, -f1-4
 python3 - "$OUT/sq" <<'PY'
 import csv, glob, sys, collections
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
