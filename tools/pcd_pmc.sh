@@ -6,7 +6,8 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pcd_pmc
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU \
+PMC=${PMC_SET:-"SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU"}
+timeout -s KILL 120 rocprofv3 --pmc $PMC \
   --output-format csv -d "$OUT/sq" -o run -- python3 "$ROOT/tools/aux_kernels.py" --reps 2 > "$OUT/sq.log" 2>&1 || exit 1
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
   -- python3 "$ROOT/tools/aux_kernels.py" --reps 2 > "$OUT/trace.log" 2>&1 || exit 1
