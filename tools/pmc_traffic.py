@@ -70,7 +70,8 @@ def run_aux(counter, outdir):
                 if row.get("Counter_Name") != counter:
                     continue
                 for k in AUX:
-                    if f"mc::{k}(" in row.get("Kernel_Name", ""):
+                    name = row.get("Kernel_Name", "")
+                    if f"mc::{k}(" in name or f"mc::{k}<" in name:   # plain or templated kernel
                         vals[k].append(float(row["Counter_Value"]))
     return {k: statistics.median(v) for k, v in vals.items() if v}, alg
 
