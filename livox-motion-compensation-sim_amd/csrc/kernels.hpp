@@ -122,6 +122,7 @@ struct DeskewArgs {
   int64_t out_C;
   const Tile* tiles;
   int32_t n_tiles;
+  int32_t xcd_order;       // SLERP: sub-tiles in XCD-contiguous order (large batches; see mc_deskew's plan)
   const float4* frame_tbl; // frame mode: 3 float4 per frame (R row i, t_i)
   const double* frame_time;
   const int64_t* frame_start;
@@ -1396,7 +1397,9 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
 
   const uint32_t b0 = NEXT ? blockIdx.x - pre : blockIdx.x, nb = NEXT ? gridDim.x - pre : gridDim.x;
   for (int64_t it = b0; it < n_sub; it += nb) {
-    const int64_t st = nb >= n_sub ? xcd_unit<(MODE == 2 ? MC_XCD_IMU : MC_XCD_SLERP)>(it, n_sub) : it;
+    const int64_t st = nb < n_sub ? it
+                       : (MODE == 2 ? xcd_unit<MC_XCD_IMU>(it, n_sub)
+                                    : (a.xcd_order ? xcd_unit<1>(it, n_sub) : xcd_unit<MC_XCD_SLERP>(it, n_sub)));
     const Tile tl = ldu(a.tiles + st / kSub);
     // IMU frames always span several samples: fetch the sub-tile window with the tile record
     FrameWin sw;

@@ -628,6 +628,8 @@ struct StepPlan {
   uint32_t lds;     // dynamic LDS reserved by the per-point launches (an occupancy cap; 0: none)
 };
 
+constexpr int64_t kSlerpXcdMinPoints = 200000000;
+
 // Diagnostic occupancy cap for the per-point kernels: $MCDESKEW_POINTS_LDS bytes of dynamic LDS
 // per workgroup (160 KB per CU), read once.
 static uint32_t points_lds_reserve() {
@@ -689,6 +691,10 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (mode != MC_MODE_FRAME && MC_POINTS_QUAD) units = in->n_tiles * kSub * (kBlock / kQuadGroups);
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
+  // SLERP sub-tile order: dealt over the XCDs for batches up to ~200 M points (326 vs 340 us at
+  // 600 x 100k), XCD-contiguous above (1682 vs 1890 us at 3000 x 100k, 3434 vs 3713 at 6000; the
+  // dealt order is also bimodal by placement at 2400) — profiles/round2/s30-s32
+  da.xcd_order = (mode == MC_MODE_POSE_SLERP && in->P >= kSlerpXcdMinPoints) ? 1 : 0;
   sp->lds = mode == MC_MODE_FRAME ? 0u : points_lds_reserve();
 }
 

@@ -29,8 +29,8 @@ BYTES = {"pose_slerp": 36, "imu": 36, "frame": 32}
 
 def setup(lib, args):
     ctx = mc.Context(0, lib_path=lib)
-    sim = mc.LiDARMotionSimulator({"duration": 120.0, "trajectory_type": "figure_eight", "max_speed": 12.0,
-                                   "lidar_fps": 10})
+    sim = mc.LiDARMotionSimulator({"duration": max(120.0, args.frames / 10.0), "trajectory_type": "figure_eight",
+                                   "max_speed": 12.0, "lidar_fps": 10})
     tr = sim.add_sensor_noise(sim.generate_trajectory())
     times = sim.lidar_times()[:args.frames]
     counts = np.full(args.frames, args.points, np.int64)
