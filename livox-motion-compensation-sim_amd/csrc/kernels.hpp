@@ -844,11 +844,6 @@ __device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a, const uint
 #endif
 constexpr int kQuadGroups = kBlock / 4;   // float4 groups per workgroup in the quad decomposition
 
-template <int K>   // quad_perm [K, K, K, K]: lane K of each quad to all four
-__device__ __forceinline__ float quad_bcast(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), K * 0x55, 0xF, 0xF, false));
-}
-
 __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uint32_t pre) {
   const int64_t n_units = (int64_t)a.n_tiles * kSub * (kBlock / kQuadGroups);
   const uint32_t nb = gridDim.x - pre;
@@ -1249,13 +1244,6 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
 #ifndef MC_POINTS_QUAD
 #define MC_POINTS_QUAD 0     // rejected: SLERP 479.9 vs 320.5 us, IMU 520.9 vs 343.7 us (3 replicas, profiles/round2/s10)
 #endif
-
-// component k (= this lane's index in its quad) of lane L's float4
-template <int L>
-__device__ __forceinline__ float quad_pick(const float4& v, int k) {
-  const float a = quad_bcast<L>(v.x), b = quad_bcast<L>(v.y), c = quad_bcast<L>(v.z), d = quad_bcast<L>(v.w);
-  return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
-}
 
 // output column k (this lane's index in its quad) of lane J's point: x, y or z (k = 3: unused)
 template <int J>

@@ -25,4 +25,17 @@ __device__ __forceinline__ int64_t xcd_unit(int64_t b, int64_t n) {
   return x * per + (x < rem ? x : rem) + i;
 }
 
+// DPP quad exchange (quad_perm): lanes 4q .. 4q + 3 of a wave form a quad.
+template <int K>   // quad_perm [K, K, K, K]: lane K of each quad to all four
+__device__ __forceinline__ float quad_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), K * 0x55, 0xF, 0xF, false));
+}
+// component k (= this lane's index in its quad) of lane L's float4: with L = 0 .. 3 over a quad
+// whose lane c holds column c of four points, lane k gets point k's columns (a 4 x 4 transpose)
+template <int L>
+__device__ __forceinline__ float quad_pick(const float4& v, int k) {
+  const float a = quad_bcast<L>(v.x), b = quad_bcast<L>(v.y), c = quad_bcast<L>(v.z), d = quad_bcast<L>(v.w);
+  return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+}
+
 }  // namespace mc
