@@ -211,7 +211,7 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   if (int r = check_frames(F, counts, doff)) return r;
   CHECK_ARG(doff[F] == 0 || src.aos || src.batch, "points pointer is NULL");
   std::vector<int64_t> units((size_t)F + 1, 0);
-  for (int32_t f = 0; f < F; ++f) units[f + 1] = units[f] + (counts[f] + kCodecBlock - 1) / kCodecBlock;
+  for (int32_t f = 0; f < F; ++f) units[f + 1] = units[f] + (counts[f] + kPcdBlock - 1) / kPcdBlock;
   const int64_t n_tiles = units[F];
   CHECK_ARG(n_tiles < (int64_t)INT32_MAX, "too many tiles for one launch");
   if (n_tiles == 0) {
@@ -240,8 +240,8 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
     const dim3 mgrid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
-    if (a.src.cols) hipLaunchKernelGGL(k_pcd_measure<true>, mgrid, dim3(kCodecBlock), 0, c->stream, a);
-    else hipLaunchKernelGGL(k_pcd_measure<false>, mgrid, dim3(kCodecBlock), 0, c->stream, a);
+    if (a.src.cols) hipLaunchKernelGGL(k_pcd_measure<true>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
+    else hipLaunchKernelGGL(k_pcd_measure<false>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());
   std::vector<int32_t> tb((size_t)n_tiles);
@@ -270,12 +270,12 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   const dim3 grid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
   if (!MC_PCD_PACKED) {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    hipLaunchKernelGGL(k_pcd_write_bytes, grid, dim3(kCodecBlock), 0, c->stream, a, (const int32_t*)nullptr);
+    hipLaunchKernelGGL(k_pcd_write_bytes, grid, dim3(kPcdBlock), 0, c->stream, a, (const int32_t*)nullptr);
   } else {
     {
       TimedRegion tr(c, &c->codec_ev, c->stream);
-      if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kCodecBlock), 0, c->stream, a);
-      else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kCodecBlock), 0, c->stream, a);
+      if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
+      else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kPcdBlock), 0, c->stream, a);
     }
     HIPCHK(hipGetLastError());
     if (!slow.empty()) {
@@ -284,7 +284,7 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
       HIPCHK(hipMemcpyAsync(a.tile_bytes, slow.data(), slow.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                             c->stream));
       TimedRegion tr(c, &c->codec_ev, c->stream);
-      hipLaunchKernelGGL(k_pcd_write_bytes, dim3((uint32_t)slow.size()), dim3(kCodecBlock), 0, c->stream, a,
+      hipLaunchKernelGGL(k_pcd_write_bytes, dim3((uint32_t)slow.size()), dim3(kPcdBlock), 0, c->stream, a,
                          (const int32_t*)a.tile_bytes);
     }
   }

@@ -39,7 +39,11 @@ constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment s
 #define MC_PCD_TILES_PER_WG 8   // 4 / 8 / 16 / 32: 1048.0 / 1023.5 / 1029.2 / 1054.9 us (profiles/round2/s26)
 #endif
 constexpr int kPcdTilesPerWG = MC_PCD_TILES_PER_WG;             // PCD tiles of kCodecBlock lines per workgroup
-constexpr int kPcdTileText = 16384;                             // LDS text buffer per tile
+#ifndef MC_PCD_BLOCK
+#define MC_PCD_BLOCK 256
+#endif
+constexpr int kPcdBlock = MC_PCD_BLOCK;                          // PCD: threads per workgroup = lines per tile
+constexpr int kPcdTileText = kPcdBlock * 64;                     // LDS text buffer per tile (packed lines <= 52 B)
 
 struct CodecFrames {
   const double* aos; int64_t ld;   // (N, ld) float64 AoS source, or
@@ -89,9 +93,10 @@ __device__ __forceinline__ int32_t codec_advance(const int64_t* __restrict__ uni
 
 // Store LDS bytes [lo, hi) to g + [lo, hi), where lds and g agree modulo 16: whole 16-byte chunks
 // with dwordx4 stores, the partial chunks at either end byte by byte.  All threads participate.
+template <int NT = kCodecBlock>   // NT: threads of the workgroup
 __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const char* lds, int lo, int hi) {
   const int c0 = lo >> 4, c1 = (hi + 15) >> 4;
-  for (int c = c0 + threadIdx.x; c < c1; c += kCodecBlock) {
+  for (int c = c0 + threadIdx.x; c < c1; c += NT) {
     const int b0 = c << 4;
     if (b0 >= lo && b0 + 16 <= hi) {
       *reinterpret_cast<uint4*>(g + b0) = *reinterpret_cast<const uint4*>(lds + b0);
@@ -372,12 +377,12 @@ __device__ __forceinline__ void pcd_emit(const PcdLine& L, char* p) {
 
 __device__ __forceinline__ int64_t pcd_row(const CodecFrames& s, int64_t u, int32_t& f, bool& valid) {
   f = codec_advance(s.unit_off, f, u);
-  const int64_t row = s.doff[f] + (u - s.unit_off[f]) * kCodecBlock + threadIdx.x;
+  const int64_t row = s.doff[f] + (u - s.unit_off[f]) * kPcdBlock + threadIdx.x;
   valid = row < s.doff[f + 1];
   return row;
 }
 
-// block-wide inclusive sum over kCodecBlock threads (4 waves)
+// block-wide inclusive sum over the kPcdBlock threads of a PCD workgroup
 __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -390,7 +395,7 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   int before = 0;
   total = 0;
 #pragma unroll
-  for (int w = 0; w < kCodecBlock / 64; ++w) {
+  for (int w = 0; w < kPcdBlock / 64; ++w) {
     const int c = s_wave[w];
     before += w < wid ? c : 0;
     total += c;
@@ -791,8 +796,8 @@ __device__ __forceinline__ void codec_point_f32(const CodecFrames& s, int32_t f,
 
 // F32: the source is a batch's float32 columns (the packed path then works in float32, above)
 template <bool F32>
-__global__ __launch_bounds__(kCodecBlock) void k_pcd_measure(const PcdArgs a) {
-  __shared__ int s_wave[kCodecBlock / 64];
+__global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
+  __shared__ int s_wave[kPcdBlock / 64];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
   if constexpr (F32 && MC_PCD_PREFETCH) {
@@ -881,13 +886,13 @@ __device__ __forceinline__ void pcd_tile_out(const PcdArgs& a, const PcdFast& P,
   if (valid) pcd_emit_fast(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
 #endif
   __syncthreads();
-  codec_store_piece(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
+  codec_store_piece<kPcdBlock>(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
   __syncthreads();   // s_wave / s_text are reused by the next tile
 }
 
 template <bool F32>
-__global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
-  __shared__ int s_wave[kCodecBlock / 64];
+__global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
+  __shared__ int s_wave[kPcdBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
@@ -929,7 +934,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
     // zero the text buffer (lines OR the dwords they share), ordered before the line writes by
     // block_scan's barrier; the byte-store writer needs no zeroing
     if (!MC_PCD_BYTES)
-      for (int i = threadIdx.x; i < kPcdTileText / 16 + 1; i += kCodecBlock) s_text4[i] = make_uint4(0, 0, 0, 0);
+      for (int i = threadIdx.x; i < kPcdTileText / 16 + 1; i += kPcdBlock) s_text4[i] = make_uint4(0, 0, 0, 0);
     PcdFast P;
     P.len = 0;
     if (valid) {
@@ -950,8 +955,8 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write(const PcdArgs a) {
 // text with codec_store_piece; a tile larger than the LDS buffer — only possible with extreme
 // magnitudes — is written line by line straight to HBM instead.  Tiles: list[blockIdx.x], or, with
 // list == nullptr, kPcdTilesPerWG consecutive tiles per workgroup (MC_PCD_PACKED=0: every tile).
-__global__ __launch_bounds__(kCodecBlock) void k_pcd_write_bytes(const PcdArgs a, const int32_t* list) {
-  __shared__ int s_wave[kCodecBlock / 64];
+__global__ __launch_bounds__(kPcdBlock) void k_pcd_write_bytes(const PcdArgs a, const int32_t* list) {
+  __shared__ int s_wave[kPcdBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
   char* const s_text = reinterpret_cast<char*>(s_text4);
   const int64_t u0 = list ? (int64_t)list[blockIdx.x]
@@ -974,7 +979,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_pcd_write_bytes(const PcdArgs a
     if (total + shift <= kPcdTileText) {
       if (valid) pcd_emit(L, s_text + shift + excl);
       __syncthreads();
-      codec_store_piece(a.out + (G - shift), s_text, shift, shift + total);
+      codec_store_piece<kPcdBlock>(a.out + (G - shift), s_text, shift, shift + total);
     } else if (valid) {
       pcd_emit(L, a.out + G + excl);
     }
