@@ -168,7 +168,10 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
     if (F > 0)
       hipLaunchKernelGGL(k_lvx_frames, dim3((F + kCodecBlock - 1) / kCodecBlock), dim3(kCodecBlock), 0, c->stream,
                          a, (int64_t)0);
-    if (n_pkg > 0)
+    if (n_pkg > 0 && a.src.cols && kLvxUnitsPerWG > 1)
+      hipLaunchKernelGGL(k_lvx_packages_cols, dim3((uint32_t)((n_pkg + kLvxUnitsPerWG - 1) / kLvxUnitsPerWG)),
+                         dim3(kCodecBlock), 0, c->stream, a);
+    else if (n_pkg > 0)
       hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());

@@ -183,6 +183,108 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
 }
 
+// Batch source, kLvxUnitsPerWG consecutive units per workgroup: unit j + 1's meta data and point
+// values are loaded while unit j is assembled and stored (one HBM round trip per workgroup, not
+// per unit); the two LDS buffers alternate, so one barrier per unit.  A unit's first row is a
+// multiple of 768 = 3 blocks into its frame, so thread t's slot j is row t of the unit's block j.
+#ifndef MC_LVX_UNITS_PER_WG
+#define MC_LVX_UNITS_PER_WG 1
+#endif
+constexpr int kLvxUnitsPerWG = MC_LVX_UNITS_PER_WG;
+constexpr int kLvxSlots = kLvxUnitPoints / kCodecBlock;   // 3
+static_assert(kLvxUnitPoints % kCodecBlock == 0 && kCodecBlock == kBlkPts, "unit = whole blocks");
+
+struct LvxUnit {
+  int64_t S;     // file offset of the unit's first package
+  int64_t p0;    // padded batch row of the unit's first point
+  uint64_t ts;
+  int k, n;      // packages, points
+  bool hi;
+};
+
+__device__ __forceinline__ LvxUnit lvx_unit(const LvxArgs& a, int32_t f, int64_t u) {
+  LvxUnit U;
+  const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
+  const int64_t fcount = a.src.doff[f + 1] - a.src.doff[f];
+  const int64_t fpkgs = (fcount + kLvxPkgPoints - 1) / kLvxPkgPoints;
+  U.k = (int)((fpkgs - pkg0) < kLvxPkgPerWG ? (fpkgs - pkg0) : kLvxPkgPerWG);
+  const int64_t rem = fcount - pkg0 * kLvxPkgPoints;
+  U.n = (int)(rem < U.k * kLvxPkgPoints ? rem : U.k * kLvxPkgPoints);
+  U.S = a.frame_pos[f] + kLvxFrameHdr + pkg0 * kLvxPkg;
+  U.p0 = a.src.poff[f] + pkg0 * kLvxPkgPoints;
+  U.ts = a.ts_ns[f];
+  U.hi = a.has_int ? a.has_int[f] != 0 : true;
+  return U;
+}
+
+__global__ __launch_bounds__(kCodecBlock) void k_lvx_packages_cols(const LvxArgs a) {
+  __shared__ uint4 s_buf[2][kLvxLds / 16 + 1];
+  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kLvxUnitsPerWG;
+  const int64_t u_end = u0 + kLvxUnitsPerWG < a.src.n_units ? u0 + kLvxUnitsPerWG : a.src.n_units;
+  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  LvxUnit nu = lvx_unit(a, f, u0);
+  float nv[kLvxSlots][4];
+  auto fetch = [&]() {
+#pragma unroll
+    for (int j = 0; j < kLvxSlots; ++j) {
+      const float* q = a.src.cols + (((nu.p0 >> 8) + j) * a.src.C) * kBlkPts + threadIdx.x;
+      const bool ok = j * kCodecBlock + (int)threadIdx.x < nu.n;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) nv[j][c] = ok ? q[c * kBlkPts] : 0.f;
+    }
+  };
+  fetch();
+  for (int64_t u = u0; u < u_end; ++u) {
+    const LvxUnit cu = nu;
+    float cv[kLvxSlots][4];
+#pragma unroll
+    for (int j = 0; j < kLvxSlots; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) cv[j][c] = nv[j][c];
+    if (u + 1 < u_end) {
+      f = codec_advance(a.src.unit_off, f, u + 1);
+      nu = lvx_unit(a, f, u + 1);
+      fetch();
+    }
+    uint4* const buf = s_buf[(u - u0) & 1];
+    uint16_t* const s16 = reinterpret_cast<uint16_t*>(buf);
+    const int shift = (int)(cu.S & 15);
+#pragma unroll
+    for (int j = 0; j < kLvxSlots; ++j) {
+      const int i = j * kCodecBlock + (int)threadIdx.x;
+      if (i >= cu.k * kLvxPkgPoints) break;
+      const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
+      uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
+      uint32_t x = 0, y = 0, z = 0, refl = 0;
+      if (i < cu.n) {
+        x = (uint32_t)lvx_fixed(cv[j][0], 1000.0, -2147483648.0, 2147483647.0, a.err);
+        y = (uint32_t)lvx_fixed(cv[j][1], 1000.0, -2147483648.0, 2147483647.0, a.err);
+        z = (uint32_t)lvx_fixed(cv[j][2], 1000.0, -2147483648.0, 2147483647.0, a.err);
+        refl = cu.hi ? (uint32_t)lvx_fixed(cv[j][3], 255.0, 0.0, 255.0, a.err) : 128u;
+      }
+      r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
+      r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
+      r[4] = (uint16_t)z; r[5] = (uint16_t)(z >> 16);
+      r[6] = (uint16_t)refl;
+    }
+    if ((int)threadIdx.x < cu.k * (kLvxPkgHdr / 2)) {   // k * 11 <= 88 header halfwords
+      const int h = threadIdx.x, pk = h / (kLvxPkgHdr / 2), w = h - pk * (kLvxPkgHdr / 2);
+      uint32_t v;
+      switch (w) {
+        case 0: v = 0x0500u; break;
+        case 1: v = 0x0100u; break;
+        case 4: v = 0x0100u; break;
+        case 5: v = 0x0002u; break;
+        case 7: case 8: case 9: case 10: v = (uint32_t)(cu.ts >> (16 * (w - 7))) & 0xffffu; break;
+        default: v = 0u;
+      }
+      s16[((shift + pk * kLvxPkg) >> 1) + w] = (uint16_t)v;
+    }
+    __syncthreads();   // the other buffer's stores (unit j - 1) were issued before this barrier
+    codec_store_piece(a.out + (cu.S - shift), reinterpret_cast<const char*>(buf), shift, shift + cu.k * kLvxPkg);
+  }
+}
+
 // LMC:178-193: frame header = own offset, next frame's offset (0 for the last), frame_id
 __global__ __launch_bounds__(kCodecBlock) void k_lvx_frames(const LvxArgs a, int64_t next_of_last_frame) {
   const int32_t f = blockIdx.x * kCodecBlock + threadIdx.x;

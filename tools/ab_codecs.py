@@ -87,12 +87,14 @@ def main():
                     a[name]()
                 a["ctx"].timing(False)
                 times[lib][name].append(a["ctx"].read_timing()["codec_ms"] / args.reps * 1e3)
-    # byte-identical outputs across arms (sampled: first and last 64 MB)
+    # byte-identical outputs across arms
     ref = arms[libs[0]]
     for lib in ([] if args.no_check else libs[1:]):
         a = arms[lib]
         for key, nbytes in (("lvx_out", ref["lvx_bytes"]), ("pcd_out", int(ref["bpos"][-1]))):
-            for lo in (0, max(0, nbytes - (64 << 20))):
+            # LVX in full, PCD text: first and last 64 MB
+            los = range(0, nbytes, 64 << 20) if key == "lvx_out" else (0, max(0, nbytes - (64 << 20)))
+            for lo in los:
                 n = min(64 << 20, nbytes - lo)
                 x = np.empty(n, np.uint8)
                 y = np.empty(n, np.uint8)
