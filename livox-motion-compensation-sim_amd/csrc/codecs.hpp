@@ -55,9 +55,20 @@ struct CodecFrames {
   int64_t n_units;           // unit_off[F]
 };
 
-// frame owning unit u: last f with unit_off[f] <= u (frames without units are skipped over)
-__device__ __forceinline__ int32_t codec_frame_of(const int64_t* __restrict__ unit_off, int32_t F, int64_t u) {
-  int32_t lo = 0, hi = F + 1;
+// frame owning unit u: last f with unit_off[f] <= u (frames without units are skipped over).
+// MC_CODEC_GUESS: first the interpolation guess u * F / n_units with its two bounds (one round of
+// loads when the frames are of similar size), the binary search (~log2 F dependent loads) otherwise.
+#ifndef MC_CODEC_GUESS
+#define MC_CODEC_GUESS 1
+#endif
+__device__ __forceinline__ int32_t codec_frame_of(const CodecFrames& s, int64_t u) {
+  const int64_t* __restrict__ unit_off = s.unit_off;
+  if (MC_CODEC_GUESS && s.n_units > 0) {
+    int64_t g = u * s.F / s.n_units;   // u < 2^31 and F < 2^31: no overflow
+    g = g < s.F - 1 ? g : s.F - 1;
+    if (unit_off[g] <= u && u < unit_off[g + 1]) return (int32_t)g;
+  }
+  int32_t lo = 0, hi = s.F + 1;
   while (lo < hi) {
     const int32_t mid = (lo + hi) >> 1;
     if (unit_off[mid] <= u) lo = mid + 1; else hi = mid;
@@ -133,7 +144,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
   const int64_t u = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x);   // grid = units exactly
-  const int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u);
+  const int32_t f = codec_frame_of(a.src, u);
   const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
   const int64_t frow = a.src.doff[f];
   const int64_t fcount = a.src.doff[f + 1] - frow;
@@ -221,7 +232,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages_cols(const LvxArgs
   __shared__ uint4 s_buf[2][kLvxLds / 16 + 1];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kLvxUnitsPerWG;
   const int64_t u_end = u0 + kLvxUnitsPerWG < a.src.n_units ? u0 + kLvxUnitsPerWG : a.src.n_units;
-  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  int32_t f = codec_frame_of(a.src, u0);
   LvxUnit nu = lvx_unit(a, f, u0);
   float nv[kLvxSlots][4];
   auto fetch = [&]() {
@@ -805,6 +816,9 @@ __device__ __forceinline__ void pcd_emit_swar(const PcdFast& P, uint32_t* base, 
 #ifndef MC_PCD_PREFETCH
 #define MC_PCD_PREFETCH 1    // float32 source: each tile's values, flag and offset loaded one tile ahead
 #endif
+#ifndef MC_PCD_MEASURE_WAVE
+#define MC_PCD_MEASURE_WAVE 0   // float32-source measure: one wave per tile (float4 loads, no barrier)
+#endif
 
 // digit fields of N = round(|v| 10^6) < 2^32: nd integer digits; D = 4 integer digits with leading
 // zeros (byte 0 = thousands); A = ". d1 d2 d3"; B = "d4 d5 d6 sep" (bytes in text order)
@@ -897,11 +911,77 @@ __device__ __forceinline__ void codec_point_f32(const CodecFrames& s, int32_t f,
 }
 
 // F32: the source is a batch's float32 columns (the packed path then works in float32, above)
+// Float32 source, MC_PCD_MEASURE_WAVE: a tile's 256 lines are one block of the batch, so one wave
+// measures a whole tile — lane l takes lines 4l .. 4l + 3 from one float4 per column (16-byte
+// lanes instead of 4-byte ones) and a wave reduction replaces the block scan: no LDS, no barrier.
+// A workgroup takes kPcdMeasureTiles tiles, each wave kPcdMeasureTiles / 4 of them, all of whose
+// loads are issued before the first is measured.
+#ifndef MC_PCD_MEASURE_TILES
+#define MC_PCD_MEASURE_TILES kPcdTilesPerWG
+#endif
+constexpr int kPcdMeasureTiles = MC_PCD_MEASURE_TILES;
+constexpr int kPcdMeasureWaveTiles = kPcdMeasureTiles / (kPcdBlock / 64);
+__device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) {
+  static_assert(kPcdBlock == kBlkPts, "a PCD tile is one batch block");
+  static_assert(kPcdMeasureTiles % (kPcdBlock / 64) == 0, "whole tiles per wave");
+  constexpr int NT = kPcdMeasureWaveTiles;
+  const int lane = threadIdx.x & 63;
+  int32_t f = codec_frame_of(a.src, u0);
+  int32_t fr[NT];
+  int64_t r0[NT], cnt[NT];
+  float4 V[NT][4];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int64_t u = u0 + (threadIdx.x >> 6) * NT + j;   // a wave's tiles are consecutive
+    cnt[j] = 0;
+    r0[j] = 0;
+    fr[j] = f;
+    if (u < a.src.n_units) {
+      f = codec_advance(a.src.unit_off, f, u);
+      fr[j] = f;
+      r0[j] = (u - a.src.unit_off[f]) * kPcdBlock + 4 * lane;   // frame-relative line of .x
+      cnt[j] = a.src.doff[f + 1] - a.src.doff[f];
+    }
+    const float* q = a.src.cols + bidx(a.src.C, 0, a.src.poff[f] + r0[j]);
+    if (r0[j] < cnt[j]) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) V[j][c] = *reinterpret_cast<const float4*>(q + c * kBlkPts);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int64_t u = u0 + (threadIdx.x >> 6) * NT + j;
+    if (u >= a.src.n_units) break;   // wave-uniform
+    int v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (r0[j] + i < cnt[j]) {
+        const float c[4] = {f4g(V[j][0], i), f4g(V[j][1], i), f4g(V[j][2], i), f4g(V[j][3], i)};
+        int l = pcd_fast_len_f32(c);
+        if (l < 0) {
+          PcdLine L;
+          pcd_line(a.src, fr[j], a.src.doff[fr[j]] + r0[j] + i, L, a.err);
+          l = L.len + (1 << 20);
+        }
+        v += l;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0)
+      a.tile_bytes[u] = (v & ((1 << 20) - 1)) | ((v >> 20) || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
+  }
+}
+
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
+  if constexpr (F32 && MC_PCD_MEASURE_WAVE) {
+    pcd_measure_waves(a, xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdMeasureTiles);
+    return;
+  }
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
-  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32 && MC_PCD_PREFETCH) {
     // as k_pcd_write: tile j + 1's values are loaded while tile j is measured
     const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
@@ -997,7 +1077,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
-  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32 && MC_PCD_PREFETCH && MC_PCD_BYTES) {
     // tile j + 1's loads are in flight while tile j is formatted and stored: one HBM round trip
     // per workgroup instead of one per tile
@@ -1064,7 +1144,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write_bytes(const PcdArgs a, 
   const int64_t u0 = list ? (int64_t)list[blockIdx.x]
                           : xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;
   const int per = list ? 1 : kPcdTilesPerWG;
-  int32_t f = codec_frame_of(a.src.unit_off, a.src.F, u0);
+  int32_t f = codec_frame_of(a.src, u0);
   for (int j = 0; j < per; ++j) {
     const int64_t u = u0 + j;
     if (u >= a.src.n_units) break;

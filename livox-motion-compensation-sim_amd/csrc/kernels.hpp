@@ -1146,16 +1146,6 @@ __device__ __forceinline__ void imu_rotate2_f32(const mcf2 th[3], mcf2& x, mcf2&
   x = x2; y = y3; z = z3;
 }
 
-__device__ __forceinline__ float& f4c(float4& v, int c) {
-  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
-}
-__device__ __forceinline__ float f4g(const float4& v, int c) {
-  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
-}
-__device__ __forceinline__ int i4c(const int4& v, int c) {
-  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
-}
-
 // window search: index of the window segment of frame-relative time t (bnd sorted, bnd[0] unused)
 __device__ __forceinline__ int win_index(const int64_t* bnd, int W, int64_t t) {
   if (W <= 4) {

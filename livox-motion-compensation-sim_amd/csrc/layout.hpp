@@ -25,6 +25,17 @@ __device__ __forceinline__ int64_t xcd_unit(int64_t b, int64_t n) {
   return x * per + (x < rem ? x : rem) + i;
 }
 
+// component c of a float4 / int4 (c a compile-time constant after unrolling)
+__device__ __forceinline__ float& f4c(float4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ float f4g(const float4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ int i4c(const int4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+
 // DPP quad exchange (quad_perm): lanes 4q .. 4q + 3 of a wave form a quad.
 template <int K>   // quad_perm [K, K, K, K]: lane K of each quad to all four
 __device__ __forceinline__ float quad_bcast(float v) {
