@@ -54,7 +54,12 @@ def setup(lib, counts, source="aos"):
         mc._lib.check(ctx.lib.mc_pcd_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), pcd_out.ptr, cap,
                                             ptr(bpos, c_int64)), "pcd_encode")
 
-    return {"ctx": ctx, "batch": b, "lvx": lvx, "pcd": pcd, "lvx_out": lvx_out, "pcd_out": pcd_out, "bpos": bpos,
+    flush_buf = ctx.batch(np.full(len(counts), int(counts.max()), np.int64), with_time=True)
+
+    def flush():
+        flush_buf.checksum()
+
+    return {"ctx": ctx, "batch": b, "lvx": lvx, "pcd": pcd, "flush": flush, "lvx_out": lvx_out, "pcd_out": pcd_out, "bpos": bpos,
             "lvx_bytes": int(pos[-1])}
 
 
@@ -65,6 +70,9 @@ def main():
     ap.add_argument("--points", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--flush", action="store_true",
+                    help="a checksum pass over a 2 GB scratch buffer before every timed call (the previous "
+                         "call's dirty lines are written back outside the timed kernels)")
     ap.add_argument("--no-check", action="store_true", help="skip the byte-identity check (diagnostic builds)")
     ap.add_argument("--source", default="aos", choices=["aos", "batch"],
                     help="encode from a device (N,4) float64 AoS array or from the batch's float32 columns")
@@ -84,6 +92,8 @@ def main():
                 a["ctx"].read_timing()
                 a["ctx"].timing(True)
                 for _ in range(args.reps):
+                    if args.flush:
+                        a["flush"]()
                     a[name]()
                 a["ctx"].timing(False)
                 times[lib][name].append(a["ctx"].read_timing()["codec_ms"] / args.reps * 1e3)
