@@ -283,6 +283,26 @@ def load_traffic(mode, frames, points):
     return e.get("hbm_bytes_per_launch"), src
 
 
+def spin_up(ctx, mode, b_in, b_out, ms, issue):
+    """Untimed: run the step itself for at least ``ms`` milliseconds before the warmup steps.  From
+    idle the device takes tens of milliseconds of sustained load to reach its steady memory
+    throughput — far longer than a few warmup steps (0.33 ms each): SLERP kernel 80.4-81.2 % of
+    peak after 5 warmup steps, 84.1 % after 50, 84.6-84.8 % after 300, same box and buffers
+    (profiles/round2/s51).  Returns the milliseconds spent."""
+    if ms <= 0:
+        return 0.0
+    ctx.timing(False)
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        if issue == "pipeline":
+            ctx.deskew_steps(b_in, b_out, 25, mode=mode, sample_every=0, pipeline=True)
+        else:
+            for _ in range(25):
+                ctx.deskew(b_in, b_out, mode=mode)
+        ctx.sync()
+    return (time.perf_counter() - t0) * 1e3
+
+
 def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipeline"):
     """Timed region: wall clock around ``steps`` steps.  ``live``: HIP events on the sampled steps'
     kernels themselves (hipExtLaunchKernel start/stop events: the dispatch's own timestamps, no
@@ -515,6 +535,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--spinup-ms", type=float, default=250.0,
+                    help="untimed: run each mode's step for this long before its warmup steps (0: off)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", default="pose_slerp", choices=list(BYTES_PER_POINT))
     ap.add_argument("--config", default="auto", choices=["auto", "1", "2", "3", "4", "5"],
@@ -580,6 +602,9 @@ def main():
     every = 10
     for mode in modes:
         steps = args.steps if mode == args.mode else max(10, args.steps // 4)
+        spun = spin_up(ctx, mode, src_of[mode], b_out, args.spinup_ms, args.issue)
+        if mode == args.mode:
+            spinup_ms = spun
         wall, tm, ev = run_mode(ctx, rdv, mode, src_of[mode], b_out, steps, args.warmup,
                                 live=not args.events_after, issue=args.issue)
         if mode == args.mode:
@@ -637,6 +662,9 @@ def main():
             "n_gpus": n_devices,
             "steps": r["steps"],
             "warmup": args.warmup,
+            "spinup": {"ms": round(spinup_ms, 1), "what": "untimed, before the warmup steps: the same step "
+                       "repeated until the device reaches its sustained memory throughput (tens of ms from "
+                       "idle; 5 warmup steps are 1.7 ms) — profiles/round2/s51"},
             "ms_per_step": r["wall_s"] / r["steps"] * 1e3,
             "higher_is_better": True,
             "scaling": scaling if not shared else f"{scaling} (NOT a scaling result: {world} ranks share "
