@@ -16,6 +16,7 @@
 namespace mc {
 struct Tile;
 struct PoseSeg;
+struct FrameRow;
 struct ImuSeg;
 struct FrameWin;
 }  // namespace mc
@@ -177,7 +178,7 @@ struct mc_batch {
   double* d_frame_time = nullptr;
   int64_t* d_frame_start = nullptr;
   // k_prep outputs, double-buffered (ctx->buf selects the half): F entries per half
-  float4* d_frame_tbl = nullptr;   // 3 float4 per frame (R row, t)
+  mc::FrameRow* d_frame_tbl = nullptr;   // 3 float64 rows per frame (R row, t)
   int2* d_trange = nullptr;        // per-frame [min, max] t_ns (valid when trange_valid)
   mc::FrameWin* d_fwin = nullptr;  // per-frame segment window
   void* d_frec = nullptr;          // 2 frame-specialised pose/IMU records per frame

@@ -52,14 +52,8 @@ namespace mc {
 #ifndef MC_NT_LOAD
 #define MC_NT_LOAD 1         // non-temporal input loads (streamed once): +5-8% measured (tools/ab.py)
 #endif
-#ifndef MC_IMU_PK
-#define MC_IMU_PK 0          // 1: IMU f32 path on float2 pairs (-3 % instructions; rejected: 327.1 vs 325.6 us)
-#endif
-#ifndef MC_EARLY_LOADS
-#define MC_EARLY_LOADS 0     // 1: point loads before the window records (rejected: SLERP 322 -> 338 us, IMU -0.3 %)
-#endif
 #ifndef MC_POINTS_WAVES
-#define MC_POINTS_WAVES 0    // min waves/SIMD requested for the per-point kernels (0: compiler's choice)
+#define MC_POINTS_WAVES 4    // min waves/SIMD requested for the per-point kernels (0: compiler's choice)
 #endif
 
 constexpr int kBlock = 256;                    // 4 waves of 64
@@ -80,22 +74,31 @@ struct Tile {
   int32_t ngroups;  // float4 groups in this tile (<= kTileGroups)
 };
 
-// One segment [k, k+1] of the pose table (trajectory), built per step by k_prep.
-struct PoseSeg {
-  float4 q0;     // unit quaternion (x,y,z,w) of orientation_imu[k]
-  float4 q1;     // of orientation_imu[k+1], sign-flipped onto q0's hemisphere (shortest arc)
-  float4 p0c;    // position[k].xyz, cos(Theta)
-  float4 dpt;    // position[k+1]-position[k], Theta = acos(q0.q1)
-  float4 misc;   // 1/sin(Theta), small-angle flag (1: LERP), 0, 0
-  double t0;     // time[k]
-  double inv_dt; // 1/(time[k+1]-time[k]), 0 for a degenerate segment
+// Frame mode pose, one row of [R | t] (LMC:774-775) in float64: the kernels do p' = R p + t in
+// float64 on the float32 points and round once on the store, so every output coordinate is the
+// reference's float64 value rounded to float32 (<= 2^-24 relative per coordinate, north_star's
+// 1e-5 with no scale floor).  3 rows per frame.
+struct FrameRow {
+  double x, y, z, w;   // R[i][0..2], t_i
 };
 
-// PoseSeg specialised to one frame: alpha = clamp(t_ns * scale + off, 0, 1).
-struct PoseWin {
-  float4 q0, q1, p0c, dpt;
-  float inv_sin, small, off, scale;
+// One segment [k, k+1] of the pose table (trajectory), built per step by k_prep, float64.  The
+// SLERP at alpha is written q(alpha) = cos(alpha th) q0 + alpha sinc(alpha th) v with
+// v = th (q1 - cos(th) q0) / sin(th): no division, no small-angle branch, and cos / sinc are even
+// polynomials in (alpha th)^2 on th <= pi/2 (slerp_point).
+struct PoseSeg {
+  double q0[4];   // unit quaternion (x,y,z,w) of orientation_imu[k]
+  double v[4];    // th * q_perp, q1 sign-flipped onto q0's hemisphere first (shortest arc)
+  double p0[3];   // position[k]
+  double dp[3];   // position[k+1] - position[k]
+  double th;      // Theta, the angle between q0 and q1 (<= pi/2)
+  double t0;      // time[k]
+  double inv_dt;  // 1/(time[k+1]-time[k]), 0 for a degenerate segment
+  double tf;      // PoseWin: the frame's time (alpha from t_frame + t_ns*1e-9 as the reference forms t)
 };
+
+// PoseSeg specialised to one frame (tf set): alpha = clamp(((tf + t_ns*1e-9) - t0) * inv_dt, 0, 1).
+typedef PoseSeg PoseWin;
 
 // One IMU record k (CSIM:1482-1516 semantics): gyro(t) = g + alpha*dg,
 // alpha = max(0, (t - ts) * inv_dt); the last record has dg = 0, inv_dt = 0.
@@ -123,7 +126,7 @@ struct DeskewArgs {
   const Tile* tiles;
   int32_t n_tiles;
   int32_t xcd_order;       // SLERP: sub-tiles in XCD-contiguous order (large batches; see mc_deskew's plan)
-  const float4* frame_tbl; // frame mode: 3 float4 per frame (R row i, t_i)
+  const FrameRow* frame_tbl; // frame mode: 3 rows per frame (R row i, t_i), float64
   const double* frame_time;
   const int64_t* frame_start;
   const FrameWin* fwin;    // per-point modes
@@ -334,27 +337,41 @@ __device__ __forceinline__ PoseSample load_pose(const double* time, const double
   return s;
 }
 
-// segment [a, b] of the pose table: shortest-arc quaternion pair, Theta, position delta
+// segment [a, b] of the pose table: shortest-arc quaternion pair, Theta, position delta.
+// Theta = 2 atan2(|q1 - q0|, |q1 + q0|) is accurate at every angle (acos(q0.q1) loses half the
+// digits below ~1e-4), and q1 - cos(Theta) q0 then has norm sin(Theta) to rounding.
 __device__ __forceinline__ PoseSeg pose_seg_of(const PoseSample& a, const PoseSample& b) {
   double q0[4], q1[4];
   euler_xyz_quat(a.r[0], a.r[1], a.r[2], q0);
   euler_xyz_quat(b.r[0], b.r[1], b.r[2], q1);
-  double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
-  if (d < 0.0) { d = -d; q1[0] = -q1[0]; q1[1] = -q1[1]; q1[2] = -q1[2]; q1[3] = -q1[3]; }
-  if (d > 1.0) d = 1.0;
-  const double th = acos(d);
-  const bool small = th < 1e-6;
-  // sin(acos(d)) from the same d (no second transcendental on the prep's serial chain)
-  const double inv_sin = small ? 0.0 : 1.0 / sqrt((1.0 - d) * (1.0 + d));
+  const double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
+  if (d < 0.0) { q1[0] = -q1[0]; q1[1] = -q1[1]; q1[2] = -q1[2]; q1[3] = -q1[3]; }
+  double dm = 0.0, dpl = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dm = fma(q1[i] - q0[i], q1[i] - q0[i], dm);
+    dpl = fma(q1[i] + q0[i], q1[i] + q0[i], dpl);
+  }
+  const double th = 2.0 * atan2(sqrt(dm), sqrt(dpl));
+  double sn, cs;
+  sincos_prep(th, &sn, &cs);
+  const double ratio = th > 0.0 ? th / sn : 1.0;   // th / sin(th), 1 at th = 0
   PoseSeg s;
-  s.q0 = make_float4((float)q0[0], (float)q0[1], (float)q0[2], (float)q0[3]);
-  s.q1 = make_float4((float)q1[0], (float)q1[1], (float)q1[2], (float)q1[3]);
-  s.p0c = make_float4((float)a.p[0], (float)a.p[1], (float)a.p[2], (float)d);
-  s.dpt = make_float4((float)(b.p[0] - a.p[0]), (float)(b.p[1] - a.p[1]), (float)(b.p[2] - a.p[2]), (float)th);
-  s.misc = make_float4((float)inv_sin, small ? 1.f : 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s.q0[i] = q0[i];
+    s.v[i] = ratio * fma(-cs, q0[i], q1[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    s.p0[i] = a.p[i];
+    s.dp[i] = b.p[i] - a.p[i];
+  }
+  s.th = th;
   s.t0 = a.t;
   const double dt = b.t - a.t;
   s.inv_dt = dt > 0.0 ? 1.0 / dt : 0.0;
+  s.tf = 0.0;
   return s;
 }
 
@@ -401,13 +418,8 @@ __device__ __forceinline__ ImuSeg make_imu_seg(const int64_t* ts, const double* 
 }
 
 __device__ __forceinline__ PoseWin make_pose_win(const PoseSeg& s, double tf) {
-  PoseWin w;
-  w.q0 = s.q0; w.q1 = s.q1; w.p0c = s.p0c; w.dpt = s.dpt;
-  w.inv_sin = s.misc.x;
-  w.small = s.misc.y;
-  // alpha = (tf + t_ns*1e-9 - t0) * inv_dt = t_ns * (1e-9*inv_dt) + (tf - t0)*inv_dt
-  w.off = (float)((tf - s.t0) * s.inv_dt);
-  w.scale = (float)(1e-9 * s.inv_dt);
+  PoseWin w = s;
+  w.tf = tf;
   return w;
 }
 
@@ -429,7 +441,7 @@ struct PrepArgs {
   const double* time; const double* pos; const double* rpy; int64_t T;   // trajectory
   const int64_t* imu_ts; const double* gyro; int64_t M;                  // IMU
   const double* frame_time; const int64_t* frame_start; const int2* trange;  // frames
-  float4* frame_tbl; PoseSeg* pose_seg; ImuSeg* imu_seg;                 // outputs
+  FrameRow* frame_tbl; PoseSeg* pose_seg; ImuSeg* imu_seg;               // outputs
   FrameWin* fwin; void* frec;
   int64_t nseg;
   // per sub-tile windows for frames whose window is wider than MC_FASTPATH_MAXW
@@ -595,8 +607,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
       double R[9];
       euler_xyz_matrix_prep(ps.r[0], ps.r[1], ps.r[2], R);
       const double t = lane == 0 ? ps.p[0] : (lane == 1 ? ps.p[1] : ps.p[2]);   // no dynamic index (no alloca)
-      a.frame_tbl[3 * f + lane] = make_float4((float)R[3 * lane], (float)R[3 * lane + 1], (float)R[3 * lane + 2],
-                                              (float)t);
+      a.frame_tbl[3 * f + lane] = FrameRow{R[3 * lane], R[3 * lane + 1], R[3 * lane + 2], t};
     }
     return;
   }
@@ -752,13 +763,21 @@ __global__ __launch_bounds__(kBlock) void k_prep(const PrepArgs a) {
 // ---------------------------------------------------------------------------------------------
 // kW: homogeneous input whose 4th column is w (CSIM:226-229 applies T to (N,4) points as they are),
 // p' = A p + b w; otherwise p' = A p + b with the 4th column passed through.
+// row r of [R | t] applied to (x, y, z) in float64 (3 FMAs), rounded once to float32; with kW the
+// translation is scaled by the homogeneous coordinate w (CSIM:226-229)
+template <bool kW = false>
+__device__ __forceinline__ float xf_row(const FrameRow& r, float x, float y, float z, float w = 1.f) {
+  const double t = kW ? r.w * (double)w : r.w;
+  return (float)fma(r.x, (double)x, fma(r.y, (double)y, fma(r.z, (double)z, t)));
+}
+
 template <bool kW>
 __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
-    const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
-    const float4 r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
-    const float4 r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
+    const FrameRow r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
+    const FrameRow r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
+    const FrameRow r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
     // group g of the tile: block pstart/256 + g/64, offset 4 (g % 64) inside it
     const float* ix = a.in + bidx((int)a.in_C, 0, tl.pstart);
     float* ox = a.out + bidx((int)a.out_C, 0, tl.pstart);
@@ -780,14 +799,12 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
       if (g < tl.ngroups) {
         float4 X = vx[it], Y = vy[it], Z = vz[it], W = vi[it];
         float4 ox4, oy4, oz4;
-#define MC_T(r, c) (kW ? r.w * W.c : r.w)
-#define MC_XF(c)                                                              \
-  ox4.c = fmaf(r0.x, X.c, fmaf(r0.y, Y.c, fmaf(r0.z, Z.c, MC_T(r0, c))));     \
-  oy4.c = fmaf(r1.x, X.c, fmaf(r1.y, Y.c, fmaf(r1.z, Z.c, MC_T(r1, c))));     \
-  oz4.c = fmaf(r2.x, X.c, fmaf(r2.y, Y.c, fmaf(r2.z, Z.c, MC_T(r2, c))));
+#define MC_XF(c)                                                  \
+  ox4.c = xf_row<kW>(r0, X.c, Y.c, Z.c, W.c);                     \
+  oy4.c = xf_row<kW>(r1, X.c, Y.c, Z.c, W.c);                     \
+  oz4.c = xf_row<kW>(r2, X.c, Y.c, Z.c, W.c);
         MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
 #undef MC_XF
-#undef MC_T
         float* o = ox + (int64_t)(g >> 6) * a.out_C * kBlkPts + 4 * (g & 63);
         st_frame(o, ox4);
         st_frame(o + kBlkPts, oy4);
@@ -811,17 +828,17 @@ __device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a, const uint
     const Tile tl = ldu(a.tiles + st / kSub);
     const int g = (int)(st % kSub) * kBlock + threadIdx.x;
     if (g >= tl.ngroups) continue;
-    const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
-    const float4 r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
-    const float4 r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
+    const FrameRow r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
+    const FrameRow r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
+    const FrameRow r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
     const int64_t p = tl.pstart + 4 * (int64_t)g;
     const float* q = a.in + bidx((int)a.in_C, 0, p);
     const float4 X = ld4(q), Y = ld4(q + kBlkPts), Z = ld4(q + 2 * kBlkPts), I = ld4(q + 3 * kBlkPts);
     float4 ox4, oy4, oz4;
 #define MC_XF(c)                                                  \
-  ox4.c = fmaf(r0.x, X.c, fmaf(r0.y, Y.c, fmaf(r0.z, Z.c, r0.w))); \
-  oy4.c = fmaf(r1.x, X.c, fmaf(r1.y, Y.c, fmaf(r1.z, Z.c, r1.w))); \
-  oz4.c = fmaf(r2.x, X.c, fmaf(r2.y, Y.c, fmaf(r2.z, Z.c, r2.w)));
+  ox4.c = xf_row(r0, X.c, Y.c, Z.c);                              \
+  oy4.c = xf_row(r1, X.c, Y.c, Z.c);                              \
+  oz4.c = xf_row(r2, X.c, Y.c, Z.c);
     MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
 #undef MC_XF
     float* o = a.out + bidx((int)a.out_C, 0, p);
@@ -836,7 +853,7 @@ __device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a, const uint
 // lane ONE column of one group (lane & 3 = x, y, z, intensity): one 16-byte load and one 16-byte
 // store per lane, four times the lanes of deskew_frame_sub.  The quad's x / y / z float4s reach
 // every lane of the quad through DPP quad broadcasts (no LDS), lane c < 3 forms output column c of
-// the four points (R row c . p + t_c, the same fmaf chain as deskew_frame_sub), lane 3 passes the
+// the four points (R row c . p + t_c in float64, xf_row), lane 3 passes the
 // intensities through.  A bare 16 B-in / 16 B-out stream runs at 6.61-6.68 TB/s with one load and
 // one store per lane vs 6.12 with four of each (tools/stage_probe.hip, profiles/round2/s07).
 #ifndef MC_FRAME_QUAD
@@ -854,12 +871,13 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
     const Tile tl = ldu(a.tiles + st / kSub);
     const int g0 = (int)(st % kSub) * kBlock + (int)(un % (kBlock / kQuadGroups)) * kQuadGroups;
     if (g0 >= tl.ngroups) continue;   // uniform: empty quarter of a short sub-tile
-    const float4 r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
-    const float4 r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
-    const float4 r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
     const int g = g0 + (threadIdx.x >> 2);
     const bool act = g < tl.ngroups;   // uniform over a quad
     const int64_t p = tl.pstart + 4 * (int64_t)g;
+    // lane c's row of [R | t] (lane 3: row 2, unused) as a vector load beside the point load: the
+    // 96-byte table row set is L2-resident, and a per-lane select of three SGPR rows would cost 32
+    // VALU instructions (two SGPR sources cannot meet in one v_cndmask)
+    const FrameRow r = *(a.frame_tbl + 3 * tl.frame + (c < 2 ? c : 2));
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (act) v = ld4(a.in + bidx((int)a.in_C, c, p));
     // every lane takes part in the broadcasts (inactive quads carry zeros)
@@ -867,12 +885,11 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
     X.x = quad_bcast<0>(v.x); X.y = quad_bcast<0>(v.y); X.z = quad_bcast<0>(v.z); X.w = quad_bcast<0>(v.w);
     Y.x = quad_bcast<1>(v.x); Y.y = quad_bcast<1>(v.y); Y.z = quad_bcast<1>(v.z); Y.w = quad_bcast<1>(v.w);
     Z.x = quad_bcast<2>(v.x); Z.y = quad_bcast<2>(v.y); Z.z = quad_bcast<2>(v.z); Z.w = quad_bcast<2>(v.w);
-    const float4 r = c == 0 ? r0 : (c == 1 ? r1 : r2);
     float4 o;
-    o.x = fmaf(r.x, X.x, fmaf(r.y, Y.x, fmaf(r.z, Z.x, r.w)));
-    o.y = fmaf(r.x, X.y, fmaf(r.y, Y.y, fmaf(r.z, Z.y, r.w)));
-    o.z = fmaf(r.x, X.z, fmaf(r.y, Y.z, fmaf(r.z, Z.z, r.w)));
-    o.w = fmaf(r.x, X.w, fmaf(r.y, Y.w, fmaf(r.z, Z.w, r.w)));
+    o.x = xf_row(r, X.x, Y.x, Z.x);
+    o.y = xf_row(r, X.y, Y.y, Z.y);
+    o.z = xf_row(r, X.z, Y.z, Z.z);
+    o.w = xf_row(r, X.w, Y.w, Z.w);
     if (act) st_frame(a.out + bidx((int)a.out_C, c, p), c == 3 ? v : o);
   }
 }
@@ -965,185 +982,159 @@ __global__ __launch_bounds__(kBlock) void k_transform_host_f64(const double* __r
 __global__ __launch_bounds__(kBlock) void k_affine_w(const DeskewArgs a) { deskew_frame_body<true>(a); }
 
 // ---------------------------------------------------------------------------------------------
-// bounded-argument sin/cos.  ocml's sincosf carries a Payne-Hanek branch for huge arguments that
-// costs ~40 VGPRs per inlined copy; every angle here is first reduced to [-pi/4, pi/4] plus a
-// quadrant (in f64 for the IMU angles, Cody-Waite in f32 for the SLERP angle alpha*Theta, which is
-// bounded by pi/2), then evaluated with the minimax polynomials of Cephes sinf/cosf (<= 2 ulp).
+// float64 per-point math.  Every per-point quantity (alpha, the interpolated quaternion / gyro, the
+// angles, their sin / cos, the rotation, the translation) is formed in float64 from the float32
+// point and the float64 tables, and each output coordinate is rounded once to float32 on the store:
+// the result is the reference's float64 value to <= 2^-24 relative per coordinate (north_star:
+// <= 1e-5 relative per coordinate, no scale floor).  FP64 FMA issues at the FP32 rate on CDNA4
+// (16 lanes / SIMD / clock), so the cost is the operation count, kept low by polynomial tiers:
+// cos(x) and sin(x)/x are even Taylor polynomials in z = x^2 whose length is picked per wave from
+// a bound on |x| (truncation < 2e-17 relative in every tier):
+//   tier 0  |x| <= 1/16   cos, sinc to z^4          (4 + 4 FMAs)
+//   tier 1  |x| <= 1/4    cos, sinc to z^6          (6 + 6)
+//   tier 2  |x| <= 1.6    cos, sinc to z^10         (10 + 10; SLERP's alpha*Theta <= Theta <= pi/2)
+//   tier 3  any angle     Cody-Waite reduction + fdlibm kernels (sincos_prep; IMU gyro spikes)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void sincos_quadrant(float r, int q, float& s, float& c) {
-  const float z = r * r;
-  float ps = fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
-  ps = fmaf(z, ps, -1.6666654611e-1f);
-  const float sr = fmaf(z * r, ps, r);
-  float pc = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
-  pc = fmaf(z, pc, 4.166664568298827e-2f);
-  const float cr = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
-  // quadrant q: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s)
-  const bool swap = (q & 1) != 0;
-  const float s0 = swap ? cr : sr;
-  const float c0 = swap ? sr : cr;
-  s = (q & 2) ? -s0 : s0;
-  c = ((q + 1) & 2) ? -c0 : c0;
-}
-// any double angle (IMU: theta = w*dt can reach tens of rad at yaw-wrap gyro spikes)
-__device__ __forceinline__ void sincos_f64arg(double x, float& s, float& c) {
-  const double k = rint(x * 0.63661977236758134);          // 2/pi
-  const float r = (float)fma(-k, 1.5707963267948966, x);    // |r| <= pi/4 (+ulps)
-  sincos_quadrant(r, (int)(int64_t)k, s, c);
-}
-// f32 angle of moderate size (|x| < 1e4): three-term Cody-Waite pi/2 reduction
-__device__ __forceinline__ void sincos_f32arg(float x, float& s, float& c) {
-  const float k = rintf(x * 0.636619772f);
-  float r = fmaf(-k, 1.5703125f, x);
-  r = fmaf(-k, 4.837512969970703125e-4f, r);
-  r = fmaf(-k, 7.54978995489188216e-8f, r);
-  sincos_quadrant(r, (int)k, s, c);
-}
+constexpr double kTier0 = 0.0625, kTier1 = 0.25, kTier2 = 1.6;
 
-// ---------------------------------------------------------------------------------------------
-// per-point compute bodies
-// ---------------------------------------------------------------------------------------------
-// quaternion SLERP + position LERP at alpha, then p' = R(q) p + pos  
-__device__ __forceinline__ void slerp_point(const PoseWin& w, int t, float& x, float& y, float& z) {
-  float al = fmaf((float)t, w.scale, w.off);
-  al = fminf(fmaxf(al, 0.f), 1.f);
-  float s0, s1;
-  if (w.small != 0.f) {
-    s1 = al; s0 = 1.f - al;
-  } else {
-    float sa, ca;
-    sincos_f32arg(al * w.dpt.w, sa, ca);
-    s1 = sa * w.inv_sin;
-    s0 = fmaf(-w.p0c.w, s1, ca);
-  }
-  const float qx = fmaf(s0, w.q0.x, s1 * w.q1.x);
-  const float qy = fmaf(s0, w.q0.y, s1 * w.q1.y);
-  const float qz = fmaf(s0, w.q0.z, s1 * w.q1.z);
-  const float qw = fmaf(s0, w.q0.w, s1 * w.q1.w);
-  // v' = v + qw*t + u x t,  t = 2 u x v
-  const float tx = 2.f * fmaf(qy, z, -qz * y);
-  const float ty = 2.f * fmaf(qz, x, -qx * z);
-  const float tz = 2.f * fmaf(qx, y, -qy * x);
-  const float rx = x + fmaf(qw, tx, fmaf(qy, tz, -qz * ty));
-  const float ry = y + fmaf(qw, ty, fmaf(qz, tx, -qx * tz));
-  const float rz = z + fmaf(qw, tz, fmaf(qx, ty, -qy * tx));
-  x = rx + fmaf(al, w.dpt.x, w.p0c.x);
-  y = ry + fmaf(al, w.dpt.y, w.p0c.y);
-  z = rz + fmaf(al, w.dpt.z, w.p0c.z);
-}
-
-// Path B body (CSIM:1447-1465): w = g + alpha*dg (alpha from the bracketing IMU samples),
-// theta = w * dt, p' = Rx(-theta_x) Ry(-theta_y) Rz(-theta_z) p.  The angle is formed in f64
-// (gyro spikes at yaw wraps reach ~1e2-1e3 rad/s) and range-reduced before the f32 polynomials.
-__device__ __forceinline__ void imu_point(const ImuSeg& w, int t, float& x, float& y, float& z) {
-  double al = (double)((int64_t)t - w.ts) * w.inv_dt;
-  al = al > 0.0 ? al : 0.0;
-  const double dt = (double)t * 1e-9;
-  float sa, ca, sb, cb, sc, cc;
-  sincos_f64arg(fma(al, w.dg[0], w.g[0]) * dt, sa, ca);
-  sincos_f64arg(fma(al, w.dg[1], w.g[1]) * dt, sb, cb);
-  sincos_f64arg(fma(al, w.dg[2], w.g[2]) * dt, sc, cc);
-  // Rz(-c)
-  const float x1 = fmaf(cc, x, sc * y);
-  const float y1 = fmaf(-sc, x, cc * y);
-  // Ry(-b)
-  const float x2 = fmaf(cb, x1, -sb * z);
-  const float z2 = fmaf(sb, x1, cb * z);
-  // Rx(-a)
-  const float y3 = fmaf(ca, y1, sa * z2);
-  const float z3 = fmaf(-sa, y1, ca * z2);
-  x = x2; y = y3; z = z3;
-}
-
-// Path B with small angles in float32.  A wave whose points all have |theta| <= 0.78 (pi/4 less a
-// margin) in every axis — every frame outside yaw-wrap gyro spikes — skips the f64 angle and the
-// range reduction: alpha, w and theta in f32 (relative error ~2e-7, i.e. <= 1.6e-7 rad here, far
-// inside the 1e-5 parity bar) and the sin/cos polynomials straight on theta.  Other waves keep
-// imu_point.
-#ifndef MC_IMU_F32
-#define MC_IMU_F32 1
-#endif
-#ifndef MC_IMU_DIAG
-#define MC_IMU_DIAG 0        // diagnostic timing build: 1 = no per-point angle vote (assumes small angles)
-#endif
-struct ImuF {
-  float g[3], dg[3], inv_dt;
-  int32_t ts;
-  bool ok;   // ts fits the int32 difference below
+// Taylor coefficients of cos and sin(x)/x after the leading 1: c[k] of z^(k+1).  They live in
+// constant memory and each tier's set is brought into SGPRs by one scalar load per wave where the
+// tier is used (poly_load): as immediates the compiler would hoist all ~20 double constants out of
+// the sub-tile loop into SGPR pairs and spill them (or keep them in VGPRs behind v_mov copies); as
+// SGPR operands every Horner step is one v_fma_f64.  (Not `const`: the compiler would fold the
+// initialiser back into immediates.)
+template <int K>
+struct Poly {
+  double c[K];   // cos:  1 + sum c[k] z^(k+1)
+  double s[K];   // sinc: 1 + sum s[k] z^(k+1)
 };
-__device__ __forceinline__ ImuF imu_f32(const ImuSeg& w) {
-  ImuF r;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) { r.g[c] = (float)w.g[c]; r.dg[c] = (float)w.dg[c]; }
-  r.inv_dt = (float)w.inv_dt;
-  r.ok = w.ts >= -(int64_t(1) << 30) && w.ts <= (int64_t(1) << 30);
-  r.ts = (int32_t)w.ts;
-  return r;
+struct NoPoly {};
+#define MC_COS_C -1.0 / 2, 1.0 / 24, -1.0 / 720, 1.0 / 40320, -1.0 / 3628800, 1.0 / 479001600, \
+    -1.0 / 87178291200.0, 1.0 / 20922789888000.0, -1.0 / 6402373705728000.0, 1.0 / 2432902008176640000.0
+#define MC_SINC_C -1.0 / 6, 1.0 / 120, -1.0 / 5040, 1.0 / 362880, -1.0 / 39916800, 1.0 / 6227020800.0, \
+    -1.0 / 1307674368000.0, 1.0 / 355687428096000.0, -1.0 / 121645100408832000.0, 1.0 / 51090942171709440000.0
+__constant__ Poly<4> kPoly4 = {{-1.0 / 2, 1.0 / 24, -1.0 / 720, 1.0 / 40320},
+                                     {-1.0 / 6, 1.0 / 120, -1.0 / 5040, 1.0 / 362880}};
+__constant__ Poly<6> kPoly6 = {{-1.0 / 2, 1.0 / 24, -1.0 / 720, 1.0 / 40320, -1.0 / 3628800, 1.0 / 479001600},
+                                     {-1.0 / 6, 1.0 / 120, -1.0 / 5040, 1.0 / 362880, -1.0 / 39916800,
+                                      1.0 / 6227020800.0}};
+__constant__ Poly<10> kPoly10 = {{MC_COS_C}, {MC_SINC_C}};
+#undef MC_COS_C
+#undef MC_SINC_C
+
+template <int TIER>
+using PolyOf = typename std::conditional<TIER == 0, Poly<4>,
+               typename std::conditional<TIER == 1, Poly<6>,
+               typename std::conditional<TIER == 2, Poly<10>, NoPoly>::type>::type>::type;
+
+// an SGPR zero the compiler cannot see through: the coefficient load below stays where the tier
+// is used instead of being hoisted out of the loop
+__device__ __forceinline__ int opaque_zero() {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
 }
-constexpr float kImuF32MaxAngle = 0.78f;
-// theta (3 axes) of frame-relative time t (|t| < 2^30 ns); returns whether all are small
-__device__ __forceinline__ bool imu_angles_f32(const ImuF& w, int t, float th[3]) {
-  const float al = fmaxf((float)(t - w.ts) * w.inv_dt, 0.f);
-  const float dt = (float)t * 1e-9f;
-  bool ok = w.ok && t > -(1 << 30) && t < (1 << 30);
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    th[c] = fmaf(al, w.dg[c], w.g[c]) * dt;
-    ok = ok && fabsf(th[c]) <= kImuF32MaxAngle;
-  }
-  return ok;
-}
-__device__ __forceinline__ void imu_rotate_f32(const float th[3], float& x, float& y, float& z) {
-  float sa, ca, sb, cb, sc, cc;
-  sincos_quadrant(th[0], 0, sa, ca);
-  sincos_quadrant(th[1], 0, sb, cb);
-  sincos_quadrant(th[2], 0, sc, cc);
-  const float x1 = fmaf(cc, x, sc * y);
-  const float y1 = fmaf(-sc, x, cc * y);
-  const float x2 = fmaf(cb, x1, -sb * z);
-  const float z2 = fmaf(sb, x1, cb * z);
-  const float y3 = fmaf(ca, y1, sa * z2);
-  const float z3 = fmaf(-sa, y1, ca * z2);
-  x = x2; y = y3; z = z3;
+template <int TIER>
+__device__ __forceinline__ PolyOf<TIER> poly_load() {
+  if constexpr (TIER == 0) return ldu(&kPoly4 + opaque_zero());
+  else if constexpr (TIER == 1) return ldu(&kPoly6 + opaque_zero());
+  else if constexpr (TIER == 2) return ldu(&kPoly10 + opaque_zero());
+  else return NoPoly{};
 }
 
-// The same f32 small-angle path for two points at once: every operation of imu_angles_f32 /
-// sincos_quadrant(q = 0) / imu_rotate_f32 on a float2, in the same order (so the same bits), which
-// the compiler issues as packed v_pk_fma_f32 / v_pk_mul_f32 — half the VALU instructions.
-typedef float mcf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ mcf2 fma2(mcf2 a, mcf2 b, mcf2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ bool imu_angles2_f32(const ImuF wa, const ImuF wb, int ta, int tb, mcf2 th[3]) {
-  const mcf2 al = {fmaxf((float)(ta - wa.ts) * wa.inv_dt, 0.f), fmaxf((float)(tb - wb.ts) * wb.inv_dt, 0.f)};
-  const mcf2 dt = mcf2{(float)ta, (float)tb} * 1e-9f;
-  bool ok = wa.ok && wb.ok && ta > -(1 << 30) && ta < (1 << 30) && tb > -(1 << 30) && tb < (1 << 30);
+template <int K>
+__device__ __forceinline__ double horner1(const double (&c)[K], double z) {   // 1 + sum c[k] z^(k+1)
+  double p = c[K - 1];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    th[c] = fma2(al, mcf2{wa.dg[c], wb.dg[c]}, mcf2{wa.g[c], wb.g[c]}) * dt;
-    ok = ok && fabsf(th[c].x) <= kImuF32MaxAngle && fabsf(th[c].y) <= kImuF32MaxAngle;
+  for (int k = K - 2; k >= 0; --k) p = fma(z, p, c[k]);
+  return fma(z, p, 1.0);
+}
+template <int K>
+__device__ __forceinline__ void cos_sinc(const Poly<K>& P, double x, double& c, double& sc) {   // cos(x), sin(x)/x
+  const double z = x * x;
+  c = horner1<K>(P.c, z);
+  sc = horner1<K>(P.s, z);
+}
+template <typename P>
+__device__ __forceinline__ void sincos_tier(const P& poly, double x, double& s, double& c) {
+  if constexpr (std::is_same<P, NoPoly>::value) {
+    sincos_prep(x, &s, &c);
+  } else {
+    double sc;
+    cos_sinc(poly, x, c, sc);
+    s = x * sc;
   }
-  return ok;
 }
-__device__ __forceinline__ void sincos2_small(mcf2 r, mcf2& s, mcf2& c) {
-  const mcf2 z = r * r;
-  mcf2 ps = fma2(z, mcf2(-1.9515295891e-4f), mcf2(8.3321608736e-3f));
-  ps = fma2(z, ps, mcf2(-1.6666654611e-1f));
-  s = fma2(z * r, ps, r);
-  mcf2 pc = fma2(z, mcf2(2.443315711809948e-5f), mcf2(-1.388731625493765e-3f));
-  pc = fma2(z, pc, mcf2(4.166664568298827e-2f));
-  c = fma2(z * z, pc, fma2(mcf2(-0.5f), z, mcf2(1.0f)));
+
+// quaternion SLERP + position LERP at the point's time, then p' = R(q) p + pos.
+// The time is formed as the reference forms it, t_frame + t_ns * 1e-9 (no contraction), and alpha
+// as the oracle's (t - t_k) / dt; TIER bounds alpha * Theta.
+template <typename P>
+__device__ __forceinline__ void slerp_point(const PoseWin& w, const P& poly, int t, float& x, float& y, float& z) {
+#if MC_NULL_COMPUTE
+  asm volatile("" : "+v"(x), "+v"(y), "+v"(z) : "v"(t));
+#else
+  const double tq = __dadd_rn(w.tf, __dmul_rn((double)t, 1e-9));
+  double al = (tq - w.t0) * w.inv_dt;
+  al = fmin(fmax(al, 0.0), 1.0);
+  double cs, sc;
+  cos_sinc(poly, al * w.th, cs, sc);
+  const double s = al * sc;
+  const double qx = fma(s, w.v[0], cs * w.q0[0]);
+  const double qy = fma(s, w.v[1], cs * w.q0[1]);
+  const double qz = fma(s, w.v[2], cs * w.q0[2]);
+  const double qw = fma(s, w.v[3], cs * w.q0[3]);
+  const double X = x, Y = y, Z = z;
+  // v' = v + 2 (qw t + u x t), t = u x v
+  const double tx = fma(qy, Z, -qz * Y);
+  const double ty = fma(qz, X, -qx * Z);
+  const double tz = fma(qx, Y, -qy * X);
+  const double cx = fma(qw, tx, fma(qy, tz, -qz * ty));
+  const double cy = fma(qw, ty, fma(qz, tx, -qx * tz));
+  const double cz = fma(qw, tz, fma(qx, ty, -qy * tx));
+  // (p + alpha dp) + p0 + 2c: one SGPR operand per instruction (no copies of the record into VGPRs)
+  x = (float)fma(2.0, cx, fma(al, w.dp[0], X) + w.p0[0]);
+  y = (float)fma(2.0, cy, fma(al, w.dp[1], Y) + w.p0[1]);
+  z = (float)fma(2.0, cz, fma(al, w.dp[2], Z) + w.p0[2]);
+#endif
 }
-__device__ __forceinline__ void imu_rotate2_f32(const mcf2 th[3], mcf2& x, mcf2& y, mcf2& z) {
-  mcf2 sa, ca, sb, cb, sc, cc;
-  sincos2_small(th[0], sa, ca);
-  sincos2_small(th[1], sb, cb);
-  sincos2_small(th[2], sc, cc);
-  const mcf2 x1 = fma2(cc, x, sc * y);
-  const mcf2 y1 = fma2(-sc, x, cc * y);
-  const mcf2 x2 = fma2(cb, x1, -sb * z);
-  const mcf2 z2 = fma2(sb, x1, cb * z);
-  const mcf2 y3 = fma2(ca, y1, sa * z2);
-  const mcf2 z3 = fma2(-sa, y1, ca * z2);
-  x = x2; y = y3; z = z3;
+
+// Path B body (CSIM:1447-1465): w = g + alpha*dg (alpha from the bracketing IMU samples, CSIM:1504-
+// 1511), theta = w * dt, dt = t_ns * 1e-9 (CSIM:1454), p' = Rx(-theta_x) Ry(-theta_y) Rz(-theta_z) p
+// (CSIM:1518-1536).  tsd = (double)w.ts: t - ts is exact in float64 (both integers below 2^53).
+template <typename P>
+__device__ __forceinline__ void imu_point(const ImuSeg& w, const P& poly, double tsd, int t, float& x, float& y,
+                                          float& z) {
+#if MC_NULL_COMPUTE
+  asm volatile("" : "+v"(x), "+v"(y), "+v"(z) : "v"(t));
+#else
+  const double td = (double)t;
+  double al = (td - tsd) * w.inv_dt;
+  al = al > 0.0 ? al : 0.0;
+  const double dt = td * 1e-9;
+  double sa, ca, sb, cb, sc, cc;
+  sincos_tier(poly, fma(al, w.dg[0], w.g[0]) * dt, sa, ca);
+  sincos_tier(poly, fma(al, w.dg[1], w.g[1]) * dt, sb, cb);
+  sincos_tier(poly, fma(al, w.dg[2], w.g[2]) * dt, sc, cc);
+  const double X = x, Y = y, Z = z;
+  // Rz(-c)
+  const double x1 = fma(cc, X, sc * Y);
+  const double y1 = fma(-sc, X, cc * Y);
+  // Ry(-b)
+  const double x2 = fma(cb, x1, -sb * Z);
+  const double z2 = fma(sb, x1, cb * Z);
+  // Rx(-a)
+  const double y3 = fma(ca, y1, sa * z2);
+  const double z3 = fma(-sa, y1, ca * z2);
+  x = (float)x2; y = (float)y3; z = (float)z3;
+#endif
+}
+
+// bound on |theta| over an IMU record's span: |g + alpha dg| <= |g| + |dg| (alpha in [0, 1] for the
+// points a window assigns to the record), times |dt|
+__device__ __forceinline__ double imu_rate_bound(const ImuSeg& w) {
+  const double a = fabs(w.g[0]) + fabs(w.dg[0]), b = fabs(w.g[1]) + fabs(w.dg[1]), c = fabs(w.g[2]) + fabs(w.dg[2]);
+  return fmax(a, fmax(b, c));
 }
 
 // window search: index of the window segment of frame-relative time t (bnd sorted, bnd[0] unused)
@@ -1162,53 +1153,76 @@ __device__ __forceinline__ int win_index(const int64_t* bnd, int W, int64_t t) {
 }
 
 template <int MODE>
-__device__ __forceinline__ void point_body(const typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type& w,
-                                           int t, float& x, float& y, float& z) {
-#if MC_NULL_COMPUTE
-  asm volatile("" : "+v"(x), "+v"(y), "+v"(z) : "v"(t));
-#else
-  if constexpr (MODE == 1) slerp_point(w, t, x, y, z);
-  else imu_point(w, t, x, y, z);
+using WinOf = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
+
+// a scheduling fence between the points of a lane: the float64 bodies (~35 live VGPRs each) run
+// one after the other instead of interleaved, which keeps the kernels at 4 waves / SIMD (128 VGPRs)
+#ifndef MC_POINT_SCHED
+#define MC_POINT_SCHED 1
 #endif
-}
+#if MC_POINT_SCHED
+#define MC_POINT_FENCE __builtin_amdgcn_sched_barrier(0);
+#else
+#define MC_POINT_FENCE
+#endif
 
-template <typename Win>
-__device__ __forceinline__ Win select_win(bool s, const Win& a, const Win& b) {
-  struct Raw { float v[sizeof(Win) / 4]; };
-  const Raw ra = __builtin_bit_cast(Raw, a), rb = __builtin_bit_cast(Raw, b);
-  Raw r;
+// one point with a wave-uniform record at a tier
+template <int MODE, typename P>
+__device__ __forceinline__ void point_at(const WinOf<MODE>& w, const P& poly, int t, float& x, float& y, float& z) {
+  if constexpr (MODE == 1) slerp_point(w, poly, t, x, y, z);
+  else imu_point(w, poly, (double)w.ts, t, x, y, z);
+}
+// the general tier of a mode (any angle)
+template <int MODE>
+constexpr int kTierAny = MODE == 1 ? 2 : 3;
+
+// The 4 points of a lane's float4 group with ONE wave-uniform record (SGPRs) at the tier that
+// covers every point of the wave.
+template <int MODE, int TIER>
+__device__ __forceinline__ void points4(const WinOf<MODE>& w, const int4& Tq, float4& X, float4& Y, float4& Z) {
+  const PolyOf<TIER> poly = poly_load<TIER>();
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(Win) / 4); ++i) r.v[i] = s ? rb.v[i] : ra.v[i];
-  return __builtin_bit_cast(Win, r);
+  for (int c = 0; c < 4; ++c) {
+    point_at<MODE>(w, poly, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
+    MC_POINT_FENCE
+  }
 }
 
-// per-point path for frames whose points span more than kWinMax segments
-template <int MODE, int NG = kBlock>   // NG float4 groups from g0 (a sub-tile, or a quad quarter)
-__device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const Tile tl, int g0) {
-  const int f = tl.frame;
-  const int e_end = 4 * min(tl.ngroups, g0 + NG);
-  for (int e = 4 * g0 + threadIdx.x; e < e_end; e += kBlock) {
-    const int64_t p = tl.pstart + e;
-    const float* q = a.in + bidx((int)a.in_C, 0, p);
-    float x = q[0], y = q[kBlkPts], z = q[2 * kBlkPts];
-    const float in = q[3 * kBlkPts];
-    const int t = __builtin_bit_cast(int, q[4 * kBlkPts]);
-    if constexpr (MODE == 1) {
-      const double tf = a.frame_time[f];
-      int64_t k = upper_bound(a.pose_time, a.ntab, tf + (double)t * 1e-9) - 1;
-      if (k > a.nseg - 1) k = a.nseg - 1;
-      if (k < 0) k = 0;
-      slerp_point(make_pose_win(a.pose_seg[k], tf), t, x, y, z);
-    } else {
-      int64_t k = upper_bound(a.imu_ts, a.ntab, a.frame_start[f] + (int64_t)t) - 1;
-      if (k < 0) k = 0;
-      ImuSeg w = a.imu_seg[k];
-      w.ts -= a.frame_start[f];
-      imu_point(w, t, x, y, z);
+// Points of one wave that fall into several segments (seg[c] = segment of the lane's point c, -1:
+// no point): the wave peels the distinct segments off one at a time, smallest first — rec_of(j)
+// returns segment j's record wave-uniformly (scalar loads, or LDS through readfirstlane), so no
+// record ever sits in VGPRs and every path keeps the fast path's register budget.
+__device__ __forceinline__ int wave_min_u(int v) { return __builtin_amdgcn_readfirstlane(wave_min(v)); }
+
+template <typename T>
+__device__ __forceinline__ T uniform_of(const T& v) {   // a value all lanes hold, moved to SGPRs
+  static_assert(sizeof(T) % 4 == 0, "dword-multiple type");
+  struct Raw { int v[sizeof(T) / 4]; };
+  Raw r = __builtin_bit_cast(Raw, v);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) r.v[i] = __builtin_amdgcn_readfirstlane(r.v[i]);
+  return __builtin_bit_cast(T, r);
+}
+
+template <int MODE, int TIER, typename RecOf>
+__device__ __forceinline__ void points_peeled(const int seg[4], RecOf rec_of, const int4& Tq, float4& X, float4& Y,
+                                              float4& Z) {
+  const PolyOf<TIER> poly = poly_load<TIER>();
+  int pend = (seg[0] >= 0 ? 1 : 0) | (seg[1] >= 0 ? 2 : 0) | (seg[2] >= 0 ? 4 : 0) | (seg[3] >= 0 ? 8 : 0);
+  while (__any(pend != 0)) {
+    int cand = INT_MAX;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) cand = ((pend >> c) & 1) ? min(cand, seg[c]) : cand;
+    const int j = wave_min_u(cand);
+    const WinOf<MODE> w = rec_of(j);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (((pend >> c) & 1) && seg[c] == j) {
+        point_at<MODE>(w, poly, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
+        pend &= ~(1 << c);
+      }
+      MC_POINT_FENCE
     }
-    float* o = a.out + bidx((int)a.out_C, 0, p);
-    o[0] = x; o[kBlkPts] = y; o[2 * kBlkPts] = z; o[3 * kBlkPts] = in;
-    if (a.copy_t) o[4 * kBlkPts] = __builtin_bit_cast(float, t);
   }
 }
 
@@ -1216,139 +1230,12 @@ __device__ __forceinline__ void deskew_subtile_slow(const DeskewArgs& a, const T
 // float4 groups (1024 points of one frame).  The frame's segment window (k_prep) decides the path,
 // uniformly for the whole workgroup:
 //   W <= 2      both frame-specialised records come in through scalar loads (SGPRs); each wave
-//               votes whether its points all sit in one segment (no LDS, no barrier);
+//               votes whether its points all sit in one segment (no LDS, no barrier) and picks the
+//               polynomial tier that covers its angles; a wave across the boundary peels its two
+//               segments;
 //   W <= 64     the window's records are staged into LDS once (one barrier), each point picks its
-//               segment by searching the boundaries;
-//   W > 64      pathological span: per-point search of the global tables.
-// ---- quad decomposition of the per-point kernels (MC_POINTS_QUAD) -----------------------------
-// As deskew_frame_quad: a workgroup covers 64 float4 groups (a quarter of a 1024-point sub-tile,
-// same windows), lane c of a quad loads column c of its group (x, y, z, intensity) plus the group's
-// t_ns float4 (the quad's four lanes read the same 16 bytes: one request).  A 4x4 transpose through
-// DPP quad broadcasts gives lane k point k's x, y, z, t; the per-point math runs once per lane on
-// one point (the same slerp_point / imu_point / float32 small-angle code, the same window and vote
-// logic per wave), and a second transpose returns output column c to lane c for one 16-byte
-// store.  Bare 5-in / 4-out blocked streams: 6.41-6.47 TB/s with four lanes per group vs
-// 6.13-6.20 with one (tools/stage_probe.hip, profiles/round2/s10/stage_probe_blocked.json) — but the kernels are not bare
-// streams: with the per-point math once per lane (4x the lanes, each carrying the window / vote
-// logic and both transposes) they ran 50 % slower, so the default stays one lane per group.
-#ifndef MC_POINTS_QUAD
-#define MC_POINTS_QUAD 0     // rejected: SLERP 479.9 vs 320.5 us, IMU 520.9 vs 343.7 us (3 replicas, profiles/round2/s10)
-#endif
-
-// output column k (this lane's index in its quad) of lane J's point: x, y or z (k = 3: unused)
-template <int J>
-__device__ __forceinline__ float quad_sel(float x, float y, float z, int k) {
-  const float bx = quad_bcast<J>(x), by = quad_bcast<J>(y), bz = quad_bcast<J>(z);
-  return k == 0 ? bx : (k == 1 ? by : bz);
-}
-
-template <int MODE>
-using WinOf = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
-
-template <int MODE>
-__device__ __forceinline__ void deskew_points_quad(const DeskewArgs& a, const uint32_t pre, WinOf<MODE>* s_win,
-                                                   int64_t* s_bnd) {
-  using Win = WinOf<MODE>;
-  constexpr int kQ = kBlock / kQuadGroups;
-  const int tid = threadIdx.x;
-  const int k = tid & 3;                 // lane in quad: loads / stores column k, computes point k
-  const int64_t n_sub = (int64_t)a.n_tiles * kSub;
-  const int64_t n_units = n_sub * kQ;
-  const uint32_t nb = gridDim.x - pre;
-  const Win* frec = reinterpret_cast<const Win*>(a.frec);
-  const Win* srec = reinterpret_cast<const Win*>(a.srec);
-  for (int64_t it = blockIdx.x - pre; it < n_units; it += nb) {
-    const int64_t un = nb >= n_units ? xcd_unit<(MODE == 2 ? MC_XCD_IMU : MC_XCD_SLERP)>(it, n_units) : it;
-    const int64_t st = un / kQ;
-    const Tile tl = ldu(a.tiles + st / kSub);
-    FrameWin sw;
-    if constexpr (MODE == 2) sw = ldu(a.swin + st);
-    const int g0 = (int)(st % kSub) * kBlock + (int)(un % kQ) * kQuadGroups;
-    if (g0 >= tl.ngroups) continue;      // uniform: empty quarter of a short sub-tile
-    const int f = tl.frame;
-    const int g = g0 + (tid >> 2);
-    const bool act = g < tl.ngroups;     // uniform over a quad
-    const int64_t p = tl.pstart + 4 * (int64_t)g;
-    const float* q = a.in + bidx((int)a.in_C, 0, p);
-    const FrameWin ff = ldu(a.fwin + f);
-    const bool sub = MC_SUBTILE_WIN && ff.W > MC_FASTPATH_MAXW;
-    if constexpr (MODE != 2) {
-      if (sub) sw = ldu(a.swin + st);
-    }
-    const FrameWin fw = sub ? sw : ff;
-    const Win* rec = sub ? srec + 2 * st : frec + 2 * f;
-    if (fw.W > kWinMax) {
-      deskew_subtile_slow<MODE, kQuadGroups>(a, tl, g0);
-      continue;
-    }
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    int t = 0;
-    if (act) {
-      v = ld4(q + k * kBlkPts);
-      t = ld1(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts) + k);   // point k's t_ns (a 16-byte run per quad)
-    }
-    // transpose in: point k's coordinates to lane k (every lane takes part in the broadcasts)
-    float x = quad_pick<0>(v, k), y = quad_pick<1>(v, k), z = quad_pick<2>(v, k);
-    if (fw.W <= MC_FASTPATH_MAXW) {
-      const Win r0 = ldu(rec);
-      bool use1 = false, mixed = false;
-      if (fw.W == 2) {
-        const int64_t b1 = fw.bnd1;
-        const bool w1 = __any(act && (int64_t)t >= b1), w0 = __any(act && (int64_t)t < b1);
-        use1 = w1 && !w0;
-        mixed = w1 && w0;
-      }
-      bool done = false;
-#if MC_IMU_F32 && !MC_NULL_COMPUTE
-      if constexpr (MODE == 2) {
-        const ImuF f0 = imu_f32(r0);
-        const ImuF f1 = imu_f32(fw.W == 2 ? ldu(rec + 1) : r0);
-        const ImuF fk = select_win((mixed ? (int64_t)t >= fw.bnd1 : use1), f0, f1);
-        float th[3];
-        const bool ok = !act || imu_angles_f32(fk, t, th);
-        if (__all(ok)) {
-          if (act) imu_rotate_f32(th, x, y, z);
-          done = true;
-        }
-      }
-#endif
-      if (act && !done) {
-        if (!mixed) {
-          point_body<MODE>(use1 ? ldu(rec + 1) : r0, t, x, y, z);
-        } else {
-          point_body<MODE>(select_win((int64_t)t >= fw.bnd1, r0, ldu(rec + 1)), t, x, y, z);
-        }
-      }
-    } else {
-      const int W = fw.W;
-      if (tid < W) {
-        const int64_t kk = fw.klo + tid;
-        if constexpr (MODE == 1) {
-          const double tf = a.frame_time[f];
-          s_win[tid] = make_pose_win(a.pose_seg[kk], tf);
-          s_bnd[tid] = rel_ns_ceil(a.pose_time[kk], tf);
-        } else {
-          ImuSeg sg = a.imu_seg[kk];
-          sg.ts -= a.frame_start[f];
-          s_win[tid] = sg;
-          s_bnd[tid] = sg.ts;
-        }
-      }
-      __syncthreads();
-      if (act) point_body<MODE>(s_win[win_index(s_bnd, W, (int64_t)t)], t, x, y, z);
-      __syncthreads();   // the LDS window is rewritten by the next unit
-    }
-    // transpose out: column k of the quad's four points to lane k (lane 3 keeps the intensities)
-    const float4 o = make_float4(quad_sel<0>(x, y, z, k), quad_sel<1>(x, y, z, k), quad_sel<2>(x, y, z, k),
-                                 quad_sel<3>(x, y, z, k));
-    if (act) {
-      float* ob = a.out + bidx((int)a.out_C, 0, p);
-      st_points<MODE>(ob + k * kBlkPts, k == 3 ? v : o);
-      if (a.copy_t && k == 3) st_points<MODE>(ob + 4 * kBlkPts, ld4(q + 4 * kBlkPts));
-    }
-  }
-}
-
+//               segment by searching the boundaries, the wave peels the segments it holds;
+//   W > 64      pathological span: per-point search of the global tables, peeled the same way.
 // NEXT: the launch also runs the next step's prep in its first `pre` workgroups (see the
 // k_deskew_frame_next comment)
 // (NEXT: at least 4 waves / SIMD like the plain kernel — the prep body alone would take 172 VGPRs)
@@ -1361,13 +1248,9 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
       return;
     }
   }
-  using Win = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
+  using Win = WinOf<MODE>;
   __shared__ Win s_win[kWinMax];
   __shared__ int64_t s_bnd[kWinMax];
-#if MC_POINTS_QUAD
-  deskew_points_quad<MODE>(a, NEXT ? pre : 0u, s_win, s_bnd);
-  return;
-#endif
   const int tid = threadIdx.x;
   const int64_t n_sub = (int64_t)a.n_tiles * kSub;
   const Win* frec = reinterpret_cast<const Win*>(a.frec);
@@ -1391,18 +1274,6 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
     float4 X, Y, Z, I;
     int4 Tq;
     const float* q = a.in + bidx((int)a.in_C, 0, p);   // the float4 group never straddles a block
-#define MC_POINT_LOADS                                          \
-    if (act) {                                                  \
-      Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts)); \
-      X = ld4(q);                                               \
-      Y = ld4(q + kBlkPts);                                     \
-      Z = ld4(q + 2 * kBlkPts);                                 \
-      I = ld4(q + 3 * kBlkPts);                                 \
-    }
-#if MC_EARLY_LOADS
-    // the point loads depend on the tile record only: in flight while the window record arrives
-    MC_POINT_LOADS
-#endif
     const FrameWin ff = ldu(a.fwin + f);
     // frames wider than the SGPR path take their sub-tile's own window (k_prep)
     const bool sub = MC_SUBTILE_WIN && ff.W > MC_FASTPATH_MAXW;
@@ -1411,17 +1282,15 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
     }
     const FrameWin fw = sub ? sw : ff;
     const Win* rec = sub ? srec + 2 * st : frec + 2 * f;
-    if (fw.W > kWinMax) {
-      deskew_subtile_slow<MODE>(a, tl, g0);
-      continue;
+    if (act) {
+      Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts));
+      X = ld4(q);
+      Y = ld4(q + kBlkPts);
+      Z = ld4(q + 2 * kBlkPts);
+      I = ld4(q + 3 * kBlkPts);
     }
-#if !MC_EARLY_LOADS
-    MC_POINT_LOADS
-#endif
-#undef MC_POINT_LOADS
 
     if (fw.W <= MC_FASTPATH_MAXW) {
-      const Win r0 = ldu(rec);
       bool use1 = false, mixed = false;
       if (fw.W == 2) {
         const int64_t b1 = fw.bnd1;
@@ -1431,78 +1300,36 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
         use1 = w1 && !w0;
         mixed = w1 && w0;
       }
-      bool done = false;
-#if MC_IMU_F32 && !MC_NULL_COMPUTE
-      if constexpr (MODE == 2) {
-        // small-angle waves in f32 (imu_angles_f32); the vote keeps the wave on one path.  The
-        // angles are formed twice (vote, then rotation) rather than held across the vote.
-        const ImuF f0 = imu_f32(r0);
-        const ImuF f1 = imu_f32(fw.W == 2 ? ldu(rec + 1) : r0);
-        bool ok = true;
-#define MC_PICK(t) ((mixed ? (int64_t)(t) >= fw.bnd1 : use1) ? f1 : f0)
-#if MC_IMU_DIAG != 1
-        if (act) {
-#if MC_IMU_PK
-#pragma unroll
-          for (int c = 0; c < 4; c += 2) {
-            const int ta = i4c(Tq, c), tb = i4c(Tq, c + 1);
-            mcf2 th[3];
-            ok = imu_angles2_f32(MC_PICK(ta), MC_PICK(tb), ta, tb, th) && ok;
-          }
-#else
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int t = i4c(Tq, c);
-            float th[3];
-            ok = imu_angles_f32(MC_PICK(t), t, th) && ok;
-          }
-#endif
-        }
-#endif
-        if (__all(ok)) {
-          if (act) {
-#if MC_IMU_PK
-#pragma unroll
-            for (int c = 0; c < 4; c += 2) {
-              const int ta = i4c(Tq, c), tb = i4c(Tq, c + 1);
-              mcf2 th[3];
-              imu_angles2_f32(MC_PICK(ta), MC_PICK(tb), ta, tb, th);
-              mcf2 x = {f4c(X, c), f4c(X, c + 1)}, y = {f4c(Y, c), f4c(Y, c + 1)}, z = {f4c(Z, c), f4c(Z, c + 1)};
-              imu_rotate2_f32(th, x, y, z);
-              f4c(X, c) = x.x; f4c(X, c + 1) = x.y;
-              f4c(Y, c) = y.x; f4c(Y, c + 1) = y.y;
-              f4c(Z, c) = z.x; f4c(Z, c + 1) = z.y;
-            }
-#else
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              const int t = i4c(Tq, c);
-              float th[3];
-              imu_angles_f32(MC_PICK(t), t, th);
-              imu_rotate_f32(th, f4c(X, c), f4c(Y, c), f4c(Z, c));
-            }
-#endif
-          }
-          done = true;
-        }
-#undef MC_PICK
-      }
-#endif
-      if (act && !done) {
-        if (!mixed) {
-          const Win w = use1 ? ldu(rec + 1) : r0;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) point_body<MODE>(w, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
+      // the tier: SLERP from Theta (alpha * Theta <= Theta), IMU from a bound on the wave's angles,
+      // (|g| + |dg|) * max |t_ns| * 1e-9
+      const int tm = (MODE == 2 && act) ? max(max(abs(Tq.x), abs(Tq.y)), max(abs(Tq.z), abs(Tq.w))) : 0;
+      auto tier_of = [&](const Win& w) -> int {
+        if constexpr (MODE == 1) {
+          return w.th <= kTier0 ? 0 : (w.th <= kTier1 ? 1 : 2);
         } else {
-          const Win r1 = ldu(rec + 1);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int t = i4c(Tq, c);
-            point_body<MODE>(select_win((int64_t)t >= fw.bnd1, r0, r1), t, f4c(X, c), f4c(Y, c), f4c(Z, c));
-          }
+          const double bound = imu_rate_bound(w) * ((double)tm * 1.000001e-9);
+          return __all(bound <= kTier0) ? 0 : (__all(bound <= kTier1) ? 1 : 3);
         }
+      };
+      if (!mixed) {
+        const Win w = ldu(rec + (use1 ? 1 : 0));
+        const int tier = tier_of(w);
+        if (act) {
+          if (tier == 0) points4<MODE, 0>(w, Tq, X, Y, Z);
+          else if (tier == 1) points4<MODE, 1>(w, Tq, X, Y, Z);
+          else points4<MODE, kTierAny<MODE>>(w, Tq, X, Y, Z);
+        }
+      } else {
+        // the wave straddles the segment boundary: both segments peeled, at the tier covering both
+        const int tier = max(tier_of(ldu(rec)), tier_of(ldu(rec + 1)));
+        int seg[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) seg[c] = act ? ((int64_t)i4c(Tq, c) >= fw.bnd1 ? 1 : 0) : -1;
+        auto rec_of = [&](int j) { return ldu(rec + j); };
+        if (tier <= 1) points_peeled<MODE, 1>(seg, rec_of, Tq, X, Y, Z);
+        else points_peeled<MODE, kTierAny<MODE>>(seg, rec_of, Tq, X, Y, Z);
       }
-    } else {
+    } else if (fw.W <= kWinMax) {
       const int W = fw.W;
       if (tid < W) {
         const int64_t k = fw.klo + tid;
@@ -1518,14 +1345,38 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
         }
       }
       __syncthreads();
-      if (act) {
+      int seg[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) seg[c] = act ? win_index(s_bnd, W, (int64_t)i4c(Tq, c)) : -1;
+      points_peeled<MODE, kTierAny<MODE>>(seg, [&](int j) { return uniform_of(s_win[j]); }, Tq, X, Y, Z);
+      __syncthreads();  // the LDS window is rewritten by the next sub-tile
+    } else {
+      // pathological span (> kWinMax segments in one sub-tile): each point's segment from the
+      // global tables (binary search), as the oracle selects it
+      int seg[4];
+      if constexpr (MODE == 1) {
+        const double tf = a.frame_time[f];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const int t = i4c(Tq, c);
-          point_body<MODE>(s_win[win_index(s_bnd, W, (int64_t)t)], t, f4c(X, c), f4c(Y, c), f4c(Z, c));
+          int64_t k = upper_bound(a.pose_time, a.ntab, __dadd_rn(tf, __dmul_rn((double)i4c(Tq, c), 1e-9))) - 1;
+          k = k > a.nseg - 1 ? a.nseg - 1 : (k < 0 ? 0 : k);
+          seg[c] = act ? (int)k : -1;
         }
+        points_peeled<MODE, kTierAny<MODE>>(seg, [&](int j) { return make_pose_win(ldu(a.pose_seg + j), tf); },
+                                            Tq, X, Y, Z);
+      } else {
+        const int64_t fs = a.frame_start[f];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int64_t k = upper_bound(a.imu_ts, a.ntab, fs + (int64_t)i4c(Tq, c)) - 1;
+          seg[c] = act ? (int)(k < 0 ? 0 : k) : -1;
+        }
+        points_peeled<MODE, kTierAny<MODE>>(seg, [&](int j) {
+          ImuSeg w = ldu(a.imu_seg + j);
+          w.ts -= fs;
+          return w;
+        }, Tq, X, Y, Z);
       }
-      __syncthreads();  // the LDS window is rewritten by the next sub-tile
     }
     if (act) {
       float* o = a.out + bidx((int)a.out_C, 0, p);

@@ -39,7 +39,8 @@ __device__ __forceinline__ int i4c(const int4& v, int c) {
 // DPP quad exchange (quad_perm): lanes 4q .. 4q + 3 of a wave form a quad.
 template <int K>   // quad_perm [K, K, K, K]: lane K of each quad to all four
 __device__ __forceinline__ float quad_bcast(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), K * 0x55, 0xF, 0xF, false));
+  // bound_ctrl: quad_perm never reads outside the quad, so no "old" value has to be set up first
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), K * 0x55, 0xF, 0xF, true));
 }
 // component k (= this lane's index in its quad) of lane L's float4: with L = 0 .. 3 over a quad
 // whose lane c holds column c of four points, lane k gets point k's columns (a 4 x 4 transpose)

@@ -643,7 +643,7 @@ static uint32_t points_lds_reserve() {
 void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int h, StepPlan* sp) {
   std::memset(sp, 0, sizeof(*sp));
   const mc_batch* pb = in;  // per-frame tables live with the input batch
-  float4* frame_tbl = pb->d_frame_tbl + 3 * (size_t)in->F * h;
+  FrameRow* frame_tbl = pb->d_frame_tbl + 3 * (size_t)in->F * h;
   FrameWin* fwin = pb->d_fwin + (size_t)in->F * h;
   void* frec = static_cast<char*>(pb->d_frec) + pb->frec_half * h;
   PoseSeg* pose_seg = c->d_pose_seg ? c->d_pose_seg + (size_t)c->T_cap * h : nullptr;
@@ -688,7 +688,6 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
   int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
   if (mode == MC_MODE_FRAME && MC_FRAME_QUAD) units = in->n_tiles * kSub * (kBlock / kQuadGroups);
-  if (mode != MC_MODE_FRAME && MC_POINTS_QUAD) units = in->n_tiles * kSub * (kBlock / kQuadGroups);
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
   // SLERP sub-tile order: dealt over the XCDs for batches up to ~200 M points (326 vs 340 us at
@@ -1184,15 +1183,14 @@ int mc_transform_affine(mc_ctx* c, const mc_batch* in, mc_batch* out, int32_t n_
   // reader of this half, the event hands it back to the next pipelined prep
   const int h = c->buf;
   c->buf ^= 1;
-  std::vector<float4> tbl(3 * (size_t)in->F);
+  std::vector<FrameRow> tbl(3 * (size_t)in->F);
   for (int32_t f = 0; f < in->F; ++f) {
     const double* m = mats + 12 * (size_t)(n_mats == 1 ? 0 : f);
-    for (int r = 0; r < 3; ++r)
-      tbl[3 * (size_t)f + r] = make_float4((float)m[4 * r], (float)m[4 * r + 1], (float)m[4 * r + 2], (float)m[4 * r + 3]);
+    for (int r = 0; r < 3; ++r) tbl[3 * (size_t)f + r] = FrameRow{m[4 * r], m[4 * r + 1], m[4 * r + 2], m[4 * r + 3]};
   }
-  float4* frame_tbl = in->d_frame_tbl + 3 * (size_t)in->F * h;
+  FrameRow* frame_tbl = in->d_frame_tbl + 3 * (size_t)in->F * h;
   HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
-  HIPCHK(hipMemcpyAsync(frame_tbl, tbl.data(), tbl.size() * sizeof(float4), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(frame_tbl, tbl.data(), tbl.size() * sizeof(FrameRow), hipMemcpyHostToDevice, s));
   if (in->n_tiles > 0) {
     DeskewArgs da;
     std::memset(&da, 0, sizeof(da));

@@ -10,10 +10,16 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# parity tolerance (north_star: <= 1e-5 relative per coordinate).  Relative to the point's
-# scale |p| + |t|: a floor-less per-coordinate relative error is meaningless on
-# coordinates that cancel to ~0 after rotation.
+# parity tolerance (north_star: <= 1e-5 relative per coordinate).  Gated two ways:
+#  * strict (the default): every output coordinate b of the reference within 1e-5 * |b|, with a
+#    floor only for coordinates that cancel to below 1e-9 of the point's scale |p| + |t| (there the
+#    1e-5 bar applies to 1e-9 * scale).  The kernels compute in float64 and round once to float32,
+#    so on float32-representable inputs (every synthetic frame) each coordinate is within 2^-24.
+#  * scaled: |a - b| <= 1e-5 * (|p| + |t|), for inputs that are not float32 values
+#    (reference float64 data staged into float32 columns): their storage rounding alone moves a
+#    coordinate that rotates to ~0 by 6e-8 * |p|.  Tests pass strict=False there and say why.
 REL_TOL = 1e-5
+STRICT_FLOOR = 1e-9
 
 
 def pytest_configure(config):
@@ -36,8 +42,25 @@ def scale_of(points_xyz, translation=None):
     return s
 
 
-def assert_scaled_close(out, ref, scale, tol=REL_TOL, what=""):
-    """max |out-ref| per coordinate <= tol * scale (per point); returns the worst ratio."""
+def naive_rel_err(out, ref, scale=None, floor=STRICT_FLOOR):
+    """Per-coordinate |a - b| / |b|; with ``scale`` (per point), |b| is floored at floor * scale."""
+    out = np.asarray(out, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    den = np.abs(ref)
+    if scale is not None:
+        sc = np.asarray(scale, dtype=np.float64)
+        if den.ndim == 2 and sc.ndim == 1:
+            sc = sc[:, None]
+        den = np.maximum(den, floor * sc)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.abs(out - ref) / den
+    return np.where(np.abs(out - ref) == 0, 0.0, r)
+
+
+def assert_scaled_close(out, ref, scale, tol=REL_TOL, what="", strict=True):
+    """Parity gate.  Scaled: max |out-ref| per coordinate <= tol * scale (per point).  Strict (the
+    default) additionally: per coordinate |out-ref| <= tol * max(|ref|, 1e-9 * scale).  Returns the
+    worst scaled ratio."""
     out = np.asarray(out, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     assert out.shape == ref.shape, f"{what}: shape {out.shape} != {ref.shape}"
@@ -46,9 +69,16 @@ def assert_scaled_close(out, ref, scale, tol=REL_TOL, what=""):
     err = np.abs(out - ref)
     if err.ndim == 2:
         err = err.max(axis=1)
-    ratio = err / np.maximum(np.asarray(scale, dtype=np.float64), 1e-30)
+    sc = np.maximum(np.asarray(scale, dtype=np.float64), 1e-30)
+    ratio = err / sc
     worst = float(ratio.max())
     assert worst <= tol, f"{what}: scaled error {worst:.3e} > {tol:.1e} at point {int(ratio.argmax())}"
+    if strict:
+        nv = naive_rel_err(out, ref, np.broadcast_to(sc, ratio.shape))
+        bad = int(np.count_nonzero(nv > tol))
+        k = int(np.argmax(nv))
+        assert bad == 0, (f"{what}: {bad} coordinates above {tol:.0e} relative per coordinate, worst "
+                          f"{float(nv.ravel()[k]):.3e} (got {out.ravel()[k]!r}, want {ref.ravel()[k]!r})")
     return worst
 
 

@@ -201,3 +201,43 @@ def test_gather_plan_rejects_narrow_shards_and_bad_totals():
     with pytest.raises(ValueError, match="root"):
         d.gather_plan([256], [4], 256, 4, root=1)
     assert d.gather_plan([0, 256], [4, 4], 256, 4)["offset"].tolist() == [0, 0]
+
+
+# ---------------------------------------------------------------------------------------------
+# bench.py --gpus N without torchrun: the bench launches its own rank processes
+# ---------------------------------------------------------------------------------------------
+def _bench(args, env_extra=None, timeout=120):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launch_control_plane(n):
+    """python bench.py --gpus N (no torchrun env): N rank processes rendezvous over the control
+    plane, rank 0 prints one line (the driver's 8-GPU command form must not run 1 rank)."""
+    rc, line, err = _bench(["--gpus", str(n), "--control-plane-only"])
+    assert rc == 0, err
+    assert line["world"] == n and line["launched_by"] == "bench.py"
+    assert [r["rank"] for r in line["ranks"]] == list(range(n))
+    assert [r["local_rank"] for r in line["ranks"]] == list(range(n))
+    assert len({r["pid"] for r in line["ranks"]}) == n
+    assert line["max_over_ranks"] == n - 1
+
+
+def test_bench_self_launch_fails_when_a_rank_fails():
+    rc, line, _ = _bench(["--gpus", "3", "--control-plane-only"],
+                         {"MCBENCH_FAIL_RANK": "2", "MCBENCH_RDV_TIMEOUT": "5"})
+    assert rc != 0 and line is None
+
+
+def test_bench_self_launch_timeout_kills_every_rank():
+    rc, line, err = _bench(["--gpus", "2", "--control-plane-only", "--launch-timeout", "4"],
+                           {"MCBENCH_HANG_RANK": "1"})
+    assert rc == 124 and line is None and "timeout" in err

@@ -1,6 +1,8 @@
 """GPU CoordinateTransformer (CSIM:153-233) and _transform_coordinates (CSIM:2107-2163) against the
-reference's own outputs (tests/golden/coords.npz).  Points live in HBM as float32, so coordinates
-are held to |gpu - ref| <= 1e-5 * (|p| + |t|) per coordinate like the deskew path."""
+reference's own outputs (tests/golden/coords.npz).  Points live in HBM as float32: the reference's
+float64 points are held to |gpu - ref| <= 1e-5 * (|p| + |t|) per coordinate (their float32 staging),
+and the oracle on the same float32 values to the strict per-coordinate 1e-5 (float64 arithmetic in
+the kernel, one rounding on the store)."""
 import logging
 
 import numpy as np
@@ -10,6 +12,10 @@ from conftest import assert_scaled_close, golden, scale_of
 from oracle import restatement as R
 
 pytestmark = pytest.mark.gpu
+
+
+def f32(a):
+    return np.asarray(a, dtype=np.float64).astype(np.float32).astype(np.float64)
 
 
 def test_transform_points_matches_reference(mc, gpu_ctx):
@@ -22,10 +28,13 @@ def test_transform_points_matches_reference(mc, gpu_ctx):
         T = ct.transformations[(a, b)]
         out = ct.transform_points(p3, a, b)
         assert out.shape == (200, 3) and out.dtype == np.float64
-        assert_scaled_close(out, g[f"tp/{a}/{b}"], scale_of(p3, T[:3, 3]), what=f"{a}->{b}")
+        assert_scaled_close(out, g[f"tp/{a}/{b}"], scale_of(p3, T[:3, 3]), what=f"{a}->{b}", strict=False)
+        assert_scaled_close(out, R.transform_points_h(f32(p3), T), scale_of(p3, T[:3, 3]), what=f"{a}->{b} oracle")
     # homogeneous (N,4): the 4th column is w
     out4 = ct.transform_points(g["p4"], "sensor", "local")
-    assert_scaled_close(out4, g["tp4/sensor/local"], scale_of(g["p4"][:, :3], ct.transformations[("sensor", "local")][:3, 3]))
+    T = ct.transformations[("sensor", "local")]
+    assert_scaled_close(out4, g["tp4/sensor/local"], scale_of(g["p4"][:, :3], T[:3, 3]), strict=False)
+    assert_scaled_close(out4, R.transform_points_h(f32(g["p4"]), T), scale_of(g["p4"][:, :3], T[:3, 3]))
     # missing pair: a warning and the very same array back
     assert ct.transform_points(p3, "vehicle", "sensor") is p3
     with pytest.raises(ValueError):
@@ -50,7 +59,7 @@ def test_transform_coordinates_matches_reference(mc, gpu_ctx):
             got = np.array([[p.x, p.y, p.z] for p in fr["points"]]).reshape(-1, 3)
             want = g[f"tc/{target}/{i}"]
             t = ct.transformations.get(("sensor", target), np.eye(4))[:3, 3]
-            assert_scaled_close(got, want, scale_of(g[f"tc/in/{i}"], t), what=f"{target}/{i}")
+            assert_scaled_close(got, want, scale_of(g[f"tc/in/{i}"], t), what=f"{target}/{i}", strict=False)
             meta = np.array([[p.intensity, p.timestamp] for p in fr["points"]], np.int64).reshape(-1, 2)
             assert np.array_equal(meta, g[f"tc/{target}/{i}/meta"])
             assert fr["coordinate_system"] == target and fr["frame_id"] == i
@@ -59,7 +68,7 @@ def test_transform_coordinates_matches_reference(mc, gpu_ctx):
 def test_transform_arrays_per_frame_matrices_large(mc, gpu_ctx):
     rng = np.random.default_rng(4)
     counts = [0, 5, 100_003, 77, 250_000]
-    frames = [rng.normal(0, 50, (n, 3)) for n in counts]
+    frames = [f32(rng.normal(0, 50, (n, 3))) for n in counts]
     Ts = np.stack([R.create_transform_matrix(rng.normal(0, 100, 3), rng.uniform(-np.pi, np.pi, 3)) for _ in counts])
     out = mc.coords.transform_arrays(frames, Ts, context=gpu_ctx)
     for f, T, o in zip(frames, Ts, out):

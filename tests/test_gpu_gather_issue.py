@@ -128,13 +128,15 @@ def test_output_reused_as_input_recomputes_time_spans(mc, gpu_ctx):
         gpu_ctx.deskew(A, B, mode="pose_slerp")
         gpu_ctx.deskew(B, C, mode="pose_slerp")
         got = C.download_aos()[:, :3]
+        mid = B.download_aos()[:, :3]        # the float32 values the second step read
         assert np.array_equal(C.download_time(), t)
         for f in range(3):
             s = slice(offs[f], offs[f + 1])
             once = R.deskew_pose_slerp(p[s], t[s], times[f], tr)
-            twice = R.deskew_pose_slerp(once, t[s], times[f], tr)
+            twice = R.deskew_pose_slerp(mid[s], t[s], times[f], tr)
             _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[f] + t[s] * 1e-9)
-            assert_scaled_close(got[s], twice, 2 * scale_of(once, pos), what=f"t window {lo_ms} ms frame {f}")
+            assert_scaled_close(mid[s], once, scale_of(p[s], pos), what=f"t window {lo_ms} ms frame {f} (B)")
+            assert_scaled_close(got[s], twice, scale_of(mid[s], pos), what=f"t window {lo_ms} ms frame {f}")
 
 
 def test_interleaved_calls_equal_isolated_calls(mc, gpu_ctx):
@@ -200,7 +202,10 @@ def test_interleaved_calls_equal_isolated_calls(mc, gpu_ctx):
         Rm = R.euler_xyz_matrix(tr["orientation_imu"][idx[f]])
         for _ in range(5):
             ref[s] = ref[s] @ Rm.T + tr["position_gps"][idx[f]]
-    assert_scaled_close(chained[:, :3], ref, 5 * (np.linalg.norm(ref, axis=1) + 100.0), what="5 chained steps")
+    # five float32 round trips between the steps: the scaled bar (a coordinate near 0 after one step
+    # carries that step's float32 rounding into the next)
+    assert_scaled_close(chained[:, :3], ref, 5 * (np.linalg.norm(ref, axis=1) + 100.0), what="5 chained steps",
+                        strict=False)
 
 
 # ---------------------------------------------------------------------------------------------

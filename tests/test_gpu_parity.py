@@ -1,7 +1,12 @@
 """GPU parity: the HIP path through the C-ABI vs the oracle and the reference's golden vectors.
 
-Tolerance (north_star: <= 1e-5 relative per coordinate): per coordinate
-|gpu - ref| <= 1e-5 * (|p| + |t|), p the input point, t the translation applied.
+Tolerance (north_star: <= 1e-5 relative per coordinate), conftest.assert_scaled_close: strict per
+coordinate |gpu - ref| <= 1e-5 * |ref| (floor at 1e-9 * (|p| + |t|)) wherever the input is made of
+float32 values — the float32 columns then hold the reference's exact inputs, and the kernels' float64
+arithmetic leaves only the final rounding (2^-24).  Random inputs are drawn as float32 values
+(``f32``) for that reason.  Reference float64 data staged into float32 columns (golden frames of the
+reference run) is compared at the scaled bar |gpu - ref| <= 1e-5 * (|p| + |t|) and,
+strictly, against the oracle on the same float32-rounded inputs.
 """
 import os
 
@@ -23,6 +28,11 @@ CFGS = {
                          "environment_complexity": "medium", "max_speed": 5.0, "lidar_fps": 20},
 }
 SCEN = {"urban_complex": [0, 1, 2, 599, 1199], "parking_detailed": [0, 300], "highway_simple": [0, 1, 55]}
+
+
+def f32(a):
+    """float64 array of float32 values (what a float32 batch column holds exactly)."""
+    return np.asarray(a, dtype=np.float64).astype(np.float32).astype(np.float64)
 
 
 def traj_of(name):
@@ -330,10 +340,11 @@ def test_slerp_matches_scipy_golden_across_yaw_wrap(mc, gpu_ctx):
     pts = np.column_stack([g["xyz"], np.linspace(0, 1, len(g["xyz"]))])
     out = sim.deskew_frames([pts], [t_ns], tr, times=[t_frame])[0]
     tq = t_frame + t_ns * 1e-9
-    ref = R.deskew_pose_slerp(g["xyz"], t_ns, t_frame, tr)
+    ref = R.deskew_pose_slerp(f32(g["xyz"]), t_ns, t_frame, tr)   # the inputs the float32 columns hold
     _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], tq)
     assert_scaled_close(out[:, :3], ref, scale_of(g["xyz"], pos), what="slerp vs oracle")
-    assert_scaled_close(out[:, :3], g["out"], scale_of(g["xyz"], pos), what="slerp vs scipy golden")
+    # the golden was made on the float64 points: their float32 staging is the only difference
+    assert_scaled_close(out[:, :3], g["out"], scale_of(g["xyz"], pos), what="slerp vs scipy golden", strict=False)
 
 
 def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
@@ -346,7 +357,7 @@ def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
     pos = np.cumsum(rng.normal(0, 0.2, (T, 3)), axis=0)
     tr = {"time": time, "position_gps": pos, "orientation_imu": rpy}
     counts = [5000, 3, 1024, 2500]
-    frames = [np.column_stack([rng.uniform(-90, 90, (n, 3)), rng.uniform(0, 1, n)]) for n in counts]
+    frames = [f32(np.column_stack([rng.uniform(-90, 90, (n, 3)), rng.uniform(0, 1, n)])) for n in counts]
     t_ns = [rng.integers(-2_000_000_000, 2_000_000_000, counts[0]),          # spans 4 s: slow path
             np.array([-10**9, 0, 10**9]),
             np.sort(rng.integers(0, 100_000_000, 1024)),
@@ -376,7 +387,7 @@ def test_wide_frames_take_subtile_windows(mc, gpu_ctx, mode):
             rng.permutation(np.arange(counts[2]) * 5000),                     # shuffled
             rng.integers(-1_500_000_000, 1_500_000_000, counts[3]),           # 3 s span
             np.array([0, 1, 2, 99_999_999, 50_000_000, 3, 4])]
-    frames = [np.column_stack([rng.uniform(-90, 90, (n, 3)), rng.uniform(0, 1, n)]) for n in counts]
+    frames = [f32(np.column_stack([rng.uniform(-90, 90, (n, 3)), rng.uniform(0, 1, n)])) for n in counts]
     times = np.array([2.0, 10.005, 20.0, 30.0, 35.0])
     sim = mc.LiDARMotionSimulator(context=gpu_ctx)
     if mode == "pose_slerp":
@@ -437,7 +448,7 @@ def test_per_point_modes_pass_t_ns_through(mc, gpu_ctx, mode):
 def test_slerp_single_pose_table(mc, gpu_ctx):
     tr = {"time": np.array([3.0]), "position_gps": np.array([[1.0, 2.0, 3.0]]),
           "orientation_imu": np.array([[0.1, -0.2, 2.5]])}
-    pts = np.column_stack([np.random.default_rng(2).normal(0, 30, (100, 3)), np.zeros(100)])
+    pts = f32(np.column_stack([np.random.default_rng(2).normal(0, 30, (100, 3)), np.zeros(100)]))
     sim = mc.LiDARMotionSimulator(context=gpu_ctx)
     out = sim.deskew_frames([pts], [np.arange(100) * 10**6], tr, times=[0.0])[0]
     ref = R.transform_pointcloud(pts, {"translation": tr["position_gps"][0], "rotation": tr["orientation_imu"][0]})
@@ -462,7 +473,12 @@ def test_compensate_point_cloud_matches_reference(mc, gpu_ctx, case):
         assert out is pts
         return
     got = np.array([[p.x, p.y, p.z] for p in out])
-    assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(xyz), what=case)
+    # the reference's float64 points are staged into float32 columns: scaled bar vs its output,
+    # strict vs the oracle on the float32-rounded points
+    assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(xyz), what=case, strict=False)
+    ref = R.compensate_arrays(f32(xyz), g[f"{case}/ts"], int(g[f"{case}/frame_start"]), g[f"{case}/imu_ts"],
+                              g[f"{case}/imu_gyro"])
+    assert_scaled_close(got, ref, scale_of(xyz), what=case + " vs oracle")
     meta = np.array([[p.intensity, p.timestamp, p.ring, p.tag] for p in out])
     assert np.array_equal(meta, g[f"{case}/out_meta"])
 
@@ -485,7 +501,7 @@ def test_compensator_disabled_and_driver(mc, gpu_ctx):
     assert all(r["motion_compensated"] for r in res) and res[2]["points"] == []
     for case, r in zip(("mid", "spike"), res):
         got = np.array([[p.x, p.y, p.z] for p in r["points"]])
-        assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case)
+        assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case, strict=False)
 
 
 def test_compensator_sees_in_place_imu_edits(mc, gpu_ctx):
@@ -493,7 +509,7 @@ def test_compensator_sees_in_place_imu_edits(mc, gpu_ctx):
     the same list object between calls (same length, same first / last timestamps) must change
     the result; a second compensator on the same context must not inherit a stale table."""
     g = golden("csim_pathb.npz")
-    xyz, ts0 = g["mid/xyz"], g["mid/ts"]
+    xyz, ts0 = f32(g["mid/xyz"]), g["mid/ts"]
     start = int(g["mid/frame_start"])
     imu = [mc.IMUData(int(t), *map(float, gy), 0.0, 0.0, 0.0) for t, gy in zip(g["mid/imu_ts"], g["mid/imu_gyro"])]
     pts = [mc.LiDARPoint(*map(float, p), 0, int(t), 0, 0) for p, t in zip(xyz, ts0)]
@@ -514,18 +530,19 @@ def test_compensator_sees_in_place_imu_edits(mc, gpu_ctx):
     assert_scaled_close(got, R.compensate_arrays(xyz, ts0, start, *mc.imu_to_arrays(imu)), scale_of(xyz))
 
 
-@pytest.mark.parametrize("rate", [2.0, 7.7, 8.5, 30.0])
-def test_imu_small_angle_f32_path_and_threshold(mc, gpu_ctx, rate):
-    """Waves whose angles stay within 0.78 rad take the float32 path, the others the f64 one:
-    constant rates that put theta = rate * dt on either side of the threshold within one 0.1 s
-    frame (time-sorted points, so whole waves land on each side), plus points before the frame
-    start and a rate change between IMU samples; all within the parity bar of the oracle."""
+@pytest.mark.parametrize("rate", [0.5, 2.0, 2.4, 7.7, 8.5, 30.0])
+def test_imu_polynomial_tiers_and_thresholds(mc, gpu_ctx, rate):
+    """Each wave evaluates sin / cos at the polynomial tier that covers its angles (|theta| <= 1/16,
+    <= 1/4, any angle with range reduction): constant rates that put theta = rate * dt on either
+    side of the tier bounds within one 0.1 s frame (time-sorted points, so whole waves land on each
+    side), plus points before the frame start and a rate change between IMU samples; strict parity
+    with the oracle."""
     rng = np.random.default_rng(int(rate * 10))
     ts = np.arange(0, 2_000_000_000, 5_000_000, dtype=np.int64)
     gyro = np.tile(np.array([rate, -0.6 * rate, 0.9 * rate]), (len(ts), 1))
     gyro[len(ts) // 2 + 3:] *= -1.0                      # rate flip inside the frame window
     n = 50_000
-    xyz = rng.uniform(-90, 90, (n, 3))
+    xyz = f32(rng.uniform(-90, 90, (n, 3)))
     start = 1_000_000_000
     t_abs = np.sort(start + rng.integers(-2_000_000, 100_000_000, n))
     comp = mc.MotionCompensator({}, context=gpu_ctx)
@@ -540,7 +557,7 @@ def test_imu_slow_path_wide_subtile(mc, gpu_ctx):
     ts = np.arange(0, 4_000_000_000, 5_000_000, dtype=np.int64)
     gyro = rng.normal(0, 2.0, (len(ts), 3))
     n = 3000
-    xyz = rng.uniform(-80, 80, (n, 3))
+    xyz = f32(rng.uniform(-80, 80, (n, 3)))
     start = 1_000_000_000
     t_abs = start + rng.integers(-500_000_000, 1_000_000_000, n)
     comp = mc.MotionCompensator({}, context=gpu_ctx)

@@ -1,0 +1,54 @@
+#!/bin/bash
+# One GPU-box session, steps chosen by $STEPS (default: tests smoke ab bench), each under its own
+# time limit; stops at the first fault / abort / timeout (any exit code other than 0 and pytest's 1).
+#   tests   python -m pytest tests -m gpu ($PYTEST_ARGS, e.g. "-k slerp")
+#   smoke   __graft_entry__.smoke()
+#   ab      tools/ab.py $AB_ARGS (interleaved A/B of build/variants/lib_*.so)
+#   bench   bench.py with the driver's flags ($BENCH_ARGS)
+#   prof    rocprofv3 --kernel-trace --stats of the same bench command
+# Usage (repo root, on the GPU box):  STEPS="tests ab" bash tools/gpu_session.sh <tag>
+set -u
+TAG=${1:-s}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+STEPS=${STEPS:-"tests smoke ab bench"}
+
+stop_if_fault() {  # $1 = rc, $2 = step
+  echo "[$2] rc=$1 $(date +%T)" | tee -a "$OUT/steps.log"
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then
+    echo "[$2] fault/abort/timeout -> stopping" | tee -a "$OUT/steps.log"
+    exit "$1"
+  fi
+}
+
+for step in $STEPS; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf -x --durations=15 --timeout 240 \
+        --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+      stop_if_fault $? tests
+      tail -25 "$OUT/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      stop_if_fault $? smoke
+      cat "$OUT/smoke.log" ;;
+    ab)
+      timeout -k 10 900 python -u tools/ab.py ${AB_ARGS:-} > "$OUT/ab.log" 2>&1
+      stop_if_fault $? ab
+      cp gpurun_out/ab.json "$OUT/ab.json" 2>/dev/null
+      cat "$OUT/ab.log" ;;
+    bench)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
+      stop_if_fault $? bench
+      cat "$OUT/bench.json"; tail -3 "$OUT/bench.err" ;;
+    prof)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu ${BENCH_ARGS:-} \
+          > "$OUT/prof_bench.json" 2> "$OUT/prof.err" )
+      stop_if_fault $? prof
+      find "$OUT/prof" -name "*kernel_stats*" -exec head -12 {} \; ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
