@@ -69,11 +69,15 @@ int need_rccl() {
 }
 }  // namespace
 
+// per rank in the plan allgather: padded length, columns, merged padded length, merged columns
+// (root), frames, frame-count hash, merged frames, merged frame-count hash (root)
+constexpr int kPlanWords = 8;
+
 struct mc_comm {
   mc_ctx* ctx = nullptr;
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
-  int64_t* d_scratch = nullptr;  // 4 (nranks + 1) int64: the (sizes, columns, merged sizes) allgather
+  int64_t* d_scratch = nullptr;  // kPlanWords (nranks + 1) int64: the per-rank plan allgather
   float* d_stage = nullptr;      // root: shards whose column count differs from the merged batch
   int64_t stage_cap = 0;
   double* d_red = nullptr;       // reduction buffer
@@ -146,7 +150,7 @@ int mc_comm_init(mc_ctx* ctx, int nranks, int rank, const char id_in[128], mc_co
   c->rank = rank;
   ncclResult_t r = g_rccl.CommInitRank(&c->comm, nranks, id, rank);
   if (r != ncclSuccess) { delete c; return fail(MC_ERR_COMM, "ncclCommInitRank: %s", g_rccl.GetErrorString(r)); }
-  if (hipMalloc(&c->d_scratch, sizeof(int64_t) * 4 * (nranks + 1)) != hipSuccess) {
+  if (hipMalloc(&c->d_scratch, sizeof(int64_t) * kPlanWords * (nranks + 1)) != hipSuccess) {
     g_rccl.CommDestroy(c->comm);
     delete c;
     return fail(MC_ERR_NOMEM, "hipMalloc failed");
@@ -176,20 +180,30 @@ int mc_comm_gather_batch(mc_comm* c, const mc_batch* local, int root, mc_batch* 
   if (is_root && merged->ctx != c->ctx) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
   HIPCHK(hipSetDevice(c->ctx->device));
   hipStream_t s = c->ctx->stream;
-  // every rank's (padded length, column count) and the root's merged (padded length, column
-  // count): all ranks then hold the whole plan and reject a bad one together, before any send
-  const int64_t mine[4] = {local->P, local->C, is_root ? merged->P : -1, is_root ? merged->C : -1};
+  // every rank's (padded length, column count, frame count, hash of its frame counts) and the
+  // root's merged ones: all ranks then hold the whole plan and reject a bad one together, before
+  // any send (equal padded totals do not make the same frame order)
+  const int64_t nan = -1;
+  const int64_t mine[kPlanWords] = {
+      local->P, local->C, is_root ? merged->P : nan, is_root ? merged->C : nan, (int64_t)local->F,
+      (int64_t)mcplan::counts_hash(local->counts.data(), local->F), is_root ? (int64_t)merged->F : nan,
+      is_root ? (int64_t)mcplan::counts_hash(merged->counts.data(), merged->F) : nan};
   const int nr = c->nranks;
-  HIPCHK(hipMemcpyAsync(c->d_scratch + 4 * nr, mine, sizeof(mine), hipMemcpyHostToDevice, s));
-  NCCLCHK(g_rccl.AllGather(c->d_scratch + 4 * nr, c->d_scratch, 4, ncclInt64, c->comm, s));
-  std::vector<int64_t> all(4 * (size_t)nr);
+  HIPCHK(hipMemcpyAsync(c->d_scratch + kPlanWords * nr, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+  NCCLCHK(g_rccl.AllGather(c->d_scratch + kPlanWords * nr, c->d_scratch, kPlanWords, ncclInt64, c->comm, s));
+  std::vector<int64_t> all(kPlanWords * (size_t)nr);
   HIPCHK(hipMemcpyAsync(all.data(), c->d_scratch, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  std::vector<int64_t> P(nr), C(nr);
-  for (int q = 0; q < nr; ++q) { P[q] = all[4 * (size_t)q]; C[q] = all[4 * (size_t)q + 1]; }
+  std::vector<int64_t> P(nr), C(nr), F(nr);
+  std::vector<uint64_t> H(nr);
+  for (int q = 0; q < nr; ++q) {
+    const int64_t* w = all.data() + kPlanWords * (size_t)q;
+    P[q] = w[0]; C[q] = w[1]; F[q] = w[4]; H[q] = (uint64_t)w[5];
+  }
+  const int64_t* wr = all.data() + kPlanWords * (size_t)root;
   mcplan::GatherPlan G;
-  const std::string perr =
-      mcplan::plan_gather(nr, root, P.data(), C.data(), all[4 * (size_t)root + 2], all[4 * (size_t)root + 3], &G);
+  std::string perr = mcplan::plan_gather(nr, root, P.data(), C.data(), wr[2], wr[3], &G);
+  if (perr.empty()) perr = mcplan::check_frame_hashes(nr, F.data(), H.data(), wr[6], (uint64_t)wr[7]);
   if (!perr.empty()) return fail(MC_ERR_INVALID, "%s", perr.c_str());
   if (!is_root) {
     if (local->P > 0) {
@@ -254,14 +268,19 @@ int mc_gather_plan(int32_t nranks, int32_t root, const int64_t* padded, const in
 int mc_gather_batches(mc_ctx* ctx, int32_t n, const mc_batch* const* shards, int32_t root, mc_batch* merged) {
   if (!ctx || !shards || !merged || n < 1) return fail(MC_ERR_INVALID, "NULL argument");
   if (merged->ctx != ctx) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
-  std::vector<int64_t> P(n), C(n);
+  std::vector<int64_t> P(n), C(n), F(n);
+  std::vector<const int64_t*> counts(n);
   for (int32_t q = 0; q < n; ++q) {
     if (!shards[q] || shards[q]->ctx != ctx) return fail(MC_ERR_INVALID, "shard %d is NULL or of another context", q);
+    if (shards[q] == merged) return fail(MC_ERR_INVALID, "shard %d is the merged batch (the copies would overlap)", q);
     P[q] = shards[q]->P;
     C[q] = shards[q]->C;
+    F[q] = shards[q]->F;
+    counts[q] = shards[q]->counts.data();
   }
   mcplan::GatherPlan G;
-  const std::string perr = mcplan::plan_gather(n, root, P.data(), C.data(), merged->P, merged->C, &G);
+  std::string perr = mcplan::plan_gather(n, root, P.data(), C.data(), merged->P, merged->C, &G);
+  if (perr.empty()) perr = mcplan::check_frame_concat(n, counts.data(), F.data(), merged->counts.data(), merged->F);
   if (!perr.empty()) return fail(MC_ERR_INVALID, "%s", perr.c_str());
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;

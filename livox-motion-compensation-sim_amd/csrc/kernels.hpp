@@ -113,7 +113,8 @@ struct ImuSeg {
 // the frame; bnd1 = frame-relative ns where segment klo+1 starts (W >= 2).
 struct FrameWin {
   int32_t klo;
-  int32_t W;
+  int16_t W;
+  int16_t tier;    // polynomial tier covering every point of the window (per_point_tier)
   int64_t bnd1;
 };
 
@@ -268,13 +269,16 @@ __device__ __forceinline__ void euler_xyz_matrix(double r, double p, double y, d
   R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
 }
 
-// f64 sin/cos for the per-step prep (k_prep), whose latency is one wave's serial f64 chain: ocml's
-// sincos carries a Payne-Hanek branch (v_trig_preop) inlined at every call site (k_prep was 7.2 k
-// instructions).  Cody-Waite reduction by pi/2 in three 33-bit parts (fdlibm's pio2_1/2/3) with
-// fma, so every product n * pio2_k is exact: the reduced argument is good to ~1e-16 absolute for
-// |x| < 2^50 rad (n exact); then the fdlibm __kernel_sin / __kernel_cos minimax polynomials on
-// |r| <= pi/4 (<= 2.4 ulp measured against long double over 2e7 arguments).  A pose angle of
-// 2^50 rad or more (or non-finite) gives NaN.
+// f64 sin/cos for the per-step prep (k_prep) and the IMU kernel's general tier, whose latency is one
+// wave's serial f64 chain: ocml's sincos carries a Payne-Hanek branch (v_trig_preop) inlined at
+// every call site (k_prep was 7.2 k instructions), and an out-of-line call costs the deskew kernels
+// a call frame (IMU kernel 351 -> 372 us).  Cody-Waite reduction by pi/2 in three 33-bit parts
+// (fdlibm's pio2_1/2/3) with fma: each fma forms n * pio2_k exactly and rounds once, so the reduced
+// argument is within ~1e-16 + 7e-27 |n| absolute (the first step's result is ~6e-11 |n|) — ~1e-16
+// up to |x| ~ 2^30 pi/2, ~1e-11 at 2^50 (the plain products alone are exact only below
+// |n| < 2^20).  Then the fdlibm __kernel_sin / __kernel_cos minimax polynomials on |r| <= pi/4
+// (<= 2.4 ulp measured against long double over 2e7 arguments).  |x| >= 2^50 rad or non-finite: NaN
+// (an angle that large carries an input rounding of >= 0.1 rad; the quadrant index would overflow).
 __device__ __forceinline__ void sincos_prep(double x, double* s, double* c) {
   if (!(fabs(x) < 1125899906842624.0)) { *s = *c = __builtin_nan(""); return; }
   const double n = rint(x * 6.36619772367581382433e-01);
@@ -574,6 +578,26 @@ __device__ __forceinline__ ImuSample fetch_imu(const ImuSample& v, int64_t base,
   return s;
 }
 
+// Polynomial tiers of the per-point sin / cos (see the float64 per-point math below), chosen per
+// window by k_prep: SLERP from the window's segment angles Theta (alpha * Theta <= Theta), IMU from
+// a bound on the window's angles, |theta| <= max_c (|g_c| + |dg_c|) * max |t_ns| * 1e-9 (alpha in
+// [0, 1] for every point a window assigns to a record).
+constexpr double kTier0 = 0.0625, kTier1 = 0.25, kTier2 = 1.6;
+template <int MODE>
+__device__ __forceinline__ int16_t window_tier(double ang) {
+  if (MODE == 1) return ang <= kTier0 ? 0 : (ang <= kTier1 ? 1 : 2);
+  return ang <= kTier0 ? 0 : (ang <= kTier1 ? 1 : 3);
+}
+// bound on |theta| over an IMU record's span: |g + alpha dg| <= |g| + |dg|
+__device__ __forceinline__ double imu_rate_bound(const ImuSeg& w) {
+  const double a = fabs(w.g[0]) + fabs(w.dg[0]), b = fabs(w.g[1]) + fabs(w.dg[1]), c = fabs(w.g[2]) + fabs(w.dg[2]);
+  return fmax(a, fmax(b, c));
+}
+__device__ __forceinline__ double imu_angle_bound(double rate, int2 tr) {   // rate * max |t| * 1e-9, rounded up
+  const double tm = fmax(fabs((double)tr.x), fabs((double)tr.y));
+  return rate * (tm * 1.000001e-9);
+}
+
 // One wave per frame (frame work), then one lane per pose segment / IMU sample (table work).
 // MODE = the deskew mode (k_prep dispatches on a.mode).
 template <int MODE>
@@ -661,13 +685,17 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
   auto bound_at = [&](int64_t k) -> int64_t { return MODE == 1 ? rel_ns_ceil(a.time[k], tf) : a.imu_ts[k] - fs; };
   // record of segment k from samples k, k+1 (clamped) / IMU k, k+1 (or k alone at the end)
   // s0, s1 come from fetch_pose / fetch_imu; write at dst[slot]
-  auto write_pose = [&](const PoseSample& s0, const PoseSample& s1, void* dst, int64_t slot) {
-    reinterpret_cast<PoseWin*>(dst)[slot] = make_pose_win(pose_seg_of(s0, s1), tf);
+  // a record (its segment's angle measure returned: Theta, or the IMU rate bound)
+  auto pose_rec = [&](const PoseSample& s0, const PoseSample& s1, void* dst, int64_t slot, bool wr) {
+    const PoseSeg sg = pose_seg_of(s0, s1);
+    if (wr) reinterpret_cast<PoseWin*>(dst)[slot] = make_pose_win(sg, tf);
+    return sg.th;
   };
-  auto write_imu = [&](const ImuSample& s0, const ImuSample& s1, bool last, void* dst, int64_t slot) {
+  auto imu_rec = [&](const ImuSample& s0, const ImuSample& s1, bool last, void* dst, int64_t slot, bool wr) {
     ImuSeg sg = imu_seg_of(s0, s1, last);
     sg.ts -= fs;
-    reinterpret_cast<ImuSeg*>(dst)[slot] = sg;
+    if (wr) reinterpret_cast<ImuSeg*>(dst)[slot] = sg;
+    return imu_rate_bound(sg);
   };
   // the frame's two records (lane 0: segment klo + the window header, lane 1: klo + 1); every lane
   // takes part in the fetches
@@ -677,16 +705,20 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     const bool writes = lane < 2 && !(lane == 1 && W < 2);
     FrameWin w;
     w.klo = (int32_t)klo;
-    w.W = W > kWinMax ? kWinMax + 1 : (int32_t)W;
+    w.W = (int16_t)(W > kWinMax ? kWinMax + 1 : W);
+    double ang;   // lane 0: segment klo, lane 1: klo + 1
     if (MODE == 1) {
       const PoseSample s0 = fetch_pose(pv, base, k, a), s1 = fetch_pose(pv, base, k1, a);
-      if (writes) write_pose(s0, s1, a.frec, 2 * f + lane);
+      ang = pose_rec(s0, s1, a.frec, 2 * f + lane, writes);
       w.bnd1 = W >= 2 ? bound_pose(s1) : INT64_MAX;   // lane 0: s1 = sample klo + 1
     } else {
       const ImuSample s0 = fetch_imu(iv, base, k, a), s1 = fetch_imu(iv, base, k1, a);
-      if (writes) write_imu(s0, s1, k + 1 >= a.M, a.frec, 2 * f + lane);
+      ang = imu_rec(s0, s1, k + 1 >= a.M, a.frec, 2 * f + lane, writes);
       w.bnd1 = W >= 2 ? bound_imu(s1) : INT64_MAX;
     }
+    const double ang1 = __shfl(ang, 1, 64);
+    if (W >= 2) ang = fmax(ang, ang1);
+    w.tier = window_tier<MODE>(MODE == 1 ? ang : imu_angle_bound(ang, tr));
     if (lane == 0) a.fwin[f] = w;
   }
   if (!MC_SUBTILE_WIN || W <= MC_FASTPATH_MAXW || !a.swin) return;
@@ -727,27 +759,25 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     const int64_t k0 = hs ? s0 : klo, n = hs ? s1 - s0 + 1 : 1;
     FrameWin w;
     w.klo = (int32_t)k0;
-    w.W = n > kWinMax ? kWinMax + 1 : (int32_t)n;
+    w.W = (int16_t)(n > kWinMax ? kWinMax + 1 : n);
     // samples k0, k0 + 1, k0 + 2 (clamped): records k0 and k0 + 1 and the boundary of k0 + 1
     const int64_t ka = clampk(k0), kb = clampk(k0 + 1), kc = clampk(k0 + 2);
     const bool rec = valid && n <= MC_FASTPATH_MAXW;
+    double ang;
     if (MODE == 1) {
       const PoseSample sa = fetch_pose(pv, base, ka, a), sb_ = fetch_pose(pv, base, kb, a);
       const PoseSample sc = fetch_pose(pv, base, kc, a);
       w.bnd1 = n >= 2 ? bound_pose(sb_) : INT64_MAX;
-      if (rec) {
-        write_pose(sa, sb_, a.srec, 2 * st);
-        if (n >= 2) write_pose(sb_, sc, a.srec, 2 * st + 1);
-      }
+      ang = pose_rec(sa, sb_, a.srec, 2 * st, rec);
+      if (n >= 2) ang = fmax(ang, pose_rec(sb_, sc, a.srec, 2 * st + 1, rec));
     } else {
       const ImuSample sa = fetch_imu(iv, base, ka, a), sb_ = fetch_imu(iv, base, kb, a);
       const ImuSample sc = fetch_imu(iv, base, kc, a);
       w.bnd1 = n >= 2 ? bound_imu(sb_) : INT64_MAX;
-      if (rec) {
-        write_imu(sa, sb_, ka + 1 >= a.M, a.srec, 2 * st);
-        if (n >= 2) write_imu(sb_, sc, kb + 1 >= a.M, a.srec, 2 * st + 1);
-      }
+      ang = imu_rec(sa, sb_, ka + 1 >= a.M, a.srec, 2 * st, rec);
+      if (n >= 2) ang = fmax(ang, imu_rec(sb_, sc, kb + 1 >= a.M, a.srec, 2 * st + 1, rec));
     }
+    w.tier = window_tier<MODE>(MODE == 1 ? ang : imu_angle_bound(ang, hs ? r : make_int2(0, 0)));
     if (valid) a.swin[st] = w;
   }
 }
@@ -995,7 +1025,6 @@ __global__ __launch_bounds__(kBlock) void k_affine_w(const DeskewArgs a) { deske
 //   tier 2  |x| <= 1.6    cos, sinc to z^10         (10 + 10; SLERP's alpha*Theta <= Theta <= pi/2)
 //   tier 3  any angle     Cody-Waite reduction + fdlibm kernels (sincos_prep; IMU gyro spikes)
 // ---------------------------------------------------------------------------------------------
-constexpr double kTier0 = 0.0625, kTier1 = 0.25, kTier2 = 1.6;
 
 // Taylor coefficients of cos and sin(x)/x after the leading 1: c[k] of z^(k+1).  They live in
 // constant memory and each tier's set is brought into SGPRs by one scalar load per wave where the
@@ -1130,13 +1159,6 @@ __device__ __forceinline__ void imu_point(const ImuSeg& w, const P& poly, double
 #endif
 }
 
-// bound on |theta| over an IMU record's span: |g + alpha dg| <= |g| + |dg| (alpha in [0, 1] for the
-// points a window assigns to the record), times |dt|
-__device__ __forceinline__ double imu_rate_bound(const ImuSeg& w) {
-  const double a = fabs(w.g[0]) + fabs(w.dg[0]), b = fabs(w.g[1]) + fabs(w.dg[1]), c = fabs(w.g[2]) + fabs(w.dg[2]);
-  return fmax(a, fmax(b, c));
-}
-
 // window search: index of the window segment of frame-relative time t (bnd sorted, bnd[0] unused)
 __device__ __forceinline__ int win_index(const int64_t* bnd, int W, int64_t t) {
   if (W <= 4) {
@@ -1178,9 +1200,9 @@ constexpr int kTierAny = MODE == 1 ? 2 : 3;
 
 // The 4 points of a lane's float4 group with ONE wave-uniform record (SGPRs) at the tier that
 // covers every point of the wave.
-template <int MODE, int TIER>
-__device__ __forceinline__ void points4(const WinOf<MODE>& w, const int4& Tq, float4& X, float4& Y, float4& Z) {
-  const PolyOf<TIER> poly = poly_load<TIER>();
+template <int MODE, typename P>
+__device__ __forceinline__ void points4(const WinOf<MODE>& w, const P& poly, const int4& Tq, float4& X, float4& Y,
+                                        float4& Z) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     point_at<MODE>(w, poly, i4c(Tq, c), f4c(X, c), f4c(Y, c), f4c(Z, c));
@@ -1204,10 +1226,9 @@ __device__ __forceinline__ T uniform_of(const T& v) {   // a value all lanes hol
   return __builtin_bit_cast(T, r);
 }
 
-template <int MODE, int TIER, typename RecOf>
-__device__ __forceinline__ void points_peeled(const int seg[4], RecOf rec_of, const int4& Tq, float4& X, float4& Y,
-                                              float4& Z) {
-  const PolyOf<TIER> poly = poly_load<TIER>();
+template <int MODE, typename RecOf, typename P>
+__device__ __forceinline__ void points_peeled(const int seg[4], RecOf rec_of, const P& poly, const int4& Tq, float4& X,
+                                              float4& Y, float4& Z) {
   int pend = (seg[0] >= 0 ? 1 : 0) | (seg[1] >= 0 ? 2 : 0) | (seg[2] >= 0 ? 4 : 0) | (seg[3] >= 0 ? 8 : 0);
   while (__any(pend != 0)) {
     int cand = INT_MAX;
@@ -1223,6 +1244,35 @@ __device__ __forceinline__ void points_peeled(const int seg[4], RecOf rec_of, co
       }
       MC_POINT_FENCE
     }
+  }
+}
+
+// The SGPR path of a window of <= 2 segments at tier TIER: each wave votes whether its points all
+// sit in one segment; a wave across the boundary peels its two segments.
+template <int MODE, int TIER>
+__device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin& fw, bool act, const int4& Tq,
+                                          float4& X, float4& Y, float4& Z) {
+  const PolyOf<TIER> poly = poly_load<TIER>();
+  bool use1 = false, mixed = false;
+  if (fw.W == 2) {
+    const int64_t b1 = fw.bnd1;
+    const bool any1 = act && ((int64_t)Tq.w >= b1 || (int64_t)Tq.x >= b1 || (int64_t)Tq.y >= b1 || (int64_t)Tq.z >= b1);
+    const bool any0 = act && ((int64_t)Tq.w < b1 || (int64_t)Tq.x < b1 || (int64_t)Tq.y < b1 || (int64_t)Tq.z < b1);
+    const bool w1 = __any(any1), w0 = __any(any0);
+    use1 = w1 && !w0;
+    mixed = w1 && w0;
+  }
+  if (!mixed) {
+    // every lane computes (a partial wave's idle lanes on zeros, their results never stored): under
+    // `if (act)` the compiler sank the record load into the divergent block as 9 per-lane vector
+    // loads of the 144-byte record instead of scalar loads
+    const WinOf<MODE> w = ldu(rec + (use1 ? 1 : 0));
+    points4<MODE>(w, poly, Tq, X, Y, Z);
+  } else {
+    int seg[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) seg[c] = act ? ((int64_t)i4c(Tq, c) >= fw.bnd1 ? 1 : 0) : -1;
+    points_peeled<MODE>(seg, [&](int j) { return ldu(rec + j); }, poly, Tq, X, Y, Z);
   }
 }
 
@@ -1288,47 +1338,17 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
       Y = ld4(q + kBlkPts);
       Z = ld4(q + 2 * kBlkPts);
       I = ld4(q + 3 * kBlkPts);
+    } else {
+      Tq = make_int4(0, 0, 0, 0);
+      X = Y = Z = I = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
     if (fw.W <= MC_FASTPATH_MAXW) {
-      bool use1 = false, mixed = false;
-      if (fw.W == 2) {
-        const int64_t b1 = fw.bnd1;
-        const bool any1 = act && ((int64_t)Tq.w >= b1 || (int64_t)Tq.x >= b1 || (int64_t)Tq.y >= b1 || (int64_t)Tq.z >= b1);
-        const bool any0 = act && ((int64_t)Tq.w < b1 || (int64_t)Tq.x < b1 || (int64_t)Tq.y < b1 || (int64_t)Tq.z < b1);
-        const bool w1 = __any(any1), w0 = __any(any0);
-        use1 = w1 && !w0;
-        mixed = w1 && w0;
-      }
-      // the tier: SLERP from Theta (alpha * Theta <= Theta), IMU from a bound on the wave's angles,
-      // (|g| + |dg|) * max |t_ns| * 1e-9
-      const int tm = (MODE == 2 && act) ? max(max(abs(Tq.x), abs(Tq.y)), max(abs(Tq.z), abs(Tq.w))) : 0;
-      auto tier_of = [&](const Win& w) -> int {
-        if constexpr (MODE == 1) {
-          return w.th <= kTier0 ? 0 : (w.th <= kTier1 ? 1 : 2);
-        } else {
-          const double bound = imu_rate_bound(w) * ((double)tm * 1.000001e-9);
-          return __all(bound <= kTier0) ? 0 : (__all(bound <= kTier1) ? 1 : 3);
-        }
-      };
-      if (!mixed) {
-        const Win w = ldu(rec + (use1 ? 1 : 0));
-        const int tier = tier_of(w);
-        if (act) {
-          if (tier == 0) points4<MODE, 0>(w, Tq, X, Y, Z);
-          else if (tier == 1) points4<MODE, 1>(w, Tq, X, Y, Z);
-          else points4<MODE, kTierAny<MODE>>(w, Tq, X, Y, Z);
-        }
-      } else {
-        // the wave straddles the segment boundary: both segments peeled, at the tier covering both
-        const int tier = max(tier_of(ldu(rec)), tier_of(ldu(rec + 1)));
-        int seg[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) seg[c] = act ? ((int64_t)i4c(Tq, c) >= fw.bnd1 ? 1 : 0) : -1;
-        auto rec_of = [&](int j) { return ldu(rec + j); };
-        if (tier <= 1) points_peeled<MODE, 1>(seg, rec_of, Tq, X, Y, Z);
-        else points_peeled<MODE, kTierAny<MODE>>(seg, rec_of, Tq, X, Y, Z);
-      }
+      // the tier k_prep chose for the window: its coefficient load is issued here, beside the point
+      // loads, not behind the vote that needs them
+      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, act, Tq, X, Y, Z);
+      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, act, Tq, X, Y, Z);
+      else fast_path<MODE, kTierAny<MODE>>(rec, fw, act, Tq, X, Y, Z);
     } else if (fw.W <= kWinMax) {
       const int W = fw.W;
       if (tid < W) {
@@ -1348,7 +1368,7 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
       int seg[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) seg[c] = act ? win_index(s_bnd, W, (int64_t)i4c(Tq, c)) : -1;
-      points_peeled<MODE, kTierAny<MODE>>(seg, [&](int j) { return uniform_of(s_win[j]); }, Tq, X, Y, Z);
+      points_peeled<MODE>(seg, [&](int j) { return uniform_of(s_win[j]); }, poly_load<kTierAny<MODE>>(), Tq, X, Y, Z);
       __syncthreads();  // the LDS window is rewritten by the next sub-tile
     } else {
       // pathological span (> kWinMax segments in one sub-tile): each point's segment from the
@@ -1362,8 +1382,8 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
           k = k > a.nseg - 1 ? a.nseg - 1 : (k < 0 ? 0 : k);
           seg[c] = act ? (int)k : -1;
         }
-        points_peeled<MODE, kTierAny<MODE>>(seg, [&](int j) { return make_pose_win(ldu(a.pose_seg + j), tf); },
-                                            Tq, X, Y, Z);
+        points_peeled<MODE>(seg, [&](int j) { return make_pose_win(ldu(a.pose_seg + j), tf); },
+                            poly_load<kTierAny<MODE>>(), Tq, X, Y, Z);
       } else {
         const int64_t fs = a.frame_start[f];
 #pragma unroll
@@ -1371,11 +1391,11 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
           int64_t k = upper_bound(a.imu_ts, a.ntab, fs + (int64_t)i4c(Tq, c)) - 1;
           seg[c] = act ? (int)(k < 0 ? 0 : k) : -1;
         }
-        points_peeled<MODE, kTierAny<MODE>>(seg, [&](int j) {
+        points_peeled<MODE>(seg, [&](int j) {
           ImuSeg w = ldu(a.imu_seg + j);
           w.ts -= fs;
           return w;
-        }, Tq, X, Y, Z);
+        }, poly_load<kTierAny<MODE>>(), Tq, X, Y, Z);
       }
     }
     if (act) {

@@ -365,10 +365,16 @@ int mc_batch_set_frame_start_ns(mc_batch* b, const int64_t* s) {
   return MC_OK;
 }
 
+// Work this context queues on its stream and leaves running when the call returns must keep the next
+// mc_deskew's prep from being issued any-order (MC_PREP_ISSUE 2): that prep may only overtake this
+// context's own deskew kernel.  Every API that returns with work in flight calls this.
+static inline void queued_async(mc_ctx* c) { c->prep_fence = true; }
+
 // device AoS -> batch columns (async, timed as a layout kernel)
 static int launch_stage(mc_batch* b, const double* d_aos, int64_t ld) {
   mc_ctx* c = b->ctx;
   if (b->n_tiles == 0) return MC_OK;
+  queued_async(c);
   {
     TimedRegion tr(c, &c->layout_ev, c->stream);
     hipLaunchKernelGGL(k_aos_to_soa, dim3(launch_grid(c, stage_units(b->n_tiles, ld))), dim3(kBlock), 0, c->stream,
@@ -381,6 +387,7 @@ static int launch_stage(mc_batch* b, const double* d_aos, int64_t ld) {
 static int launch_fetch(mc_batch* b, double* d_aos) {
   mc_ctx* c = b->ctx;
   if (b->n_tiles == 0) return MC_OK;
+  queued_async(c);
   {
     TimedRegion tr(c, &c->layout_ev, c->stream);
     hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, stage_units(b->n_tiles, 4))), dim3(kBlock), 0, c->stream,
@@ -1189,7 +1196,10 @@ int mc_transform_affine(mc_ctx* c, const mc_batch* in, mc_batch* out, int32_t n_
     for (int r = 0; r < 3; ++r) tbl[3 * (size_t)f + r] = FrameRow{m[4 * r], m[4 * r + 1], m[4 * r + 2], m[4 * r + 3]};
   }
   FrameRow* frame_tbl = in->d_frame_tbl + 3 * (size_t)in->F * h;
-  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
+#if MC_PREP_ISSUE == 0
+  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));   // the side-stream prep that last wrote half h
+#endif
+  queued_async(c);
   HIPCHK(hipMemcpyAsync(frame_tbl, tbl.data(), tbl.size() * sizeof(FrameRow), hipMemcpyHostToDevice, s));
   if (in->n_tiles > 0) {
     DeskewArgs da;

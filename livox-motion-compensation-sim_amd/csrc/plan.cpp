@@ -7,9 +7,10 @@
 
 namespace mcplan {
 
-static std::string msg(const char* fmt, long long a, long long b = 0, long long c = 0) {
-  char buf[256];
-  std::snprintf(buf, sizeof(buf), fmt, a, b, c);
+static std::string msg(const char* fmt, long long a, long long b = 0, long long c = 0, long long d = 0,
+                       long long e = 0) {
+  char buf[320];
+  std::snprintf(buf, sizeof(buf), fmt, a, b, c, d, e);
   return buf;
 }
 
@@ -78,6 +79,57 @@ std::string plan_gather(int32_t nranks, int32_t root, const int64_t* P, const in
   }
   if (o != merged_P)
     return msg("merged batch holds %lld padded points, ranks sent %lld", merged_P, o);
+  return "";
+}
+
+namespace {
+constexpr uint64_t kHashBase = 0x9E3779B97F4A7C15ull;   // odd: multiplication is a bijection mod 2^64
+uint64_t pow_mod(uint64_t b, int64_t e) {
+  uint64_t r = 1;
+  while (e > 0) {
+    if (e & 1) r *= b;
+    b *= b;
+    e >>= 1;
+  }
+  return r;
+}
+}  // namespace
+
+uint64_t counts_hash(const int64_t* counts, int64_t n) {
+  uint64_t h = 0;
+  for (int64_t i = 0; i < n; ++i) h = h * kHashBase + (uint64_t)counts[i] + 1;
+  return h;
+}
+
+uint64_t hash_concat(uint64_t ha, uint64_t hb, int64_t nb) { return ha * pow_mod(kHashBase, nb) + hb; }
+
+std::string check_frame_concat(int32_t nranks, const int64_t* const* shard_counts, const int64_t* shard_F,
+                               const int64_t* merged_counts, int64_t merged_F) {
+  int64_t f = 0;
+  for (int32_t q = 0; q < nranks; ++q) {
+    if (shard_F[q] > merged_F - f)
+      return msg("the shards hold more frames than the merged batch (%lld)", merged_F);
+    for (int64_t i = 0; i < shard_F[q]; ++i, ++f)
+      if (shard_counts[q][i] != merged_counts[f])
+        return msg("merged frame %lld holds %lld points, shard %lld's frame %lld holds %lld (the merged batch must "
+                   "be the rank-ordered concatenation of the shards)", f, merged_counts[f], q, i, shard_counts[q][i]);
+  }
+  if (f != merged_F) return msg("the shards hold %lld frames, the merged batch %lld", f, merged_F);
+  return "";
+}
+
+std::string check_frame_hashes(int32_t nranks, const int64_t* F, const uint64_t* H, int64_t merged_F,
+                               uint64_t merged_H) {
+  uint64_t h = 0;
+  int64_t f = 0;
+  for (int32_t q = 0; q < nranks; ++q) {
+    if (F[q] < 0) return msg("rank %lld sent %lld frames", q, F[q]);
+    h = hash_concat(h, H[q], F[q]);
+    f += F[q];
+  }
+  if (f != merged_F) return msg("the ranks hold %lld frames, the merged batch %lld", f, merged_F);
+  if (h != merged_H)
+    return "the merged batch's frame counts are not the rank-ordered concatenation of the shards' frame counts";
   return "";
 }
 

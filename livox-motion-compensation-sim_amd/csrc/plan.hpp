@@ -49,6 +49,18 @@ struct GatherPlan {
 std::string plan_gather(int32_t nranks, int32_t root, const int64_t* P, const int64_t* C, int64_t merged_P,
                         int64_t merged_C, GatherPlan* out);
 
+// The merged batch's frames must be the rank-ordered concatenation of the shards' frames, not
+// merely the same padded total ([300, 100] and [100, 300] pad alike).  In one process the counts
+// are compared directly (check_frame_concat); across ranks each shard sends (frame count, rolling
+// hash of its counts) and the root checks the merged batch's hash against the chained shard hashes:
+// H(a ++ b) = H(a) * B^len(b) + H(b) (mod 2^64).
+uint64_t counts_hash(const int64_t* counts, int64_t n);
+uint64_t hash_concat(uint64_t ha, uint64_t hb, int64_t nb);
+std::string check_frame_concat(int32_t nranks, const int64_t* const* shard_counts, const int64_t* shard_F,
+                               const int64_t* merged_counts, int64_t merged_F);
+std::string check_frame_hashes(int32_t nranks, const int64_t* F, const uint64_t* H, int64_t merged_F,
+                               uint64_t merged_H);
+
 // Where rank q's C[q] * P[q] values are received: in place in the merged batch, or staged.
 inline float* gather_dst(const GatherPlan& G, int32_t q, float* merged, int64_t merged_C, float* stage) {
   return G.stage_off[q] >= 0 ? stage + G.stage_off[q] : merged + G.off[q] * merged_C;

@@ -6,6 +6,7 @@
 // Exit status = number of failed checks (capped at 255).
 #include "plan.hpp"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -148,10 +149,68 @@ static void test_gather(std::mt19937_64& g) {
   CHECK(staged_runs > 100 && errors > 100, "coverage");
 }
 
+// the merged batch's frames must be the rank-ordered concatenation of the shards'
+// frames — [300, 100] and [100, 300] pad to the same total.  Exact check (one process) and the
+// chained-hash check (across ranks) must agree on every split, swap and perturbation.
+static void test_frame_order(std::mt19937_64& g) {
+  int64_t accepted = 0, rejected = 0;
+  for (int trial = 0; trial < 4000; ++trial) {
+    const int32_t W = 1 + (int32_t)(g() % 8);
+    const int64_t Fm = (int64_t)(g() % 30);
+    std::vector<int64_t> merged(Fm);
+    for (auto& c : merged) c = (int64_t)(g() % 5 == 0 ? 0 : g() % 200000);
+    // a split of the merged frames over W ranks
+    std::vector<int64_t> cut(W + 1, 0);
+    cut[W] = Fm;
+    for (int32_t q = 1; q < W; ++q) cut[q] = Fm ? (int64_t)(g() % (Fm + 1)) : 0;
+    std::sort(cut.begin(), cut.end());
+    std::vector<std::vector<int64_t>> sh(W);
+    for (int32_t q = 0; q < W; ++q) sh[q].assign(merged.begin() + cut[q], merged.begin() + cut[q + 1]);
+    const int kind = trial % 4;   // 0: correct, 1: two shards swapped, 2: one count changed, 3: a frame moved
+    bool should_fail = false;
+    if (kind == 1 && W >= 2) {
+      const int32_t a = (int32_t)(g() % W), b = (int32_t)(g() % W);
+      should_fail = sh[a] != sh[b];
+      std::swap(sh[a], sh[b]);
+    } else if (kind == 2 && Fm > 0) {
+      const int32_t q = (int32_t)(g() % W);
+      if (!sh[q].empty()) { sh[q][g() % sh[q].size()] += 1 + (int64_t)(g() % 7); should_fail = true; }
+    } else if (kind == 3 && W >= 2) {
+      const int32_t q = (int32_t)(g() % (W - 1));
+      if (!sh[q].empty()) { sh[q + 1].insert(sh[q + 1].begin(), sh[q].back()); sh[q].pop_back(); }
+    }
+    std::vector<int64_t> cat;
+    for (int32_t q = 0; q < W; ++q) cat.insert(cat.end(), sh[q].begin(), sh[q].end());
+    should_fail = cat != merged;   // a swap of equal (or empty) neighbours leaves the concatenation alone
+    std::vector<const int64_t*> ptr(W);
+    std::vector<int64_t> F(W);
+    std::vector<uint64_t> H(W);
+    for (int32_t q = 0; q < W; ++q) {
+      ptr[q] = sh[q].data();
+      F[q] = (int64_t)sh[q].size();
+      H[q] = counts_hash(sh[q].data(), F[q]);
+    }
+    const std::string e1 = check_frame_concat(W, ptr.data(), F.data(), merged.data(), Fm);
+    const std::string e2 = check_frame_hashes(W, F.data(), H.data(), Fm, counts_hash(merged.data(), Fm));
+    CHECK(e1.empty() == !should_fail, "exact check kind %d: '%s'", kind, e1.c_str());
+    CHECK(e1.empty() == e2.empty(), "hash check disagrees (kind %d): '%s' vs '%s'", kind, e1.c_str(), e2.c_str());
+    (e1.empty() ? accepted : rejected) += 1;
+  }
+  // the advisor's example
+  const int64_t a[2] = {300, 100}, b[2] = {100, 300};
+  const int64_t* one[1] = {a};
+  const int64_t F1[1] = {2};
+  CHECK(!check_frame_concat(1, one, F1, b, 2).empty(), "[300,100] accepted as [100,300]");
+  CHECK(counts_hash(a, 2) != counts_hash(b, 2), "hash collision on the swap");
+  std::printf("frame-order checks: %ld accepted, %ld rejected\n", accepted, rejected);
+  CHECK(accepted > 500 && rejected > 500, "coverage");
+}
+
 int main() {
   std::mt19937_64 g(12345);
   test_batch(g);
   test_gather(g);
+  test_frame_order(g);
   std::printf("bad %d\n", bad);
   return bad > 255 ? 255 : bad;
 }

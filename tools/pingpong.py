@@ -7,6 +7,14 @@ step's buffers?  One step reads 1.2 GB and writes 0.96 GB (600 x 100k, SLERP), s
   pp4       four sets (8.6 GB)
   flush     set A, but a 2 GB streaming copy of unrelated buffers runs before every step
             (untimed; the kernel's events time the deskew kernel only)
+  fread     set A after a read-only 2 GB pass (mc_batch_checksum of an unrelated batch): the
+            Infinity Cache left full of clean lines
+  fwrite    set A after a write-only 2 GB pass (mc_batch_synth of that batch): left full of dirty
+            lines, whose write-back lands in the next kernel
+
+--libs runs every arm for several library builds in one process (one context per library), e.g.
+the production SLERP store policy (sc1 write-through) against a build with nt stores
+(-DMC_STORE_POINTS=1): which arm costs which store policy names the mechanism.
 
 Each arm: HIP events on every deskew launch (hipExtLaunchKernel start/stop); arms interleave over
 rounds in one process.  Each set is a separate allocation, so placement differs per set: the
@@ -50,8 +58,21 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pingpong.json"))
+    ap.add_argument("--libs", default="", help="comma list of library builds (default: the in-tree one)")
+    ap.add_argument("--arms", default="same,pp2,pp4,flush,fread,fwrite")
     args = ap.parse_args()
-    ctx = mc.Context(0)
+    libs = [l for l in args.libs.split(",") if l] or [None]
+    res = {}
+    for lib in libs:
+        run_lib(args, lib, res)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def run_lib(args, lib, res):
+    name = os.path.basename(lib) if lib else "in-tree"
+    ctx = mc.Context(0, lib_path=lib) if lib else mc.Context(0)
     sim = mc.LiDARMotionSimulator({"duration": 120.0, "trajectory_type": "figure_eight", "max_speed": 12.0,
                                    "lidar_fps": 10})
     tr = sim.add_sensor_noise(sim.generate_trajectory())
@@ -64,8 +85,10 @@ def main():
     n = int(counts.sum())
     flush_a = ctx.device_buffer(2 << 30)
     flush_b = ctx.device_buffer(2 << 30)
-    arms = {"same": [0], "pp2": [0, 1], "pp4": [0, 1, 2, 3], "flush": [0]}
-    res = {}
+    sweep = ctx.batch(np.full(1000, 100_000, np.int64), with_time=True)   # 100 M points x 5 columns = 2 GB
+    sweep.synth(seed=99, frame_id_base=0)
+    all_arms = {"same": [0], "pp2": [0, 1], "pp4": [0, 1, 2, 3], "flush": [0], "fread": [0], "fwrite": [0]}
+    arms = {a: all_arms[a] for a in args.arms.split(",")}
     for mode in args.modes.split(","):
         key = "xyz" if mode == "frame" else "in"
         per = {a: [] for a in arms}
@@ -83,6 +106,11 @@ def main():
                     if arm == "flush":                  # evict the MALL: 2 GB D2D copy, untimed
                         mc._lib.check(ctx.lib.mc_memcpy_d2d(ctx.handle, flush_b.ptr, flush_a.ptr, flush_a.nbytes),
                                       "memcpy_d2d")
+                    elif arm == "fread":                # 2 GB read-only sweep (clean lines)
+                        sweep.checksum()
+                    elif arm == "fwrite":               # 2 GB write-only sweep (dirty lines)
+                        sweep.synth(seed=99, frame_id_base=0)
+                        ctx.sync()
                     ctx.timing(True)
                     ctx.deskew(s[key], s["out"], mode=mode)
                     ctx.timing(False)
@@ -93,15 +121,18 @@ def main():
                     per_set[arm][s_id].append(us)
         for arm in arms:
             med = statistics.median(per[arm])
-            res[f"{mode}/{arm}"] = {"median_us": med, "min_us": min(per[arm]), "max_us": max(per[arm]),
+            res[f"{name}/{mode}/{arm}"] = {"median_us": med, "min_us": min(per[arm]), "max_us": max(per[arm]),
                                    "frac": BYTES[mode] * n / (med * 1e-6) / 8e12,
                                    "per_set_median_us": {str(s): statistics.median(v) for s, v in per_set[arm].items()}}
-            print(f"{mode:10s} {arm:6s} median {med:7.1f} us  ({BYTES[mode] * n / (med * 1e-6) / 1e9:6.0f} GB/s)  "
+            print(f"{name:16s} {mode:10s} {arm:6s} median {med:7.1f} us  ({BYTES[mode] * n / (med * 1e-6) / 1e9:6.0f} GB/s)  "
                   f"per set: {', '.join(f'{s}:{statistics.median(v):.1f}' for s, v in per_set[arm].items())}",
                   flush=True)
-    os.makedirs(os.path.dirname(args.out), exist_ok=True)
-    with open(args.out, "w") as f:
-        json.dump(res, f, indent=1)
+    sweep.close()
+    flush_a.close()
+    flush_b.close()
+    for s in sets:
+        for b in s.values():
+            b.close()
 
 
 if __name__ == "__main__":
