@@ -105,6 +105,24 @@ struct mc_ctx {
   // launch): set by async writers of the prep's inputs (t_ns spans) and by step-graph replays;
   // cleared by mc_deskew, whose deskew kernel then ends the queue (see mc_deskew)
   bool prep_fence = true;
+  // Per-call speculation (mc_deskew): a call whose inputs equal the previous call's launches its
+  // deskew fused with the prep of an identical next call into the other table half (the pipelined
+  // launch of mc_deskew_steps); the next call, if its key still matches, finds its tables ready and
+  // issues no k_prep.  Keys: the input batch's uid, mode, pose selection and the versions of every
+  // prep input (trajectory, IMU, the batch's frame times / starts / t_ns spans).
+  struct PrepKey {
+    uint64_t batch = 0, traj = 0, imu = 0, frames = 0;
+    int mode = -1, pose_select = -1;
+    bool operator==(const PrepKey& o) const {
+      return batch == o.batch && traj == o.traj && imu == o.imu && frames == o.frames && mode == o.mode &&
+             pose_select == o.pose_select;
+    }
+  };
+  PrepKey last_call;            // the previous mc_deskew's key (batch 0: none)
+  PrepKey spec_key;             // what the tables in half spec_half were prepared for
+  bool spec_valid = false;
+  int spec_half = 0;
+  uint64_t traj_ver = 0, imu_ver = 0;   // bumped by mc_set_trajectory / mc_set_imu
   hipEvent_t ev_main_done[2] = {nullptr, nullptr};
   hipEvent_t ev_prep_done[2] = {nullptr, nullptr};
   hipEvent_t ev_order = nullptr;  // orders side-stream prep after async main-stream staging
@@ -160,6 +178,8 @@ struct mc_ctx {
 
 struct mc_batch {
   mc_ctx* ctx = nullptr;
+  uint64_t uid = 0;         // unique per batch ever created (a key can never match a new batch)
+  uint64_t prep_ver = 0;    // bumped whenever frame times, frame starts or the t_ns spans change
   int32_t F = 0;
   int64_t N = 0;    // valid points
   int64_t P = 0;    // padded points (poff[F]; every frame starts on a kBlkPts boundary)

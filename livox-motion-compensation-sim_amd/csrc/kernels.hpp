@@ -52,8 +52,14 @@ namespace mc {
 #ifndef MC_NT_LOAD
 #define MC_NT_LOAD 1         // non-temporal input loads (streamed once): +5-8% measured (tools/ab.py)
 #endif
-#ifndef MC_POINTS_WAVES
-#define MC_POINTS_WAVES 4    // min waves/SIMD requested for the per-point kernels (0: compiler's choice)
+#ifndef MC_SLERP_WAVES
+#define MC_SLERP_WAVES 4     // waves/SIMD the SLERP kernel is compiled for (VGPR budget 512 / waves)
+#endif
+#ifndef MC_IMU_PRELOAD
+#define MC_IMU_PRELOAD 1     // IMU: both window records loaded before the wave's segment vote
+#endif
+#ifndef MC_IMU_WAVES
+#define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
 #endif
 
 constexpr int kBlock = 256;                    // 4 waves of 64
@@ -721,7 +727,8 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     w.tier = window_tier<MODE>(MODE == 1 ? ang : imu_angle_bound(ang, tr));
     if (lane == 0) a.fwin[f] = w;
   }
-  if (!MC_SUBTILE_WIN || W <= MC_FASTPATH_MAXW || !a.swin) return;
+  // (IMU: every frame, so the deskew kernel reads only its sub-tile's window, one scalar load)
+  if (!MC_SUBTILE_WIN || (MODE == 1 && W <= MC_FASTPATH_MAXW) || !a.swin) return;
   // A wide frame (IMU: ~20 samples per 0.1 s frame): each 1024-point sub-tile of a time-ordered
   // frame spans ~1 ms, so its own window is 1-2 segments and takes the SGPR path (no LDS staging,
   // no barrier: -10 % kernel time on SLERP, tools/ab.py).  Lane per sub-tile; segment of t =
@@ -891,38 +898,58 @@ __device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a, const uint
 #endif
 constexpr int kQuadGroups = kBlock / 4;   // float4 groups per workgroup in the quad decomposition
 
+// MC_FRAME_QUAD_U quarters (64 float4 groups each) per workgroup: each lane issues U column loads
+// before any arithmetic, so a wave keeps U KB in flight through its longer float64 chain.
+#ifndef MC_FRAME_QUAD_U
+#define MC_FRAME_QUAD_U 2    // frame f64: 294.8 us vs 304.0 (U=1), 308.0 (U=4), 297.9 (one group per lane), r2 f32 292.6 (profiles/round3/s05)
+#endif
+constexpr int kQuadU = MC_FRAME_QUAD_U;
+static_assert(kQuadU == 1 || kQuadU == 2 || kQuadU == 4, "quarters per workgroup: 1, 2 or 4");
+constexpr int kQuadUnitsPerSub = kBlock / kQuadGroups / kQuadU;   // workgroup units per sub-tile
+
 __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uint32_t pre) {
-  const int64_t n_units = (int64_t)a.n_tiles * kSub * (kBlock / kQuadGroups);
+  const int64_t n_units = (int64_t)a.n_tiles * kSub * kQuadUnitsPerSub;
   const uint32_t nb = gridDim.x - pre;
   const int c = threadIdx.x & 3;
   for (int64_t it = blockIdx.x - pre; it < n_units; it += nb) {
     const int64_t un = nb >= n_units ? xcd_unit<MC_XCD_FRAME>(it, n_units) : it;
-    const int64_t st = un / (kBlock / kQuadGroups);
+    const int64_t st = un / kQuadUnitsPerSub;
     const Tile tl = ldu(a.tiles + st / kSub);
-    const int g0 = (int)(st % kSub) * kBlock + (int)(un % (kBlock / kQuadGroups)) * kQuadGroups;
-    if (g0 >= tl.ngroups) continue;   // uniform: empty quarter of a short sub-tile
-    const int g = g0 + (threadIdx.x >> 2);
-    const bool act = g < tl.ngroups;   // uniform over a quad
-    const int64_t p = tl.pstart + 4 * (int64_t)g;
+    const int g0 = (int)(st % kSub) * kBlock + (int)(un % kQuadUnitsPerSub) * kQuadGroups * kQuadU;
+    if (g0 >= tl.ngroups) continue;   // uniform: empty part of a short sub-tile
     // lane c's row of [R | t] (lane 3: row 2, unused) as a vector load beside the point load: the
     // 96-byte table row set is L2-resident, and a per-lane select of three SGPR rows would cost 32
     // VALU instructions (two SGPR sources cannot meet in one v_cndmask)
     const FrameRow r = *(a.frame_tbl + 3 * tl.frame + (c < 2 ? c : 2));
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (act) v = ld4(a.in + bidx((int)a.in_C, c, p));
-    // every lane takes part in the broadcasts (inactive quads carry zeros)
-    float4 X, Y, Z;
-    X.x = quad_bcast<0>(v.x); X.y = quad_bcast<0>(v.y); X.z = quad_bcast<0>(v.z); X.w = quad_bcast<0>(v.w);
-    Y.x = quad_bcast<1>(v.x); Y.y = quad_bcast<1>(v.y); Y.z = quad_bcast<1>(v.z); Y.w = quad_bcast<1>(v.w);
-    Z.x = quad_bcast<2>(v.x); Z.y = quad_bcast<2>(v.y); Z.z = quad_bcast<2>(v.z); Z.w = quad_bcast<2>(v.w);
-    float4 o;
-    o.x = xf_row(r, X.x, Y.x, Z.x);
-    o.y = xf_row(r, X.y, Y.y, Z.y);
-    o.z = xf_row(r, X.z, Y.z, Z.z);
-    o.w = xf_row(r, X.w, Y.w, Z.w);
-    if (act) st_frame(a.out + bidx((int)a.out_C, c, p), c == 3 ? v : o);
+    float4 v[kQuadU];
+    bool act[kQuadU];
+    int64_t p[kQuadU];
+#pragma unroll
+    for (int u = 0; u < kQuadU; ++u) {
+      const int g = g0 + u * kQuadGroups + (threadIdx.x >> 2);
+      act[u] = g < tl.ngroups;   // uniform over a quad
+      p[u] = tl.pstart + 4 * (int64_t)g;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (act[u]) v[u] = ld4(a.in + bidx((int)a.in_C, c, p[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < kQuadU; ++u) {
+      // every lane takes part in the broadcasts (inactive quads carry zeros)
+      const float4 w = v[u];
+      float4 X, Y, Z;
+      X.x = quad_bcast<0>(w.x); X.y = quad_bcast<0>(w.y); X.z = quad_bcast<0>(w.z); X.w = quad_bcast<0>(w.w);
+      Y.x = quad_bcast<1>(w.x); Y.y = quad_bcast<1>(w.y); Y.z = quad_bcast<1>(w.z); Y.w = quad_bcast<1>(w.w);
+      Z.x = quad_bcast<2>(w.x); Z.y = quad_bcast<2>(w.y); Z.z = quad_bcast<2>(w.z); Z.w = quad_bcast<2>(w.w);
+      float4 o;
+      o.x = xf_row(r, X.x, Y.x, Z.x);
+      o.y = xf_row(r, X.y, Y.y, Z.y);
+      o.z = xf_row(r, X.z, Y.z, Z.z);
+      o.w = xf_row(r, X.w, Y.w, Z.w);
+      if (act[u]) st_frame(a.out + bidx((int)a.out_C, c, p[u]), c == 3 ? w : o);
+    }
   }
 }
+
 
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
 #if MC_FRAME_QUAD
@@ -1247,12 +1274,30 @@ __device__ __forceinline__ void points_peeled(const int seg[4], RecOf rec_of, co
   }
 }
 
+// a or b by a wave-uniform condition, dword by dword (s_cselect; no private array)
+template <typename T>
+__device__ __forceinline__ T select_rec(bool second, const T& a, const T& b) {
+  struct Raw { int v[sizeof(T) / 4]; };
+  const Raw ra = __builtin_bit_cast(Raw, a), rb = __builtin_bit_cast(Raw, b);
+  Raw r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) r.v[i] = second ? rb.v[i] : ra.v[i];
+  return __builtin_bit_cast(T, r);
+}
+
 // The SGPR path of a window of <= 2 segments at tier TIER: each wave votes whether its points all
 // sit in one segment; a wave across the boundary peels its two segments.
 template <int MODE, int TIER>
 __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin& fw, bool act, const int4& Tq,
                                           float4& X, float4& Y, float4& Z) {
   const PolyOf<TIER> poly = poly_load<TIER>();
+  // IMU: both 64-byte records in SGPRs before the vote (their scalar-load latency then overlaps the
+  // point loads instead of following the vote); a 144-byte SLERP record pair would not fit
+  WinOf<MODE> r0, r1;
+  if constexpr (MODE == 2 && MC_IMU_PRELOAD) {
+    r0 = ldu(rec);
+    r1 = ldu(rec + (fw.W == 2 ? 1 : 0));
+  }
   bool use1 = false, mixed = false;
   if (fw.W == 2) {
     const int64_t b1 = fw.bnd1;
@@ -1266,13 +1311,18 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
     // every lane computes (a partial wave's idle lanes on zeros, their results never stored): under
     // `if (act)` the compiler sank the record load into the divergent block as 9 per-lane vector
     // loads of the 144-byte record instead of scalar loads
-    const WinOf<MODE> w = ldu(rec + (use1 ? 1 : 0));
+    WinOf<MODE> w;
+    if constexpr (MODE == 2 && MC_IMU_PRELOAD) w = select_rec(use1, r0, r1);
+    else w = ldu(rec + (use1 ? 1 : 0));
     points4<MODE>(w, poly, Tq, X, Y, Z);
   } else {
     int seg[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) seg[c] = act ? ((int64_t)i4c(Tq, c) >= fw.bnd1 ? 1 : 0) : -1;
-    points_peeled<MODE>(seg, [&](int j) { return ldu(rec + j); }, poly, Tq, X, Y, Z);
+    if constexpr (MODE == 2 && MC_IMU_PRELOAD)
+      points_peeled<MODE>(seg, [&](int j) { return select_rec(j != 0, r0, r1); }, poly, Tq, X, Y, Z);
+    else
+      points_peeled<MODE>(seg, [&](int j) { return ldu(rec + j); }, poly, Tq, X, Y, Z);
   }
 }
 
@@ -1290,7 +1340,7 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
 // k_deskew_frame_next comment)
 // (NEXT: at least 4 waves / SIMD like the plain kernel — the prep body alone would take 172 VGPRs)
 template <int MODE, bool NEXT = false>
-__global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS_WAVES : 1)) void k_deskew_points(
+__global__ __launch_bounds__(kBlock, MODE == 1 ? MC_SLERP_WAVES : MC_IMU_WAVES) void k_deskew_points(
     const DeskewArgs a, const PrepArgs pn, const uint32_t pre) {
   if constexpr (NEXT) {
     if (blockIdx.x < pre) {
@@ -1313,35 +1363,26 @@ __global__ __launch_bounds__(kBlock, NEXT ? 4 : (MC_POINTS_WAVES > 0 ? MC_POINTS
                                     : (a.xcd_order ? xcd_unit<1>(it, n_sub) : xcd_unit<MC_XCD_SLERP>(it, n_sub)));
     const Tile tl = ldu(a.tiles + st / kSub);
     // IMU frames always span several samples: fetch the sub-tile window with the tile record
-    FrameWin sw;
-    if constexpr (MODE == 2) sw = ldu(a.swin + st);
     const int g0 = (int)(st % kSub) * kBlock;
     if (g0 >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
     const int f = tl.frame;
     const int g = g0 + tid;
     const bool act = g < tl.ngroups;
     const int64_t p = tl.pstart + 4 * (int64_t)g;
-    float4 X, Y, Z, I;
-    int4 Tq;
-    const float* q = a.in + bidx((int)a.in_C, 0, p);   // the float4 group never straddles a block
-    const FrameWin ff = ldu(a.fwin + f);
-    // frames wider than the SGPR path take their sub-tile's own window (k_prep)
-    const bool sub = MC_SUBTILE_WIN && ff.W > MC_FASTPATH_MAXW;
-    if constexpr (MODE != 2) {
-      if (sub) sw = ldu(a.swin + st);
-    }
-    const FrameWin fw = sub ? sw : ff;
+    // Every lane loads and computes (a short sub-tile's idle lanes re-read its first group; their
+    // results are never stored): no divergent load block, so nothing makes the point loads wait for
+    // the window records, and the records stay scalar loads in uniform control flow.
+    const float* q = a.in + bidx((int)a.in_C, 0, act ? p : tl.pstart + 4 * (int64_t)g0);
+    const int4 Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts));
+    float4 X = ld4(q), Y = ld4(q + kBlkPts), Z = ld4(q + 2 * kBlkPts);
+    const float4 I = ld4(q + 3 * kBlkPts);
+    // frames wider than the SGPR path take their sub-tile's own window (k_prep writes one for every
+    // IMU sub-tile).  One scalar load of the chosen record (a select of two loaded structs became a
+    // vector load of bnd1 whose wait held back the point loads)
+    bool sub = true;
+    if constexpr (MODE != 2) sub = MC_SUBTILE_WIN && ldu(a.fwin + f).W > MC_FASTPATH_MAXW;
+    const FrameWin fw = ldu(sub ? a.swin + st : a.fwin + f);
     const Win* rec = sub ? srec + 2 * st : frec + 2 * f;
-    if (act) {
-      Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts));
-      X = ld4(q);
-      Y = ld4(q + kBlkPts);
-      Z = ld4(q + 2 * kBlkPts);
-      I = ld4(q + 3 * kBlkPts);
-    } else {
-      Tq = make_int4(0, 0, 0, 0);
-      X = Y = Z = I = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
 
     if (fw.W <= MC_FASTPATH_MAXW) {
       // the tier k_prep chose for the window: its coefficient load is issued here, beside the point

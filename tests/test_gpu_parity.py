@@ -577,7 +577,9 @@ def test_timing_counts_launches(mc, gpu_ctx):
         gpu_ctx.deskew(b, out, mode="pose_slerp")
     t = gpu_ctx.read_timing()
     gpu_ctx.timing(False)
-    assert t["main_launches"] == 3 and t["prep_launches"] == 3 and t["main_ms"] > 0
+    # calls 1 and 2 run k_prep; call 2's launch also prepares call 3's tables (identical key), so
+    # call 3 needs none (mc_deskew's per-call speculation, test_gpu_steps.py)
+    assert t["main_launches"] == 3 and t["prep_launches"] == 2 and t["main_ms"] > 0
 
 
 def test_rccl_gather_single_rank(mc, gpu_ctx):

@@ -173,3 +173,68 @@ def test_steps_argument_errors(mc, gpu_ctx):
         gpu_ctx.deskew_steps(b, other, 2, mode="frame")
     for x in (other, out, b):
         x.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# per-call speculation (mc_deskew): a repeated call finds its tables prepared by the previous launch
+# ---------------------------------------------------------------------------------------------
+def _fresh(mc, counts, mode, setup):
+    """The reference bytes: the same call on a fresh context (no speculation history)."""
+    ctx = mc.Context(0)
+    b, tr, times = _setup(mc, ctx, counts)
+    setup(ctx, b)
+    out = ctx.deskew(b, ctx.batch(b.counts), mode=mode)
+    return _cols(out)
+
+
+@pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
+def test_repeated_calls_speculate_and_every_input_change_misses(mc, gpu_ctx, mode):
+    """Identical calls after the first skip their k_prep (the previous launch prepared the tables);
+    any change to a prep input between calls — trajectory, IMU table, frame times, frame starts, t_ns,
+    another batch in between, a step sequence in between — must give the bytes of a fresh call."""
+    counts = [3000, 0, 1, 257, 20_000, 1023, 4097]
+    ctx = gpu_ctx
+    b, tr, times = _setup(mc, ctx, counts)
+    out = ctx.batch(b.counts)
+    ref = _fresh(mc, counts, mode, lambda c, bb: None)
+    ctx.read_timing()
+    ctx.timing(True)
+    for _ in range(5):
+        ctx.deskew(b, out, mode=mode)
+        assert np.array_equal(_cols(out), ref)
+    t = ctx.read_timing()
+    ctx.timing(False)
+    assert t["main_launches"] == 5
+    assert t["prep_launches"] == 2, t      # calls 1 and 2 prepare; 3.. find the tables ready
+    rng = np.random.default_rng(5)
+    tr2 = {k: v.copy() for k, v in tr.items()}
+    tr2["orientation_imu"] = tr2["orientation_imu"] + rng.normal(0, 0.05, tr2["orientation_imu"].shape)
+    tr2["position_gps"] = tr2["position_gps"] + 1.5
+    ts, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    t_new = rng.integers(0, 100_000_000, int(np.sum(counts))).astype(np.int32)
+    changes = [
+        ("trajectory", lambda c, bb: c.set_trajectory(tr2["time"], tr2["position_gps"], tr2["orientation_imu"])),
+        ("imu", lambda c, bb: c.set_imu(ts, gyro * 1.7)),
+        ("frame_times", lambda c, bb: bb.set_frame_times(times + 0.013)),
+        ("frame_starts", lambda c, bb: bb.set_frame_starts((times * 1e9).astype(np.int64) + 7_000_000)),
+        ("t_ns", lambda c, bb: bb.upload_time(t_new)),
+    ]
+    applied = []
+    for name, fn in changes:
+        fn(ctx, b)
+        applied.append(fn)
+        want = _fresh(mc, counts, mode, lambda c, bb, fs=tuple(applied): [f(c, bb) for f in fs])
+        for _ in range(3):   # the miss, then speculation on the new inputs
+            ctx.deskew(b, out, mode=mode)
+            assert np.array_equal(_cols(out), want), name
+    # another batch in between (its own key), then back; a pipelined step sequence in between
+    other = ctx.batch(np.asarray([500, 7]), with_time=True)
+    other.synth(seed=9, frame_id_base=0)
+    other.set_frame_times(times[:2])
+    other.set_frame_starts((times[:2] * 1e9).astype(np.int64))
+    o2 = ctx.batch(other.counts)
+    for k in range(6):
+        ctx.deskew(other if k % 2 else b, o2 if k % 2 else out, mode=mode)
+    ctx.deskew_steps(b, out, 3, mode=mode, pipeline=True)
+    ctx.deskew(b, out, mode=mode)
+    assert np.array_equal(_cols(out), want)

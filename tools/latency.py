@@ -27,6 +27,43 @@ def timed(fn, calls):
     return (time.perf_counter() - t0) / calls
 
 
+def per_call_deskew(ctx, tr, sim, calls=200):
+    """The drop-in per-call API on device-resident batches (Context.deskew = mc_deskew, each call
+    synchronised like the reference's synchronous calls): wall time per call vs the deskew kernel's
+    HIP-event time, per mode and frame shape.  Repeated identical calls hit mc_deskew's speculation
+    (the previous launch prepared this call's tables), so the gap is launch + sync only."""
+    res = {}
+    ts, g = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    ctx.set_imu(ts, g)
+    times_all = sim.lidar_times()
+    for frames, n in ((1, 1600), (1, 100_000), (600, 100_000)):
+        times = times_all[:frames]
+        b = ctx.batch(np.full(frames, n, np.int64), with_time=True)
+        b.synth(seed=0, frame_id_base=1000)
+        b.set_frame_times(times)
+        b.set_frame_starts((times * 1e9).astype(np.int64))
+        o = ctx.batch(b.counts)
+        for mode in ("pose_slerp", "imu", "frame"):
+            for _ in range(5):
+                ctx.deskew(b, o, mode=mode)
+            ctx.sync()
+            ctx.read_timing()
+            ctx.timing(True)
+            t0 = time.perf_counter()
+            for _ in range(calls):
+                ctx.deskew(b, o, mode=mode)
+                ctx.sync()
+            wall = (time.perf_counter() - t0) / calls * 1e6
+            ctx.timing(False)
+            t = ctx.read_timing()
+            kern = t["main_ms"] / max(t["main_launches"], 1) * 1e3
+            res[f"{mode}/{frames}x{n}"] = {"call_us": wall, "kernel_us": kern, "gap_us": wall - kern,
+                                           "prep_launches": t["prep_launches"], "calls": calls}
+        b.close()
+        o.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=1600)
@@ -65,6 +102,7 @@ def main():
         mc._lib.check(ctx.lib.mc_align_frames_host_f64(ctx.handle, F, fp, pt(counts, c_int64), pt(lds, c_int64),
                                                        pt(tt, c_double), 0, op))
     out["align_call_only_ms"] = timed(call, 5) * 1e3
+    out["mc_deskew_per_call"] = per_call_deskew(ctx, tr, sim)
     idx = R.select_pose_index(tr["time"], times)
     t = timed(lambda: [R.transform_pointcloud(s, {"translation": tr["position_gps"][k],
                                                   "rotation": tr["orientation_imu"][k]})
