@@ -1607,7 +1607,60 @@ __device__ __forceinline__ void stage_tile_lds_out(const LayoutArgs& a, const Ti
 constexpr int kStageQuarters = kTileGroups / kQuadGroups;   // 256-point units per tile
 constexpr int kUnitRow = kQuadGroups * 4 + 4;              // LDS floats per column (+4: banks)
 
+// MC_STAGE_UNITS consecutive 256-point units (one tile's) per workgroup pass: every lane issues its
+// U column loads before the first LDS write, so a workgroup keeps U x 4 KB of reads in flight
+// through its barrier-separated store phase.
+#ifndef MC_STAGE_UNITS
+#define MC_STAGE_UNITS 1
+#endif
+constexpr int kStageU = MC_STAGE_UNITS;
+static_assert(kStageQuarters % kStageU == 0, "a pass stays inside one tile");
+
+template <int U>
+__device__ __forceinline__ void soa_to_aos_units(const LayoutArgs& a, double* __restrict__ aos) {
+  __shared__ float s[U][4 * kUnitRow];
+  const int64_t n_passes = (int64_t)a.n_tiles * (kStageQuarters / U);
+  const int t = threadIdx.x;
+  const int c = t >> 6, gi = t & 63;
+  for (int64_t it = blockIdx.x; it < n_passes; it += gridDim.x) {
+    const int64_t ps = gridDim.x >= n_passes ? xcd_unit<MC_XCD_STAGE>(it, n_passes) : it;
+    const Tile tl = ldu(a.tiles + ps / (kStageQuarters / U));
+    const int gb = (int)(ps % (kStageQuarters / U)) * U * kQuadGroups;   // first group of the pass
+    if (gb >= tl.ngroups) continue;   // uniform
+    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = gb + u * kQuadGroups + gi;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (g < tl.ngroups) v[u] = ld4(a.cols + bidx(a.C, c, tl.pstart + 4 * (int64_t)g));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) *reinterpret_cast<float4*>(&s[u][c * kUnitRow + 4 * gi]) = v[u];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p0 = tl.pstart + 4 * (int64_t)(gb + u * kQuadGroups);
+      const int64_t loc0 = p0 - poff;
+      v2d* d = reinterpret_cast<v2d*>(aos + (doff - a.dbase + loc0) * 4);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int i = t + h2 * kBlock, r = i >> 1, h = i & 1;
+        if (loc0 + r < cnt) {
+          const v2d w = {(double)s[u][(2 * h) * kUnitRow + r], (double)s[u][(2 * h + 1) * kUnitRow + r]};
+          st_pol<MC_STAGE_ST>(reinterpret_cast<float*>(d + i), __builtin_bit_cast(float4, w));
+        }
+      }
+    }
+    __syncthreads();   // s is rewritten by the next pass
+  }
+}
+
 __device__ __forceinline__ void soa_to_aos_unit(const LayoutArgs& a, double* __restrict__ aos) {
+  if constexpr (kStageU > 1) {
+    soa_to_aos_units<kStageU>(a, aos);
+    return;
+  }
   __shared__ float s[4 * kUnitRow];
   const int64_t n_units = (int64_t)a.n_tiles * kStageQuarters;
   const int t = threadIdx.x;

@@ -50,6 +50,10 @@ static_assert(mcimpl::kBatchBlock == kBlkPts && mcplan::kBlk == kBlkPts, "batch 
 static int32_t stage_units(int32_t n_tiles, int64_t ld) {
   return (MC_STAGE_QUAD && ld == 4) ? n_tiles * kStageQuarters : n_tiles;
 }
+// ... of the SoA -> AoS launch (kStageU units per workgroup pass)
+static int32_t fetch_units(int32_t n_tiles) {
+  return MC_STAGE_QUAD ? n_tiles * (kStageQuarters / kStageU) : n_tiles;
+}
 static_assert(sizeof(mcplan::TileRec) == sizeof(Tile) && offsetof(mcplan::TileRec, frame) == offsetof(Tile, frame) &&
                   offsetof(mcplan::TileRec, ngroups) == offsetof(Tile, ngroups),
               "host tile records are uploaded as mc::Tile");
@@ -397,7 +401,7 @@ static int launch_fetch(mc_batch* b, double* d_aos) {
   queued_async(c);
   {
     TimedRegion tr(c, &c->layout_ev, c->stream);
-    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, stage_units(b->n_tiles, 4))), dim3(kBlock), 0, c->stream,
+    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, fetch_units(b->n_tiles))), dim3(kBlock), 0, c->stream,
                        layout_of(b), d_aos);
   }
   HIPCHK(hipGetLastError());
@@ -533,7 +537,7 @@ int mc_batch_download_frames_aos_f64(mc_batch* b, int32_t f0, int32_t f1, double
   a.n_tiles = b->ftile[f1] - b->ftile[f0];
   a.dbase = b->doff[f0];
   if (a.n_tiles > 0)
-    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, stage_units(a.n_tiles, 4))), dim3(kBlock), 0, c->stream, a,
+    hipLaunchKernelGGL(k_soa_to_aos, dim3(launch_grid(c, fetch_units(a.n_tiles))), dim3(kBlock), 0, c->stream, a,
                        static_cast<double*>(st));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(aos, st, (size_t)rows * 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));

@@ -11,6 +11,10 @@ step's buffers?  One step reads 1.2 GB and writes 0.96 GB (600 x 100k, SLERP), s
             Infinity Cache left full of clean lines
   fwrite    set A after a write-only 2 GB pass (mc_batch_synth of that batch): left full of dirty
             lines, whose write-back lands in the next kernel
+  f256      as flush, with a 256 MB copy (the Infinity Cache's size) instead of 2 GB
+  fslerp    set A after a SLERP deskew of the unrelated 100 M-point batch (1.6 GB written with the
+            production SLERP store policy)
+  fidle     set A after 2 ms of host sleep (the device idles between steps)
 
 --libs runs every arm for several library builds in one process (one context per library), e.g.
 the production SLERP store policy (sc1 write-through) against a build with nt stores
@@ -29,6 +33,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 import numpy as np
 
@@ -87,7 +92,10 @@ def run_lib(args, lib, res):
     flush_b = ctx.device_buffer(2 << 30)
     sweep = ctx.batch(np.full(1000, 100_000, np.int64), with_time=True)   # 100 M points x 5 columns = 2 GB
     sweep.synth(seed=99, frame_id_base=0)
-    all_arms = {"same": [0], "pp2": [0, 1], "pp4": [0, 1, 2, 3], "flush": [0], "fread": [0], "fwrite": [0]}
+    sweep.set_frame_times(sim.lidar_times()[:1000])
+    sweep_out = ctx.batch(sweep.counts)
+    all_arms = {"same": [0], "pp2": [0, 1], "pp4": [0, 1, 2, 3], "flush": [0], "fread": [0], "fwrite": [0],
+                "f256": [0], "fslerp": [0], "fidle": [0]}
     arms = {a: all_arms[a] for a in args.arms.split(",")}
     for mode in args.modes.split(","):
         key = "xyz" if mode == "frame" else "in"
@@ -111,6 +119,14 @@ def run_lib(args, lib, res):
                     elif arm == "fwrite":               # 2 GB write-only sweep (dirty lines)
                         sweep.synth(seed=99, frame_id_base=0)
                         ctx.sync()
+                    elif arm == "f256":                 # 256 MB D2D copy
+                        mc._lib.check(ctx.lib.mc_memcpy_d2d(ctx.handle, flush_b.ptr, flush_a.ptr, 256 << 20),
+                                      "memcpy_d2d")
+                    elif arm == "fslerp":               # SLERP deskew of another 100 M points
+                        ctx.deskew(sweep, sweep_out, mode="pose_slerp")
+                    elif arm == "fidle":                # the device idles 2 ms
+                        ctx.sync()
+                        time.sleep(0.002)
                     ctx.timing(True)
                     ctx.deskew(s[key], s["out"], mode=mode)
                     ctx.timing(False)
@@ -128,6 +144,7 @@ def run_lib(args, lib, res):
                   f"per set: {', '.join(f'{s}:{statistics.median(v):.1f}' for s, v in per_set[arm].items())}",
                   flush=True)
     sweep.close()
+    sweep_out.close()
     flush_a.close()
     flush_b.close()
     for s in sets:
