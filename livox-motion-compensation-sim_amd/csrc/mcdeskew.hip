@@ -718,9 +718,10 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (mode == MC_MODE_FRAME && MC_FRAME_QUAD) units = in->n_tiles * kSub * kQuadUnitsPerSub;
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
-  // SLERP sub-tile order: dealt over the XCDs for batches up to ~200 M points (326 vs 340 us at
-  // 600 x 100k), XCD-contiguous above (1682 vs 1890 us at 3000 x 100k, 3434 vs 3713 at 6000; the
-  // dealt order is also bimodal by placement at 2400) — profiles/round2/s30-s32
+  // SLERP sub-tile order: XCD-contiguous at every size since round 3 (MC_XCD_SLERP=1; float64 math:
+  // 342.9 vs 356.0 us at 600 x 100k, profiles/round3/s08).  A build with MC_XCD_SLERP=0 keeps the
+  // round-2 rule: dealt up to ~200 M points, XCD-contiguous above (1682 vs 1890 us at 3000 x 100k,
+  // 3434 vs 3713 at 6000; profiles/round2/s30-s32)
   da.xcd_order = (mode == MC_MODE_POSE_SLERP && in->P >= kSlerpXcdMinPoints) ? 1 : 0;
   sp->lds = mode == MC_MODE_FRAME ? 0u : points_lds_reserve();
 }
