@@ -527,6 +527,59 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     return rep
 
 
+def measure_deskew_pcd(ctx, b_in, b_out, mode, n_rank, reps):
+    """SURVEY §8f row 3 fused with the path, both pipelines on the same batch, interleaved:
+      separate  mc_deskew, then mc_pcd_encode_batch (measure pass + write pass)
+      fused     mc_deskew_pcd: the deskew kernel also sums each 256-point block's ASCII PCD text
+                bytes, then the write pass alone
+    The fused PCD's cost is the write pass plus what the sums add to the deskew kernel (fused kernel
+    minus the separate pipeline's plain kernel)."""
+    from ctypes import c_int64
+    counts = np.ascontiguousarray(b_out.counts, np.int64)
+    pos = np.zeros(len(counts) + 1, np.int64)
+    cap = int(counts.sum()) * 48
+    buf = ctx.device_buffer(cap)
+    ptr = mc._lib.ptr
+    arms = {"separate": [], "fused": []}
+    try:
+        def separate():
+            ctx.deskew(b_in, b_out, mode=mode)
+            mc._lib.check(ctx.lib.mc_pcd_encode_batch(ctx.handle, b_out.handle, buf.ptr, cap, ptr(pos, c_int64)),
+                          "pcd_encode_batch")
+
+        def fused():
+            mc._lib.check(ctx.lib.mc_deskew_pcd(ctx.handle, b_in.handle, b_out.handle, mc._lib.MODES[mode],
+                                                mc._lib.POSE_SELECT["searchsorted"], buf.ptr, cap, ptr(pos, c_int64)),
+                          "deskew_pcd")
+        for fn in (separate, fused):
+            fn()
+        ctx.sync()
+        ctx.read_timing()
+        for _ in range(reps):
+            for name, fn in (("separate", separate), ("fused", fused)):
+                ctx.timing(True)
+                fn()
+                ctx.timing(False)
+                arms[name].append(ctx.read_timing())
+    finally:
+        buf.close()
+
+    def med(name, key):
+        return float(np.median([t[key + "_ms"] / max(t[key + "_launches"], 1) * t[key + "_launches"] for t in arms[name]]))
+    k_sep, k_fus = med("separate", "main"), med("fused", "main")
+    c_sep, c_fus = med("separate", "codec"), med("fused", "codec")
+    text_b = int(pos[-1])
+    alg = 16 * n_rank + text_b
+    pcd_fused_ms = c_fus + max(k_fus - k_sep, 0.0)
+    return {"mode": mode, "reps": reps, "text_bytes": text_b,
+            "separate": {"deskew_kernel_us": k_sep * 1e3, "pcd_kernels_ms": c_sep, "total_ms": k_sep + c_sep},
+            "fused": {"deskew_pcd_kernel_us": k_fus * 1e3, "write_ms": c_fus, "total_ms": k_fus + c_fus},
+            "pcd_ms": pcd_fused_ms, "GBs": alg / pcd_fused_ms / 1e6, "frac": alg / pcd_fused_ms / 1e6 / HBM_PEAK_GBS,
+            "frac_separate": alg / c_sep / 1e6 / HBM_PEAK_GBS,
+            "note": "fused PCD cost = write pass + (deskew_pcd kernel - plain deskew kernel), medians over interleaved "
+                    "calls; HBM bytes = 16 B/pt read + the text written (as codecs.pcd_ascii)"}
+
+
 # ---------------------------------------------------------------------------------------------
 # the merged-cloud gather (N > 1)
 # ---------------------------------------------------------------------------------------------
@@ -774,6 +827,7 @@ def main():
         ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
         ctx.deskew(b_in, b_out, mode=args.mode)
         codecs = measure_codecs(ctx, b_out, n_rank, 5, 0.0 if (args.no_cpu or world > 1) else 1.0)
+        codecs["pcd_ascii_fused"] = measure_deskew_pcd(ctx, src_of[args.mode], b_out, args.mode, n_rank, 5)
 
     imu = (ts_imu, gyro)
     F_all = len(counts_all)

@@ -187,6 +187,15 @@ int mc_pcd_encode(mc_ctx* ctx, const double* d_aos, int64_t ld, int32_t n_frames
 int mc_lvx_encode_batch(mc_ctx* ctx, const mc_batch* b, const uint64_t* frame_ids, const uint64_t* timestamp_ns,
                         void* d_out, int64_t out_bytes);
 int mc_pcd_encode_batch(mc_ctx* ctx, const mc_batch* b, void* d_out, int64_t out_bytes, int64_t* body_pos);
+/* Deskew -> ASCII PCD in one call: mc_deskew(in -> out) (out != in), whose kernel also sums each
+ * output block's text bytes, then the PCD lines of out as mc_pcd_encode_batch writes them, with no
+ * separate measure pass over out (the reference's LMC:831 -> 887-889 -> 932-948 sequence on
+ * device-resident frames; a block holding a value beyond the packed formatter, |v| >= 4294 / NaN /
+ * inf, falls back to the measure pass).  MC_ERR_SPACE as mc_pcd_encode_batch: out is deskewed and
+ * body_pos filled, no text written.  The deskew kernel is timed under mc_timing_read, the writer
+ * under mc_timing_read_codec. */
+int mc_deskew_pcd(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select, void* d_out,
+                  int64_t out_bytes, int64_t* body_pos);
 int mc_timing_read_codec(mc_ctx* ctx, double* ms_total, int64_t* launches);
 
 /* Synthetic Mid-70 frames generated on the device (counter-hash RNG, bit-identical to

@@ -89,6 +89,7 @@ _SIGS = {
     "mc_pcd_encode": (c_int, [c_void_p, c_void_p, c_int64, c_int32, _pi64, c_void_p, c_int64, _pi64]),
     "mc_lvx_encode_batch": (c_int, [c_void_p, c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_void_p, c_int64]),
     "mc_pcd_encode_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, _pi64]),
+    "mc_deskew_pcd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, _pi64]),
     "mc_timing_read_codec": (c_int, [c_void_p, _pd, _pi64]),
     "mc_batch_synth": (c_int, [c_void_p, c_uint64, c_int64]),
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),

@@ -10,6 +10,9 @@ the host only adds the constant headers and writes the bytes.
   save_pcd(points, filename)                                   LMC:932-948
   encode_lvx / encode_pcd / encode_pcd_frames                  the bytes, without a file
   encode_lvx_batch / encode_pcd_batch                          straight from a device Batch
+  deskew_pcd_batch / deskew_pcd_frames                         deskew -> PCD lines, the deskew
+                                                                kernel measuring the text (no
+                                                                separate measure pass)
 """
 from __future__ import annotations
 
@@ -228,6 +231,43 @@ def encode_pcd_batch(batch: Batch) -> List[bytes]:
             out.close()
         return [pcd_header(c) + text[pos[f]:pos[f + 1]] for f, c in enumerate(counts)]
     raise _lib.McError("pcd_encode_batch: output size changed between passes")
+
+
+def deskew_pcd_batch(inp: Batch, out: Batch, mode: str = "frame", pose_select: str = "searchsorted",
+                     text=None):
+    """Deskew ``inp`` into ``out`` and write out's ASCII PCD point lines, both on the device
+    (mc_deskew_pcd: the deskew kernel sums each block's text bytes, so the writer needs no measure
+    pass over ``out``) — LMC:831 -> 887-889 -> 932-948 on device-resident frames.  Returns
+    (device text buffer, body_pos) with frame f's lines at [body_pos[f], body_pos[f+1]); ``text``: a
+    DeviceBuffer to reuse (grown when too small)."""
+    ctx = inp.ctx
+    if out is inp:
+        raise ValueError("deskew_pcd needs an output batch other than the input")
+    counts = np.ascontiguousarray(out.counts, np.int64)
+    pos = np.zeros(len(counts) + 1, np.int64)
+    cap = max(int(counts.sum()) * 48, 64)
+    if text is None or text.nbytes < cap:
+        if text is not None:
+            text.close()
+        text = ctx.device_buffer(cap)
+    rc = ctx.lib.mc_deskew_pcd(ctx.handle, inp.handle, out.handle, _lib.MODES[mode], _lib.POSE_SELECT[pose_select],
+                               text.ptr, text.nbytes, ptr(pos, c_int64))
+    if rc == _lib.MC_ERR_SPACE:   # out is deskewed: the plain writer with the size it reported
+        text.close()
+        text = ctx.device_buffer(int(pos[-1]))
+        rc = ctx.lib.mc_pcd_encode_batch(ctx.handle, out.handle, text.ptr, text.nbytes, ptr(pos, c_int64))
+    check(rc, f"deskew_pcd[{mode}]")
+    return text, pos
+
+
+def deskew_pcd_frames(inp: Batch, out: Batch, mode: str = "frame", pose_select: str = "searchsorted") -> List[bytes]:
+    """:func:`deskew_pcd_batch` with each frame's whole PCD file (header + lines) on the host."""
+    text, pos = deskew_pcd_batch(inp, out, mode, pose_select)
+    try:
+        body = text.to_host(np.uint8, count=int(pos[-1])).tobytes() if pos[-1] else b""
+    finally:
+        text.close()
+    return [pcd_header(int(c)) + body[pos[f]:pos[f + 1]] for f, c in enumerate(out.counts)]
 
 
 def save_pcd(points, filename: str, context: Context | None = None) -> None:

@@ -83,7 +83,7 @@ CodecFrames frames_of(const Source& src, const int64_t* d_doff, const int64_t* d
 int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, const uint64_t* frame_ids,
                const uint64_t* ts_ns, const uint8_t* has_int, void* d_out, int64_t out_bytes);
 int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, void* d_out, int64_t out_bytes,
-               int64_t* body_pos);
+               int64_t* body_pos, const int32_t* d_measured = nullptr);
 
 }  // namespace
 
@@ -204,12 +204,36 @@ int mc_pcd_encode_batch(mc_ctx* c, const mc_batch* b, void* d_out, int64_t out_b
   return pcd_encode(c, src, b->F, b->counts.data(), d_out, out_bytes, body_pos);
 }
 
+int mc_deskew_pcd(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, void* d_out,
+                  int64_t out_bytes, int64_t* body_pos) {
+  CHECK_ARG(c && in && out && body_pos, "NULL argument");
+  CHECK_ARG(out != in, "mc_deskew_pcd needs an output batch other than the input");
+  CHECK_ARG(out->ctx == c, "batch belongs to another context");
+  DeviceGuard g(c->device);
+  // one text-byte slot per 256-point block of the output batch (= one PCD tile)
+  const int64_t blocks = out->P / kBlkPts;
+  if (blocks > c->pcd_len_cap) {
+    if (c->d_pcd_len) { (void)hipStreamSynchronize(c->stream); dev_free(c->d_pcd_len); c->d_pcd_len = nullptr; }
+    c->pcd_len_cap = 0;
+    if (int r = dev_alloc(&c->d_pcd_len, (size_t)blocks)) return r;
+    c->pcd_len_cap = blocks;
+  }
+  if (int r = mcimpl::deskew_call(c, in, out, mode, pose_select, blocks > 0 ? c->d_pcd_len : nullptr)) return r;
+  Source src;
+  src.batch = out;
+  return pcd_encode(c, src, out->F, out->counts.data(), d_out, out_bytes, body_pos, c->d_pcd_len);
+}
+
 }  // extern "C"
 
 namespace {
 
+// d_measured (mc_deskew_pcd): the tiles' text bytes already written by the deskew kernel that
+// produced the batch (pcd_value_len sums per 256-point block = per tile); the measure pass is then
+// skipped unless a tile holds a value outside the packed path, whose exact length only the measure
+// pass forms.
 int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, void* d_out, int64_t out_bytes,
-               int64_t* body_pos) {
+               int64_t* body_pos, const int32_t* d_measured) {
   std::vector<int64_t> doff;
   if (int r = check_frames(F, counts, doff)) return r;
   CHECK_ARG(doff[F] == 0 || src.aos || src.batch, "points pointer is NULL");
@@ -240,17 +264,26 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   a.tile_pos = reinterpret_cast<const int64_t*>(d + o_tp);
   a.out = static_cast<char*>(d_out);
   a.err = c->d_codec_err;
-  {
-    TimedRegion tr(c, &c->codec_ev, c->stream);
-    const int per = a.src.cols && MC_PCD_MEASURE_WAVE ? kPcdMeasureTiles : kPcdTilesPerWG;
-    const dim3 mgrid((uint32_t)((n_tiles + per - 1) / per));
-    if (a.src.cols) hipLaunchKernelGGL(k_pcd_measure<true>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
-    else hipLaunchKernelGGL(k_pcd_measure<false>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
-  }
-  HIPCHK(hipGetLastError());
   std::vector<int32_t> tb((size_t)n_tiles);
+  bool measured = false;
+  if (d_measured) {
+    HIPCHK(hipMemcpyAsync(tb.data(), d_measured, tb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    measured = std::all_of(tb.begin(), tb.end(), [](int32_t v) { return v >= 0 && v < kPcdSlowValue; });
+    if (measured) a.tile_bytes = const_cast<int32_t*>(d_measured);   // the write pass reads it (no slow flags)
+  }
+  if (!measured) {
+    {
+      TimedRegion tr(c, &c->codec_ev, c->stream);
+      const int per = a.src.cols && MC_PCD_MEASURE_WAVE ? kPcdMeasureTiles : kPcdTilesPerWG;
+      const dim3 mgrid((uint32_t)((n_tiles + per - 1) / per));
+      if (a.src.cols) hipLaunchKernelGGL(k_pcd_measure<true>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
+      else hipLaunchKernelGGL(k_pcd_measure<false>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(tb.data(), a.tile_bytes, tb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  }
   int err = 0;
-  HIPCHK(hipMemcpyAsync(tb.data(), a.tile_bytes, tb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(&err, c->d_codec_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (err) return fail(MC_ERR_INVALID, "a value has |v| >= 2^107, beyond the device %%.6f formatter");

@@ -157,6 +157,9 @@ struct mc_ctx {
   size_t codec_bytes = 0;
   int* d_codec_err = nullptr;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> codec_ev;
+  // mc_deskew_pcd: ASCII PCD text bytes per 256-point output block, written by the deskew kernel
+  int32_t* d_pcd_len = nullptr;
+  int64_t pcd_len_cap = 0;
   // pinned, device-mapped host buffer of the single-call drop-in path
   void* h_pin = nullptr;
   size_t pin_bytes = 0;
@@ -212,3 +215,9 @@ struct mc_batch {
   double* d_partial = nullptr;
   bool has_times = false, has_starts = false, trange_valid = false;
 };
+
+namespace mcimpl {
+// mc_deskew's body; pcd_len != nullptr: the *_pcd deskew kernels also write each output block's
+// ASCII PCD text bytes there (mc_deskew_pcd)
+int deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t* pcd_len);
+}  // namespace mcimpl

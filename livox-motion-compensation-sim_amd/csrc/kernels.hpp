@@ -146,6 +146,11 @@ struct DeskewArgs {
   const ImuSeg* imu_seg;   // M
   int64_t nseg;            // segments (SLERP: max(T-1,1); IMU: M)
   int64_t ntab;            // T or M (length of the time table)
+  // deskew -> PCD (mc_deskew_pcd, the *_pcd kernels): ASCII PCD text bytes of each output block's
+  // valid lines (pcd_value_len sums; index = global block), so the PCD writer needs no measure pass
+  int32_t* pcd_len;
+  const int64_t* fpoff;    // the output batch's per-frame padded offsets and point counts
+  const int64_t* fcount;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -165,7 +170,9 @@ __device__ __forceinline__ T ldu(const T* p) {
 }
 
 // XCD-contiguous sub-tile order per kernel (tools/ab.py, profiles/r13/ab_xcd*.log): frame -7 %,
-// IMU -4 %; SLERP +3 % slower with it under every store policy, so it keeps the dealt order
+// IMU -4 %.  SLERP: +3 % slower with it in rounds 1-2 (float32 math), but with the float64 math of
+// round 3 the XCD order is faster and steadier at 600 x 100k: 342.9 us (replicas 342.8-345.0) vs
+// 356.0 (351.6-367.7) dealt (profiles/round3/s08/ab_slerp.log)
 #ifndef MC_XCD_FRAME
 #define MC_XCD_FRAME 1
 #endif
@@ -173,7 +180,7 @@ __device__ __forceinline__ T ldu(const T* p) {
 #define MC_XCD_IMU 1
 #endif
 #ifndef MC_XCD_SLERP
-#define MC_XCD_SLERP 0
+#define MC_XCD_SLERP 1
 #endif
 #ifndef MC_XCD_STAGE
 #define MC_XCD_STAGE 1       // the LDS stager pair's tile order
@@ -907,10 +914,14 @@ constexpr int kQuadU = MC_FRAME_QUAD_U;
 static_assert(kQuadU == 1 || kQuadU == 2 || kQuadU == 4, "quarters per workgroup: 1, 2 or 4");
 constexpr int kQuadUnitsPerSub = kBlock / kQuadGroups / kQuadU;   // workgroup units per sub-tile
 
+// PCD: each quarter is one 256-point block; its four waves' text bytes meet in LDS (two barriers per
+// workgroup pass, this variant only).
+template <bool PCD = false>
 __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uint32_t pre) {
   const int64_t n_units = (int64_t)a.n_tiles * kSub * kQuadUnitsPerSub;
   const uint32_t nb = gridDim.x - pre;
   const int c = threadIdx.x & 3;
+  __shared__ int s_part[PCD ? kQuadU : 1][kBlock / 64];
   for (int64_t it = blockIdx.x - pre; it < n_units; it += nb) {
     const int64_t un = nb >= n_units ? xcd_unit<MC_XCD_FRAME>(it, n_units) : it;
     const int64_t st = un / kQuadUnitsPerSub;
@@ -946,6 +957,26 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
       o.z = xf_row(r, X.z, Y.z, Z.z);
       o.w = xf_row(r, X.w, Y.w, Z.w);
       if (act[u]) st_frame(a.out + bidx((int)a.out_C, c, p[u]), c == 3 ? w : o);
+      if constexpr (PCD) {
+        // lane c's column of its group's four points (a whole line is the quad's four lanes)
+        const float4 val = c == 3 ? w : o;
+        const int64_t i0 = p[u] - ldu(a.fpoff + tl.frame), n = ldu(a.fcount + tl.frame);
+        PcdCount pc;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pc.add(PcdCount::lanes(act[u] && i0 + k < n), f4g(val, k));
+        if ((threadIdx.x & 63) == 0) s_part[PCD ? u : 0][threadIdx.x >> 6] = pc.bytes();
+      }
+    }
+    if constexpr (PCD) {
+      __syncthreads();
+      if (threadIdx.x < kQuadU) {
+        const int g = g0 + (int)threadIdx.x * kQuadGroups;   // the quarter's first group
+        if (g < tl.ngroups) {
+          const int* q = s_part[PCD ? threadIdx.x : 0];
+          a.pcd_len[(tl.pstart + 4 * (int64_t)g) >> 8] = q[0] + q[1] + q[2] + q[3];
+        }
+      }
+      __syncthreads();   // s_part is rewritten by the next pass
     }
   }
 }
@@ -960,6 +991,9 @@ __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
   deskew_frame_body<false>(a);
 #endif
 }
+
+// Path A with the ASCII PCD text bytes of every output block (mc_deskew_pcd)
+__global__ __launch_bounds__(kBlock) void k_deskew_frame_pcd(const DeskewArgs a) { deskew_frame_quad<true>(a, 0u); }
 
 // Many frames on host-resident rows (LMC:802-832 on host arrays): frame f's rows [doff[f],
 // doff[f+1]) of the pinned input get pose[12 f ..] = R (row-major) | t (float64, from k_scan_pose).
@@ -1339,7 +1373,9 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
 // NEXT: the launch also runs the next step's prep in its first `pre` workgroups (see the
 // k_deskew_frame_next comment)
 // (NEXT: at least 4 waves / SIMD like the plain kernel — the prep body alone would take 172 VGPRs)
-template <int MODE, bool NEXT = false>
+// PCD (mc_deskew_pcd): a wave's 64 groups are one 256-point block of the output batch; it also
+// writes that block's ASCII PCD text bytes (a wave reduction, no barrier).
+template <int MODE, bool NEXT = false, bool PCD = false>
 __global__ __launch_bounds__(kBlock, MODE == 1 ? MC_SLERP_WAVES : MC_IMU_WAVES) void k_deskew_points(
     const DeskewArgs a, const PrepArgs pn, const uint32_t pre) {
   if constexpr (NEXT) {
@@ -1446,6 +1482,20 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? MC_SLERP_WAVES : MC_IMU_WAVES) 
       st_points<MODE>(o + 2 * kBlkPts, Z);
       st_points<MODE>(o + 3 * kBlkPts, I);
       if (a.copy_t) st_points<MODE>(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
+    }
+    if constexpr (PCD) {
+      const int64_t i0 = p - ldu(a.fpoff + f), n = ldu(a.fcount + f);
+      PcdCount pc;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const auto v = PcdCount::lanes(act && i0 + c < n);
+        pc.add(v, f4g(X, c));
+        pc.add(v, f4g(Y, c));
+        pc.add(v, f4g(Z, c));
+        pc.add(v, f4g(I, c));
+      }
+      const int wg = g0 + (tid & ~63);   // the wave's first group
+      if ((tid & 63) == 0 && wg < tl.ngroups) a.pcd_len[(tl.pstart + 4 * (int64_t)wg) >> 8] = pc.bytes();
     }
   }
 }

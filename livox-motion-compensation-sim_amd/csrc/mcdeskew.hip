@@ -164,6 +164,7 @@ int mc_destroy(mc_ctx* c) {
   dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis); dev_free(c->d_scan_bits);
   if (c->d_codec) (void)hipFree(c->d_codec);
   dev_free(c->d_codec_err);
+  dev_free(c->d_pcd_len);
   if (c->h_pin) (void)hipHostFree(c->h_pin);
   if (c->h_pipe) (void)hipHostFree(c->h_pipe);
   if (c->d_pipe) (void)hipFree(c->d_pipe);
@@ -657,6 +658,9 @@ struct StepPlan {
 };
 
 constexpr int64_t kSlerpXcdMinPoints = 200000000;
+#ifndef MC_SLERP_ALT
+#define MC_SLERP_ALT 0       // experiment (with MC_XCD_SLERP=0): odd table halves = odd steps take the XCD order
+#endif
 
 // Diagnostic occupancy cap for the per-point kernels: $MCDESKEW_POINTS_LDS bytes of dynamic LDS
 // per workgroup (160 KB per CU), read once.
@@ -704,6 +708,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // per-point modes pass the timestamps through (CSIM:1472) when out is another batch with t_ns
   da.copy_t = mode != MC_MODE_FRAME && out != in && out->has_t();
   da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
+  da.fpoff = out->d_poff; da.fcount = out->d_counts;   // (the PCD kernels' valid-point test)
   da.frame_tbl = frame_tbl;
   da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start;
   da.fwin = fwin; da.frec = frec;
@@ -722,7 +727,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // 342.9 vs 356.0 us at 600 x 100k, profiles/round3/s08).  A build with MC_XCD_SLERP=0 keeps the
   // round-2 rule: dealt up to ~200 M points, XCD-contiguous above (1682 vs 1890 us at 3000 x 100k,
   // 3434 vs 3713 at 6000; profiles/round2/s30-s32)
-  da.xcd_order = (mode == MC_MODE_POSE_SLERP && in->P >= kSlerpXcdMinPoints) ? 1 : 0;
+  da.xcd_order = (mode == MC_MODE_POSE_SLERP && (in->P >= kSlerpXcdMinPoints || (MC_SLERP_ALT && h == 1))) ? 1 : 0;
   sp->lds = mode == MC_MODE_FRAME ? 0u : points_lds_reserve();
 }
 
@@ -736,6 +741,13 @@ void launch_prep(const StepPlan& sp, hipStream_t sd, hipEvent_t e0 = nullptr, hi
 
 void launch_main(const StepPlan& sp, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
   const dim3 grid(sp.grid), block(kBlock);
+  if (sp.da.pcd_len) {   // mc_deskew_pcd (never graph-captured)
+    if (sp.kernel == MC_MODE_FRAME) hipExtLaunchKernelGGL(k_deskew_frame_pcd, grid, block, 0, s, e0, e1, 0u, sp.da);
+    else if (sp.kernel == MC_MODE_POSE_SLERP)
+      hipExtLaunchKernelGGL((k_deskew_points<1, false, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+    else hipExtLaunchKernelGGL((k_deskew_points<2, false, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+    return;
+  }
   if (!e0) {
     if (sp.kernel == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, sp.da);
     else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, sp.lds, s, sp.da, sp.pa, 0u);
@@ -769,6 +781,12 @@ int ensure_trange(mc_batch* in, int mode) {
 }  // namespace
 
 int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select) {
+  return mcimpl::deskew_call(c, in, out, mode, pose_select, nullptr);
+}
+
+}  // extern "C"
+
+int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t* pcd_len) {
   if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
   if (in->F == 0) return MC_OK;
   DeviceGuard g(c->device);
@@ -789,6 +807,7 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   c->buf ^= 1;
   StepPlan sp;
   deskew_plan(c, in, out, mode, pose_select, h, &sp);
+  sp.da.pcd_len = pcd_len;
   // a per-point deskew that carries t_ns into another batch rewrites that batch's time column:
   // its cached [min, max] spans no longer describe it
   if (sp.kernel >= 0 && sp.da.copy_t) out->trange_valid = false;
@@ -815,7 +834,8 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
   // key, if it did; then this call needs no k_prep at all.
   const mc_ctx::PrepKey key{in->uid, c->traj_ver, c->imu_ver, in->prep_ver, mode, pose_select};
   const bool hit = MC_SPEC_PREP && c->spec_valid && c->spec_half == h && c->spec_key == key;
-  const bool speculate = MC_SPEC_PREP && sp.kernel >= 0 && c->last_call == key;
+  // (the fused next-call launch has no PCD variant: a PCD call never speculates, it may hit)
+  const bool speculate = MC_SPEC_PREP && sp.kernel >= 0 && c->last_call == key && !pcd_len;
   c->last_call = key;
   c->spec_valid = false;
   if (!hit) {
@@ -866,6 +886,8 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
 #endif
   return MC_OK;
 }
+
+extern "C" {
 
 // ---- n steps as one HIP graph ---------------------------------------------------------------
 // The step sequence of n mc_deskew calls (prep on the side stream one step ahead, kernel on the

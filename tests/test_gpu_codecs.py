@@ -202,3 +202,67 @@ def test_save_results_files_match_reference(mc, gpu_ctx, tmp_path, tag):
     assert sorted(got) == sorted(want)
     for k in want:
         assert got[k] == want[k], k
+
+
+def _deskew_setup(mc, ctx, counts, with_big=False):
+    sim = mc.LiDARMotionSimulator({"duration": 20.0, "trajectory_type": "figure_eight", "max_speed": 12.0},
+                                  context=ctx)
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:len(counts)]
+    b = ctx.batch(counts, with_time=True)
+    b.synth(seed=4, frame_id_base=700)
+    if with_big:   # a frame with values beyond the packed formatter (|v| >= 4294 after the deskew)
+        pts = b.download_aos()
+        t_ns = b.download_time()
+        pts[:50, 0] = 6000.0
+        b.upload_aos(pts)
+        b.upload_time(t_ns)
+    b.set_frame_times(times)
+    b.set_frame_starts((times * 1e9).astype(np.int64))
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    ts, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    ctx.set_imu(ts, gyro)
+    return b
+
+
+@pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
+@pytest.mark.parametrize("big", [False, True])
+def test_deskew_pcd_equals_deskew_then_encode(mc, gpu_ctx, mode, big):
+    """mc_deskew_pcd (the deskew kernel sums each block's PCD text bytes, the writer skips its
+    measure pass) produces the same deskewed batch and the same PCD bytes as mc_deskew followed by
+    mc_pcd_encode_batch: ragged frames (empty, < 4, one block, a block + 1, several tiles); with
+    ``big`` a frame holds values >= 4294, whose blocks take the measure-pass fallback."""
+    counts = np.array([4096, 3, 2500, 0, 10_000, 7, 256, 257, 100_003, 1], np.int64)
+    b = _deskew_setup(mc, gpu_ctx, counts, with_big=big)
+    ref_out = gpu_ctx.deskew(b, gpu_ctx.batch(counts), mode=mode)
+    want = mc.codecs.encode_pcd_batch(ref_out)
+    out = gpu_ctx.batch(counts)
+    gpu_ctx.sync()
+    gpu_ctx.read_timing()
+    gpu_ctx.timing(True)
+    got = mc.codecs.deskew_pcd_frames(b, out, mode=mode)
+    gpu_ctx.timing(False)
+    tm = gpu_ctx.read_timing()
+    assert np.array_equal(out.download_aos(), ref_out.download_aos())
+    assert len(got) == len(want)
+    for f, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (mode, f)
+    # fast case: the write pass only (one codec launch); fallback: measure + write (+ the byte path)
+    assert tm["codec_launches"] >= 2 if big else tm["codec_launches"] == 1
+    assert tm["main_launches"] == 1
+
+
+def test_deskew_pcd_space_and_errors(mc, gpu_ctx):
+    counts = np.array([300, 0, 1000], np.int64)
+    b = _deskew_setup(mc, gpu_ctx, counts)
+    out = gpu_ctx.batch(counts)
+    small = gpu_ctx.device_buffer(64)
+    text, pos = mc.codecs.deskew_pcd_batch(b, out, mode="frame", text=small)   # regrows after MC_ERR_SPACE
+    body = text.to_host(np.uint8, count=int(pos[-1])).tobytes()
+    text.close()
+    want = mc.codecs.encode_pcd_batch(gpu_ctx.deskew(b, gpu_ctx.batch(counts), mode="frame"))
+    assert [mc.codecs.pcd_header(int(c)) + body[pos[f]:pos[f + 1]] for f, c in enumerate(counts)] == want
+    with pytest.raises(ValueError):
+        mc.codecs.deskew_pcd_batch(b, b, mode="frame")
+    with pytest.raises(ValueError):
+        mc.codecs.deskew_pcd_batch(b, gpu_ctx.batch([300, 1, 1000]), mode="frame")

@@ -28,10 +28,11 @@ def timed(fn, calls):
 
 
 def per_call_deskew(ctx, tr, sim, calls=200):
-    """The drop-in per-call API on device-resident batches (Context.deskew = mc_deskew, each call
-    synchronised like the reference's synchronous calls): wall time per call vs the deskew kernel's
-    HIP-event time, per mode and frame shape.  Repeated identical calls hit mc_deskew's speculation
-    (the previous launch prepared this call's tables), so the gap is launch + sync only."""
+    """The drop-in per-call API on device-resident batches (Context.deskew = mc_deskew): wall time per
+    call vs the deskew kernel's HIP-event time, per mode and frame shape, each call synchronised like
+    the reference's synchronous calls (call_us: launch + completion + host wake-up) and queued back to
+    back (async_*: what a call costs the device beyond its kernel).  Repeated identical calls hit
+    mc_deskew's speculation (the previous launch prepared this call's tables): no k_prep."""
     res = {}
     ts, g = mc.trajectory.imu_from_trajectory(tr, 200.0)
     ctx.set_imu(ts, g)
@@ -57,8 +58,23 @@ def per_call_deskew(ctx, tr, sim, calls=200):
             ctx.timing(False)
             t = ctx.read_timing()
             kern = t["main_ms"] / max(t["main_launches"], 1) * 1e3
+            # the same calls queued back to back (no host sync per call, as a caller streaming
+            # frames would issue them): per-call cost on the device beyond the kernel
+            ctx.sync()
+            ctx.timing(True)
+            t0 = time.perf_counter()
+            for _ in range(calls):
+                ctx.deskew(b, o, mode=mode)
+            ctx.sync()
+            wall_a = (time.perf_counter() - t0) / calls * 1e6
+            ctx.timing(False)
+            ta = ctx.read_timing()
+            kern_a = ta["main_ms"] / max(ta["main_launches"], 1) * 1e3
             res[f"{mode}/{frames}x{n}"] = {"call_us": wall, "kernel_us": kern, "gap_us": wall - kern,
-                                           "prep_launches": t["prep_launches"], "calls": calls}
+                                           "prep_launches": t["prep_launches"], "calls": calls,
+                                           "async_call_us": wall_a, "async_kernel_us": kern_a,
+                                           "async_gap_us": wall_a - kern_a,
+                                           "async_prep_launches": ta["prep_launches"]}
         b.close()
         o.close()
     return res
