@@ -964,7 +964,8 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
         PcdCount pc;
 #pragma unroll
         for (int k = 0; k < 4; ++k) pc.add(PcdCount::lanes(act[u] && i0 + k < n), f4g(val, k));
-        if ((threadIdx.x & 63) == 0) s_part[PCD ? u : 0][threadIdx.x >> 6] = pc.bytes();
+        const int bytes = pc.bytes();   // (every lane: the per-lane variant reduces across the wave)
+        if ((threadIdx.x & 63) == 0) s_part[PCD ? u : 0][threadIdx.x >> 6] = bytes;
       }
     }
     if constexpr (PCD) {
@@ -1494,8 +1495,9 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? MC_SLERP_WAVES : MC_IMU_WAVES) 
         pc.add(v, f4g(Z, c));
         pc.add(v, f4g(I, c));
       }
+      const int bytes = pc.bytes();      // (every lane: the per-lane variant reduces across the wave)
       const int wg = g0 + (tid & ~63);   // the wave's first group
-      if ((tid & 63) == 0 && wg < tl.ngroups) a.pcd_len[(tl.pstart + 4 * (int64_t)wg) >> 8] = pc.bytes();
+      if ((tid & 63) == 0 && wg < tl.ngroups) a.pcd_len[(tl.pstart + 4 * (int64_t)wg) >> 8] = bytes;
     }
   }
 }

@@ -1,7 +1,7 @@
 set -u
 OUT=gpurun_out/r3s12; mkdir -p $OUT
 V=build/variants
-PYTEST_ARGS="-k deskew_pcd" STEPS="tests" bash tools/gpu_session.sh r3s12 || exit $?
+PYTEST_ARGS="-k codecs" STEPS="tests" bash tools/gpu_session.sh r3s12 || exit $?
 MCDESKEW_LIB=$PWD/$V/lib_pc1.so timeout -k 10 300 python -u -m pytest tests/test_gpu_codecs.py -m gpu -k deskew_pcd -q -x --timeout 120 --timeout-method thread > $OUT/pytest_pc1.log 2>&1 || exit $?
 tail -2 $OUT/pytest_pc1.log
 timeout -k 10 600 python -u tools/ab_pcd_fused.py --libs $V/lib_pc0.so,$V/lib_pc1.so --modes pose_slerp,frame,imu > $OUT/ab_pcd_fused.log 2>&1 || exit $?

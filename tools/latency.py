@@ -60,13 +60,18 @@ def per_call_deskew(ctx, tr, sim, calls=200):
             kern = t["main_ms"] / max(t["main_launches"], 1) * 1e3
             # the same calls queued back to back (no host sync per call, as a caller streaming
             # frames would issue them): per-call cost on the device beyond the kernel
+            # (untimed: per-launch events would add their own packets; the kernel time is the
+            # back-to-back kernels' own, from a timed repeat of the same queue)
             ctx.sync()
-            ctx.timing(True)
             t0 = time.perf_counter()
             for _ in range(calls):
                 ctx.deskew(b, o, mode=mode)
             ctx.sync()
             wall_a = (time.perf_counter() - t0) / calls * 1e6
+            ctx.timing(True)
+            for _ in range(calls):
+                ctx.deskew(b, o, mode=mode)
+            ctx.sync()
             ctx.timing(False)
             ta = ctx.read_timing()
             kern_a = ta["main_ms"] / max(ta["main_launches"], 1) * 1e3
