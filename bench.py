@@ -51,9 +51,9 @@ HBM_PEAK_GBS = 8000.0                                          # MI355X_MICROARC
 KERNEL = {"pose_slerp": "k_deskew_points<1", "imu": "k_deskew_points<2", "frame": "k_deskew_frame"}
 # the kernel each issue mode times (pipeline: the step's deskew with the next step's prep in its first
 # workgroups; the last step's launch is the plain kernel)
-KERNEL_OF = {"pipeline": {"pose_slerp": "k_deskew_points<1, true>", "imu": "k_deskew_points<2, true>",
+KERNEL_OF = {"pipeline": {"pose_slerp": "k_deskew_points<1, false, false>", "imu": "k_deskew_points<2, true, false>",
                           "frame": "k_deskew_frame_next"},
-             "calls": {"pose_slerp": "k_deskew_points<1, false>", "imu": "k_deskew_points<2, false>",
+             "calls": {"pose_slerp": "k_deskew_points<1, false, false>", "imu": "k_deskew_points<2, false, false>",
                        "frame": "k_deskew_frame"}}
 KERNEL_OF["graph"] = KERNEL_OF["calls"]
 REL_TOL = 1e-5                                                 # north_star, relative per coordinate
@@ -316,6 +316,13 @@ def load_traffic(mode, frames, points):
            "how": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes of bench.py (tools/pmc_traffic.py; "
                   "FETCH_SIZE x2 gfx950 correction), measured in that session, not in this run"}
     return e.get("hbm_bytes_per_launch"), src
+
+
+def tune(ctx, mode, b_in, b_out):
+    """Untimed, before the spin-up: the device picks the mode's sub-tile order (dealt over the XCDs or
+    XCD-contiguous, Context.tune_order / mc_tune_order): which one streams faster differs between
+    MI355X boxes by up to 7 % for the same kernel."""
+    return ctx.tune_order(b_in, b_out, mode=mode, launches=8, rounds=4)
 
 
 def spin_up(ctx, mode, b_in, b_out, ms, issue):
@@ -710,6 +717,8 @@ def single_gpu_same_job(ctx, args, tr, times_all, counts_all, steps, warmup):
         if args.mode == "imu":
             b_in.set_frame_starts((times_all * 1e9).astype(np.int64))
         rdv1 = mc.dist.Rendezvous(0, 1)
+        if not args.no_tune:
+            tune(ctx, args.mode, b_in, b_out)
         spin_up(ctx, args.mode, b_in, b_out, args.spinup_ms, args.issue)
         wall, tm, _ = run_mode(ctx, rdv1, args.mode, b_in, b_out, steps, warmup, issue=args.issue)
         n = int(counts_all.sum())
@@ -756,6 +765,7 @@ def main():
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
                     help="self-launch (--gpus N > 1 without torchrun): kill every rank after this many seconds")
     ap.add_argument("--no-single-gpu", action="store_true", help="N > 1: skip rank 0's same-job 1-GPU run")
+    ap.add_argument("--no-tune", action="store_true", help="keep each mode's default sub-tile order (no mc_tune_order)")
     args = ap.parse_args()
     if args.graph:
         args.issue = "graph"
@@ -800,9 +810,12 @@ def main():
 
     modes = [args.mode] + ([] if args.no_extra_modes else [m for m in BYTES_PER_POINT if m != args.mode])
     results = {}
+    tuned = {}
     every = 10
     for mode in modes:
         steps = args.steps if mode == args.mode else max(10, args.steps // 4)
+        if not args.no_tune and n_rank:
+            tuned[mode] = tune(ctx, mode, src_of[mode], b_out)
         spun = spin_up(ctx, mode, src_of[mode], b_out, args.spinup_ms, args.issue)
         if mode == args.mode:
             spinup_ms = spun
@@ -902,13 +915,16 @@ def main():
                                          f"HIP events (hipExtLaunchKernel start/stop, the dispatch's own timestamps) "
                                          f"on the kernels of {r['timed_launches']} of the {r['steps']} timed steps "
                                          f"(every {every}th), on the kernel's stream")},
+            "order_tune": tuned or None,
             "step_over_kernel": (r["wall_s"] / r["steps"] * 1e6) / r["main_avg_us"] if r["main_avg_us"] else None,
             "prep_avg_us": r["prep_avg_us"],
             "step_issue": {"calls": "per-call launches; prep as an any-order packet on the kernel's queue",
                            "graph": f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
-                           "pipeline": f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
-                                       "k_prep, then each step's deskew kernel with the next step's prep in its "
-                                       "first workgroups (every step runs its own prep, one launch ahead)"}[args.issue],
+                           "pipeline": (f"Context.deskew_steps(pipeline=True): per step an any-order k_prep packet and "
+                                        f"the plain deskew kernel ({2 * r['steps']} launches)" if args.mode == "pose_slerp"
+                                        else f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
+                                        "k_prep, then each step's deskew kernel with the next step's prep in its first "
+                                        "workgroups (every step runs its own prep, one launch ahead)")}[args.issue],
             "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
                           "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"],
                           "ms_per_step": v["wall_s"] / v["steps"] * 1e3}

@@ -208,6 +208,15 @@ int mc_batch_checksum(mc_batch* b, double* sums5);
 /* out must have the same frame counts as in (it may be the same batch: in-place). */
 int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select);
 
+/* Measure, on this device, which sub-tile order streams the mode's deskew kernel faster for batches
+ * shaped like `in` (dealt over the 8 XCDs vs XCD-contiguous: the faster one differs between MI355X
+ * boxes by up to 7 %) and use it for every later launch of that mode on batches of the same padded
+ * size.  Runs the kernel `launches` times per order and round (in -> out, out != in; the results do
+ * not depend on the order), alternating the orders over `rounds`.  us_out[2] (may be NULL) receives
+ * the median microseconds per launch of {dealt, XCD-contiguous}; *chosen (may be NULL) the order
+ * kept (0 / 1; -1 for an empty batch).  Synchronous. */
+int mc_tune_order(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t launches,
+                  int32_t rounds, double* us_out, int32_t* chosen);
 /* n_steps consecutive mc_deskew calls (same arguments), LMC:802-832 n times over one batch.
  * Default: one HIP graph: each step's pose prep and deskew kernel run exactly as in mc_deskew
  * (prep one step ahead on a second queue), the graph's edges replacing the per-call cross-queue

@@ -95,6 +95,7 @@ _SIGS = {
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),
     "mc_deskew": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "mc_deskew_steps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int32, c_int32, c_int]),
+    "mc_tune_order": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int32, c_int32, _pd, _pi32]),
     "mc_transform_affine": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, _pd, c_int]),
     "mc_transform_pointcloud_f64": (c_int, [c_void_p, _pd, c_int64, c_int64, _pd, _pd, _pd]),
     # frames / outs: arrays of row pointers (passed as the address of a uintp array)

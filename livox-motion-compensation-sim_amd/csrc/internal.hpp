@@ -123,6 +123,12 @@ struct mc_ctx {
   bool spec_valid = false;
   int spec_half = 0;
   uint64_t traj_ver = 0, imu_ver = 0;   // bumped by mc_set_trajectory / mc_set_imu
+  // sub-tile order per mode measured by mc_tune_order for batches of P padded points (-1: none)
+  struct OrderTune {
+    int64_t P = -1;
+    int32_t order = -1;
+  };
+  OrderTune order_tune[3];
   hipEvent_t ev_main_done[2] = {nullptr, nullptr};
   hipEvent_t ev_prep_done[2] = {nullptr, nullptr};
   hipEvent_t ev_order = nullptr;  // orders side-stream prep after async main-stream staging

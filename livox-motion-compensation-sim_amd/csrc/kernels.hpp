@@ -55,6 +55,9 @@ namespace mc {
 #ifndef MC_SLERP_WAVES
 #define MC_SLERP_WAVES 4     // waves/SIMD the SLERP kernel is compiled for (VGPR budget 512 / waves)
 #endif
+#ifndef MC_SLERP_NEXT_WAVES
+#define MC_SLERP_NEXT_WAVES MC_SLERP_WAVES   // the SLERP kernel carrying the next step's prep
+#endif
 #ifndef MC_IMU_PRELOAD
 #define MC_IMU_PRELOAD 1     // IMU: both window records loaded before the wave's segment vote
 #endif
@@ -132,7 +135,8 @@ struct DeskewArgs {
   int64_t out_C;
   const Tile* tiles;
   int32_t n_tiles;
-  int32_t xcd_order;       // SLERP: sub-tiles in XCD-contiguous order (large batches; see mc_deskew's plan)
+  int32_t xcd_order;       // sub-tiles in XCD-contiguous order (1) or dealt (0): the mode's default or
+                           // what mc_tune_order measured faster on this device (deskew_plan)
   const FrameRow* frame_tbl; // frame mode: 3 rows per frame (R row i, t_i), float64
   const double* frame_time;
   const int64_t* frame_start;
@@ -170,9 +174,11 @@ __device__ __forceinline__ T ldu(const T* p) {
 }
 
 // XCD-contiguous sub-tile order per kernel (tools/ab.py, profiles/r13/ab_xcd*.log): frame -7 %,
-// IMU -4 %.  SLERP: +3 % slower with it in rounds 1-2 (float32 math), but with the float64 math of
-// round 3 the XCD order is faster and steadier at 600 x 100k: 342.9 us (replicas 342.8-345.0) vs
-// 356.0 (351.6-367.7) dealt (profiles/round3/s08/ab_slerp.log)
+// IMU -4 %.  SLERP keeps the dealt order below ~200 M points (deskew_plan's default_order): with
+// the float64 math its fused next-step kernel ran the dealt order 6-10 % slower (scratch spills,
+// profiles/round3/s08-s12), but the plain kernel SLERP now uses (MC_FUSE_SLERP=0) streams it
+// fastest: 317.2 vs 333.8 us XCD-contiguous (profiles/round3/s15).  These are the defaults;
+// mc_tune_order measures both orders on the device at hand (the runtime field DeskewArgs::xcd_order)
 #ifndef MC_XCD_FRAME
 #define MC_XCD_FRAME 1
 #endif
@@ -180,7 +186,7 @@ __device__ __forceinline__ T ldu(const T* p) {
 #define MC_XCD_IMU 1
 #endif
 #ifndef MC_XCD_SLERP
-#define MC_XCD_SLERP 1
+#define MC_XCD_SLERP 0
 #endif
 #ifndef MC_XCD_STAGE
 #define MC_XCD_STAGE 1       // the LDS stager pair's tile order
@@ -923,7 +929,7 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
   const int c = threadIdx.x & 3;
   __shared__ int s_part[PCD ? kQuadU : 1][kBlock / 64];
   for (int64_t it = blockIdx.x - pre; it < n_units; it += nb) {
-    const int64_t un = nb >= n_units ? xcd_unit<MC_XCD_FRAME>(it, n_units) : it;
+    const int64_t un = nb >= n_units ? (a.xcd_order ? xcd_unit<1>(it, n_units) : it) : it;
     const int64_t st = un / kQuadUnitsPerSub;
     const Tile tl = ldu(a.tiles + st / kSub);
     const int g0 = (int)(st % kSub) * kBlock + (int)(un % kQuadUnitsPerSub) * kQuadGroups * kQuadU;
@@ -1377,7 +1383,7 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
 // PCD (mc_deskew_pcd): a wave's 64 groups are one 256-point block of the output batch; it also
 // writes that block's ASCII PCD text bytes (a wave reduction, no barrier).
 template <int MODE, bool NEXT = false, bool PCD = false>
-__global__ __launch_bounds__(kBlock, MODE == 1 ? MC_SLERP_WAVES : MC_IMU_WAVES) void k_deskew_points(
+__global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : MC_SLERP_WAVES) : MC_IMU_WAVES) void k_deskew_points(
     const DeskewArgs a, const PrepArgs pn, const uint32_t pre) {
   if constexpr (NEXT) {
     if (blockIdx.x < pre) {
@@ -1396,8 +1402,7 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? MC_SLERP_WAVES : MC_IMU_WAVES) 
   const uint32_t b0 = NEXT ? blockIdx.x - pre : blockIdx.x, nb = NEXT ? gridDim.x - pre : gridDim.x;
   for (int64_t it = b0; it < n_sub; it += nb) {
     const int64_t st = nb < n_sub ? it
-                       : (MODE == 2 ? xcd_unit<MC_XCD_IMU>(it, n_sub)
-                                    : (a.xcd_order ? xcd_unit<1>(it, n_sub) : xcd_unit<MC_XCD_SLERP>(it, n_sub)));
+                       : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
     const Tile tl = ldu(a.tiles + st / kSub);
     // IMU frames always span several samples: fetch the sub-tile window with the tile record
     const int g0 = (int)(st % kSub) * kBlock;

@@ -609,10 +609,21 @@ int mc_batch_checksum(mc_batch* b, double* sums) {
 #ifndef MC_SPEC_PREP
 #define MC_SPEC_PREP 1       // per-call speculation of the next identical call's prep (mc_ctx::PrepKey)
 #endif
+// Whether a mode's steps carry the next step's prep in their own launch (k_deskew_points<MODE, true>
+// / k_deskew_frame_next; mc_deskew's speculation and mc_deskew_steps' pipeline).  Not for SLERP since
+// round 3: with the float64 math its fused kernel spills the prep branch to scratch at 4 waves /
+// SIMD, and the prep as an any-order packet before the plain kernel streams faster — dealt order
+// 317.2 vs 345.1 us per launch over 2 replicas, step wall 320.6-323.8 vs 326.1-364.6 us
+// (profiles/round3/s15/ab_slerp_fused.log).  IMU's and frame's fused kernels need no scratch.
+#ifndef MC_FUSE_SLERP
+#define MC_FUSE_SLERP 0
+#endif
 #ifndef MC_DIAG_NO_PREP
 #define MC_DIAG_NO_PREP 0    // diagnostic timing build: after 4 calls, no k_prep (tables of earlier calls)
 #endif
 namespace {
+bool fuse_next(int mode) { return mode != MC_MODE_POSE_SLERP || MC_FUSE_SLERP; }
+
 // Table halves written outside mc_deskew's key bookkeeping: no speculated tables stay valid, and the
 // next mc_deskew does not speculate from a key seen before this call.
 void forget_speculation(mc_ctx* c) {
@@ -672,6 +683,15 @@ static uint32_t points_lds_reserve() {
   return v;
 }
 
+// sub-tile order of a mode's kernel without a tuned choice: XCD-contiguous for the frame and IMU
+// kernels (rounds 1-2), and for SLERP since round 3 (MC_XCD_SLERP; a MC_XCD_SLERP=0 build keeps the
+// round-2 rule: dealt below kSlerpXcdMinPoints)
+int32_t default_order(int mode, int64_t P, int h) {
+  if (mode == MC_MODE_FRAME) return MC_XCD_FRAME;
+  if (mode == MC_MODE_IMU) return MC_XCD_IMU;
+  return (MC_XCD_SLERP || P >= kSlerpXcdMinPoints || (MC_SLERP_ALT && h == 1)) ? 1 : 0;
+}
+
 void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int h, StepPlan* sp) {
   std::memset(sp, 0, sizeof(*sp));
   const mc_batch* pb = in;  // per-frame tables live with the input batch
@@ -723,11 +743,11 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (mode == MC_MODE_FRAME && MC_FRAME_QUAD) units = in->n_tiles * kSub * kQuadUnitsPerSub;
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
-  // SLERP sub-tile order: XCD-contiguous at every size since round 3 (MC_XCD_SLERP=1; float64 math:
-  // 342.9 vs 356.0 us at 600 x 100k, profiles/round3/s08).  A build with MC_XCD_SLERP=0 keeps the
-  // round-2 rule: dealt up to ~200 M points, XCD-contiguous above (1682 vs 1890 us at 3000 x 100k,
-  // 3434 vs 3713 at 6000; profiles/round2/s30-s32)
-  da.xcd_order = (mode == MC_MODE_POSE_SLERP && (in->P >= kSlerpXcdMinPoints || (MC_SLERP_ALT && h == 1))) ? 1 : 0;
+  // sub-tile order: default_order, or mc_tune_order's measured choice
+  da.xcd_order = default_order(mode, in->P, h);
+  // a device-measured choice for this mode and batch size (mc_tune_order) overrides the default
+  const mc_ctx::OrderTune& ot = c->order_tune[mode];
+  if (ot.order >= 0 && ot.P == in->P) da.xcd_order = ot.order;
   sp->lds = mode == MC_MODE_FRAME ? 0u : points_lds_reserve();
 }
 
@@ -835,7 +855,7 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
   const mc_ctx::PrepKey key{in->uid, c->traj_ver, c->imu_ver, in->prep_ver, mode, pose_select};
   const bool hit = MC_SPEC_PREP && c->spec_valid && c->spec_half == h && c->spec_key == key;
   // (the fused next-call launch has no PCD variant: a PCD call never speculates, it may hit)
-  const bool speculate = MC_SPEC_PREP && sp.kernel >= 0 && c->last_call == key && !pcd_len;
+  const bool speculate = MC_SPEC_PREP && sp.kernel >= 0 && c->last_call == key && !pcd_len && fuse_next(mode);
   c->last_call = key;
   c->spec_valid = false;
   if (!hit) {
@@ -957,12 +977,34 @@ int build_step_graph(mc_ctx* c, const StepPlan* plan, int32_t n_steps, int32_t e
 }  // namespace
 
 namespace {
+// The launches of n steps over the two table halves of `plan` (step i reads half i & 1 of plan):
+// fused modes (fuse_next) issue step 0's k_prep, then n deskew launches of which the first n - 1
+// carry the next step's prep; SLERP issues per step an any-order k_prep packet and the plain kernel.
+// Every `every`-th step's kernel (and prep) is timed.
+void issue_steps(mc_ctx* c, const StepPlan* plan, int mode, int32_t n_steps, int32_t every) {
+  hipStream_t s = c->stream;
+  const bool fuse = fuse_next(mode);
+  auto sampled = [&](int32_t i) { return every > 0 && i % every == every / 2; };
+  for (int32_t i = 0; i < n_steps; ++i) {
+    if (i == 0 || !fuse) {
+      // any-order right behind this context's own deskew kernel, as in mc_deskew
+      const bool ao = MC_PREP_ISSUE == 2 && (i > 0 || !c->prep_fence);
+      LaunchEvents ev(c, sampled(i));
+      launch_prep(plan[i & 1], s, ev.e0, ev.e1, ao ? hipExtAnyOrderLaunch : 0u);
+      ev.keep(&c->prep_ev);
+    }
+    LaunchEvents ev(c, sampled(i));
+    if (fuse && i + 1 < n_steps) launch_fused(plan[i & 1], plan[(i + 1) & 1], s, ev.e0, ev.e1);
+    else launch_main(plan[i & 1], s, ev.e0, ev.e1);
+    ev.keep(&c->main_ev);
+  }
+}
+
 // n steps as n launches, step i's launch carrying step i+1's prep (MC_STEPS_PIPELINE): one
 // standalone k_prep for step 0, then n deskew launches; the kernel boundaries order each prep
 // before the step that reads it, as in mc_deskew.  Step i reads half h0 ^ (i & 1).
 int deskew_steps_pipelined(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select,
                            int32_t n_steps, int32_t every) {
-  hipStream_t s = c->stream;
   forget_speculation(c);
   if (mode != MC_MODE_FRAME && !in->trange_valid) {
     if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
@@ -973,27 +1015,79 @@ int deskew_steps_pipelined(mc_ctx* c, const mc_batch* in, mc_batch* out, int mod
   deskew_plan(c, in, out, mode, pose_select, h0, &plan[0]);
   deskew_plan(c, in, out, mode, pose_select, h0 ^ 1, &plan[1]);
   if (plan[0].da.copy_t) out->trange_valid = false;
-  auto sampled = [&](int32_t i) { return every > 0 && i % every == every / 2; };
-  {
-    // step 0's prep: any-order right behind this context's own deskew kernel, as in mc_deskew
-    const unsigned fl = (MC_PREP_ISSUE == 2 && !c->prep_fence) ? hipExtAnyOrderLaunch : 0u;
-    LaunchEvents ev(c, sampled(0));
-    launch_prep(plan[0], s, ev.e0, ev.e1, fl);
-    ev.keep(&c->prep_ev);
-    HIPCHK(hipGetLastError());
-  }
-  for (int32_t i = 0; i < n_steps; ++i) {
-    LaunchEvents ev(c, sampled(i));
-    if (i + 1 < n_steps) launch_fused(plan[i & 1], plan[(i + 1) & 1], s, ev.e0, ev.e1);
-    else launch_main(plan[i & 1], s, ev.e0, ev.e1);
-    ev.keep(&c->main_ev);
-    HIPCHK(hipGetLastError());
-  }
+  issue_steps(c, plan, mode, n_steps, every);
+  HIPCHK(hipGetLastError());
   c->buf = h0 ^ (n_steps & 1);   // the half the last launch did not read
   c->prep_fence = false;
   return MC_OK;
 }
 }  // namespace
+
+// Which sub-tile order streams faster depends on the device, not only on the kernel: with the float64
+// math the dealt order measured 318-370 us for the same SLERP step on different MI355X boxes, the
+// XCD-contiguous one 327-347 us (profiles/round3/s04-s13).  The candidates run back to back, rounds
+// alternating between them (drift hits both), each round after a few untimed launches of its own
+// order (a kernel's speed depends on what the previous one left in the caches, profiles/round3/s09
+// pingpong); the median per-launch time decides.
+int mc_tune_order(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t launches,
+                  int32_t rounds, double* us_out, int32_t* chosen) {
+  if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
+  CHECK_ARG(out != in, "mc_tune_order runs the kernel repeatedly: it needs an output batch other than the input");
+  CHECK_ARG(launches >= 1 && launches <= 1000 && rounds >= 1 && rounds <= 100, "launches / rounds out of range");
+  c->order_tune[mode] = mc_ctx::OrderTune{};
+  if (in->n_tiles == 0) {
+    if (us_out) us_out[0] = us_out[1] = 0.0;
+    if (chosen) *chosen = -1;
+    return MC_OK;
+  }
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
+  forget_speculation(c);
+  // the candidates run as the steps of mc_deskew_steps do (issue_steps: prep packets or fused launches)
+  const int h0 = c->buf;
+  StepPlan plan[2];
+  deskew_plan(c, in, out, mode, pose_select, h0, &plan[0]);
+  deskew_plan(c, in, out, mode, pose_select, h0 ^ 1, &plan[1]);
+  if (plan[0].da.copy_t) out->trange_valid = false;
+  c->prep_fence = true;   // the first prep is an ordinary packet: waits for everything queued before it
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPCHK(hipEventCreate(&e0));
+  if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return fail(MC_ERR_HIP, "event create"); }
+  std::vector<double> t[2];
+  hipError_t e = hipSuccess;
+  const bool timing = c->timing;
+  c->timing = false;
+  for (int32_t r = 0; r < rounds && e == hipSuccess; ++r)
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+      const int cand = (r & 1) ? 1 - k : k;
+      plan[0].da.xcd_order = plan[1].da.xcd_order = cand;
+      issue_steps(c, plan, mode, 2, 0);   // untimed: this order's own steady state
+      c->prep_fence = false;
+      e = hipEventRecord(e0, s);
+      issue_steps(c, plan, mode, launches, 0);
+      if (e == hipSuccess) e = hipEventRecord(e1, s);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      float ms = 0.f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      t[cand].push_back(1e3 * ms / launches);
+    }
+  c->timing = timing;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (e != hipSuccess) return fail(MC_ERR_HIP, "tune_order: %s", hipGetErrorString(e));
+  double med[2];
+  for (int k = 0; k < 2; ++k) {
+    std::sort(t[k].begin(), t[k].end());
+    med[k] = t[k][t[k].size() / 2];
+  }
+  const int best = med[1] <= med[0] ? 1 : 0;
+  c->order_tune[mode] = mc_ctx::OrderTune{in->P, best};
+  c->prep_fence = true;   // the next prep is an ordinary packet
+  if (us_out) { us_out[0] = med[0]; us_out[1] = med[1]; }
+  if (chosen) *chosen = best;
+  return MC_OK;
+}
 
 int mc_deskew_steps(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t n_steps,
                     int32_t sample_every, int flags) {
@@ -1278,6 +1372,7 @@ int mc_transform_affine(mc_ctx* c, const mc_batch* in, mc_batch* out, int32_t n_
     da.out = out->d_cols; da.out_C = out->C;
     da.tiles = in->d_tiles; da.n_tiles = in->n_tiles;
     da.frame_tbl = frame_tbl;
+    da.xcd_order = MC_XCD_FRAME;
     const dim3 grid(launch_grid(c, in->n_tiles)), block(kBlock);
     TimedRegion tr(c, &c->main_ev, s);
     if (w_column) hipLaunchKernelGGL(k_affine_w, grid, block, 0, s, da);

@@ -107,6 +107,19 @@ class Context:
                                        flags), f"deskew_steps[{mode}]")
         return out
 
+    def tune_order(self, inp: "Batch", out: "Batch", mode: str = "frame", pose_select: str = "searchsorted",
+                   launches: int = 8, rounds: int = 4) -> dict:
+        """Measure which sub-tile order (dealt / XCD-contiguous) runs ``mode``'s kernel faster on this
+        device for batches shaped like ``inp`` and keep it for later launches (mc_tune_order; the
+        output does not depend on the order).  Returns {"dealt_us", "xcd_us", "chosen"}."""
+        us = np.zeros(2, np.float64)
+        ch = c_int32(-1)
+        check(self.lib.mc_tune_order(self.handle, inp.handle, out.handle, _lib.MODES[mode], _lib.POSE_SELECT[pose_select],
+                                     int(launches), int(rounds), ptr(us, c_double), ctypes.byref(ch)),
+              f"tune_order[{mode}]")
+        return {"dealt_us": float(us[0]), "xcd_us": float(us[1]),
+                "chosen": {0: "dealt", 1: "xcd"}.get(ch.value, None)}
+
     def transform_affine(self, inp: "Batch", out: "Batch | None" = None, mats=None, w_column: bool = False) -> "Batch":
         """p' = A p + b (CSIM:214-233) with one 3x4 [A | b] for all frames or one per frame;
         ``w_column``: the 4th column is the homogeneous w (p' = A p + b w).  Synchronous."""

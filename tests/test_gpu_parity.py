@@ -569,17 +569,23 @@ def test_imu_slow_path_wide_subtile(mc, gpu_ctx):
 # ---------------------------------------------------------------------------------------------
 # timing hooks and single-rank RCCL gather
 # ---------------------------------------------------------------------------------------------
-def test_timing_counts_launches(mc, gpu_ctx):
+@pytest.mark.parametrize("mode", ["pose_slerp", "imu", "frame"])
+def test_timing_counts_launches(mc, gpu_ctx, mode):
     b, tr, times = _c2_batch(mc, gpu_ctx, frames=8, n=10_000)
+    b.set_frame_starts((times * 1e9).astype(np.int64))
+    gpu_ctx.set_imu(*mc.trajectory.imu_from_trajectory(tr, 200.0))
     out = gpu_ctx.batch(b.counts)
+    gpu_ctx.read_timing()
     gpu_ctx.timing(True)
     for _ in range(3):
-        gpu_ctx.deskew(b, out, mode="pose_slerp")
+        gpu_ctx.deskew(b, out, mode=mode)
     t = gpu_ctx.read_timing()
     gpu_ctx.timing(False)
-    # calls 1 and 2 run k_prep; call 2's launch also prepares call 3's tables (identical key), so
-    # call 3 needs none (mc_deskew's per-call speculation, test_gpu_steps.py)
-    assert t["main_launches"] == 3 and t["prep_launches"] == 2 and t["main_ms"] > 0
+    # IMU / frame: calls 1 and 2 run k_prep; call 2's launch also prepares call 3's tables (identical
+    # key), so call 3 needs none (mc_deskew's per-call speculation, test_gpu_steps.py).  SLERP issues
+    # its prep before the plain kernel on every call (MC_FUSE_SLERP=0)
+    preps = 3 if mode == "pose_slerp" else 2
+    assert t["main_launches"] == 3 and t["prep_launches"] == preps and t["main_ms"] > 0
 
 
 def test_rccl_gather_single_rank(mc, gpu_ctx):

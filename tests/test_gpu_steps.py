@@ -205,7 +205,9 @@ def test_repeated_calls_speculate_and_every_input_change_misses(mc, gpu_ctx, mod
     t = ctx.read_timing()
     ctx.timing(False)
     assert t["main_launches"] == 5
-    assert t["prep_launches"] == 2, t      # calls 1 and 2 prepare; 3.. find the tables ready
+    # calls 1 and 2 prepare; 3.. find the tables ready.  SLERP prepares every call (no fused
+    # next-call kernel, MC_FUSE_SLERP=0)
+    assert t["prep_launches"] == (5 if mode == "pose_slerp" else 2), t
     rng = np.random.default_rng(5)
     tr2 = {k: v.copy() for k, v in tr.items()}
     tr2["orientation_imu"] = tr2["orientation_imu"] + rng.normal(0, 0.05, tr2["orientation_imu"].shape)
@@ -238,3 +240,32 @@ def test_repeated_calls_speculate_and_every_input_change_misses(mc, gpu_ctx, mod
     ctx.deskew_steps(b, out, 3, mode=mode, pipeline=True)
     ctx.deskew(b, out, mode=mode)
     assert np.array_equal(_cols(out), want)
+
+
+# ---------------------------------------------------------------------------------------------
+# device-measured sub-tile order (mc_tune_order)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
+def test_tune_order_keeps_bytes_and_applies_per_size(mc, gpu_ctx, mode):
+    """mc_tune_order times both sub-tile orders and keeps the faster one for the mode and batch size;
+    the deskew output is the same bytes whichever order runs (every later call, incl. pipelined
+    steps), and a batch of another size keeps the default order."""
+    counts = [3000, 0, 1, 257, 20_000, 1023, 4097]
+    ctx = mc.Context(0)
+    b, tr, times = _setup(mc, ctx, counts)
+    ref = _fresh(mc, counts, mode, lambda c, bb: None)
+    out = ctx.batch(b.counts)
+    r = ctx.tune_order(b, out, mode=mode, launches=3, rounds=2)
+    assert r["chosen"] in ("dealt", "xcd") and r["dealt_us"] > 0 and r["xcd_us"] > 0, r
+    assert np.array_equal(_cols(out), ref)        # the tuning launches wrote the same output
+    out2 = ctx.batch(b.counts)
+    ctx.deskew(b, out2, mode=mode)
+    assert np.array_equal(_cols(out2), ref)
+    ctx.deskew_steps(b, out2, 3, mode=mode, pipeline=True)
+    assert np.array_equal(_cols(out2), ref)
+    with pytest.raises(ValueError):               # in place: repeated launches would compound
+        ctx.tune_order(b, b, mode=mode)
+    empty = ctx.batch([0, 0], with_time=True)
+    empty.set_frame_times(times[:2])
+    empty.set_frame_starts((times[:2] * 1e9).astype(np.int64))
+    assert ctx.tune_order(empty, ctx.batch([0, 0]), mode=mode)["chosen"] is None
