@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0                                          # MI355X_MICROARC
 KERNEL = {"pose_slerp": "k_deskew_points<1", "imu": "k_deskew_points<2", "frame": "k_deskew_frame"}
 # the kernel each issue mode times (pipeline: the step's deskew with the next step's prep in its first
 # workgroups; the last step's launch is the plain kernel)
-KERNEL_OF = {"pipeline": {"pose_slerp": "k_deskew_points<1, false, false>", "imu": "k_deskew_points<2, true, false>",
+KERNEL_OF = {"pipeline": {"pose_slerp": "k_deskew_points<1, true, false>", "imu": "k_deskew_points<2, true, false>",
                           "frame": "k_deskew_frame_next"},
              "calls": {"pose_slerp": "k_deskew_points<1, false, false>", "imu": "k_deskew_points<2, false, false>",
                        "frame": "k_deskew_frame"}}
@@ -920,11 +920,9 @@ def main():
             "prep_avg_us": r["prep_avg_us"],
             "step_issue": {"calls": "per-call launches; prep as an any-order packet on the kernel's queue",
                            "graph": f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
-                           "pipeline": (f"Context.deskew_steps(pipeline=True): per step an any-order k_prep packet and "
-                                        f"the plain deskew kernel ({2 * r['steps']} launches)" if args.mode == "pose_slerp"
-                                        else f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
-                                        "k_prep, then each step's deskew kernel with the next step's prep in its first "
-                                        "workgroups (every step runs its own prep, one launch ahead)")}[args.issue],
+                           "pipeline": f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
+                                       "k_prep, then each step's deskew kernel with the next step's prep in its "
+                                       "first workgroups (every step runs its own prep, one launch ahead)"}[args.issue],
             "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
                           "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"],
                           "ms_per_step": v["wall_s"] / v["steps"] * 1e3}

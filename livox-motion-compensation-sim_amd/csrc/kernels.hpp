@@ -55,6 +55,9 @@ namespace mc {
 #ifndef MC_SLERP_WAVES
 #define MC_SLERP_WAVES 4     // waves/SIMD the SLERP kernel is compiled for (VGPR budget 512 / waves)
 #endif
+#ifndef MC_DIAG_FUSED_NOPREP
+#define MC_DIAG_FUSED_NOPREP 0   // diagnostic timing build: the fused kernels' prep workgroups do nothing
+#endif
 #ifndef MC_SLERP_NEXT_WAVES
 #define MC_SLERP_NEXT_WAVES MC_SLERP_WAVES   // the SLERP kernel carrying the next step's prep
 #endif
@@ -360,13 +363,26 @@ __device__ __forceinline__ PoseSample load_pose(const double* time, const double
   return s;
 }
 
+// A pose sample with its orientation as a unit quaternion (k_prep's SLERP records: each probe lane
+// converts its own sample once, so a record needs no sincos of its two samples' Euler angles — 194
+// -> fewer VGPRs for the SLERP prep, which the fused next-step kernel must fit in 128).
+struct QSample {
+  double t, q[4], p[3];
+};
+__device__ __forceinline__ QSample qsample_of(const PoseSample& s) {
+  QSample r;
+  r.t = s.t;
+  euler_xyz_quat(s.r[0], s.r[1], s.r[2], r.q);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) r.p[c] = s.p[c];
+  return r;
+}
+
 // segment [a, b] of the pose table: shortest-arc quaternion pair, Theta, position delta.
 // Theta = 2 atan2(|q1 - q0|, |q1 + q0|) is accurate at every angle (acos(q0.q1) loses half the
 // digits below ~1e-4), and q1 - cos(Theta) q0 then has norm sin(Theta) to rounding.
-__device__ __forceinline__ PoseSeg pose_seg_of(const PoseSample& a, const PoseSample& b) {
-  double q0[4], q1[4];
-  euler_xyz_quat(a.r[0], a.r[1], a.r[2], q0);
-  euler_xyz_quat(b.r[0], b.r[1], b.r[2], q1);
+// Theta of the quaternion pair (q0, q1), q1 flipped onto q0's hemisphere first (in place)
+__device__ __forceinline__ double quat_theta(const double q0[4], double q1[4]) {
   const double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
   if (d < 0.0) { q1[0] = -q1[0]; q1[1] = -q1[1]; q1[2] = -q1[2]; q1[3] = -q1[3]; }
   double dm = 0.0, dpl = 0.0;
@@ -375,7 +391,14 @@ __device__ __forceinline__ PoseSeg pose_seg_of(const PoseSample& a, const PoseSa
     dm = fma(q1[i] - q0[i], q1[i] - q0[i], dm);
     dpl = fma(q1[i] + q0[i], q1[i] + q0[i], dpl);
   }
-  const double th = 2.0 * atan2(sqrt(dm), sqrt(dpl));
+  return 2.0 * atan2(sqrt(dm), sqrt(dpl));
+}
+
+__device__ __forceinline__ PoseSeg pose_seg_q(const QSample& a, const QSample& b) {
+  double q0[4], q1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { q0[i] = a.q[i]; q1[i] = b.q[i]; }
+  const double th = quat_theta(q0, q1);
   double sn, cs;
   sincos_prep(th, &sn, &cs);
   const double ratio = th > 0.0 ? th / sn : 1.0;   // th / sin(th), 1 at th = 0
@@ -396,6 +419,9 @@ __device__ __forceinline__ PoseSeg pose_seg_of(const PoseSample& a, const PoseSa
   s.inv_dt = dt > 0.0 ? 1.0 / dt : 0.0;
   s.tf = 0.0;
   return s;
+}
+__device__ __forceinline__ PoseSeg pose_seg_of(const PoseSample& a, const PoseSample& b) {
+  return pose_seg_q(qsample_of(a), qsample_of(b));
 }
 
 // segment k of the pose table (k + 1 clamped to the last sample)
@@ -589,6 +615,30 @@ __device__ __forceinline__ PoseSample fetch_pose(const PoseSample& v, int64_t ba
   }
   return s;
 }
+// QSample k of the pose table whose window [base, base + 64) the lanes hold as QSamples (v); a sample
+// outside the window is loaded and converted.  Every lane of the wave must call it.
+__device__ __forceinline__ QSample fetch_q(const QSample& v, int64_t base, int64_t k, const PrepArgs& a) {
+  const int64_t j = k - base;
+  const bool in = j >= 0 && j < 64;
+  const int src = in ? (int)j : 0;
+  QSample s;
+  s.t = __shfl(v.t, src, 64);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s.q[c] = __shfl(v.q[c], src, 64);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) s.p[c] = __shfl(v.p[c], src, 64);
+  if (!in) s = qsample_of(load_pose(a.time, a.pos, a.rpy, k));
+  return s;
+}
+// the orientation quaternion of pose sample k alone, the same way
+__device__ __forceinline__ void fetch_quat(const QSample& v, int64_t base, int64_t k, const PrepArgs& a, double q[4]) {
+  const int64_t j = k - base;
+  const bool in = j >= 0 && j < 64;
+  const int src = in ? (int)j : 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) q[c] = __shfl(v.q[c], src, 64);
+  if (!in) euler_xyz_quat(a.rpy[3 * k], a.rpy[3 * k + 1], a.rpy[3 * k + 2], q);
+}
 __device__ __forceinline__ ImuSample fetch_imu(const ImuSample& v, int64_t base, int64_t k, const PrepArgs& a) {
   ImuSample s;
   s.ts = fetch(v.ts, base, k, a.imu_ts, 1);
@@ -662,13 +712,13 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
   const int64_t fs = MODE == 2 ? a.frame_start[f] : 0;
   // the probe window and its samples (one round)
   int64_t base = INT64_MIN / 2;   // no window: every fetch loads
-  PoseSample pv{};
+  QSample pv{};
   ImuSample iv{};
   if (MC_PREP_PROBE) {
     if (MODE == 1) {
       const double xm = has ? tf + 0.5e-9 * ((double)tr.x + (double)tr.y) : tf;
       base = probe_base<double>(a.T, a.time[0], a.time[a.T - 1], xm);
-      if (base + lane < a.T) pv = load_pose(a.time, a.pos, a.rpy, base + lane);
+      if (base + lane < a.T) pv = qsample_of(load_pose(a.time, a.pos, a.rpy, base + lane));
     } else {
       const double xm = (double)fs + (has ? 0.5 * ((double)tr.x + (double)tr.y) : 0.0);
       base = probe_base<int64_t>(a.M, a.imu_ts[0], a.imu_ts[a.M - 1], xm);
@@ -699,14 +749,14 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
   const int64_t W = khi - klo + 1;
   auto clampk = [&](int64_t k) { return k < n_tab - 1 ? k : n_tab - 1; };
   // frame-relative ns where the segment of sample s starts (the LDS path's s_bnd, the SGPR path's bnd1)
-  auto bound_pose = [&](const PoseSample& s) -> int64_t { return rel_ns_ceil(s.t, tf); };
+  auto bound_pose = [&](const QSample& s) -> int64_t { return rel_ns_ceil(s.t, tf); };
   auto bound_imu = [&](const ImuSample& s) -> int64_t { return s.ts - fs; };
   auto bound_at = [&](int64_t k) -> int64_t { return MODE == 1 ? rel_ns_ceil(a.time[k], tf) : a.imu_ts[k] - fs; };
   // record of segment k from samples k, k+1 (clamped) / IMU k, k+1 (or k alone at the end)
   // s0, s1 come from fetch_pose / fetch_imu; write at dst[slot]
   // a record (its segment's angle measure returned: Theta, or the IMU rate bound)
-  auto pose_rec = [&](const PoseSample& s0, const PoseSample& s1, void* dst, int64_t slot, bool wr) {
-    const PoseSeg sg = pose_seg_of(s0, s1);
+  auto pose_rec = [&](const QSample& s0, const QSample& s1, void* dst, int64_t slot, bool wr) {
+    const PoseSeg sg = pose_seg_q(s0, s1);
     if (wr) reinterpret_cast<PoseWin*>(dst)[slot] = make_pose_win(sg, tf);
     return sg.th;
   };
@@ -727,7 +777,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     w.W = (int16_t)(W > kWinMax ? kWinMax + 1 : W);
     double ang;   // lane 0: segment klo, lane 1: klo + 1
     if (MODE == 1) {
-      const PoseSample s0 = fetch_pose(pv, base, k, a), s1 = fetch_pose(pv, base, k1, a);
+      const QSample s0 = fetch_q(pv, base, k, a), s1 = fetch_q(pv, base, k1, a);
       ang = pose_rec(s0, s1, a.frec, 2 * f + lane, writes);
       w.bnd1 = W >= 2 ? bound_pose(s1) : INT64_MAX;   // lane 0: s1 = sample klo + 1
     } else {
@@ -753,7 +803,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
   int64_t my_bnd = INT64_MAX;
   if (in_regs) {
     const int64_t kb = clampk(klo + lane);
-    const int64_t b = MODE == 1 ? bound_pose(fetch_pose(pv, base, kb, a)) : bound_imu(fetch_imu(iv, base, kb, a));
+    const int64_t b = MODE == 1 ? rel_ns_ceil(fetch(pv.t, base, kb, a.time, 1), tf) : bound_imu(fetch_imu(iv, base, kb, a));
     my_bnd = lane == 0 ? INT64_MIN : (lane < W ? b : INT64_MAX);
   }
   auto seg_of = [&](int64_t t) {
@@ -768,6 +818,20 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
       if (bound_at(mid) <= t) lo = mid; else hi = mid - 1;
     }
     return lo;
+  };
+  // SLERP: lane j holds Theta of the probe window's segment base + j (samples base + j and the next);
+  // a segment outside the window counts as pi/2, the largest Theta (tier 2 covers every segment)
+  double th_lane = 0.0;
+  if (MODE == 1) {
+    double qn[4], q0[4] = {pv.q[0], pv.q[1], pv.q[2], pv.q[3]};
+    fetch_quat(pv, base, clampk(base + lane + 1), a, qn);
+    th_lane = quat_theta(q0, qn);
+  }
+  auto theta_of = [&](int64_t k) {   // every lane must call it (a cross-lane read)
+    const int64_t j = k - base;
+    const bool in = j >= 0 && j < 64;
+    const double v = __shfl(th_lane, in ? (int)j : 0, 64);
+    return in ? v : 1.5707963267948966;
   };
   const int64_t st0 = (int64_t)a.ftile[f] * kSub, st1 = (int64_t)a.ftile[f + 1] * kSub;
   for (int64_t sb = st0; sb < st1; sb += 64) {   // a uniform trip count: the shuffles see every lane
@@ -785,11 +849,17 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     const bool rec = valid && n <= MC_FASTPATH_MAXW;
     double ang;
     if (MODE == 1) {
-      const PoseSample sa = fetch_pose(pv, base, ka, a), sb_ = fetch_pose(pv, base, kb, a);
-      const PoseSample sc = fetch_pose(pv, base, kc, a);
-      w.bnd1 = n >= 2 ? bound_pose(sb_) : INT64_MAX;
-      ang = pose_rec(sa, sb_, a.srec, 2 * st, rec);
-      if (n >= 2) ang = fmax(ang, pose_rec(sb_, sc, a.srec, 2 * st + 1, rec));
+      // SLERP: no sub-tile records — the deskew kernel reads segments k0, k0 + 1 of the step's
+      // segment table (pose_seg) and adds the frame time; here only the window, its boundary and
+      // the tier from the two segments' Theta (building the records here held three samples and two
+      // segments live: 200 VGPRs, more than the fused next-step kernel's 128)
+      const double t_kb = fetch(pv.t, base, kb, a.time, 1);   // every lane (a cross-lane read)
+      w.bnd1 = n >= 2 ? rel_ns_ceil(t_kb, tf) : INT64_MAX;
+      ang = theta_of(ka);
+      const double ang1 = theta_of(kb);
+      if (n >= 2) ang = fmax(ang, ang1);
+      (void)kc;
+      (void)rec;
     } else {
       const ImuSample sa = fetch_imu(iv, base, ka, a), sb_ = fetch_imu(iv, base, kb, a);
       const ImuSample sc = fetch_imu(iv, base, kc, a);
@@ -1328,10 +1398,18 @@ __device__ __forceinline__ T select_rec(bool second, const T& a, const T& b) {
 
 // The SGPR path of a window of <= 2 segments at tier TIER: each wave votes whether its points all
 // sit in one segment; a wave across the boundary peels its two segments.
+// set_tf (SLERP sub-tile windows): rec points into the segment table; its records get the frame time tf
 template <int MODE, int TIER>
-__device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin& fw, bool act, const int4& Tq,
-                                          float4& X, float4& Y, float4& Z) {
+__device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin& fw, bool set_tf, double tf,
+                                          bool act, const int4& Tq, float4& X, float4& Y, float4& Z) {
   const PolyOf<TIER> poly = poly_load<TIER>();
+  auto load_rec = [&](int j) {
+    WinOf<MODE> w = ldu(rec + j);
+    if constexpr (MODE == 1) {
+      if (set_tf) w.tf = tf;
+    }
+    return w;
+  };
   // IMU: both 64-byte records in SGPRs before the vote (their scalar-load latency then overlaps the
   // point loads instead of following the vote); a 144-byte SLERP record pair would not fit
   WinOf<MODE> r0, r1;
@@ -1354,7 +1432,7 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
     // loads of the 144-byte record instead of scalar loads
     WinOf<MODE> w;
     if constexpr (MODE == 2 && MC_IMU_PRELOAD) w = select_rec(use1, r0, r1);
-    else w = ldu(rec + (use1 ? 1 : 0));
+    else w = load_rec(use1 ? 1 : 0);
     points4<MODE>(w, poly, Tq, X, Y, Z);
   } else {
     int seg[4];
@@ -1363,7 +1441,7 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
     if constexpr (MODE == 2 && MC_IMU_PRELOAD)
       points_peeled<MODE>(seg, [&](int j) { return select_rec(j != 0, r0, r1); }, poly, Tq, X, Y, Z);
     else
-      points_peeled<MODE>(seg, [&](int j) { return ldu(rec + j); }, poly, Tq, X, Y, Z);
+      points_peeled<MODE>(seg, [&](int j) { return load_rec(j); }, poly, Tq, X, Y, Z);
   }
 }
 
@@ -1387,7 +1465,9 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
     const DeskewArgs a, const PrepArgs pn, const uint32_t pre) {
   if constexpr (NEXT) {
     if (blockIdx.x < pre) {
+#if !MC_DIAG_FUSED_NOPREP
       prep_body<MODE>(pn, blockIdx.x);
+#endif
       return;
     }
   }
@@ -1424,14 +1504,17 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
     bool sub = true;
     if constexpr (MODE != 2) sub = MC_SUBTILE_WIN && ldu(a.fwin + f).W > MC_FASTPATH_MAXW;
     const FrameWin fw = ldu(sub ? a.swin + st : a.fwin + f);
-    const Win* rec = sub ? srec + 2 * st : frec + 2 * f;
+    // SLERP sub-tile windows point into the step's segment table, whose records carry no frame time
+    const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) + fw.klo : srec + 2 * st) : frec + 2 * f;
+    const bool set_tf = MODE == 1 && sub;
 
     if (fw.W <= MC_FASTPATH_MAXW) {
       // the tier k_prep chose for the window: its coefficient load is issued here, beside the point
       // loads, not behind the vote that needs them
-      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, act, Tq, X, Y, Z);
-      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, act, Tq, X, Y, Z);
-      else fast_path<MODE, kTierAny<MODE>>(rec, fw, act, Tq, X, Y, Z);
+      const double tf = set_tf ? ldu(a.frame_time + f) : 0.0;
+      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, set_tf, tf, act, Tq, X, Y, Z);
+      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, set_tf, tf, act, Tq, X, Y, Z);
+      else fast_path<MODE, kTierAny<MODE>>(rec, fw, set_tf, tf, act, Tq, X, Y, Z);
     } else if (fw.W <= kWinMax) {
       const int W = fw.W;
       if (tid < W) {

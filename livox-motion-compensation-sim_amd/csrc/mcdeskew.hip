@@ -610,13 +610,13 @@ int mc_batch_checksum(mc_batch* b, double* sums) {
 #define MC_SPEC_PREP 1       // per-call speculation of the next identical call's prep (mc_ctx::PrepKey)
 #endif
 // Whether a mode's steps carry the next step's prep in their own launch (k_deskew_points<MODE, true>
-// / k_deskew_frame_next; mc_deskew's speculation and mc_deskew_steps' pipeline).  Not for SLERP since
-// round 3: with the float64 math its fused kernel spills the prep branch to scratch at 4 waves /
-// SIMD, and the prep as an any-order packet before the plain kernel streams faster — dealt order
-// 317.2 vs 345.1 us per launch over 2 replicas, step wall 320.6-323.8 vs 326.1-364.6 us
-// (profiles/round3/s15/ab_slerp_fused.log).  IMU's and frame's fused kernels need no scratch.
+// / k_deskew_frame_next; mc_deskew's speculation and mc_deskew_steps' pipeline).  MC_FUSE_SLERP=0
+// issues SLERP's prep as an any-order packet before the plain kernel instead: the round-3 float64 prep
+// spilled the fused kernel to scratch (345.1 vs 317.2 us, profiles/round3/s15); with the slimmed
+// prep (78 VGPRs, no scratch) the fused launch is ahead again, step wall 320.2-328.3 vs 329.5-329.6 us
+// (profiles/round3/s19/ab_fuse.log).
 #ifndef MC_FUSE_SLERP
-#define MC_FUSE_SLERP 0
+#define MC_FUSE_SLERP 1
 #endif
 #ifndef MC_DIAG_NO_PREP
 #define MC_DIAG_NO_PREP 0    // diagnostic timing build: after 4 calls, no k_prep (tables of earlier calls)

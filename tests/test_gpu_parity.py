@@ -581,11 +581,11 @@ def test_timing_counts_launches(mc, gpu_ctx, mode):
         gpu_ctx.deskew(b, out, mode=mode)
     t = gpu_ctx.read_timing()
     gpu_ctx.timing(False)
-    # IMU / frame: calls 1 and 2 run k_prep; call 2's launch also prepares call 3's tables (identical
-    # key), so call 3 needs none (mc_deskew's per-call speculation, test_gpu_steps.py).  SLERP issues
-    # its prep before the plain kernel on every call (MC_FUSE_SLERP=0)
-    preps = 3 if mode == "pose_slerp" else 2
-    assert t["main_launches"] == 3 and t["prep_launches"] == preps and t["main_ms"] > 0
+    # calls 1 and 2 run k_prep; call 2's launch also prepares call 3's tables (identical key), so
+    # call 3 needs none (mc_deskew's per-call speculation, test_gpu_steps.py).  A build without the
+    # fused SLERP kernel (MC_FUSE_SLERP=0) issues the SLERP prep before the plain kernel on every call
+    assert t["main_launches"] == 3 and t["main_ms"] > 0
+    assert t["prep_launches"] == 2 or (mode == "pose_slerp" and t["prep_launches"] == 3), t
 
 
 def test_rccl_gather_single_rank(mc, gpu_ctx):

@@ -205,9 +205,9 @@ def test_repeated_calls_speculate_and_every_input_change_misses(mc, gpu_ctx, mod
     t = ctx.read_timing()
     ctx.timing(False)
     assert t["main_launches"] == 5
-    # calls 1 and 2 prepare; 3.. find the tables ready.  SLERP prepares every call (no fused
-    # next-call kernel, MC_FUSE_SLERP=0)
-    assert t["prep_launches"] == (5 if mode == "pose_slerp" else 2), t
+    # calls 1 and 2 prepare; 3.. find the tables ready.  A build without the fused SLERP kernel
+    # (MC_FUSE_SLERP=0) prepares every SLERP call
+    assert t["prep_launches"] == 2 or (mode == "pose_slerp" and t["prep_launches"] == 5), t
     rng = np.random.default_rng(5)
     tr2 = {k: v.copy() for k, v in tr.items()}
     tr2["orientation_imu"] = tr2["orientation_imu"] + rng.normal(0, 0.05, tr2["orientation_imu"].shape)
