@@ -16,6 +16,9 @@
 
 #include "layout.hpp"
 
+#ifndef MC_CODEC_NT_STORE
+#define MC_CODEC_NT_STORE 0  // LVX / PCD file bytes stored non-temporally (written once, never re-read)
+#endif
 #ifndef MC_XCD_CODEC
 #define MC_XCD_CODEC 1       // LVX / PCD unit order (XCD-contiguous, layout.hpp)
 #endif
@@ -110,7 +113,13 @@ __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const ch
   for (int c = c0 + threadIdx.x; c < c1; c += NT) {
     const int b0 = c << 4;
     if (b0 >= lo && b0 + 16 <= hi) {
+#if MC_CODEC_NT_STORE
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
+      __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));
+#else
       *reinterpret_cast<uint4*>(g + b0) = *reinterpret_cast<const uint4*>(lds + b0);
+#endif
     } else {
       const int e = b0 + 16 < hi ? b0 + 16 : hi;
       for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];

@@ -64,6 +64,9 @@ namespace mc {
 #ifndef MC_IMU_PRELOAD
 #define MC_IMU_PRELOAD 1     // IMU: both window records loaded before the wave's segment vote
 #endif
+#ifndef MC_IMU_R1_UNCOND
+#define MC_IMU_R1_UNCOND 0   // IMU: load the second record without waiting for the window's W
+#endif
 #ifndef MC_IMU_WAVES
 #define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
 #endif
@@ -1415,7 +1418,7 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
   WinOf<MODE> r0, r1;
   if constexpr (MODE == 2 && MC_IMU_PRELOAD) {
     r0 = ldu(rec);
-    r1 = ldu(rec + (fw.W == 2 ? 1 : 0));
+    r1 = ldu(rec + (MC_IMU_R1_UNCOND || fw.W == 2 ? 1 : 0));   // (slot 1 exists for every window)
   }
   bool use1 = false, mixed = false;
   if (fw.W == 2) {

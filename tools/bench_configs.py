@@ -44,7 +44,7 @@ def main():
         line = json.loads(p.stdout.strip().splitlines()[-1])
         res[name] = {"config": line["config"], "value_Mpoints_s": line["value"], "ms_per_step": line["ms_per_step"],
                      "modes": line["modes"], "roofline": line["roofline"], "parity": line.get("parity"),
-                     "step_over_kernel": line.get("step_over_kernel")}
+                     "step_over_kernel": line.get("step_over_kernel"), "order_tune": line.get("order_tune")}
         print(name, {m: round(v["frac"], 4) for m, v in line["modes"].items()}, flush=True)
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
