@@ -571,8 +571,8 @@ def measure_deskew_pcd(ctx, b_in, b_out, mode, n_rank, reps):
     finally:
         buf.close()
 
-    def med(name, key):
-        return float(np.median([t[key + "_ms"] / max(t[key + "_launches"], 1) * t[key + "_launches"] for t in arms[name]]))
+    def med(name, key):   # median over the calls of the milliseconds the call's kernels of that kind took
+        return float(np.median([t[key + "_ms"] for t in arms[name]]))
     k_sep, k_fus = med("separate", "main"), med("fused", "main")
     c_sep, c_fus = med("separate", "codec"), med("fused", "codec")
     text_b = int(pos[-1])
