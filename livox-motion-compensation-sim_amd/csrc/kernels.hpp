@@ -68,6 +68,9 @@ namespace mc {
 #define MC_IMU_R1_UNCOND 1   // IMU: load the second record without waiting for the window's W:
                              // 333.0 vs 353.8 us over 3 replicas (profiles/round3/s21/ab_imu_r1.log)
 #endif
+#ifndef MC_IMU_HOIST
+#define MC_IMU_HOIST 0       // IMU: the sub-tile's two records loaded before its window record
+#endif
 #ifndef MC_IMU_WAVES
 #define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
 #endif
@@ -1405,7 +1408,8 @@ __device__ __forceinline__ T select_rec(bool second, const T& a, const T& b) {
 // set_tf (SLERP sub-tile windows): rec points into the segment table; its records get the frame time tf
 template <int MODE, int TIER>
 __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin& fw, bool set_tf, double tf,
-                                          bool act, const int4& Tq, float4& X, float4& Y, float4& Z) {
+                                          bool act, const int4& Tq, float4& X, float4& Y, float4& Z,
+                                          const WinOf<MODE>* pre0 = nullptr, const WinOf<MODE>* pre1 = nullptr) {
   const PolyOf<TIER> poly = poly_load<TIER>();
   auto load_rec = [&](int j) {
     WinOf<MODE> w = ldu(rec + j);
@@ -1418,8 +1422,13 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
   // point loads instead of following the vote); a 144-byte SLERP record pair would not fit
   WinOf<MODE> r0, r1;
   if constexpr (MODE == 2 && MC_IMU_PRELOAD) {
-    r0 = ldu(rec);
-    r1 = ldu(rec + (MC_IMU_R1_UNCOND || fw.W == 2 ? 1 : 0));   // (slot 1 exists for every window)
+    if (MC_IMU_HOIST) {   // loaded by the caller before the window record
+      r0 = *pre0;
+      r1 = *pre1;
+    } else {
+      r0 = ldu(rec);
+      r1 = ldu(rec + (MC_IMU_R1_UNCOND || fw.W == 2 ? 1 : 0));   // (slot 1 exists for every window)
+    }
   }
   bool use1 = false, mixed = false;
   if (fw.W == 2) {
@@ -1507,6 +1516,13 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
     // vector load of bnd1 whose wait held back the point loads)
     bool sub = true;
     if constexpr (MODE != 2) sub = MC_SUBTILE_WIN && ldu(a.fwin + f).W > MC_FASTPATH_MAXW;
+    // IMU (MC_IMU_HOIST): the sub-tile's two records are at srec + 2 st whatever its window says, so
+    // they are loaded beside the window record instead of after it
+    Win hr0, hr1;
+    if constexpr (MODE == 2 && MC_IMU_HOIST) {
+      hr0 = ldu(srec + 2 * st);
+      hr1 = ldu(srec + 2 * st + 1);
+    }
     const FrameWin fw = ldu(sub ? a.swin + st : a.fwin + f);
     // SLERP sub-tile windows point into the step's segment table, whose records carry no frame time
     const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) + fw.klo : srec + 2 * st) : frec + 2 * f;
@@ -1516,9 +1532,9 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
       // the tier k_prep chose for the window: its coefficient load is issued here, beside the point
       // loads, not behind the vote that needs them
       const double tf = set_tf ? ldu(a.frame_time + f) : 0.0;
-      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, set_tf, tf, act, Tq, X, Y, Z);
-      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, set_tf, tf, act, Tq, X, Y, Z);
-      else fast_path<MODE, kTierAny<MODE>>(rec, fw, set_tf, tf, act, Tq, X, Y, Z);
+      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1);
+      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1);
+      else fast_path<MODE, kTierAny<MODE>>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1);
     } else if (fw.W <= kWinMax) {
       const int W = fw.W;
       if (tid < W) {

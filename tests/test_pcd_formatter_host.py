@@ -33,3 +33,33 @@ def test_line_writers_match_printf(tmp_path, writer):
     r = subprocess.run([str(exe), "200000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
     assert "bad 0" in r.stdout
+
+
+def test_deskew_pcd_value_length_rule():
+    """The per-value byte count the fused deskew -> PCD kernels sum (layout.hpp PcdCount:
+    9 + [v < 0] + [|v| >= 10] + [|v| >= 100] + [|v| >= 1000] for |v| < 4294, a float32 value widened to
+    float64 and written "%.6f" + separator, LMC:948) against Python's own formatting: every float32
+    within 4096 ulps of +-10 / 100 / 1000, of the 4294 cut-off and of 0, and random float32 values."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    vals = [np.float32(0.0), np.float32(-0.0)]
+    for c in (1e-38, 10.0, 100.0, 1000.0, 4294.0, 1.0):
+        for sgn in (1.0, -1.0):
+            x = np.float32(sgn * c)
+            lo = x
+            for _ in range(4096):
+                lo = np.nextafter(lo, np.float32(0.0))
+            hi = x
+            for _ in range(4096):
+                hi = np.nextafter(hi, np.float32(sgn * np.inf))
+            vals += list(np.linspace(lo, hi, 8193, dtype=np.float32))
+    vals += list((rng.uniform(-4300, 4300, 200_000)).astype(np.float32))
+    vals += list((rng.standard_normal(50_000) * 10.0 ** rng.uniform(-9, 3.6, 50_000)).astype(np.float32))
+    v = np.asarray(vals, dtype=np.float32)
+    a = np.abs(v)
+    fast = a < np.float32(4294.0)
+    rule = 9 + np.signbit(v) + (a >= 10) + (a >= 100) + (a >= 1000)
+    want = np.array([len("%.6f" % float(x)) + 1 for x in v[fast]])
+    bad = np.flatnonzero(rule[fast] != want)
+    assert bad.size == 0, [(float(v[fast][i]), int(rule[fast][i]), int(want[i])) for i in bad[:5]]
+    assert not fast[np.isclose(np.abs(v), 4294.0, atol=0) & (np.abs(v) >= 4294.0)].any()
