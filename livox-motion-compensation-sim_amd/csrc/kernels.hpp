@@ -66,10 +66,14 @@ namespace mc {
 #endif
 #ifndef MC_IMU_R1_UNCOND
 #define MC_IMU_R1_UNCOND 1   // IMU: load the second record without waiting for the window's W:
-                             // 333.0 vs 353.8 us over 3 replicas (profiles/round3/s21/ab_imu_r1.log)
+                             // 333.0 vs 353.8 us over 3 replicas in one process (profiles/round3/s21),
+                             // not reproduced on the next box (339.7 vs 333.9, s23); in bench.py's
+                             // own steps 351.7 / 354.2 vs 358.3 / 358.3 us (s23), so it stays on
 #endif
 #ifndef MC_IMU_HOIST
 #define MC_IMU_HOIST 0       // IMU: the sub-tile's two records loaded before its window record
+                             // (rejected: 338.7 vs 339.7 us, bench 355.7-357.4; the plain IMU kernel
+                             // then spills a VGPR, profiles/round3/s23)
 #endif
 #ifndef MC_IMU_WAVES
 #define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
