@@ -20,6 +20,9 @@
 #define MC_CODEC_NT_STORE 1  // LVX / PCD file bytes stored non-temporally (written once, never re-read):
                              // LVX 308.4 vs 325.2 us, PCD 1005.5 vs 1057.8 us (profiles/round3/s21/ab_codec_nt.log)
 #endif
+#ifndef MC_CODEC_NT_LOAD
+#define MC_CODEC_NT_LOAD 0   // PCD: the batch's float32 columns read non-temporally
+#endif
 #ifndef MC_XCD_CODEC
 #define MC_XCD_CODEC 1       // LVX / PCD unit order (XCD-contiguous, layout.hpp)
 #endif
@@ -917,7 +920,12 @@ constexpr int32_t kPcdSlowTile = 1 << 30;
 // columns 0..3 of dense row `row` of a batch source as float32 (codec_point widens them)
 __device__ __forceinline__ void codec_point_f32(const CodecFrames& s, int32_t f, int64_t row, float c[4]) {
   const float* q = s.cols + bidx(s.C, 0, s.poff[f] + (row - s.doff[f]));
+#if MC_CODEC_NT_LOAD
+  c[0] = __builtin_nontemporal_load(q); c[1] = __builtin_nontemporal_load(q + kBlkPts);
+  c[2] = __builtin_nontemporal_load(q + 2 * kBlkPts); c[3] = __builtin_nontemporal_load(q + 3 * kBlkPts);
+#else
   c[0] = q[0]; c[1] = q[kBlkPts]; c[2] = q[2 * kBlkPts]; c[3] = q[3 * kBlkPts];
+#endif
 }
 
 // F32: the source is a batch's float32 columns (the packed path then works in float32, above)
