@@ -38,7 +38,9 @@ namespace mc {
 #define MC_STORE_POINTS 2    // per-point kernels output stores: sc1 write-through (see st_pol)
 #endif
 #ifndef MC_STORE_IMU
-#define MC_STORE_IMU 1       // the IMU kernel's output stores: nt (-4 % vs sc1, tools/ab.py)
+#define MC_STORE_IMU 4       // the IMU kernel's output stores: sc1 nt — bench 334.5-338.0 vs 353.2-363.1 us
+                             // with nt (3 runs each, profiles/round3/s30); in tools/ab.py 331.6 vs 340.6
+                             // over 4 replicas (s29; round 2 measured nt 4 % ahead of sc1)
 #endif
 #ifndef MC_FASTPATH_MAXW
 #define MC_FASTPATH_MAXW 2   // frames spanning <= this many segments take the SGPR (no-LDS) path
@@ -75,6 +77,15 @@ namespace mc {
                              // (rejected: 338.7 vs 339.7 us, bench 355.7-357.4; the plain IMU kernel
                              // then spills a VGPR, profiles/round3/s23)
 #endif
+#ifndef MC_IMU_SEGREC
+#define MC_IMU_SEGREC 1      // IMU: a sub-tile's records are segments klo, klo + 1 of the step's
+                             // segment table (shared by the ~5 sub-tiles of a 5 ms segment, as SLERP's
+                             // sub-tile windows) instead of its own two records written by k_prep:
+                             // identical output, 7.5 MB less prep writes per 60 M-point step, 329.1 vs
+                             // 349.3 us over 5 replicas (tools/ab.py), bench 353.7-358.2 vs 354.3-361.5
+                             // (profiles/round3/s28)
+#endif
+static_assert(!(MC_IMU_HOIST && MC_IMU_SEGREC), "MC_IMU_HOIST loads the per-sub-tile records");
 #ifndef MC_IMU_WAVES
 #define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
 #endif
@@ -211,15 +222,20 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 //   0 plain, 1 nt (builtin), 2 sc1 write-through, 3 sc0 sc1, 4 sc1 nt.
 // The per-point kernels run 10-12% faster with sc1 write-through stores (the line leaves L2 at
 // once instead of being retained dirty); the frame kernel is 2% faster with nt.
+// The inline-asm stores end in `s_nop 1`: a store of more than 8 bytes reads its data VGPRs after
+// issue, and on gfx940+ a VALU write to them needs 2 wait states after the store.  The compiler
+// inserts those wait states after its own stores but cannot see a store inside asm; without them
+// a VALU that reuses the first data register pair right behind the store corrupts the stored
+// line's first 8 bytes (the stager's sc1 build lost x and z, profiles/round3/s08, s24).
 template <int POL>
 __device__ __forceinline__ void st_pol(float* p, const float4& v) {
   v4f t = {v.x, v.y, v.z, v.w};
   if constexpr (POL == 2) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
   } else if constexpr (POL == 3) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(t) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
   } else if constexpr (POL == 4) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(t) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
   } else if constexpr (POL == 1) {
     __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
   } else {
@@ -857,7 +873,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     w.W = (int16_t)(n > kWinMax ? kWinMax + 1 : n);
     // samples k0, k0 + 1, k0 + 2 (clamped): records k0 and k0 + 1 and the boundary of k0 + 1
     const int64_t ka = clampk(k0), kb = clampk(k0 + 1), kc = clampk(k0 + 2);
-    const bool rec = valid && n <= MC_FASTPATH_MAXW;
+    const bool rec = valid && n <= MC_FASTPATH_MAXW && !MC_IMU_SEGREC;
     double ang;
     if (MODE == 1) {
       // SLERP: no sub-tile records — the deskew kernel reads segments k0, k0 + 1 of the step's
@@ -1413,12 +1429,15 @@ __device__ __forceinline__ T select_rec(bool second, const T& a, const T& b) {
 template <int MODE, int TIER>
 __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin& fw, bool set_tf, double tf,
                                           bool act, const int4& Tq, float4& X, float4& Y, float4& Z,
-                                          const WinOf<MODE>* pre0 = nullptr, const WinOf<MODE>* pre1 = nullptr) {
+                                          const WinOf<MODE>* pre0 = nullptr, const WinOf<MODE>* pre1 = nullptr,
+                                          int64_t fs = 0, int j1 = 1) {
   const PolyOf<TIER> poly = poly_load<TIER>();
   auto load_rec = [&](int j) {
     WinOf<MODE> w = ldu(rec + j);
     if constexpr (MODE == 1) {
       if (set_tf) w.tf = tf;
+    } else if constexpr (MC_IMU_SEGREC) {
+      w.ts -= fs;   // the segment table's absolute ns -> frame-relative
     }
     return w;
   };
@@ -1430,8 +1449,8 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
       r0 = *pre0;
       r1 = *pre1;
     } else {
-      r0 = ldu(rec);
-      r1 = ldu(rec + (MC_IMU_R1_UNCOND || fw.W == 2 ? 1 : 0));   // (slot 1 exists for every window)
+      r0 = load_rec(0);
+      r1 = load_rec(MC_IMU_R1_UNCOND || fw.W == 2 ? j1 : 0);   // (slot j1 exists for every window)
     }
   }
   bool use1 = false, mixed = false;
@@ -1529,16 +1548,21 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
     }
     const FrameWin fw = ldu(sub ? a.swin + st : a.fwin + f);
     // SLERP sub-tile windows point into the step's segment table, whose records carry no frame time
-    const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) + fw.klo : srec + 2 * st) : frec + 2 * f;
+    const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) + fw.klo
+                                      : (MC_IMU_SEGREC ? reinterpret_cast<const Win*>(a.imu_seg) + fw.klo : srec + 2 * st))
+                         : frec + 2 * f;
     const bool set_tf = MODE == 1 && sub;
 
     if (fw.W <= MC_FASTPATH_MAXW) {
       // the tier k_prep chose for the window: its coefficient load is issued here, beside the point
       // loads, not behind the vote that needs them
       const double tf = set_tf ? ldu(a.frame_time + f) : 0.0;
-      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1);
-      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1);
-      else fast_path<MODE, kTierAny<MODE>>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1);
+      // IMU segment-table records: the frame start, and slot 1 only inside the table
+      const int64_t fs = MODE == 2 && MC_IMU_SEGREC ? ldu(a.frame_start + f) : 0;
+      const int j1 = MODE == 2 && MC_IMU_SEGREC ? (fw.klo + 1 < a.ntab ? 1 : 0) : 1;
+      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1, fs, j1);
+      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1, fs, j1);
+      else fast_path<MODE, kTierAny<MODE>>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1, fs, j1);
     } else if (fw.W <= kWinMax) {
       const int W = fw.W;
       if (tid < W) {

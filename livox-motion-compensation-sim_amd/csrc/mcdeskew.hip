@@ -296,8 +296,10 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
     if ((r = dev_alloc(&b->d_ftile, F + 1))) return bail(r);
     if ((r = dev_alloc(&b->d_strange, n_sub))) return bail(r);
     if ((r = dev_alloc(&b->d_swin, 2 * n_sub))) return bail(r);
-    b->srec_half = 2 * n_sub * std::max(sizeof(PoseWin), sizeof(ImuSeg));
-    if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_srec), 2 * b->srec_half))) return bail(r);
+    if (!MC_IMU_SEGREC) {   // per-sub-tile IMU records (with MC_IMU_SEGREC the kernel reads the segment table)
+      b->srec_half = 2 * n_sub * std::max(sizeof(PoseWin), sizeof(ImuSeg));
+      if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_srec), 2 * b->srec_half))) return bail(r);
+    }
   }
   if ((r = dev_alloc(&b->d_partial, 5 * (size_t)b->n_tiles))) return bail(r);
   hipStream_t s = c->stream;

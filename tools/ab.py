@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--grids", default="0", help="comma list of max-grid caps tried with every lib (0: one "
                                                   "workgroup per (sub-)tile)")
+    ap.add_argument("--check", action="store_true",
+                    help="after each mode, download every arm's output batch and compare it byte for byte with "
+                         "the first arm's (variants that must not change results)")
     ap.add_argument("--replicas", type=int, default=1,
                     help="independent allocations (contexts) per library: where a batch's pages land moves a "
                          "kernel by up to ~10 %% (DESIGN.md section 8), so a variant is judged by the median "
@@ -104,6 +107,22 @@ def main():
                 ctx.timing(False)
                 t = ctx.read_timing()
                 per[lib].append(t["main_ms"] / t["main_launches"] * 1e3)
+        if args.check:
+            ref = None
+            for lib in libs:
+                ctx, (bt, bx), bo, grid = runs[lib]
+                ctx.deskew(bx if mode == "frame" else bt, bo, mode=mode)
+                ctx.sync()
+                cols = np.stack([np.ascontiguousarray(c) for c in bo.download_columns()[:4]])
+                if ref is None:
+                    ref = cols
+                    continue
+                diff = int(np.count_nonzero(cols.view(np.uint32) != ref.view(np.uint32)))
+                print(f"{mode:10s} {os.path.basename(lib):22s} output vs {os.path.basename(libs[0])}: "
+                      f"{'identical' if diff == 0 else f'{diff} values differ'}", flush=True)
+                if diff:
+                    raise SystemExit(f"{mode}: {lib} output differs")
+            del ref
         for lib in libs:
             v = per[lib]
             med = statistics.median(v)

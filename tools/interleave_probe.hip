@@ -10,7 +10,7 @@
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void st_sc1nt(float* p, v4f v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // in block pitch PI floats, out block pitch PO floats, out at out_base (same or another buffer)

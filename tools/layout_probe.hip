@@ -10,7 +10,7 @@
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void st_sc1(float* p, v4f v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // layout A: column c of point p at c*cap + p; one workgroup per 1024-point sub-tile

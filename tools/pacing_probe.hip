@@ -10,8 +10,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 
 template <int POL>
 __device__ __forceinline__ void st(float* p, v4f v) {
-  if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-  else if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
   else __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
 }
 

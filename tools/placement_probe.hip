@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void k_pass(const float* __restrict__ in, floa
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const v4f r = v[c] * 1.0001f + v[4];
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(bo + c * 256), "v"(r) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(bo + c * 256), "v"(r) : "memory");
   }
 }
 

@@ -13,7 +13,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 
 template <int POL>
 __device__ __forceinline__ void st(v4f* p, v4f v) {
-  if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
   else if constexpr (POL == 2) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
