@@ -86,6 +86,11 @@ namespace mc {
                              // (profiles/round3/s28)
 #endif
 static_assert(!(MC_IMU_HOIST && MC_IMU_SEGREC), "MC_IMU_HOIST loads the per-sub-tile records");
+#ifndef MC_IMU_WIN_FIRST
+#define MC_IMU_WIN_FIRST 1   // IMU: the sub-tile's window record loaded before (beside) its tile record:
+                             // bench 336.2 / 340.8 / 337.4 vs 338.2 / 341.6 / 338.4 us, alternating runs
+                             // (profiles/round3/s35), identical output
+#endif
 #ifndef MC_IMU_WAVES
 #define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
 #endif
@@ -1519,6 +1524,10 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
   for (int64_t it = b0; it < n_sub; it += nb) {
     const int64_t st = nb < n_sub ? it
                        : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
+    // IMU (MC_IMU_WIN_FIRST): the sub-tile window does not depend on the tile record, so both
+    // scalar loads are in flight together instead of one behind the other
+    FrameWin fw_first{};
+    if constexpr (MODE == 2 && MC_IMU_WIN_FIRST) fw_first = ldu(a.swin + st);
     const Tile tl = ldu(a.tiles + st / kSub);
     // IMU frames always span several samples: fetch the sub-tile window with the tile record
     const int g0 = (int)(st % kSub) * kBlock;
@@ -1546,7 +1555,7 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
       hr0 = ldu(srec + 2 * st);
       hr1 = ldu(srec + 2 * st + 1);
     }
-    const FrameWin fw = ldu(sub ? a.swin + st : a.fwin + f);
+    const FrameWin fw = MODE == 2 && MC_IMU_WIN_FIRST ? fw_first : ldu(sub ? a.swin + st : a.fwin + f);
     // SLERP sub-tile windows point into the step's segment table, whose records carry no frame time
     const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) + fw.klo
                                       : (MC_IMU_SEGREC ? reinterpret_cast<const Win*>(a.imu_seg) + fw.klo : srec + 2 * st))
