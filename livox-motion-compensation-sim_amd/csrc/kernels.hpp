@@ -91,6 +91,13 @@ static_assert(!(MC_IMU_HOIST && MC_IMU_SEGREC), "MC_IMU_HOIST loads the per-sub-
                              // bench 336.2 / 340.8 / 337.4 vs 338.2 / 341.6 / 338.4 us, alternating runs
                              // (profiles/round3/s35), identical output
 #endif
+#ifndef MC_SWIN_PERM
+#define MC_SWIN_PERM 0       // sub-tile windows stored so that the sub-tiles one XCD runs in the dealt
+                             // order (st = x mod 8) share 128-byte lines (slot xcd_unit(st)); the
+                             // XCD-contiguous order keeps slot st
+                             // (rejected: IMU dealt 337.8 vs 338.3 us over 3 replicas, bench within
+                             // noise, profiles/round3/s36)
+#endif
 #ifndef MC_IMU_WAVES
 #define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
 #endif
@@ -147,6 +154,11 @@ struct ImuSeg {
   double inv_dt;
   int64_t ts;    // absolute ns in the global table; frame-relative ns in a frame window
 };
+
+// slot of sub-tile st's window in swin: grouped by the XCD that runs it in the dealt order
+__device__ __forceinline__ int64_t swin_slot(int64_t st, int64_t n_sub, bool perm) {
+  return MC_SWIN_PERM && perm ? xcd_unit<1>(st, n_sub) : st;
+}
 
 // Per-frame segment window, written by k_prep: segments [klo, klo+W) cover every point of
 // the frame; bnd1 = frame-relative ns where segment klo+1 starts (W >= 2).
@@ -529,6 +541,8 @@ struct PrepArgs {
   const int32_t* ftile;    // first tile of frame f (F+1 entries)
   const int2* strange;     // per sub-tile [min, max] t_ns (recorded with trange)
   FrameWin* swin; void* srec;
+  int64_t n_sub;           // sub-tiles of the batch (the swin slot permutation's range)
+  int32_t swin_perm;       // 1: swin slot of sub-tile st is xcd_unit(st, n_sub) (MC_SWIN_PERM, dealt order)
 };
 
 // Wave-cooperative searches over a sorted table: 64 lanes probe evenly spaced entries per round,
@@ -900,7 +914,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
       if (n >= 2) ang = fmax(ang, imu_rec(sb_, sc, kb + 1 >= a.M, a.srec, 2 * st + 1, rec));
     }
     w.tier = window_tier<MODE>(MODE == 1 ? ang : imu_angle_bound(ang, hs ? r : make_int2(0, 0)));
-    if (valid) a.swin[st] = w;
+    if (valid) a.swin[swin_slot(st, a.n_sub, a.swin_perm != 0)] = w;
   }
 }
 
@@ -1527,7 +1541,7 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
     // IMU (MC_IMU_WIN_FIRST): the sub-tile window does not depend on the tile record, so both
     // scalar loads are in flight together instead of one behind the other
     FrameWin fw_first{};
-    if constexpr (MODE == 2 && MC_IMU_WIN_FIRST) fw_first = ldu(a.swin + st);
+    if constexpr (MODE == 2 && MC_IMU_WIN_FIRST) fw_first = ldu(a.swin + swin_slot(st, n_sub, a.xcd_order == 0));
     const Tile tl = ldu(a.tiles + st / kSub);
     // IMU frames always span several samples: fetch the sub-tile window with the tile record
     const int g0 = (int)(st % kSub) * kBlock;
@@ -1555,7 +1569,7 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
       hr0 = ldu(srec + 2 * st);
       hr1 = ldu(srec + 2 * st + 1);
     }
-    const FrameWin fw = MODE == 2 && MC_IMU_WIN_FIRST ? fw_first : ldu(sub ? a.swin + st : a.fwin + f);
+    const FrameWin fw = MODE == 2 && MC_IMU_WIN_FIRST ? fw_first : ldu(sub ? a.swin + swin_slot(st, n_sub, a.xcd_order == 0) : a.fwin + f);
     // SLERP sub-tile windows point into the step's segment table, whose records carry no frame time
     const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) + fw.klo
                                       : (MC_IMU_SEGREC ? reinterpret_cast<const Win*>(a.imu_seg) + fw.klo : srec + 2 * st))

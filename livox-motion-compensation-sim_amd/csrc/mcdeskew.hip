@@ -750,6 +750,9 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // a device-measured choice for this mode and batch size (mc_tune_order) overrides the default
   const mc_ctx::OrderTune& ot = c->order_tune[mode];
   if (ot.order >= 0 && ot.P == in->P) da.xcd_order = ot.order;
+  // the prep writes the sub-tile windows in the layout this order reads them in
+  pa.n_sub = (int64_t)in->n_tiles * kSub;
+  pa.swin_perm = da.xcd_order == 0 ? 1 : 0;
   sp->lds = mode == MC_MODE_FRAME ? 0u : points_lds_reserve();
 }
 
