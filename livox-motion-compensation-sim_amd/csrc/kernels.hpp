@@ -185,7 +185,7 @@ struct DeskewArgs {
   const FrameWin* fwin;    // per-point modes
   const void* frec;        // 2 frame-specialised records per frame (PoseWin or ImuSeg)
   const FrameWin* swin;    // per sub-tile: the same, for frames whose window exceeds MC_FASTPATH_MAXW
-  const void* srec;        // 2 frame-specialised records per sub-tile
+  const void* srec;        // 2 frame-specialised IMU records per sub-tile (MC_IMU_SEGREC=0 only; else null)
   const double* pose_time; // T
   const PoseSeg* pose_seg; // nseg
   const int64_t* imu_ts;   // M
