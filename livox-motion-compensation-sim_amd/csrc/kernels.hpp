@@ -98,6 +98,13 @@ static_assert(!(MC_IMU_HOIST && MC_IMU_SEGREC), "MC_IMU_HOIST loads the per-sub-
                              // (rejected: IMU dealt 337.8 vs 338.3 us over 3 replicas, bench within
                              // noise, profiles/round3/s36)
 #endif
+#ifndef MC_POINTS_PAIR
+#define MC_POINTS_PAIR 0     // per-point kernels (bit MODE: 2 SLERP, 4 IMU): a workgroup per tile, both
+                             // sub-tiles' points loaded up front (IMU then spills: 128 VGPRs + 15)
+                             // (rejected: SLERP 363.6-367.0 vs 322.5-327.8 us in the bench, the
+                             // second sub-tile's loads in flight during the first's math cost 13 %,
+                             // profiles/round3/s42)
+#endif
 #ifndef MC_IMU_WAVES
 #define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
 #endif
@@ -1535,28 +1542,29 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
   const Win* srec = reinterpret_cast<const Win*>(a.srec);
 
   const uint32_t b0 = NEXT ? blockIdx.x - pre : blockIdx.x, nb = NEXT ? gridDim.x - pre : gridDim.x;
-  for (int64_t it = b0; it < n_sub; it += nb) {
-    const int64_t st = nb < n_sub ? it
-                       : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
-    // IMU (MC_IMU_WIN_FIRST): the sub-tile window does not depend on the tile record, so both
-    // scalar loads are in flight together instead of one behind the other
-    FrameWin fw_first{};
-    if constexpr (MODE == 2 && MC_IMU_WIN_FIRST) fw_first = ldu(a.swin + swin_slot(st, n_sub, a.xcd_order == 0));
-    const Tile tl = ldu(a.tiles + st / kSub);
-    // IMU frames always span several samples: fetch the sub-tile window with the tile record
+  // the points of sub-tile st of tile tl, every lane (a short sub-tile's idle lanes re-read its first
+  // group, an empty sub-tile's lanes the tile's first group; their results are never stored): no
+  // divergent load block, so nothing makes the point loads wait for the window records, and the
+  // records stay scalar loads in uniform control flow
+  auto load_sub = [&](int64_t st, const Tile& tl, int4& Tq, float4& X, float4& Y, float4& Z, float4& I) {
     const int g0 = (int)(st % kSub) * kBlock;
-    if (g0 >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
+    const int g = g0 + tid;
+    const int gl = g < tl.ngroups ? g : (g0 < tl.ngroups ? g0 : 0);
+    const float* q = a.in + bidx((int)a.in_C, 0, tl.pstart + 4 * (int64_t)gl);
+    Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts));
+    X = ld4(q);
+    Y = ld4(q + kBlkPts);
+    Z = ld4(q + 2 * kBlkPts);
+    I = ld4(q + 3 * kBlkPts);
+  };
+  // one non-empty sub-tile whose points are loaded: records, per-point math, stores
+  auto sub_tile = [&](const int64_t st, const Tile& tl, const FrameWin& fw_first, const int4& Tq, float4 X, float4 Y,
+                      float4 Z, const float4& I) {
+    const int g0 = (int)(st % kSub) * kBlock;
     const int f = tl.frame;
     const int g = g0 + tid;
     const bool act = g < tl.ngroups;
     const int64_t p = tl.pstart + 4 * (int64_t)g;
-    // Every lane loads and computes (a short sub-tile's idle lanes re-read its first group; their
-    // results are never stored): no divergent load block, so nothing makes the point loads wait for
-    // the window records, and the records stay scalar loads in uniform control flow.
-    const float* q = a.in + bidx((int)a.in_C, 0, act ? p : tl.pstart + 4 * (int64_t)g0);
-    const int4 Tq = ld4(reinterpret_cast<const int32_t*>(q + 4 * kBlkPts));
-    float4 X = ld4(q), Y = ld4(q + kBlkPts), Z = ld4(q + 2 * kBlkPts);
-    const float4 I = ld4(q + 3 * kBlkPts);
     // frames wider than the SGPR path take their sub-tile's own window (k_prep writes one for every
     // IMU sub-tile).  One scalar load of the chosen record (a select of two loaded structs became a
     // vector load of bnd1 whose wait held back the point loads)
@@ -1657,6 +1665,41 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
       const int bytes = pc.bytes();      // (every lane: the per-lane variant reduces across the wave)
       const int wg = g0 + (tid & ~63);   // the wave's first group
       if ((tid & 63) == 0 && wg < tl.ngroups) a.pcd_len[(tl.pstart + 4 * (int64_t)wg) >> 8] = bytes;
+    }
+  };
+  // the sub-tile window of an IMU sub-tile does not depend on the tile record (MC_IMU_WIN_FIRST), so
+  // both scalar loads are in flight together instead of one behind the other
+  auto win_first = [&](int64_t st) {
+    FrameWin w{};
+    if constexpr (MODE == 2 && MC_IMU_WIN_FIRST) w = ldu(a.swin + swin_slot(st, n_sub, a.xcd_order == 0));
+    return w;
+  };
+  if constexpr ((MC_POINTS_PAIR >> MODE) & 1) {
+    // a workgroup per tile: both sub-tiles' points loaded up front, so the second one's loads are in
+    // flight during the first one's math and stores
+    static_assert(kSub == 2, "MC_POINTS_PAIR pairs the two sub-tiles of a tile");
+    const int64_t n_t = a.n_tiles;
+    for (int64_t it = b0; it < n_t; it += nb) {
+      const int64_t t = nb < n_t ? it : (a.xcd_order ? xcd_unit<1>(it, n_t) : it);
+      const FrameWin w0 = win_first(2 * t), w1 = win_first(2 * t + 1);
+      const Tile tl = ldu(a.tiles + t);
+      int4 Tq0, Tq1;
+      float4 X0, Y0, Z0, I0, X1, Y1, Z1, I1;
+      load_sub(2 * t, tl, Tq0, X0, Y0, Z0, I0);
+      load_sub(2 * t + 1, tl, Tq1, X1, Y1, Z1, I1);
+      sub_tile(2 * t, tl, w0, Tq0, X0, Y0, Z0, I0);
+      if (kBlock < tl.ngroups) sub_tile(2 * t + 1, tl, w1, Tq1, X1, Y1, Z1, I1);   // uniform
+    }
+  } else {
+    for (int64_t it = b0; it < n_sub; it += nb) {
+      const int64_t st = nb < n_sub ? it : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
+      const FrameWin w = win_first(st);
+      const Tile tl = ldu(a.tiles + st / kSub);
+      if ((int)(st % kSub) * kBlock >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
+      int4 Tq;
+      float4 X, Y, Z, I;
+      load_sub(st, tl, Tq, X, Y, Z, I);
+      sub_tile(st, tl, w, Tq, X, Y, Z, I);
     }
   }
 }

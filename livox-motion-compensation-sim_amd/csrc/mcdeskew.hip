@@ -742,6 +742,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
   int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
+  if (mode != MC_MODE_FRAME && ((MC_POINTS_PAIR >> mode) & 1)) units = in->n_tiles;   // a workgroup per tile (both sub-tiles)
   if (mode == MC_MODE_FRAME && MC_FRAME_QUAD) units = in->n_tiles * kSub * kQuadUnitsPerSub;
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
