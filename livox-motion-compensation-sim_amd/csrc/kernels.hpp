@@ -38,9 +38,9 @@ namespace mc {
 #define MC_STORE_POINTS 2    // per-point kernels output stores: sc1 write-through (see st_pol)
 #endif
 #ifndef MC_STORE_IMU
-#define MC_STORE_IMU 4       // the IMU kernel's output stores: sc1 nt — bench 334.5-338.0 vs 353.2-363.1 us
-                             // with nt (3 runs each, profiles/round3/s30); in tools/ab.py 331.6 vs 340.6
-                             // over 4 replicas (s29; round 2 measured nt 4 % ahead of sc1)
+#define MC_STORE_IMU 2       // the IMU kernel's output stores: sc1 write-through, as SLERP — bench (dealt
+                             // order) 327.8-330.1 vs 337.9-343.9 us with sc1 nt (profiles/round3/s46),
+                             // which beat nt (334.5-338.0 vs 353.2-363.1, s30; round 2 had nt ahead)
 #endif
 #ifndef MC_FASTPATH_MAXW
 #define MC_FASTPATH_MAXW 2   // frames spanning <= this many segments take the SGPR (no-LDS) path

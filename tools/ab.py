@@ -43,7 +43,7 @@ def setup(lib, args):
     b_xyz.synth(seed=0, frame_id_base=1000)
     b_xyz.set_frame_times(times)
     ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
-    ts, g = mc.trajectory.imu_from_trajectory(tr, 200.0)
+    ts, g = mc.trajectory.imu_from_trajectory(tr, args.imu_hz)
     ctx.set_imu(ts, g)
     return ctx, (b_in, b_xyz), b_out
 
@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--grids", default="0", help="comma list of max-grid caps tried with every lib (0: one "
                                                   "workgroup per (sub-)tile)")
+    ap.add_argument("--imu-hz", type=float, default=200.0, help="IMU sample rate of the workload (the reference's: 200)")
     ap.add_argument("--check", action="store_true",
                     help="after each mode, download every arm's output batch and compare it byte for byte with "
                          "the first arm's (variants that must not change results)")
