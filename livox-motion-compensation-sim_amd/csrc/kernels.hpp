@@ -32,7 +32,8 @@ namespace mc {
 #define MC_KITERS 2          // float4 groups per thread per tile in frame mode
 #endif
 #ifndef MC_STORE_FRAME
-#define MC_STORE_FRAME 4     // frame kernel output stores: sc1 nt (see st_pol; -3 % vs nt with MC_FRAME_SUB)
+#define MC_STORE_FRAME 2     // frame kernel output stores: sc1 (see st_pol): 298.2-298.9 vs 300.3-301.3 us
+                             // with sc1 nt in the bench's XCD order (profiles/round3/s48, s33)
 #endif
 #ifndef MC_STORE_POINTS
 #define MC_STORE_POINTS 2    // per-point kernels output stores: sc1 write-through (see st_pol)
