@@ -19,6 +19,8 @@
 #ifndef MC_CODEC_NT_STORE
 #define MC_CODEC_NT_STORE 1  // LVX / PCD file bytes stored non-temporally (written once, never re-read):
                              // LVX 308.4 vs 325.2 us, PCD 1005.5 vs 1057.8 us (profiles/round3/s21/ab_codec_nt.log)
+                             // (2: sc1 write-through, rejected: LVX 381.6 vs 302.9 us, PCD 1164.8 vs
+                             // 1014.7 us, profiles/round3/s50)
 #endif
 #ifndef MC_CODEC_NT_LOAD
 #define MC_CODEC_NT_LOAD 0   // PCD: the batch's float32 columns read non-temporally
@@ -117,7 +119,12 @@ __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const ch
   for (int c = c0 + threadIdx.x; c < c1; c += NT) {
     const int b0 = c << 4;
     if (b0 >= lo && b0 + 16 <= hi) {
-#if MC_CODEC_NT_STORE
+#if MC_CODEC_NT_STORE == 2   // sc1 write-through (inline asm: s_nop 1 for the store-data wait states)
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
+      const v4u t = {v.x, v.y, v.z, v.w};
+      asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(g + b0), "v"(t) : "memory");
+#elif MC_CODEC_NT_STORE
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
       const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
       __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));

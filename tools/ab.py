@@ -43,7 +43,7 @@ def setup(lib, args):
     b_xyz.synth(seed=0, frame_id_base=1000)
     b_xyz.set_frame_times(times)
     ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
-    ts, g = mc.trajectory.imu_from_trajectory(tr, args.imu_hz)
+    ts, g = mc.trajectory.imu_from_trajectory(tr, getattr(args, "imu_hz", 200.0))   # (setup is shared: ab_pcd_fused.py)
     ctx.set_imu(ts, g)
     return ctx, (b_in, b_xyz), b_out
 
