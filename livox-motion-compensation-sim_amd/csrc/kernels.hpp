@@ -54,6 +54,9 @@ namespace mc {
 #endif
 #ifndef MC_NT_LOAD
 #define MC_NT_LOAD 1         // non-temporal input loads (streamed once): +5-8% measured (tools/ab.py)
+                             // (rechecked with the sc1 stores, bench: SLERP 318.4-322.5 vs 351.7-358.9 us,
+                             // IMU 324.5-325.4 vs 341.9-342.9, frame 298.0-299.9 vs 312.0-312.1 without,
+                             // profiles/round3/s54)
 #endif
 #ifndef MC_SLERP_WAVES
 #define MC_SLERP_WAVES 4     // waves/SIMD the SLERP kernel is compiled for (VGPR budget 512 / waves)
