@@ -236,7 +236,8 @@ __device__ __forceinline__ T ldu(const T* p) {
 #define MC_XCD_FRAME 1
 #endif
 #ifndef MC_XCD_IMU
-#define MC_XCD_IMU 1
+#define MC_XCD_IMU 0         // IMU: dealt since its sc1 stores — mc_tune_order picked dealt in every bench
+                             // line of s46-s54 (330.8 vs 352.3 us XCD-contiguous, profiles/round3/s52)
 #endif
 #ifndef MC_XCD_SLERP
 #define MC_XCD_SLERP 0
