@@ -26,7 +26,12 @@
 #define MC_CODEC_NT_LOAD 0   // PCD: the batch's float32 columns read non-temporally
 #endif
 #ifndef MC_XCD_CODEC
-#define MC_XCD_CODEC 1       // LVX / PCD unit order (XCD-contiguous, layout.hpp)
+#define MC_XCD_CODEC 1       // PCD unit order (XCD-contiguous, layout.hpp)
+#endif
+#ifndef MC_XCD_LVX
+#define MC_XCD_LVX 0         // LVX unit order: dealt — 304.5 / 305.5 / 305.1 vs 310.6 / 314.9 / 319.5 us
+                             // XCD-contiguous, 3 interleaved A/Bs (profiles/round3/s58, s59); the PCD
+                             // kernels' A/Bs were mixed (987.0-1024.9 vs 1003.7-1021.5), so they keep XCD
 #endif
 
 namespace mc {
@@ -163,7 +168,7 @@ __device__ __forceinline__ int32_t lvx_fixed(double v, double scale, double lo, 
 __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
-  const int64_t u = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x);   // grid = units exactly
+  const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
   const int32_t f = codec_frame_of(a.src, u);
   const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
   const int64_t frow = a.src.doff[f];
@@ -250,7 +255,7 @@ __device__ __forceinline__ LvxUnit lvx_unit(const LvxArgs& a, int32_t f, int64_t
 
 __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages_cols(const LvxArgs a) {
   __shared__ uint4 s_buf[2][kLvxLds / 16 + 1];
-  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kLvxUnitsPerWG;
+  const int64_t u0 = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x) * kLvxUnitsPerWG;
   const int64_t u_end = u0 + kLvxUnitsPerWG < a.src.n_units ? u0 + kLvxUnitsPerWG : a.src.n_units;
   int32_t f = codec_frame_of(a.src, u0);
   LvxUnit nu = lvx_unit(a, f, u0);
