@@ -26,12 +26,13 @@
 #define MC_CODEC_NT_LOAD 0   // PCD: the batch's float32 columns read non-temporally
 #endif
 #ifndef MC_XCD_CODEC
-#define MC_XCD_CODEC 1       // PCD unit order (XCD-contiguous, layout.hpp)
+#define MC_XCD_CODEC 0       // PCD unit order: dealt — write pass 807.5 / 800.7 vs 832.8 / 831.0 us
+                             // XCD-contiguous, fused PCD share 0.514 / 0.519 vs 0.502 / 0.500, measure +
+                             // write 1012.1 vs 1024.1 us (profiles/round3/s61)
 #endif
 #ifndef MC_XCD_LVX
 #define MC_XCD_LVX 0         // LVX unit order: dealt — 304.5 / 305.5 / 305.1 vs 310.6 / 314.9 / 319.5 us
-                             // XCD-contiguous, 3 interleaved A/Bs (profiles/round3/s58, s59); the PCD
-                             // kernels' A/Bs were mixed (987.0-1024.9 vs 1003.7-1021.5), so they keep XCD
+                             // XCD-contiguous, 3 interleaved A/Bs (profiles/round3/s58, s59)
 #endif
 
 namespace mc {
