@@ -87,7 +87,8 @@ namespace mc {
                              // sub-tile windows) instead of its own two records written by k_prep:
                              // identical output, 7.5 MB less prep writes per 60 M-point step, 329.1 vs
                              // 349.3 us over 5 replicas (tools/ab.py), bench 353.7-358.2 vs 354.3-361.5
-                             // (profiles/round3/s28)
+                             // (profiles/round3/s28); with sc1 stores in the dealt order 327.4-328.2
+                             // vs 334.4-339.2 us with the per-sub-tile records (s63)
 #endif
 static_assert(!(MC_IMU_HOIST && MC_IMU_SEGREC), "MC_IMU_HOIST loads the per-sub-tile records");
 #ifndef MC_IMU_WIN_FIRST
@@ -100,7 +101,8 @@ static_assert(!(MC_IMU_HOIST && MC_IMU_SEGREC), "MC_IMU_HOIST loads the per-sub-
                              // order (st = x mod 8) share 128-byte lines (slot xcd_unit(st)); the
                              // XCD-contiguous order keeps slot st
                              // (rejected: IMU dealt 337.8 vs 338.3 us over 3 replicas, bench within
-                             // noise, profiles/round3/s36)
+                             // noise, profiles/round3/s36; with sc1 stores 329.5-330.4 vs 327.4-328.2,
+                             // s63)
 #endif
 #ifndef MC_POINTS_PAIR
 #define MC_POINTS_PAIR 0     // per-point kernels (bit MODE: 2 SLERP, 4 IMU): a workgroup per tile, both
