@@ -319,9 +319,10 @@ def load_traffic(mode, frames, points):
 
 
 def tune(ctx, mode, b_in, b_out):
-    """Untimed, before the spin-up: the device picks the mode's sub-tile order (dealt over the XCDs or
-    XCD-contiguous, Context.tune_order / mc_tune_order): which one streams faster differs between
-    MI355X boxes by up to 7 % for the same kernel."""
+    """Untimed, between the two halves of the spin-up (at sustained clocks): the device picks the
+    mode's sub-tile order (dealt over the XCDs or XCD-contiguous, Context.tune_order /
+    mc_tune_order): which one streams faster differs between kernels, store policies and MI355X
+    boxes by up to 7 % for the same kernel."""
     return ctx.tune_order(b_in, b_out, mode=mode, launches=8, rounds=6)
 
 
