@@ -228,12 +228,11 @@ __device__ __forceinline__ T ldu(const T* p) {
   return __builtin_bit_cast(T, r);
 }
 
-// XCD-contiguous sub-tile order per kernel (tools/ab.py, profiles/r13/ab_xcd*.log): frame -7 %,
-// IMU -4 %.  SLERP keeps the dealt order below ~200 M points (deskew_plan's default_order): with
-// the float64 math its fused next-step kernel ran the dealt order 6-10 % slower (scratch spills,
-// profiles/round3/s08-s12), but the plain kernel SLERP now uses (MC_FUSE_SLERP=0) streams it
-// fastest: 317.2 vs 333.8 us XCD-contiguous (profiles/round3/s15).  These are the defaults;
-// mc_tune_order measures both orders on the device at hand (the runtime field DeskewArgs::xcd_order)
+// Sub-tile order defaults (deskew_plan's default_order; mc_tune_order measures both orders on the
+// device at hand, the runtime field DeskewArgs::xcd_order): XCD-contiguous for the frame kernel
+// (-7 %, profiles/r13/ab_xcd*.log; tuned XCD in every round-3 line); dealt for SLERP below ~200 M
+// points (the slimmed fused next-step kernel streams it fastest: 317-320 vs 342-354 us,
+// profiles/round3/s52-s64) and for IMU since its sc1 stores (327.9 vs 349.9 us, s52, s56)
 #ifndef MC_XCD_FRAME
 #define MC_XCD_FRAME 1
 #endif

@@ -616,7 +616,8 @@ int mc_batch_checksum(mc_batch* b, double* sums) {
 // issues SLERP's prep as an any-order packet before the plain kernel instead: the round-3 float64 prep
 // spilled the fused kernel to scratch (345.1 vs 317.2 us, profiles/round3/s15); with the slimmed
 // prep (78 VGPRs, no scratch) the fused launch is ahead again, step wall 320.2-328.3 vs 329.5-329.6 us
-// (profiles/round3/s19/ab_fuse.log).
+// (profiles/round3/s19/ab_fuse.log); in the final tree's bench, step 317.5-320.8 vs 324.9-325.5 us
+// (profiles/round3/s64).
 #ifndef MC_FUSE_SLERP
 #define MC_FUSE_SLERP 1
 #endif
