@@ -51,7 +51,10 @@ constexpr int kLvxPkgPerWG = MC_LVX_PKG_PER_WG;                 // one unit = up
 constexpr int kLvxUnitPoints = kLvxPkgPerWG * kLvxPkgPoints;    // 768
 constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment shift
 #ifndef MC_PCD_TILES_PER_WG
-#define MC_PCD_TILES_PER_WG 8   // 4 / 8 / 16 / 32: 1048.0 / 1023.5 / 1029.2 / 1054.9 us (profiles/round2/s26)
+#define MC_PCD_TILES_PER_WG 4   // 4 / 8 / 16 / 32: 1048.0 / 1023.5 / 1029.2 / 1054.9 us (profiles/round2/s26,
+                                // XCD unit order); in the dealt order 4 wins: write pass 788.0 / 741.0 vs
+                                // 822.6 / 772.1 us (SLERP / frame source), fused PCD share 0.527 / 0.561 vs
+                                // 0.507 / 0.537 (profiles/round3/s66, s67)
 #endif
 constexpr int kPcdTilesPerWG = MC_PCD_TILES_PER_WG;             // PCD tiles of kCodecBlock lines per workgroup
 #ifndef MC_PCD_BLOCK
