@@ -846,7 +846,9 @@ __device__ __forceinline__ void pcd_emit_swar(const PcdFast& P, uint32_t* base, 
 #define MC_PCD_PREFETCH 1    // float32 source: each tile's values, flag and offset loaded one tile ahead
 #endif
 #ifndef MC_PCD_MEASURE_WAVE
-#define MC_PCD_MEASURE_WAVE 0   // float32-source measure: one wave per tile (float4 loads, no barrier)
+#define MC_PCD_MEASURE_WAVE 1   // float32-source measure: one wave per tile (float4 loads, no barrier):
+                                // in the dealt unit order measure + write 893.5 / 939.0 vs 989.4 / 1022.2 us
+                                // (profiles/round3/s70; within noise in the XCD order, round 2)
 #endif
 
 // digit fields of N = round(|v| 10^6) < 2^32: nd integer digits; D = 4 integer digits with leading
