@@ -275,8 +275,7 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   if (!measured) {
     {
       TimedRegion tr(c, &c->codec_ev, c->stream);
-      const int per = a.src.cols && MC_PCD_MEASURE_WAVE ? kPcdMeasureTiles : kPcdTilesPerWG;
-      const dim3 mgrid((uint32_t)((n_tiles + per - 1) / per));
+      const dim3 mgrid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
       if (a.src.cols) hipLaunchKernelGGL(k_pcd_measure<true>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
       else hipLaunchKernelGGL(k_pcd_measure<false>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
     }
@@ -305,25 +304,20 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   CHECK_ARG(d_out, "d_out is NULL");
   HIPCHK(hipMemcpyAsync(d + o_tp, tpos.data(), tpos.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
   const dim3 grid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
-  if (!MC_PCD_PACKED) {
+  {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    hipLaunchKernelGGL(k_pcd_write_bytes, grid, dim3(kPcdBlock), 0, c->stream, a, (const int32_t*)nullptr);
-  } else {
-    {
-      TimedRegion tr(c, &c->codec_ev, c->stream);
-      if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
-      else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kPcdBlock), 0, c->stream, a);
-    }
-    HIPCHK(hipGetLastError());
-    if (!slow.empty()) {
-      // the list rides in the scratch blob's tile-byte slots, which k_pcd_write has finished reading
-      // (same stream); the byte path reads no tile bytes
-      HIPCHK(hipMemcpyAsync(a.tile_bytes, slow.data(), slow.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                            c->stream));
-      TimedRegion tr(c, &c->codec_ev, c->stream);
-      hipLaunchKernelGGL(k_pcd_write_bytes, dim3((uint32_t)slow.size()), dim3(kPcdBlock), 0, c->stream, a,
-                         (const int32_t*)a.tile_bytes);
-    }
+    if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
+    else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kPcdBlock), 0, c->stream, a);
+  }
+  HIPCHK(hipGetLastError());
+  if (!slow.empty()) {
+    // the list rides in the scratch blob's tile-byte slots, which k_pcd_write has finished reading
+    // (same stream); the byte path reads no tile bytes
+    HIPCHK(hipMemcpyAsync(a.tile_bytes, slow.data(), slow.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                          c->stream));
+    TimedRegion tr(c, &c->codec_ev, c->stream);
+    hipLaunchKernelGGL(k_pcd_write_bytes, dim3((uint32_t)slow.size()), dim3(kPcdBlock), 0, c->stream, a,
+                       (const int32_t*)a.tile_bytes);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

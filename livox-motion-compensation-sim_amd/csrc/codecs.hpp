@@ -16,15 +16,10 @@
 
 #include "layout.hpp"
 
-#ifndef MC_CODEC_NT_STORE
-#define MC_CODEC_NT_STORE 1  // LVX / PCD file bytes stored non-temporally (written once, never re-read):
-                             // LVX 308.4 vs 325.2 us, PCD 1005.5 vs 1057.8 us (profiles/round3/s21/ab_codec_nt.log)
-                             // (2: sc1 write-through, rejected: LVX 381.6 vs 302.9 us, PCD 1164.8 vs
-                             // 1014.7 us, profiles/round3/s50)
-#endif
-#ifndef MC_CODEC_NT_LOAD
-#define MC_CODEC_NT_LOAD 0   // PCD: the batch's float32 columns read non-temporally
-#endif
+// File bytes are stored non-temporally (written once, never re-read): LVX 308.4 vs 325.2 us, PCD
+// 1005.5 vs 1057.8 us with plain stores (profiles/round3/s21/ab_codec_nt.log); sc1 write-through was
+// slower still (LVX 381.6 vs 302.9 us, PCD 1164.8 vs 1014.7 us, s50).  Non-temporal loads of the
+// batch's columns gave nothing (1000.6 vs 1004.1 us PCD, s24).
 #ifndef MC_XCD_CODEC
 #define MC_XCD_CODEC 0       // PCD unit order: dealt — write pass 807.5 / 800.7 vs 832.8 / 831.0 us
                              // XCD-contiguous, fused PCD share 0.514 / 0.519 vs 0.502 / 0.500, measure +
@@ -44,10 +39,7 @@ constexpr int kLvxPkgHdr = 22;
 constexpr int kLvxPkg = kLvxPkgHdr + kLvxPkgPoints * kLvxRec;   // 1366 bytes
 constexpr int kLvxFrameHdr = 24;
 constexpr int kLvxFileHdr = 88;
-#ifndef MC_LVX_PKG_PER_WG
-#define MC_LVX_PKG_PER_WG 8
-#endif
-constexpr int kLvxPkgPerWG = MC_LVX_PKG_PER_WG;                 // one unit = up to this many packages of a frame
+constexpr int kLvxPkgPerWG = 8;                                 // one unit = up to this many packages of a frame
 constexpr int kLvxUnitPoints = kLvxPkgPerWG * kLvxPkgPoints;    // 768
 constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment shift
 #ifndef MC_PCD_TILES_PER_WG
@@ -57,10 +49,7 @@ constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment s
                                 // 0.507 / 0.537 (profiles/round3/s66, s67)
 #endif
 constexpr int kPcdTilesPerWG = MC_PCD_TILES_PER_WG;             // PCD tiles of kCodecBlock lines per workgroup
-#ifndef MC_PCD_BLOCK
-#define MC_PCD_BLOCK 256
-#endif
-constexpr int kPcdBlock = MC_PCD_BLOCK;                          // PCD: threads per workgroup = lines per tile
+constexpr int kPcdBlock = 256;   // PCD: threads per workgroup = lines per tile (512: 1088 / 1085 vs 1080 us, profiles/round2/s40)
 constexpr int kPcdTileText = kPcdBlock * 64;                     // LDS text buffer per tile (packed lines <= 52 B)
 
 struct CodecFrames {
@@ -74,14 +63,11 @@ struct CodecFrames {
 };
 
 // frame owning unit u: last f with unit_off[f] <= u (frames without units are skipped over).
-// MC_CODEC_GUESS: first the interpolation guess u * F / n_units with its two bounds (one round of
-// loads when the frames are of similar size), the binary search (~log2 F dependent loads) otherwise.
-#ifndef MC_CODEC_GUESS
-#define MC_CODEC_GUESS 1
-#endif
+// First the interpolation guess u * F / n_units with its two bounds (one round of loads when the
+// frames are of similar size), the binary search (~log2 F dependent loads) otherwise.
 __device__ __forceinline__ int32_t codec_frame_of(const CodecFrames& s, int64_t u) {
   const int64_t* __restrict__ unit_off = s.unit_off;
-  if (MC_CODEC_GUESS && s.n_units > 0) {
+  if (s.n_units > 0) {
     int64_t g = u * s.F / s.n_units;   // u < 2^31 and F < 2^31: no overflow
     g = g < s.F - 1 ? g : s.F - 1;
     if (unit_off[g] <= u && u < unit_off[g + 1]) return (int32_t)g;
@@ -128,18 +114,9 @@ __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const ch
   for (int c = c0 + threadIdx.x; c < c1; c += NT) {
     const int b0 = c << 4;
     if (b0 >= lo && b0 + 16 <= hi) {
-#if MC_CODEC_NT_STORE == 2   // sc1 write-through (inline asm: s_nop 1 for the store-data wait states)
-      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-      const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
-      const v4u t = {v.x, v.y, v.z, v.w};
-      asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(g + b0), "v"(t) : "memory");
-#elif MC_CODEC_NT_STORE
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
       const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
       __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));
-#else
-      *reinterpret_cast<uint4*>(g + b0) = *reinterpret_cast<const uint4*>(lds + b0);
-#endif
     } else {
       const int e = b0 + 16 < hi ? b0 + 16 : hi;
       for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];
@@ -223,14 +200,12 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
 }
 
-// Batch source, kLvxUnitsPerWG consecutive units per workgroup: unit j + 1's meta data and point
-// values are loaded while unit j is assembled and stored (one HBM round trip per workgroup, not
-// per unit); the two LDS buffers alternate, so one barrier per unit.  A unit's first row is a
-// multiple of 768 = 3 blocks into its frame, so thread t's slot j is row t of the unit's block j.
-#ifndef MC_LVX_UNITS_PER_WG
-#define MC_LVX_UNITS_PER_WG 1
-#endif
-constexpr int kLvxUnitsPerWG = MC_LVX_UNITS_PER_WG;
+// Batch source.  The loop takes kLvxUnitsPerWG consecutive units per workgroup, unit j + 1's meta
+// data and point values loaded while unit j is assembled and stored (two LDS buffers, one barrier per
+// unit); one unit per workgroup ships (2 / 4 / 8: 305.0 / 306.6 vs 333.9 / 338.5, 356.3 / 356.4 us in
+// the dealt order, profiles/round3/s69).  A unit's first row is a multiple of 768 = 3 blocks into its
+// frame, so thread t's slot j is row t of the unit's block j.
+constexpr int kLvxUnitsPerWG = 1;
 constexpr int kLvxSlots = kLvxUnitPoints / kCodecBlock;   // 3
 static_assert(kLvxUnitPoints % kCodecBlock == 0 && kCodecBlock == kBlkPts, "unit = whole blocks");
 
@@ -524,14 +499,23 @@ __device__ __forceinline__ int64_t pcd_row(const CodecFrames& s, int64_t u, int3
   return row;
 }
 
+// wave-wide inclusive sum with DPP (no LDS round trips): row_shr 1 / 2 / 4 / 8 inside each 16-lane
+// row (bound_ctrl: lanes shifted in from outside the row add 0), then row_bcast:15 carries row 0's and
+// row 2's totals into rows 1 and 3, row_bcast:31 the first two rows' total into rows 2 and 3
+__device__ __forceinline__ int wave_scan_incl(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
+  return x;
+}
+
 // block-wide inclusive sum over the kPcdBlock threads of a PCD workgroup
 __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  x = wave_scan_incl(x);
   if (lane == 63) s_wave[wid] = x;
   __syncthreads();
   int before = 0;
@@ -546,25 +530,17 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
 }
 
 // ---- packed line path (every value of the line |v| < 4294, ties included) ----------------------
-// The common LiDAR line is formatted from four 32-bit integers N = round(|v| * 10^6): its text is
-// assembled in registers (digits packed four to a dword with multiply-shift division) and written to
-// LDS as dwords, instead of ~40 single-byte LDS stores per line.  Lines share their first and last
-// dwords with their neighbours: those go through ds_or_b32 into a zeroed buffer.  Tiles holding a
-// line with any other value (NaN, inf, |v| >= 4294) take the byte path (fmt6_prepare / pcd_emit,
-// k_pcd_write_bytes).  Two writers: the SWAR one (default, below) and the per-field LdsLine one.
-#ifndef MC_PCD_PACKED
-#define MC_PCD_PACKED 1
-#endif
-#ifndef MC_PCD_DIAG
-#define MC_PCD_DIAG 0        // diagnostic timing builds (wrong output): 1 no LDS text stores, 2 no digit math
-#endif
-#ifndef MC_PCD_FORCE_SLOW
-#define MC_PCD_FORCE_SLOW 0  // diagnostic: every tile through the byte path (slow-tile list)
-#endif
-
+// The common LiDAR line is formatted from four 32-bit integers N = round(|v| * 10^6): the digits come
+// out of a 200-byte "00".."99" pair table in LDS (five 2-digit groups per value: three of the six
+// fraction digits' pairs, two of the integer part's), and each value goes to the tile's LDS text as an
+// 8-byte ". dddddd sep" field plus its [-] + 1..4 digit head (pcd_emit_pairs).  Tiles holding a line
+// with any other value (NaN, inf, |v| >= 4294) take the byte path (fmt6_prepare / pcd_emit,
+// k_pcd_write_bytes).  (Round 3's writer built the digits with multiply-shift SWAR arithmetic and
+// byte stores: 368 VALU wave-instructions per 64 lines, profiles/r16/pmc_pcd_instructions.csv.)
 struct PcdFast {
   uint32_t n[4];   // round-half-even(|v| * 10^6)
   uint32_t neg;    // bit k: value k is negative (signbit)
+  int nd[4];       // integer digits of value k (1 .. 4)
   int len;         // line length in bytes
   bool ok;         // all four values took the fast path
 };
@@ -601,7 +577,8 @@ __device__ __forceinline__ void pcd_fast(const CodecFrames& s, int32_t f, int64_
     P.ok &= fmt6_fast(c[k], P.n[k]);
     const uint32_t ng = signbit(c[k]) ? 1u : 0u;
     P.neg |= ng << k;
-    P.len += (int)ng + fast_nd(P.n[k]);
+    P.nd[k] = fast_nd(P.n[k]);
+    P.len += (int)ng + P.nd[k];
   }
 }
 
@@ -627,7 +604,8 @@ __device__ __forceinline__ void pcd_fast_vals_f32(const float c[4], PcdFast& P) 
     const float a = fabsf(c[k]);
     const uint32_t ng = signbit(c[k]) ? 1u : 0u;
     P.neg |= ng << k;
-    P.len += (int)ng + 1 + (a >= 10.0f) + (a >= 100.0f) + (a >= 1000.0f);
+    P.nd[k] = 1 + (a >= 10.0f) + (a >= 100.0f) + (a >= 1000.0f);
+    P.len += (int)ng + P.nd[k];
   }
 }
 
@@ -644,271 +622,69 @@ __device__ __forceinline__ int pcd_fast_len_f32(const float c[4]) {
   return ok ? len : -1;
 }
 
-// three decimal digits of x < 1000 as characters in bytes 0..2 (most significant first)
-__device__ __forceinline__ uint32_t pack3(uint32_t x) {
-  const uint32_t h = __umul24(x, 41u) >> 12;
-  const uint32_t r = x - h * 100u;
-  const uint32_t t = __umul24(r, 103u) >> 10;
-  return (h | (t << 8) | ((r - t * 10u) << 16)) + 0x303030u;
+// The pair table: entry x < 100 = the two ASCII digits of x, tens in the low byte.
+constexpr int kPcdPairs = 100;
+__device__ __forceinline__ uint16_t pcd_pair_entry(uint32_t x) {
+  const uint32_t t = x / 10u;
+  return (uint16_t)((0x30u + t) | ((0x30u + x - 10u * t) << 8));
 }
 
-// byte stream into LDS dwords, 32-bit operations only: `w` holds the n < 4 pending bytes that start
-// at dword `pos`; every completed dword is stored at once.  (A first version kept up to 7 pending
-// bytes in a 64-bit register and shifted by up to 56 bits: whole waves then wrote some fields at the
-// wrong place on gfx950, tools/pcd_check.py — so no 64-bit variable shifts here.)
-struct LdsLine {
-  uint32_t* base;
-  uint32_t w;
-  int n, pos;
-  bool first;
-  // append the k <= 4 bytes of x (bytes above k are zero)
-  __device__ __forceinline__ void put(uint32_t x, int k) {
-#if MC_PCD_DIAG == 1   // diagnostic: no LDS stores (timing only)
-    w = (w ^ x) + (uint32_t)k;
-    return;
-#endif
-    const int sh = 8 * n;
-    w |= x << sh;
-    const uint32_t spill = (x >> 1) >> (31 - sh);   // the bytes beyond the dword (0 when sh == 0)
-    n += k;
-    if (n >= 4) {
-      if (first) {   // shared with the previous line
-        __hip_atomic_fetch_or(base + pos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        first = false;
-      } else {
-        base[pos] = w;
-      }
-      ++pos;
-      w = spill;
-      n -= 4;
-    }
-  }
-  // a partial last dword is shared with the next line
-  __device__ __forceinline__ void finish() {
-    if (n > 0) __hip_atomic_fetch_or(base + pos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-};
+// unaligned LDS stores (ds_write_b32 / b64 at any byte address: the HSA runtime runs the LDS in its
+// unaligned access mode, and the compiler emits them for these 1-aligned types)
+typedef uint32_t pcd_u32_ua __attribute__((aligned(1)));
+typedef uint64_t pcd_u64_ua __attribute__((aligned(1)));
+__device__ __forceinline__ void pcd_st32(uint8_t* p, uint32_t v) { *reinterpret_cast<pcd_u32_ua*>(p) = v; }
+__device__ __forceinline__ void pcd_st64(uint8_t* p, uint64_t v) { *reinterpret_cast<pcd_u64_ua*>(p) = v; }
 
-// "%.6f" of one fast value plus its separator, appended to the line
-__device__ __forceinline__ void fast_value(LdsLine& w, uint32_t n, bool neg, uint32_t sep) {
-#if MC_PCD_DIAG == 2   // diagnostic: no digit arithmetic (timing only)
-  w.put(n | 0x30303030u, 4);
-  w.put(n ^ 0x2e2e2e2eu, 3 + (int)neg);
-  w.put(n + sep, 4);
-  w.put(sep, 2);
-  return;
-#endif
-  const uint32_t ip = n / 1000000u, fp = n - ip * 1000000u;
-  const int nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
-  // integer digits (ip < 10^4): thousands | hundreds | tens | units, keep the last nd
-  const uint32_t th = __umul24(ip, 8389u) >> 23;
-  const uint32_t d4 = ((th + 0x30u) | (pack3(ip - th * 1000u) << 8)) >> (8 * (4 - nd));
-  // [-] digits '.': nd + 1 (+1) <= 6 bytes, as a 4-byte and a 0..2-byte piece
-  uint32_t h0, h1;
-  if (neg) {
-    h0 = '-' | (d4 << 8);
-    h1 = nd == 4 ? (d4 >> 24) | ('.' << 8) : (nd == 3 ? '.' : 0u);
-    if (nd < 3) h0 |= (uint32_t)'.' << (8 * (nd + 1));
-  } else {
-    h0 = nd == 4 ? d4 : d4 | ((uint32_t)'.' << (8 * nd));
-    h1 = nd == 4 ? '.' : 0u;
-  }
-  const int hl = nd + 1 + (neg ? 1 : 0);
-  w.put(h0, hl < 4 ? hl : 4);
-  w.put(h1, hl - 4 > 0 ? hl - 4 : 0);
-  const uint32_t fh = fp / 1000u;
-  const uint32_t f0 = pack3(fh), f1 = pack3(fp - fh * 1000u);
-  w.put(f0 | (f1 << 24), 4);                    // 3 digits + first of the next 3
-  w.put((f1 >> 8) | (sep << 16), 3);            // 2 digits + separator
-}
-
-__device__ __forceinline__ void pcd_emit_fast(const PcdFast& P, uint32_t* base, int off) {
-  LdsLine w;
-  w.base = base;
-  w.n = off & 3;
-  w.pos = off >> 2;
-  w.w = 0;
-  w.first = true;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) fast_value(w, P.n[k], (P.neg >> k) & 1u, k < 3 ? ' ' : '\n');
-  w.finish();
-#if MC_PCD_DIAG == 1
-  base[w.pos] = w.w;
-#endif
-}
-
-// ---- SWAR line writer (MC_PCD_SWAR) ----------------------------------------------------------
-// The same bytes as pcd_emit_fast with about half the VALU work: the six fraction digits of all
-// values come out of one 32-bit word holding two 3-digit halves (multiply-shift division on both
-// 16-bit halves at once), the integer digits likewise from two 2-digit halves, and bytes are
-// placed with v_perm_b32; each value's text ([-]digits, then the fixed 8 bytes ".dddddd" + separator)
-// sits right-aligned in four dwords and is moved to the line's byte position with v_alignbyte_b32,
-// so the line writer stores whole dwords with no per-field bookkeeping.
-#ifndef MC_PCD_SWAR
-#define MC_PCD_SWAR 1
-#endif
-
-// y * 41 as two shift-adds (y*9, then + y*32): the compiler folds the plain product into a
-// quarter-rate v_mul_lo_u32
-__device__ __forceinline__ uint32_t mul41(uint32_t y) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t y9, r;
-  asm("v_lshl_add_u32 %0, %1, 3, %1" : "=v"(y9) : "v"(y));
-  asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(y), "v"(y9));
-  return r;
-#else
-  return y * 41u;
-#endif
-}
-
-// one value of the line: pending n (< 4) bytes in w start at dword pos; FIRST: the pending bytes
-// belong to the previous line, so the first dword is ORed
-template <bool FIRST>
-__device__ __forceinline__ void swar_value(uint32_t* base, int& pos, int& n, uint32_t& w, uint32_t N, bool neg,
-                                           uint32_t sep) {
+// Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
+// zeros (byte 0 = thousands), T = ". d1 d2 d3 d4 d5 d6 sep" (bytes in text order).  Divisions by
+// constants as multiply-shifts, exact on their ranges: fp / 10^4 = (fp * 429497) >> 32 for fp < 10^6
+// (error < 6.3e-5 < 10^-4), x / 100 = (x * 5243) >> 19 for x < 43699.
+__device__ __forceinline__ void pair_fields(const uint16_t* tbl, uint32_t N, uint32_t sep, uint32_t& D, uint64_t& T) {
   const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
-  const int nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
-  // fraction: halves fh = fp / 1000 (low) and fl (high) -> hundreds / tens / units of both.
-  // fh = (fp * 4294968) >> 32 is exact for fp < 10^6 (error fp * 0.704 / 2^32 < 1.7e-4 < 1/1000)
-  // and both factors fit 24 bits: one full-rate v_mul_hi_u32_u24 instead of v_mul_hi_u32.
-  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32);
-  const uint32_t y = fh | ((fp - fh * 1000u) << 16);
-  const uint32_t h = ((mul41(y)) >> 12) & 0x000F000Fu;           // y*41 < 2^32: halves < 1000
-  const uint32_t r = y - h * 100u;
-  const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;    // r halves < 100
-  const uint32_t ht = h | (t << 8);                               // [h_lo t_lo h_hi t_hi]
-  const uint32_t u = r - t * 10u;                                 // [u_lo 0 u_hi 0]
-  const uint32_t A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;             // . d1 d2 d3
-  const uint32_t B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);  // d4 d5 d6 sep
-  // integer part ip < 10^4: halves ip / 100 (low) and ip % 100 (high) -> tens / units
-  const uint32_t hi2 = __umul24(ip, 5243u) >> 19;
-  const uint32_t y2 = hi2 | ((ip - hi2 * 100u) << 16);
-  const uint32_t t2 = (__umul24(y2, 103u) >> 10) & 0x000F000Fu;
-  const uint32_t u2 = y2 - t2 * 10u;
-  uint32_t D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;   // 4 digits, leading zeros
-  uint32_t T0 = 0u;
-  if (neg) {   // the sign goes in front of the nd digits: byte 3 - nd of D, or byte 3 of T0
-    if (nd == 4) T0 = 0x2D000000u;
-    else {
-      const int sh = 8 * (3 - nd);
-      D = (D & ~(0xFFu << sh)) | (0x2Du << sh);
-    }
-  }
-  // text = bytes [s, 16) of T0 D A B, s = 8 - (neg + nd); move byte s to byte n
-  const int L = (neg ? 1 : 0) + nd + 8;
-  const int rs = 16 - L - n;                  // 0 .. 7
-  const bool q = rs >= 4;
-  const uint32_t m = (uint32_t)(rs & 3);
-  const uint32_t S0 = q ? D : T0, S1 = q ? A : D, S2 = q ? B : A, S3 = q ? 0u : B;
-  uint32_t U0 = __builtin_amdgcn_alignbyte(S1, S0, m);
-  const uint32_t U1 = __builtin_amdgcn_alignbyte(S2, S1, m);
-  const uint32_t U2 = __builtin_amdgcn_alignbyte(S3, S2, m);
-  const uint32_t U3 = __builtin_amdgcn_alignbyte(0u, S3, m);
-  U0 = (U0 & (0xFFFFFFFFu << (8 * n))) | w;  // n <= 3
-  const int M = n + L;                        // 9 .. 16 bytes from dword pos
-  if (FIRST) {
-    __hip_atomic_fetch_or(base + pos, U0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    base[pos + 1] = U1;
-  } else {
-    base[pos] = U0;
-    base[pos + 1] = U1;
-  }
-  if (M >= 12) base[pos + 2] = U2;
-  if (M >= 16) base[pos + 3] = U3;
-  w = M >= 12 ? (M >= 16 ? 0u : U3) : U2;
-  pos += M >> 2;
-  n = M & 3;
+  const uint32_t p0 = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32);
+  const uint32_t r = fp - p0 * 10000u;
+  const uint32_t p1 = __umul24(r, 5243u) >> 19;
+  const uint32_t p2 = r - p1 * 100u;
+  const uint32_t q0 = __umul24(ip, 5243u) >> 19;
+  const uint32_t q1 = ip - q0 * 100u;
+  const uint32_t P0 = tbl[p0], P1 = tbl[p1], P2 = tbl[p2];
+  D = (uint32_t)tbl[q0] | ((uint32_t)tbl[q1] << 16);
+  const uint32_t A = 0x2Eu | (P0 << 8) | (P1 << 24);       // . d1 d2 d3
+  const uint32_t B = (P1 >> 8) | (P2 << 8) | (sep << 24);   // d4 d5 d6 sep
+  T = (uint64_t)A | ((uint64_t)B << 32);
 }
 
-__device__ __forceinline__ void pcd_emit_swar(const PcdFast& P, uint32_t* base, int off) {
-  int pos = off >> 2, n = off & 3;
-  uint32_t w = 0u;
-  swar_value<true>(base, pos, n, w, P.n[0], P.neg & 1u, ' ');
-  swar_value<false>(base, pos, n, w, P.n[1], (P.neg >> 1) & 1u, ' ');
-  swar_value<false>(base, pos, n, w, P.n[2], (P.neg >> 2) & 1u, ' ');
-  swar_value<false>(base, pos, n, w, P.n[3], (P.neg >> 3) & 1u, '\n');
-  if (n > 0) __hip_atomic_fetch_or(base + pos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// ---- byte-store line writer (MC_PCD_BYTES) ----------------------------------------------------
-// The same digits as swar_value, but the text goes to LDS with byte stores at its final offsets
-// instead of being aligned in registers and stored as dwords (which needed a zeroed buffer and
-// ds_or for the dwords two lines share): ".ddd" and "ddd" + separator are 8 bytes at a known
-// offset, the head ([-] and nd integer digits) sits right before them.  Values go in reverse
-// order, and every value but the line's first stores its 4-digit field and a '-' unconditionally
-// (at most 5 bytes before its '.'): bytes left of its own head fall inside the previous value of
-// the same line, which is written afterwards and overwrites them.  The line's first value stores
-// exactly its own bytes, so no lane ever writes another line's text: no zeroing, no atomics.
-#ifndef MC_PCD_BYTES
-#define MC_PCD_BYTES 1
-#endif
-#ifndef MC_PCD_PREFETCH
-#define MC_PCD_PREFETCH 1    // float32 source: each tile's values, flag and offset loaded one tile ahead
-#endif
-#ifndef MC_PCD_MEASURE_WAVE
-#define MC_PCD_MEASURE_WAVE 1   // float32-source measure: one wave per tile (float4 loads, no barrier):
-                                // in the dealt unit order measure + write 893.5 / 939.0 vs 989.4 / 1022.2 us
-                                // (profiles/round3/s70; within noise in the XCD order, round 2)
-#endif
-
-// digit fields of N = round(|v| 10^6) < 2^32: nd integer digits; D = 4 integer digits with leading
-// zeros (byte 0 = thousands); A = ". d1 d2 d3"; B = "d4 d5 d6 sep" (bytes in text order)
-__device__ __forceinline__ void fmt6_fields(uint32_t N, uint32_t sep, int& nd, uint32_t& D, uint32_t& A, uint32_t& B) {
-  const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
-  nd = 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
-  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32);   // fp / 1000, exact
-  const uint32_t y = fh | ((fp - fh * 1000u) << 16);
-  const uint32_t h = ((mul41(y)) >> 12) & 0x000F000Fu;
-  const uint32_t r = y - h * 100u;
-  const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;
-  const uint32_t ht = h | (t << 8);
-  const uint32_t u = r - t * 10u;
-  A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;
-  B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);
-  const uint32_t hi2 = __umul24(ip, 5243u) >> 19;
-  const uint32_t y2 = hi2 | ((ip - hi2 * 100u) << 16);
-  const uint32_t t2 = (__umul24(y2, 103u) >> 10) & 0x000F000Fu;
-  const uint32_t u2 = y2 - t2 * 10u;
-  D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;
-}
-
-__device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
-  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
-}
-
-// one value whose text starts at byte o of the tile buffer; EXACT: the line's first value
-template <bool EXACT>
-__device__ __forceinline__ void bytes_value(uint8_t* base, int o, uint32_t N, bool neg, uint32_t sep) {
-  int nd;
-  uint32_t D, A, B;
-  fmt6_fields(N, sep, nd, D, A, B);
-  uint8_t* pa = base + o + nd + (neg ? 1 : 0);   // the '.'
-  put4(pa, A);
-  put4(pa + 4, B);
-  if (EXACT) {
-    pa[-1] = (uint8_t)(D >> 24);
-    if (nd >= 2) pa[-2] = (uint8_t)(D >> 16);
-    if (nd >= 3) pa[-3] = (uint8_t)(D >> 8);
-    if (nd >= 4) pa[-4] = (uint8_t)D;
-    if (neg) pa[-nd - 1] = '-';
-  } else {
-    put4(pa - 4, D);          // leading zeros land in the previous value (rewritten after)
-    pa[-nd - 1] = '-';        // the sign slot, or a byte of the previous value
-  }
-}
-
-__device__ __forceinline__ void pcd_emit_bytes(const PcdFast& P, uint8_t* base, int off) {
-  int len[4];
+// One packed line at byte `off` of the tile text.  Exactly the line's own bytes end up written, so
+// lanes never touch each other's text (no zeroing, no atomics, no ordering between lanes):
+//   1. the first value's head ([-] + nd digits, left-aligned) as 8 bytes from `off`: its stray bytes
+//      land inside value 0's fraction field;
+//   2. values 1-3: the 4 digit bytes (leading zeros) right against the value's '.' and a '-' in the
+//      sign slot: stray bytes (<= 3) land inside the previous value's fraction field;
+//   3. the four fixed 8-byte fraction fields, which overwrite every stray byte.
+// A lane's LDS stores complete in program order.
+__device__ __forceinline__ void pcd_emit_pairs(const PcdFast& P, const uint16_t* tbl, uint8_t* base, int off) {
+  uint64_t T[4];
+  int pa[4];
+  int o = off;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint32_t ip = P.n[k] / 1000000u;
-    len[k] = 8 + (int)((P.neg >> k) & 1u) + 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
+    uint32_t D;
+    pair_fields(tbl, P.n[k], k < 3 ? 0x20u : 0x0Au, D, T[k]);
+    const int nd = P.nd[k];
+    const bool neg = (P.neg >> k) & 1u;
+    pa[k] = o + nd + (neg ? 1 : 0);   // the '.'
+    if (k == 0) {
+      const uint64_t H = (uint64_t)(D >> (8 * (4 - nd)));   // the nd digits, left-aligned
+      pcd_st64(base + o, neg ? (H << 8) | 0x2Du : H);
+    } else {
+      pcd_st32(base + pa[k] - 4, D);
+      base[pa[k] - nd - 1] = 0x2D;    // '-': the sign slot, or a stray byte
+    }
+    o = pa[k] + 8;
   }
-  const int o1 = off + len[0], o2 = o1 + len[1], o3 = o2 + len[2];
-  bytes_value<false>(base, o3, P.n[3], (P.neg >> 3) & 1u, '\n');
-  bytes_value<false>(base, o2, P.n[2], (P.neg >> 2) & 1u, ' ');
-  bytes_value<false>(base, o1, P.n[1], (P.neg >> 1) & 1u, ' ');
-  bytes_value<true>(base, off, P.n[0], P.neg & 1u, ' ');
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pcd_st64(base + pa[k], T[k]);
 }
 
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
@@ -938,28 +714,22 @@ constexpr int32_t kPcdSlowTile = 1 << 30;
 // columns 0..3 of dense row `row` of a batch source as float32 (codec_point widens them)
 __device__ __forceinline__ void codec_point_f32(const CodecFrames& s, int32_t f, int64_t row, float c[4]) {
   const float* q = s.cols + bidx(s.C, 0, s.poff[f] + (row - s.doff[f]));
-#if MC_CODEC_NT_LOAD
-  c[0] = __builtin_nontemporal_load(q); c[1] = __builtin_nontemporal_load(q + kBlkPts);
-  c[2] = __builtin_nontemporal_load(q + 2 * kBlkPts); c[3] = __builtin_nontemporal_load(q + 3 * kBlkPts);
-#else
   c[0] = q[0]; c[1] = q[kBlkPts]; c[2] = q[2 * kBlkPts]; c[3] = q[3 * kBlkPts];
-#endif
 }
 
-// F32: the source is a batch's float32 columns (the packed path then works in float32, above)
-// Float32 source, MC_PCD_MEASURE_WAVE: a tile's 256 lines are one block of the batch, so one wave
-// measures a whole tile — lane l takes lines 4l .. 4l + 3 from one float4 per column (16-byte
-// lanes instead of 4-byte ones) and a wave reduction replaces the block scan: no LDS, no barrier.
-// A workgroup takes kPcdMeasureTiles tiles, each wave kPcdMeasureTiles / 4 of them, all of whose
-// loads are issued before the first is measured.
-#ifndef MC_PCD_MEASURE_TILES
-#define MC_PCD_MEASURE_TILES kPcdTilesPerWG
-#endif
-constexpr int kPcdMeasureTiles = MC_PCD_MEASURE_TILES;
-constexpr int kPcdMeasureWaveTiles = kPcdMeasureTiles / (kPcdBlock / 64);
+__device__ __forceinline__ int32_t pcd_tile_word(int v) {   // scanned bytes (+ 2^20 per byte-path line)
+  return (v & ((1 << 20) - 1)) | ((v >> 20) ? kPcdSlowTile : 0);
+}
+
+// Float32 source: a tile's 256 lines are one block of the batch, so one wave measures a whole tile —
+// lane l takes lines 4l .. 4l + 3 from one float4 per column (16-byte lanes) and a wave reduction
+// replaces the block scan: no LDS, no barrier (measure + write 893.5 / 939.0 vs 989.4 / 1022.2 us with
+// a block per tile, profiles/round3/s70).  A workgroup takes kPcdTilesPerWG tiles, each wave
+// kPcdTilesPerWG / 4 of them, all of whose loads are issued before the first is measured.
+constexpr int kPcdMeasureWaveTiles = kPcdTilesPerWG / (kPcdBlock / 64);
 __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) {
   static_assert(kPcdBlock == kBlkPts, "a PCD tile is one batch block");
-  static_assert(kPcdMeasureTiles % (kPcdBlock / 64) == 0, "whole tiles per wave");
+  static_assert(kPcdTilesPerWG % (kPcdBlock / 64) == 0, "whole tiles per wave");
   constexpr int NT = kPcdMeasureWaveTiles;
   const int lane = threadIdx.x & 63;
   int32_t f = codec_frame_of(a.src, u0);
@@ -1004,105 +774,53 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0)
-      a.tile_bytes[u] = (v & ((1 << 20) - 1)) | ((v >> 20) || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
+    if (lane == 0) a.tile_bytes[u] = pcd_tile_word(v);
   }
 }
 
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
-  __shared__ int s_wave[kPcdBlock / 64];
-  if constexpr (F32 && MC_PCD_MEASURE_WAVE) {
-    pcd_measure_waves(a, xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdMeasureTiles);
-    return;
-  }
-  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
-  int32_t f = codec_frame_of(a.src, u0);
-  if constexpr (F32 && MC_PCD_PREFETCH) {
-    // as k_pcd_write: tile j + 1's values are loaded while tile j is measured
-    const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
-    float cn[4] = {0.f, 0.f, 0.f, 0.f};
-    bool vn = false;
-    int64_t rn = 0;
-    int32_t fn = f;
-    auto fetch = [&](int64_t u) {
-      rn = pcd_row(a.src, u, f, vn);
-      fn = f;
-      if (vn) codec_point_f32(a.src, f, rn, cn);
-    };
-    if (u0 < u_end) fetch(u0);
-    for (int64_t u = u0; u < u_end; ++u) {
-      const float c[4] = {cn[0], cn[1], cn[2], cn[3]};
-      const bool valid = vn;
-      const int64_t row = rn;
-      const int32_t fr = fn;
-      if (u + 1 < u_end) fetch(u + 1);
+  if constexpr (F32) {
+    pcd_measure_waves(a, xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG);
+  } else {
+    __shared__ int s_wave[kPcdBlock / 64];
+    const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
+    int32_t f = codec_frame_of(a.src, u0);
+    for (int j = 0; j < kPcdTilesPerWG; ++j) {
+      const int64_t u = u0 + j;
+      if (u >= a.src.n_units) break;
+      bool valid;
+      const int64_t row = pcd_row(a.src, u, f, valid);
+      // scanned value: line bytes + (byte-path line ? 1 << 20 : 0); a tile's bytes stay < 2^20 and
+      // its byte-path line count < 2^11, so one scan yields both (no extra barrier)
       int v = 0;
       if (valid) {
-        v = pcd_fast_len_f32(c);
+        double c[4];
+        codec_point(a.src, f, row, c);
+        v = pcd_fast_len(c);
         if (v < 0) {
           PcdLine L;
-          pcd_line(a.src, fr, row, L, a.err);
+          pcd_line(a.src, f, row, L, a.err);
           v = L.len + (1 << 20);
         }
       }
       int total;
       block_scan(v, s_wave, total);
-      if (threadIdx.x == 0)
-        a.tile_bytes[u] = (total & ((1 << 20) - 1)) | ((total >> 20) || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
+      if (threadIdx.x == 0) a.tile_bytes[u] = pcd_tile_word(total);
       __syncthreads();   // s_wave is reused by the next tile
     }
-    return;
-  }
-  for (int j = 0; j < kPcdTilesPerWG; ++j) {
-    const int64_t u = u0 + j;
-    if (u >= a.src.n_units) break;
-    bool valid;
-    const int64_t row = pcd_row(a.src, u, f, valid);
-    // scanned value: line bytes + (byte-path line ? 1 << 20 : 0); a tile's bytes stay < 2^20 and
-    // its byte-path line count < 2^11, so one scan yields both (no extra barrier)
-    int v = 0;
-    if (valid) {
-      if constexpr (F32) {
-        float c[4];
-        codec_point_f32(a.src, f, row, c);
-        v = pcd_fast_len_f32(c);
-      } else {
-        double c[4];
-        codec_point(a.src, f, row, c);
-        v = pcd_fast_len(c);
-      }
-      if (v < 0) {
-        PcdLine L;
-        pcd_line(a.src, f, row, L, a.err);
-        v = L.len + (1 << 20);
-      }
-    }
-    int total;
-    block_scan(v, s_wave, total);
-    if (threadIdx.x == 0)
-      a.tile_bytes[u] = (total & ((1 << 20) - 1)) | ((total >> 20) || MC_PCD_FORCE_SLOW ? kPcdSlowTile : 0);
-    __syncthreads();   // s_wave is reused by the next tile
   }
 }
 
-// Packed tiles: every line is formatted in registers and written to LDS as dwords (the tile's text
-// sits at its HBM offset modulo 16), then stored with codec_store_piece.  Tiles flagged slow are
-// skipped (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text
-// always fits the LDS buffer.
-// One packed tile: scan the line lengths, write the lines into LDS, store the text.
+// Packed tiles: every line is formatted into the tile's LDS text (which sits at its HBM offset
+// modulo 16), then stored with codec_store_piece.  Tiles flagged slow are skipped
+// (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text always fits.
 __device__ __forceinline__ void pcd_tile_out(const PcdArgs& a, const PcdFast& P, bool valid, int64_t G, int* s_wave,
-                                             uint4* s_text4) {
+                                             const uint16_t* s_pairs, uint4* s_text4) {
   int total;
   const int excl = block_scan(P.len, s_wave, total) - P.len;
   const int shift = (int)(G & 15);
-#if MC_PCD_BYTES
-  if (valid) pcd_emit_bytes(P, reinterpret_cast<uint8_t*>(s_text4), shift + excl);
-#elif MC_PCD_SWAR
-  if (valid) pcd_emit_swar(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
-#else
-  if (valid) pcd_emit_fast(P, reinterpret_cast<uint32_t*>(s_text4), shift + excl);
-#endif
+  if (valid) pcd_emit_pairs(P, s_pairs, reinterpret_cast<uint8_t*>(s_text4), shift + excl);
   __syncthreads();
   codec_store_piece<kPcdBlock>(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
   __syncthreads();   // s_wave / s_text are reused by the next tile
@@ -1111,10 +829,12 @@ __device__ __forceinline__ void pcd_tile_out(const PcdArgs& a, const PcdFast& P,
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
+  __shared__ uint16_t s_pairs[kPcdPairs];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
+  if (threadIdx.x < kPcdPairs) s_pairs[threadIdx.x] = pcd_pair_entry(threadIdx.x);   // read after block_scan's barrier
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
-  if constexpr (F32 && MC_PCD_PREFETCH && MC_PCD_BYTES) {
+  if constexpr (F32) {
     // tile j + 1's loads are in flight while tile j is formatted and stored: one HBM round trip
     // per workgroup instead of one per tile
     const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
@@ -1139,40 +859,28 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       PcdFast P;
       P.len = 0;
       if (valid) pcd_fast_vals_f32(c, P);
-      pcd_tile_out(a, P, valid, G, s_wave, s_text4);
+      pcd_tile_out(a, P, valid, G, s_wave, s_pairs, s_text4);
     }
-    return;
-  }
-  for (int j = 0; j < kPcdTilesPerWG; ++j) {
-    const int64_t u = u0 + j;
-    if (u >= a.src.n_units) break;
-    if (a.tile_bytes[u] & kPcdSlowTile) continue;   // workgroup-uniform
-    bool valid;
-    const int64_t row = pcd_row(a.src, u, f, valid);
-    // zero the text buffer (lines OR the dwords they share), ordered before the line writes by
-    // block_scan's barrier; the byte-store writer needs no zeroing
-    if (!MC_PCD_BYTES)
-      for (int i = threadIdx.x; i < kPcdTileText / 16 + 1; i += kPcdBlock) s_text4[i] = make_uint4(0, 0, 0, 0);
-    PcdFast P;
-    P.len = 0;
-    if (valid) {
-      if constexpr (F32) {
-        float c[4];
-        codec_point_f32(a.src, f, row, c);
-        pcd_fast_vals_f32(c, P);
-      } else {
-        pcd_fast(a.src, f, row, P);
-      }
+  } else {
+    for (int j = 0; j < kPcdTilesPerWG; ++j) {
+      const int64_t u = u0 + j;
+      if (u >= a.src.n_units) break;
+      if (a.tile_bytes[u] & kPcdSlowTile) continue;   // workgroup-uniform
+      bool valid;
+      const int64_t row = pcd_row(a.src, u, f, valid);
+      PcdFast P;
+      P.len = 0;
+      if (valid) pcd_fast(a.src, f, row, P);
+      const int64_t G = a.tile_pos[u];   // issued before the scan's barrier
+      pcd_tile_out(a, P, valid, G, s_wave, s_pairs, s_text4);
     }
-    const int64_t G = a.tile_pos[u];   // issued before the scan's barrier
-    pcd_tile_out(a, P, valid, G, s_wave, s_text4);
   }
 }
 
 // Byte path (any %.6f value): every tile formats its lines byte by byte into LDS and stores the
 // text with codec_store_piece; a tile larger than the LDS buffer — only possible with extreme
 // magnitudes — is written line by line straight to HBM instead.  Tiles: list[blockIdx.x], or, with
-// list == nullptr, kPcdTilesPerWG consecutive tiles per workgroup (MC_PCD_PACKED=0: every tile).
+// list == nullptr, kPcdTilesPerWG consecutive tiles per workgroup.
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write_bytes(const PcdArgs a, const int32_t* list) {
   __shared__ int s_wave[kPcdBlock / 64];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];

@@ -27,96 +27,23 @@
 
 namespace mc {
 
-// Build-time knobs (tools/ab.py builds variants of these and times them in one process):
-#ifndef MC_KITERS
-#define MC_KITERS 2          // float4 groups per thread per tile in frame mode
-#endif
-#ifndef MC_STORE_FRAME
-#define MC_STORE_FRAME 2     // frame kernel output stores: sc1 (see st_pol): 298.2-298.9 vs 300.3-301.3 us
-                             // with sc1 nt in the bench's XCD order (profiles/round3/s48, s33)
-#endif
-#ifndef MC_STORE_POINTS
-#define MC_STORE_POINTS 2    // per-point kernels output stores: sc1 write-through (see st_pol)
-#endif
-#ifndef MC_STORE_IMU
-#define MC_STORE_IMU 2       // the IMU kernel's output stores: sc1 write-through, as SLERP — bench (dealt
-                             // order) 327.8-330.1 vs 337.9-343.9 us with sc1 nt (profiles/round3/s46),
-                             // which beat nt (334.5-338.0 vs 353.2-363.1, s30; round 2 had nt ahead)
-#endif
-#ifndef MC_FASTPATH_MAXW
-#define MC_FASTPATH_MAXW 2   // frames spanning <= this many segments take the SGPR (no-LDS) path
-#endif
-#ifndef MC_SUBTILE_WIN
-#define MC_SUBTILE_WIN 1     // per sub-tile segment windows for frames wider than the SGPR path
-#endif
-#ifndef MC_NULL_COMPUTE
-#define MC_NULL_COMPUTE 0    // diagnostic build: skip the per-point math, keep loads/stores
-#endif
-#ifndef MC_NT_LOAD
-#define MC_NT_LOAD 1         // non-temporal input loads (streamed once): +5-8% measured (tools/ab.py)
-                             // (rechecked with the sc1 stores, bench: SLERP 318.4-322.5 vs 351.7-358.9 us,
-                             // IMU 324.5-325.4 vs 341.9-342.9, frame 298.0-299.9 vs 312.0-312.1 without,
-                             // profiles/round3/s54)
-#endif
-#ifndef MC_SLERP_WAVES
-#define MC_SLERP_WAVES 4     // waves/SIMD the SLERP kernel is compiled for (VGPR budget 512 / waves)
-#endif
-#ifndef MC_DIAG_FUSED_NOPREP
-#define MC_DIAG_FUSED_NOPREP 0   // diagnostic timing build: the fused kernels' prep workgroups do nothing
-#endif
-#ifndef MC_SLERP_NEXT_WAVES
-#define MC_SLERP_NEXT_WAVES MC_SLERP_WAVES   // the SLERP kernel carrying the next step's prep
-#endif
-#ifndef MC_IMU_PRELOAD
-#define MC_IMU_PRELOAD 1     // IMU: both window records loaded before the wave's segment vote
-#endif
-#ifndef MC_IMU_R1_UNCOND
-#define MC_IMU_R1_UNCOND 1   // IMU: load the second record without waiting for the window's W:
-                             // 333.0 vs 353.8 us over 3 replicas in one process (profiles/round3/s21),
-                             // not reproduced on the next box (339.7 vs 333.9, s23); in bench.py's
-                             // own steps 351.7 / 354.2 vs 358.3 / 358.3 us (s23), so it stays on
-#endif
-#ifndef MC_IMU_HOIST
-#define MC_IMU_HOIST 0       // IMU: the sub-tile's two records loaded before its window record
-                             // (rejected: 338.7 vs 339.7 us, bench 355.7-357.4; the plain IMU kernel
-                             // then spills a VGPR, profiles/round3/s23)
-#endif
-#ifndef MC_IMU_SEGREC
-#define MC_IMU_SEGREC 1      // IMU: a sub-tile's records are segments klo, klo + 1 of the step's
-                             // segment table (shared by the ~5 sub-tiles of a 5 ms segment, as SLERP's
-                             // sub-tile windows) instead of its own two records written by k_prep:
-                             // identical output, 7.5 MB less prep writes per 60 M-point step, 329.1 vs
-                             // 349.3 us over 5 replicas (tools/ab.py), bench 353.7-358.2 vs 354.3-361.5
-                             // (profiles/round3/s28); with sc1 stores in the dealt order 327.4-328.2
-                             // vs 334.4-339.2 us with the per-sub-tile records (s63)
-#endif
-static_assert(!(MC_IMU_HOIST && MC_IMU_SEGREC), "MC_IMU_HOIST loads the per-sub-tile records");
-#ifndef MC_IMU_WIN_FIRST
-#define MC_IMU_WIN_FIRST 1   // IMU: the sub-tile's window record loaded before (beside) its tile record:
-                             // bench 336.2 / 340.8 / 337.4 vs 338.2 / 341.6 / 338.4 us, alternating runs
-                             // (profiles/round3/s35), identical output
-#endif
-#ifndef MC_SWIN_PERM
-#define MC_SWIN_PERM 0       // sub-tile windows stored so that the sub-tiles one XCD runs in the dealt
-                             // order (st = x mod 8) share 128-byte lines (slot xcd_unit(st)); the
-                             // XCD-contiguous order keeps slot st
-                             // (rejected: IMU dealt 337.8 vs 338.3 us over 3 replicas, bench within
-                             // noise, profiles/round3/s36; with sc1 stores 329.5-330.4 vs 327.4-328.2,
-                             // s63)
-#endif
-#ifndef MC_POINTS_PAIR
-#define MC_POINTS_PAIR 0     // per-point kernels (bit MODE: 2 SLERP, 4 IMU): a workgroup per tile, both
-                             // sub-tiles' points loaded up front (IMU then spills: 128 VGPRs + 15)
-                             // (rejected: SLERP 363.6-367.0 vs 322.5-327.8 us in the bench, the
-                             // second sub-tile's loads in flight during the first's math cost 13 %,
-                             // profiles/round3/s42)
-#endif
-#ifndef MC_IMU_WAVES
-#define MC_IMU_WAVES 4       // the IMU kernel's (5: 66 VGPR spills)
-#endif
+// Shipping configuration.  The A/B history of every choice below (and of the arms that lost) is in
+// DESIGN.md §4 / §9 and profiles/; the kernels carry only the configuration that ships.
+//   * output stores: sc1 write-through (st_pol<2>) in the frame, SLERP and IMU kernels — SLERP +7 %
+//     vs nt; IMU 327.8-330.1 vs 337.9-343.9 us with sc1 nt (profiles/round3/s46); frame 298.2-298.9
+//     vs 300.3-301.3 us with sc1 nt (s48);
+//   * non-temporal input loads: SLERP 318.4-322.5 vs 351.7-358.9 us without (profiles/round3/s54);
+//   * 4 waves / SIMD for the per-point kernels (128 VGPRs; 5 waves spills, -8 to -11 %, s41);
+//   * frames spanning <= 2 segments take the SGPR path, wider ones per-sub-tile windows (§4);
+//   * IMU: both window records loaded before the wave's vote, the second one without waiting for the
+//     window's W (s21, s23); sub-tile records = segments klo, klo + 1 of the step's IMU segment table
+//     (329.1 vs 349.3 us over 5 replicas, s28); the sub-tile window loaded beside the tile record (s35).
+constexpr int kStorePol = 2;       // st_pol policy of the deskew kernels' output stores (sc1)
+constexpr int kPointsWaves = 4;    // __launch_bounds__ waves / SIMD of k_deskew_points
+constexpr int kFastMaxW = 2;       // frames spanning <= this many segments take the SGPR (no-LDS) path
 
 constexpr int kBlock = 256;                    // 4 waves of 64
-constexpr int kIters = MC_KITERS;              // float4 groups per thread per tile (frame mode)
+constexpr int kIters = 2;                      // float4 groups per thread per tile (k_affine_w)
 constexpr int kTileGroups = kBlock * kIters;   // 512 groups = 2048 points per tile
 constexpr int kSub = kTileGroups / kBlock;     // per-point modes: sub-tiles of kBlock groups
 constexpr int kWinMax = 64;                    // LDS window capacity (segments per frame)
@@ -168,11 +95,6 @@ struct ImuSeg {
   int64_t ts;    // absolute ns in the global table; frame-relative ns in a frame window
 };
 
-// slot of sub-tile st's window in swin: grouped by the XCD that runs it in the dealt order
-__device__ __forceinline__ int64_t swin_slot(int64_t st, int64_t n_sub, bool perm) {
-  return MC_SWIN_PERM && perm ? xcd_unit<1>(st, n_sub) : st;
-}
-
 // Per-frame segment window, written by k_prep: segments [klo, klo+W) cover every point of
 // the frame; bnd1 = frame-relative ns where segment klo+1 starts (W >= 2).
 struct FrameWin {
@@ -197,7 +119,7 @@ struct DeskewArgs {
   const int64_t* frame_start;
   const FrameWin* fwin;    // per-point modes
   const void* frec;        // 2 frame-specialised records per frame (PoseWin or ImuSeg)
-  const FrameWin* swin;    // per sub-tile: the same, for frames whose window exceeds MC_FASTPATH_MAXW
+  const FrameWin* swin;    // per sub-tile: the same, for frames whose window exceeds kFastMaxW
   const void* srec;        // 2 frame-specialised IMU records per sub-tile (MC_IMU_SEGREC=0 only; else null)
   const double* pose_time; // T
   const PoseSeg* pose_seg; // nseg
@@ -272,38 +194,20 @@ __device__ __forceinline__ void st_pol(float* p, const float4& v) {
     *reinterpret_cast<v4f*>(p) = t;
   }
 }
-__device__ __forceinline__ void st_frame(float* p, const float4& v) { st_pol<MC_STORE_FRAME>(p, v); }
-template <int MODE>
-__device__ __forceinline__ void st_points(float* p, const float4& v) {
-  st_pol<MODE == 2 ? MC_STORE_IMU : MC_STORE_POINTS>(p, v);
-}
+__device__ __forceinline__ void st_out(float* p, const float4& v) { st_pol<kStorePol>(p, v); }
 
 // 16-byte streaming loads of the input columns
 typedef int v4i __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const float* p) {
-#if MC_NT_LOAD
   const v4f t = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
   return make_float4(t.x, t.y, t.z, t.w);
-#else
-  return *reinterpret_cast<const float4*>(p);
-#endif
 }
 __device__ __forceinline__ int4 ld4(const int32_t* p) {
-#if MC_NT_LOAD
   const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
   return make_int4(t.x, t.y, t.z, t.w);
-#else
-  return *reinterpret_cast<const int4*>(p);
-#endif
 }
 
-__device__ __forceinline__ int ld1(const int32_t* p) {
-#if MC_NT_LOAD
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
+__device__ __forceinline__ int ld1(const int32_t* p) { return __builtin_nontemporal_load(p); }
 
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
@@ -550,7 +454,7 @@ struct PrepArgs {
   FrameRow* frame_tbl; PoseSeg* pose_seg; ImuSeg* imu_seg;               // outputs
   FrameWin* fwin; void* frec;
   int64_t nseg;
-  // per sub-tile windows for frames whose window is wider than MC_FASTPATH_MAXW
+  // per sub-tile windows for frames whose window is wider than kFastMaxW
   const int32_t* ftile;    // first tile of frame f (F+1 entries)
   const int2* strange;     // per sub-tile [min, max] t_ns (recorded with trange)
   FrameWin* swin; void* srec;
@@ -628,9 +532,6 @@ __global__ __launch_bounds__(64) void k_stamp(unsigned long long* dst) {
 // over the lanes (exact whenever the answer lies inside the window, checked; otherwise the full
 // wave-cooperative search), and the samples the records need are shuffled from the lanes that
 // hold them (a sample outside the window is loaded).  Frame: 2 memory round trips instead of 5-6.
-#ifndef MC_PREP_PROBE
-#define MC_PREP_PROBE 1
-#endif
 
 // first index of the 64-entry window [base, base + 64) around the guess for x in a[0..n)
 template <typename T>
@@ -746,14 +647,14 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
       ps = load_pose(a.time, a.pos, a.rpy, f);   // explicit per-frame transformation (host checks T == n_frames)
     } else {
       const double tf = a.frame_time[f];
-      const int64_t base = MC_PREP_PROBE ? probe_base<double>(a.T, a.time[0], a.time[a.T - 1], tf) : 0;
+      const int64_t base = probe_base<double>(a.T, a.time[0], a.time[a.T - 1], tf);
       const int64_t pi = base + lane;
       PoseSample pv{};
-      if (MC_PREP_PROBE && pi < a.T) pv = load_pose(a.time, a.pos, a.rpy, pi);
-      int64_t idx = MC_PREP_PROBE ? probe_count<true>(pv.t, base, a.T, tf) : -1;
+      if (pi < a.T) pv = load_pose(a.time, a.pos, a.rpy, pi);
+      int64_t idx = probe_count<true>(pv.t, base, a.T, tf);
       if (idx < 0) idx = wave_count<true>(a.time, a.T, tf);   // searchsorted 'left'
       if (idx > a.T - 1) idx = a.T - 1;
-      ps = fetch_pose(pv, MC_PREP_PROBE ? base : INT64_MIN / 2, idx, a);
+      ps = fetch_pose(pv, base, idx, a);
     }
     if (lane < 3) {   // lane i writes row i of R and t_i
       double R[9];
@@ -770,26 +671,25 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
   const double tf = MODE == 1 ? a.frame_time[f] : 0.0;
   const int64_t fs = MODE == 2 ? a.frame_start[f] : 0;
   // the probe window and its samples (one round)
-  int64_t base = INT64_MIN / 2;   // no window: every fetch loads
+  int64_t base;
   QSample pv{};
   ImuSample iv{};
-  if (MC_PREP_PROBE) {
-    if (MODE == 1) {
-      const double xm = has ? tf + 0.5e-9 * ((double)tr.x + (double)tr.y) : tf;
-      base = probe_base<double>(a.T, a.time[0], a.time[a.T - 1], xm);
-      if (base + lane < a.T) pv = qsample_of(load_pose(a.time, a.pos, a.rpy, base + lane));
-    } else {
-      const double xm = (double)fs + (has ? 0.5 * ((double)tr.x + (double)tr.y) : 0.0);
-      base = probe_base<int64_t>(a.M, a.imu_ts[0], a.imu_ts[a.M - 1], xm);
-      if (base + lane < a.M) iv = load_imu(a.imu_ts, a.gyro, base + lane);
-    }
+  if (MODE == 1) {
+    const double xm = has ? tf + 0.5e-9 * ((double)tr.x + (double)tr.y) : tf;
+    base = probe_base<double>(a.T, a.time[0], a.time[a.T - 1], xm);
+    if (base + lane < a.T) pv = qsample_of(load_pose(a.time, a.pos, a.rpy, base + lane));
+  } else {
+    const double xm = (double)fs + (has ? 0.5 * ((double)tr.x + (double)tr.y) : 0.0);
+    base = probe_base<int64_t>(a.M, a.imu_ts[0], a.imu_ts[a.M - 1], xm);
+    if (base + lane < a.M) iv = load_imu(a.imu_ts, a.gyro, base + lane);
   }
   int64_t klo = 0, khi = 0;
   if (has) {
     int64_t c0 = -1, c1 = -1;
     if (MODE == 1) {
       const double x0 = tf + (double)tr.x * 1e-9, x1 = tf + (double)tr.y * 1e-9;
-      if (MC_PREP_PROBE) { c0 = probe_count<false>(pv.t, base, a.T, x0); c1 = probe_count<false>(pv.t, base, a.T, x1); }
+      c0 = probe_count<false>(pv.t, base, a.T, x0);
+      c1 = probe_count<false>(pv.t, base, a.T, x1);
       if (c0 < 0 || c1 < 0) wave_count2<false>(a.time, a.T, x0, x1, &c0, &c1);
       klo = c0 - 1;
       khi = c1 - 1;
@@ -797,7 +697,8 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
       khi = khi < 0 ? 0 : (khi > a.nseg - 1 ? a.nseg - 1 : khi);
     } else {
       const int64_t x0 = fs + (int64_t)tr.x, x1 = fs + (int64_t)tr.y;
-      if (MC_PREP_PROBE) { c0 = probe_count<false>(iv.ts, base, a.M, x0); c1 = probe_count<false>(iv.ts, base, a.M, x1); }
+      c0 = probe_count<false>(iv.ts, base, a.M, x0);
+      c1 = probe_count<false>(iv.ts, base, a.M, x1);
       if (c0 < 0 || c1 < 0) wave_count2<false>(a.imu_ts, a.M, x0, x1, &c0, &c1);
       klo = c0 - 1;
       khi = c1 - 1;
@@ -850,7 +751,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     if (lane == 0) a.fwin[f] = w;
   }
   // (IMU: every frame, so the deskew kernel reads only its sub-tile's window, one scalar load)
-  if (!MC_SUBTILE_WIN || (MODE == 1 && W <= MC_FASTPATH_MAXW) || !a.swin) return;
+  if ((MODE == 1 && W <= kFastMaxW) || !a.swin) return;
   // A wide frame (IMU: ~20 samples per 0.1 s frame): each 1024-point sub-tile of a time-ordered
   // frame spans ~1 ms, so its own window is 1-2 segments and takes the SGPR path (no LDS staging,
   // no barrier: -10 % kernel time on SLERP, tools/ab.py).  Lane per sub-tile; segment of t =
@@ -903,9 +804,9 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
     FrameWin w;
     w.klo = (int32_t)k0;
     w.W = (int16_t)(n > kWinMax ? kWinMax + 1 : n);
-    // samples k0, k0 + 1, k0 + 2 (clamped): records k0 and k0 + 1 and the boundary of k0 + 1
+    // samples k0, k0 + 1, k0 + 2 (clamped): the boundary of k0 + 1 and the angle bound of segments
+    // k0, k0 + 1 (the deskew kernel reads the records themselves from the step's segment table)
     const int64_t ka = clampk(k0), kb = clampk(k0 + 1), kc = clampk(k0 + 2);
-    const bool rec = valid && n <= MC_FASTPATH_MAXW && !MC_IMU_SEGREC;
     double ang;
     if (MODE == 1) {
       // SLERP: no sub-tile records — the deskew kernel reads segments k0, k0 + 1 of the step's
@@ -918,16 +819,15 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a, int64_t block) {
       const double ang1 = theta_of(kb);
       if (n >= 2) ang = fmax(ang, ang1);
       (void)kc;
-      (void)rec;
     } else {
       const ImuSample sa = fetch_imu(iv, base, ka, a), sb_ = fetch_imu(iv, base, kb, a);
       const ImuSample sc = fetch_imu(iv, base, kc, a);
       w.bnd1 = n >= 2 ? bound_imu(sb_) : INT64_MAX;
-      ang = imu_rec(sa, sb_, ka + 1 >= a.M, a.srec, 2 * st, rec);
-      if (n >= 2) ang = fmax(ang, imu_rec(sb_, sc, kb + 1 >= a.M, a.srec, 2 * st + 1, rec));
+      ang = imu_rec(sa, sb_, ka + 1 >= a.M, nullptr, 0, false);
+      if (n >= 2) ang = fmax(ang, imu_rec(sb_, sc, kb + 1 >= a.M, nullptr, 0, false));
     }
     w.tier = window_tier<MODE>(MODE == 1 ? ang : imu_angle_bound(ang, hs ? r : make_int2(0, 0)));
-    if (valid) a.swin[swin_slot(st, a.n_sub, a.swin_perm != 0)] = w;
+    if (valid) a.swin[st] = w;
   }
 }
 
@@ -985,67 +885,28 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
         MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
 #undef MC_XF
         float* o = ox + (int64_t)(g >> 6) * a.out_C * kBlkPts + 4 * (g & 63);
-        st_frame(o, ox4);
-        st_frame(o + kBlkPts, oy4);
-        st_frame(o + 2 * kBlkPts, oz4);
-        st_frame(o + 3 * kBlkPts, vi[it]);
+        st_out(o, ox4);
+        st_out(o + kBlkPts, oy4);
+        st_out(o + 2 * kBlkPts, oz4);
+        st_out(o + 3 * kBlkPts, vi[it]);
       }
     }
   }
 }
 
-#ifndef MC_FRAME_SUB
-#define MC_FRAME_SUB 1       // frame kernel over kBlock-group sub-tiles, one group per thread (-3 %)
-#endif
-// the per-point kernels' decomposition applied to frame mode (MC_FRAME_SUB=1)
-// pre: workgroups ahead of the deskew part of the grid (0 unless fused with a prep)
-__device__ __forceinline__ void deskew_frame_sub(const DeskewArgs& a, const uint32_t pre) {
-  const int64_t n_sub = (int64_t)a.n_tiles * kSub;
-  const uint32_t nb = gridDim.x - pre;
-  for (int64_t it = blockIdx.x - pre; it < n_sub; it += nb) {
-    const int64_t st = nb >= n_sub ? xcd_unit<MC_XCD_FRAME>(it, n_sub) : it;
-    const Tile tl = ldu(a.tiles + st / kSub);
-    const int g = (int)(st % kSub) * kBlock + threadIdx.x;
-    if (g >= tl.ngroups) continue;
-    const FrameRow r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
-    const FrameRow r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
-    const FrameRow r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
-    const int64_t p = tl.pstart + 4 * (int64_t)g;
-    const float* q = a.in + bidx((int)a.in_C, 0, p);
-    const float4 X = ld4(q), Y = ld4(q + kBlkPts), Z = ld4(q + 2 * kBlkPts), I = ld4(q + 3 * kBlkPts);
-    float4 ox4, oy4, oz4;
-#define MC_XF(c)                                                  \
-  ox4.c = xf_row(r0, X.c, Y.c, Z.c);                              \
-  oy4.c = xf_row(r1, X.c, Y.c, Z.c);                              \
-  oz4.c = xf_row(r2, X.c, Y.c, Z.c);
-    MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
-#undef MC_XF
-    float* o = a.out + bidx((int)a.out_C, 0, p);
-    st_frame(o, ox4);
-    st_frame(o + kBlkPts, oy4);
-    st_frame(o + 2 * kBlkPts, oz4);
-    st_frame(o + 3 * kBlkPts, I);
-  }
-}
-
-// Quad decomposition (MC_FRAME_QUAD): a workgroup covers 64 float4 groups of a sub-tile and each
+// Frame kernel, quad decomposition: a workgroup covers 64 float4 groups of a sub-tile and each
 // lane ONE column of one group (lane & 3 = x, y, z, intensity): one 16-byte load and one 16-byte
-// store per lane, four times the lanes of deskew_frame_sub.  The quad's x / y / z float4s reach
+// store per lane (four times the lanes of one group per lane: 293 vs 298-319 us, profiles/round2/s08).  The quad's x / y / z float4s reach
 // every lane of the quad through DPP quad broadcasts (no LDS), lane c < 3 forms output column c of
 // the four points (R row c . p + t_c in float64, xf_row), lane 3 passes the
 // intensities through.  A bare 16 B-in / 16 B-out stream runs at 6.61-6.68 TB/s with one load and
 // one store per lane vs 6.12 with four of each (tools/stage_probe.hip, profiles/round2/s07).
-#ifndef MC_FRAME_QUAD
-#define MC_FRAME_QUAD 1
-#endif
 constexpr int kQuadGroups = kBlock / 4;   // float4 groups per workgroup in the quad decomposition
 
-// MC_FRAME_QUAD_U quarters (64 float4 groups each) per workgroup: each lane issues U column loads
-// before any arithmetic, so a wave keeps U KB in flight through its longer float64 chain.
-#ifndef MC_FRAME_QUAD_U
-#define MC_FRAME_QUAD_U 2    // frame f64: 294.8 us vs 304.0 (U=1), 308.0 (U=4), 297.9 (one group per lane), r2 f32 292.6 (profiles/round3/s05)
-#endif
-constexpr int kQuadU = MC_FRAME_QUAD_U;
+// kQuadU quarters (64 float4 groups each) per workgroup: each lane issues U column loads before any
+// arithmetic, so a wave keeps U KB in flight through its longer float64 chain (frame f64: 294.8 us vs
+// 304.0 with U = 1, 308.0 with U = 4, profiles/round3/s05; 299.8-301.0 vs 316.0-319.1 with sc1 stores, s74).
+constexpr int kQuadU = 2;
 static_assert(kQuadU == 1 || kQuadU == 2 || kQuadU == 4, "quarters per workgroup: 1, 2 or 4");
 constexpr int kQuadUnitsPerSub = kBlock / kQuadGroups / kQuadU;   // workgroup units per sub-tile
 
@@ -1091,7 +952,7 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
       o.y = xf_row(r, X.y, Y.y, Z.y);
       o.z = xf_row(r, X.z, Y.z, Z.z);
       o.w = xf_row(r, X.w, Y.w, Z.w);
-      if (act[u]) st_frame(a.out + bidx((int)a.out_C, c, p[u]), c == 3 ? w : o);
+      if (act[u]) st_out(a.out + bidx((int)a.out_C, c, p[u]), c == 3 ? w : o);
       if constexpr (PCD) {
         // lane c's column of its group's four points (a whole line is the quad's four lanes)
         const float4 val = c == 3 ? w : o;
@@ -1118,15 +979,7 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
 }
 
 
-__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
-#if MC_FRAME_QUAD
-  deskew_frame_quad(a, 0u);
-#elif MC_FRAME_SUB
-  deskew_frame_sub(a, 0u);
-#else
-  deskew_frame_body<false>(a);
-#endif
-}
+__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) { deskew_frame_quad(a, 0u); }
 
 // Path A with the ASCII PCD text bytes of every output block (mc_deskew_pcd)
 __global__ __launch_bounds__(kBlock) void k_deskew_frame_pcd(const DeskewArgs a) { deskew_frame_quad<true>(a, 0u); }
@@ -1297,9 +1150,6 @@ __device__ __forceinline__ void sincos_tier(const P& poly, double x, double& s, 
 // as the oracle's (t - t_k) / dt; TIER bounds alpha * Theta.
 template <typename P>
 __device__ __forceinline__ void slerp_point(const PoseWin& w, const P& poly, int t, float& x, float& y, float& z) {
-#if MC_NULL_COMPUTE
-  asm volatile("" : "+v"(x), "+v"(y), "+v"(z) : "v"(t));
-#else
   const double tq = __dadd_rn(w.tf, __dmul_rn((double)t, 1e-9));
   double al = (tq - w.t0) * w.inv_dt;
   al = fmin(fmax(al, 0.0), 1.0);
@@ -1322,7 +1172,6 @@ __device__ __forceinline__ void slerp_point(const PoseWin& w, const P& poly, int
   x = (float)fma(2.0, cx, fma(al, w.dp[0], X) + w.p0[0]);
   y = (float)fma(2.0, cy, fma(al, w.dp[1], Y) + w.p0[1]);
   z = (float)fma(2.0, cz, fma(al, w.dp[2], Z) + w.p0[2]);
-#endif
 }
 
 // Path B body (CSIM:1447-1465): w = g + alpha*dg (alpha from the bracketing IMU samples, CSIM:1504-
@@ -1331,9 +1180,6 @@ __device__ __forceinline__ void slerp_point(const PoseWin& w, const P& poly, int
 template <typename P>
 __device__ __forceinline__ void imu_point(const ImuSeg& w, const P& poly, double tsd, int t, float& x, float& y,
                                           float& z) {
-#if MC_NULL_COMPUTE
-  asm volatile("" : "+v"(x), "+v"(y), "+v"(z) : "v"(t));
-#else
   const double td = (double)t;
   double al = (td - tsd) * w.inv_dt;
   al = al > 0.0 ? al : 0.0;
@@ -1353,7 +1199,6 @@ __device__ __forceinline__ void imu_point(const ImuSeg& w, const P& poly, double
   const double y3 = fma(ca, y1, sa * z2);
   const double z3 = fma(-sa, y1, ca * z2);
   x = (float)x2; y = (float)y3; z = (float)z3;
-#endif
 }
 
 // window search: index of the window segment of frame-relative time t (bnd sorted, bnd[0] unused)
@@ -1376,14 +1221,7 @@ using WinOf = typename std::conditional<MODE == 1, PoseWin, ImuSeg>::type;
 
 // a scheduling fence between the points of a lane: the float64 bodies (~35 live VGPRs each) run
 // one after the other instead of interleaved, which keeps the kernels at 4 waves / SIMD (128 VGPRs)
-#ifndef MC_POINT_SCHED
-#define MC_POINT_SCHED 1
-#endif
-#if MC_POINT_SCHED
 #define MC_POINT_FENCE __builtin_amdgcn_sched_barrier(0);
-#else
-#define MC_POINT_FENCE
-#endif
 
 // one point with a wave-uniform record at a tier
 template <int MODE, typename P>
@@ -1458,32 +1296,29 @@ __device__ __forceinline__ T select_rec(bool second, const T& a, const T& b) {
 // The SGPR path of a window of <= 2 segments at tier TIER: each wave votes whether its points all
 // sit in one segment; a wave across the boundary peels its two segments.
 // set_tf (SLERP sub-tile windows): rec points into the segment table; its records get the frame time tf
+// IMU (rec = segment klo of the step's IMU segment table): fs = the frame start (the table's
+// absolute ns -> frame-relative), j1 = 1 inside the table, 0 at its last sample.
 template <int MODE, int TIER>
 __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin& fw, bool set_tf, double tf,
                                           bool act, const int4& Tq, float4& X, float4& Y, float4& Z,
-                                          const WinOf<MODE>* pre0 = nullptr, const WinOf<MODE>* pre1 = nullptr,
                                           int64_t fs = 0, int j1 = 1) {
   const PolyOf<TIER> poly = poly_load<TIER>();
   auto load_rec = [&](int j) {
     WinOf<MODE> w = ldu(rec + j);
     if constexpr (MODE == 1) {
       if (set_tf) w.tf = tf;
-    } else if constexpr (MC_IMU_SEGREC) {
+    } else {
       w.ts -= fs;   // the segment table's absolute ns -> frame-relative
     }
     return w;
   };
   // IMU: both 64-byte records in SGPRs before the vote (their scalar-load latency then overlaps the
-  // point loads instead of following the vote); a 144-byte SLERP record pair would not fit
+  // point loads instead of following the vote), the second one without waiting for the window's W
+  // (slot j1 exists for every window); a 144-byte SLERP record pair would not fit
   WinOf<MODE> r0, r1;
-  if constexpr (MODE == 2 && MC_IMU_PRELOAD) {
-    if (MC_IMU_HOIST) {   // loaded by the caller before the window record
-      r0 = *pre0;
-      r1 = *pre1;
-    } else {
-      r0 = load_rec(0);
-      r1 = load_rec(MC_IMU_R1_UNCOND || fw.W == 2 ? j1 : 0);   // (slot j1 exists for every window)
-    }
+  if constexpr (MODE == 2) {
+    r0 = load_rec(0);
+    r1 = load_rec(j1);
   }
   bool use1 = false, mixed = false;
   if (fw.W == 2) {
@@ -1499,14 +1334,14 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
     // `if (act)` the compiler sank the record load into the divergent block as 9 per-lane vector
     // loads of the 144-byte record instead of scalar loads
     WinOf<MODE> w;
-    if constexpr (MODE == 2 && MC_IMU_PRELOAD) w = select_rec(use1, r0, r1);
+    if constexpr (MODE == 2) w = select_rec(use1, r0, r1);
     else w = load_rec(use1 ? 1 : 0);
     points4<MODE>(w, poly, Tq, X, Y, Z);
   } else {
     int seg[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) seg[c] = act ? ((int64_t)i4c(Tq, c) >= fw.bnd1 ? 1 : 0) : -1;
-    if constexpr (MODE == 2 && MC_IMU_PRELOAD)
+    if constexpr (MODE == 2)
       points_peeled<MODE>(seg, [&](int j) { return select_rec(j != 0, r0, r1); }, poly, Tq, X, Y, Z);
     else
       points_peeled<MODE>(seg, [&](int j) { return load_rec(j); }, poly, Tq, X, Y, Z);
@@ -1529,13 +1364,11 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
 // PCD (mc_deskew_pcd): a wave's 64 groups are one 256-point block of the output batch; it also
 // writes that block's ASCII PCD text bytes (a wave reduction, no barrier).
 template <int MODE, bool NEXT = false, bool PCD = false>
-__global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : MC_SLERP_WAVES) : MC_IMU_WAVES) void k_deskew_points(
-    const DeskewArgs a, const PrepArgs pn, const uint32_t pre) {
+__global__ __launch_bounds__(kBlock, kPointsWaves) void k_deskew_points(const DeskewArgs a, const PrepArgs pn,
+                                                                         const uint32_t pre) {
   if constexpr (NEXT) {
     if (blockIdx.x < pre) {
-#if !MC_DIAG_FUSED_NOPREP
       prep_body<MODE>(pn, blockIdx.x);
-#endif
       return;
     }
   }
@@ -1545,7 +1378,6 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
   const int tid = threadIdx.x;
   const int64_t n_sub = (int64_t)a.n_tiles * kSub;
   const Win* frec = reinterpret_cast<const Win*>(a.frec);
-  const Win* srec = reinterpret_cast<const Win*>(a.srec);
 
   const uint32_t b0 = NEXT ? blockIdx.x - pre : blockIdx.x, nb = NEXT ? gridDim.x - pre : gridDim.x;
   // the points of sub-tile st of tile tl, every lane (a short sub-tile's idle lanes re-read its first
@@ -1572,34 +1404,27 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
     const bool act = g < tl.ngroups;
     const int64_t p = tl.pstart + 4 * (int64_t)g;
     // frames wider than the SGPR path take their sub-tile's own window (k_prep writes one for every
-    // IMU sub-tile).  One scalar load of the chosen record (a select of two loaded structs became a
-    // vector load of bnd1 whose wait held back the point loads)
+    // IMU sub-tile, loaded by the caller beside the tile record).  One scalar load of the chosen
+    // record (a select of two loaded structs became a vector load of bnd1 whose wait held back the
+    // point loads)
     bool sub = true;
-    if constexpr (MODE != 2) sub = MC_SUBTILE_WIN && ldu(a.fwin + f).W > MC_FASTPATH_MAXW;
-    // IMU (MC_IMU_HOIST): the sub-tile's two records are at srec + 2 st whatever its window says, so
-    // they are loaded beside the window record instead of after it
-    Win hr0, hr1;
-    if constexpr (MODE == 2 && MC_IMU_HOIST) {
-      hr0 = ldu(srec + 2 * st);
-      hr1 = ldu(srec + 2 * st + 1);
-    }
-    const FrameWin fw = MODE == 2 && MC_IMU_WIN_FIRST ? fw_first : ldu(sub ? a.swin + swin_slot(st, n_sub, a.xcd_order == 0) : a.fwin + f);
-    // SLERP sub-tile windows point into the step's segment table, whose records carry no frame time
-    const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) + fw.klo
-                                      : (MC_IMU_SEGREC ? reinterpret_cast<const Win*>(a.imu_seg) + fw.klo : srec + 2 * st))
+    if constexpr (MODE != 2) sub = ldu(a.fwin + f).W > kFastMaxW;
+    const FrameWin fw = MODE == 2 ? fw_first : ldu(sub ? a.swin + st : a.fwin + f);
+    // sub-tile windows point into the step's segment table (SLERP: whose records carry no frame time)
+    const Win* rec = sub ? (MODE == 1 ? reinterpret_cast<const Win*>(a.pose_seg) : reinterpret_cast<const Win*>(a.imu_seg)) + fw.klo
                          : frec + 2 * f;
     const bool set_tf = MODE == 1 && sub;
 
-    if (fw.W <= MC_FASTPATH_MAXW) {
+    if (fw.W <= kFastMaxW) {
       // the tier k_prep chose for the window: its coefficient load is issued here, beside the point
       // loads, not behind the vote that needs them
       const double tf = set_tf ? ldu(a.frame_time + f) : 0.0;
       // IMU segment-table records: the frame start, and slot 1 only inside the table
-      const int64_t fs = MODE == 2 && MC_IMU_SEGREC ? ldu(a.frame_start + f) : 0;
-      const int j1 = MODE == 2 && MC_IMU_SEGREC ? (fw.klo + 1 < a.ntab ? 1 : 0) : 1;
-      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1, fs, j1);
-      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1, fs, j1);
-      else fast_path<MODE, kTierAny<MODE>>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, &hr0, &hr1, fs, j1);
+      const int64_t fs = MODE == 2 ? ldu(a.frame_start + f) : 0;
+      const int j1 = MODE == 2 ? (fw.klo + 1 < a.ntab ? 1 : 0) : 1;
+      if (fw.tier == 0) fast_path<MODE, 0>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, fs, j1);
+      else if (fw.tier == 1) fast_path<MODE, 1>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, fs, j1);
+      else fast_path<MODE, kTierAny<MODE>>(rec, fw, set_tf, tf, act, Tq, X, Y, Z, fs, j1);
     } else if (fw.W <= kWinMax) {
       const int W = fw.W;
       if (tid < W) {
@@ -1651,11 +1476,11 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
     }
     if (act) {
       float* o = a.out + bidx((int)a.out_C, 0, p);
-      st_points<MODE>(o, X);
-      st_points<MODE>(o + kBlkPts, Y);
-      st_points<MODE>(o + 2 * kBlkPts, Z);
-      st_points<MODE>(o + 3 * kBlkPts, I);
-      if (a.copy_t) st_points<MODE>(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
+      st_out(o, X);
+      st_out(o + kBlkPts, Y);
+      st_out(o + 2 * kBlkPts, Z);
+      st_out(o + 3 * kBlkPts, I);
+      if (a.copy_t) st_out(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
     }
     if constexpr (PCD) {
       const int64_t i0 = p - ldu(a.fpoff + f), n = ldu(a.fcount + f);
@@ -1673,40 +1498,22 @@ __global__ __launch_bounds__(kBlock, MODE == 1 ? (NEXT ? MC_SLERP_NEXT_WAVES : M
       if ((tid & 63) == 0 && wg < tl.ngroups) a.pcd_len[(tl.pstart + 4 * (int64_t)wg) >> 8] = bytes;
     }
   };
-  // the sub-tile window of an IMU sub-tile does not depend on the tile record (MC_IMU_WIN_FIRST), so
-  // both scalar loads are in flight together instead of one behind the other
+  // the sub-tile window of an IMU sub-tile does not depend on the tile record, so both scalar loads
+  // are in flight together instead of one behind the other
   auto win_first = [&](int64_t st) {
     FrameWin w{};
-    if constexpr (MODE == 2 && MC_IMU_WIN_FIRST) w = ldu(a.swin + swin_slot(st, n_sub, a.xcd_order == 0));
+    if constexpr (MODE == 2) w = ldu(a.swin + st);
     return w;
   };
-  if constexpr ((MC_POINTS_PAIR >> MODE) & 1) {
-    // a workgroup per tile: both sub-tiles' points loaded up front, so the second one's loads are in
-    // flight during the first one's math and stores
-    static_assert(kSub == 2, "MC_POINTS_PAIR pairs the two sub-tiles of a tile");
-    const int64_t n_t = a.n_tiles;
-    for (int64_t it = b0; it < n_t; it += nb) {
-      const int64_t t = nb < n_t ? it : (a.xcd_order ? xcd_unit<1>(it, n_t) : it);
-      const FrameWin w0 = win_first(2 * t), w1 = win_first(2 * t + 1);
-      const Tile tl = ldu(a.tiles + t);
-      int4 Tq0, Tq1;
-      float4 X0, Y0, Z0, I0, X1, Y1, Z1, I1;
-      load_sub(2 * t, tl, Tq0, X0, Y0, Z0, I0);
-      load_sub(2 * t + 1, tl, Tq1, X1, Y1, Z1, I1);
-      sub_tile(2 * t, tl, w0, Tq0, X0, Y0, Z0, I0);
-      if (kBlock < tl.ngroups) sub_tile(2 * t + 1, tl, w1, Tq1, X1, Y1, Z1, I1);   // uniform
-    }
-  } else {
-    for (int64_t it = b0; it < n_sub; it += nb) {
-      const int64_t st = nb < n_sub ? it : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
-      const FrameWin w = win_first(st);
-      const Tile tl = ldu(a.tiles + st / kSub);
-      if ((int)(st % kSub) * kBlock >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
-      int4 Tq;
-      float4 X, Y, Z, I;
-      load_sub(st, tl, Tq, X, Y, Z, I);
-      sub_tile(st, tl, w, Tq, X, Y, Z, I);
-    }
+  for (int64_t it = b0; it < n_sub; it += nb) {
+    const int64_t st = nb < n_sub ? it : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
+    const FrameWin w = win_first(st);
+    const Tile tl = ldu(a.tiles + st / kSub);
+    if ((int)(st % kSub) * kBlock >= tl.ngroups) continue;  // uniform: empty sub-tile of a short tile
+    int4 Tq;
+    float4 X, Y, Z, I;
+    load_sub(st, tl, Tq, X, Y, Z, I);
+    sub_tile(st, tl, w, Tq, X, Y, Z, I);
   }
 }
 
@@ -1723,11 +1530,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_deskew_frame_next(const DeskewArg
     prep_body<0>(p, blockIdx.x);
     return;
   }
-#if MC_FRAME_QUAD
   deskew_frame_quad(a, pre);
-#else
-  deskew_frame_sub(a, pre);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1752,175 +1555,23 @@ __device__ __forceinline__ int64_t local_index(const LayoutArgs& a, const Tile& 
 
 // The stager pair: the reference's (N, ld) float64 AoS [x,y,z,intensity,...]
 // (LMC:770) <-> the padded SoA float32 columns, both on the device.  48 algorithmic bytes per
-// point either way.  Mapping: one lane per 16-byte AoS chunk (half a row: (x,y) or (z,i)), so
-// every AoS access of a wave is 1 KB contiguous; the SoA side is 4-byte lanes, 2 x 128 B runs
-// per instruction.  (A lane-per-4-points mapping, 8 x 16 B at a 128-B lane stride, measured 7 %
-// / 35 % of peak.)  kStageUnroll chunks per lane are in flight at once.
+// point either way.
+//
+// 256-point units: a workgroup moves 256 points (64 float4 groups, one 256-point block of the batch)
+// per unit, so every lane issues ONE 16-byte load and two 16-byte stores (SoA -> AoS) or two loads and
+// one store (AoS -> SoA), each wave instruction covering 1 KB contiguous on both sides, transposed
+// through a 4 KB LDS tile; non-temporal loads and stores (st_pol<1>).  Bare streams of these lane
+// shapes: 6.11 TB/s (16 B in / 32 B out, 1 / 2 per lane) vs 5.22-5.34 with a 2048-point tile's 8 / 16
+// per lane; 6.42 TB/s (32 B in / 16 B out, 2 / 1) (tools/stage_probe.hip, profiles/round2/s07).
+// Rejected: 2048-point LDS tiles (71 / 75 % of peak), register-only quad transposes
+// (16-byte holes in every row-side store, profiles/round2/s11-s12), 2 / 4 units per workgroup pass
+// (profiles/round3/s09), sc1 / sc1 nt stores (s31), the dealt unit order (s57).
 typedef double v2d __attribute__((ext_vector_type(2)));
-constexpr int kStageUnroll = 4;
-#ifndef MC_STAGE_LDS
-#define MC_STAGE_LDS 1       // transpose each tile through LDS (16-byte lanes on both sides):
-                             // -11 % / -15 % kernel time vs the direct mapping (tools/ab_stager.py)
-#endif
-#ifndef MC_STAGE_ST
-#define MC_STAGE_ST 1        // LDS stager output stores (st_pol policy)
-#endif
-#ifndef MC_STAGE_BATCH
-#define MC_STAGE_BATCH 8     // LDS stager: 16-byte HBM loads per lane batched ahead of its LDS
-                             // writes (0: one at a time)
-#endif
-constexpr int kStageBatch = MC_STAGE_BATCH > 0 ? MC_STAGE_BATCH : 1;
-constexpr int kTilePts = 4 * kTileGroups;
-constexpr int kStageRow = kTilePts + 16;   // LDS row pad: the 4 rows start in different banks
-
-// LDS-transposed stager: the tile's 4 x 2048 float32 values sit in LDS between a 16-byte-per-lane
-// AoS pass and a float4-per-lane SoA pass.
-__device__ __forceinline__ void stage_tile_lds_in(const LayoutArgs& a, const Tile& tl, const v2d* __restrict__ s2,
-                                                  int nv, float (*s)[kStageRow]) {
-  const int np = 4 * tl.ngroups;
-#if MC_STAGE_BATCH
-  // kStageBatch 16-byte loads in flight per lane before the first LDS write (one at a time, the
-  // lane waits out a full HBM latency per load)
-  for (int q0 = 0; q0 < 2 * np; q0 += kStageBatch * kBlock) {
-    v2d v[kStageBatch];
-#pragma unroll
-    for (int u = 0; u < kStageBatch; ++u) {
-      const int q = q0 + u * kBlock + threadIdx.x;
-      v[u] = q < 2 * nv ? __builtin_nontemporal_load(s2 + q) : v2d{0.0, 0.0};
-    }
-#pragma unroll
-    for (int u = 0; u < kStageBatch; ++u) {
-      const int q = q0 + u * kBlock + threadIdx.x;
-      if (q < 2 * np) {
-        const int j = q >> 1, h = q & 1;
-        s[2 * h][j] = (float)v[u].x;
-        s[2 * h + 1][j] = (float)v[u].y;
-      }
-    }
-  }
-#else
-  for (int q = threadIdx.x; q < 2 * np; q += kBlock) {
-    const v2d v = q < 2 * nv ? __builtin_nontemporal_load(s2 + q) : v2d{0.0, 0.0};
-    const int j = q >> 1, h = q & 1;
-    s[2 * h][j] = (float)v.x;
-    s[2 * h + 1][j] = (float)v.y;
-  }
-#endif
-  __syncthreads();
-  float* cx = a.cols + bidx(a.C, 0, tl.pstart);
-  for (int g = threadIdx.x; g < tl.ngroups; g += kBlock)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      st_pol<MC_STAGE_ST>(cx + ((g >> 6) * a.C + c) * kBlkPts + 4 * (g & 63),
-                          *reinterpret_cast<const float4*>(&s[c][4 * g]));
-  __syncthreads();
-}
-
-__device__ __forceinline__ void stage_tile_lds_out(const LayoutArgs& a, const Tile& tl, v2d* __restrict__ d2, int nv,
-                                                   float (*s)[kStageRow]) {
-  const float* cx = a.cols + bidx(a.C, 0, tl.pstart);
-#if MC_STAGE_BATCH
-  for (int g0 = 0; g0 < (nv + 3) / 4; g0 += 2 * kBlock) {
-    float4 t[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int g = g0 + u * kBlock + threadIdx.x;
-      if (g < (nv + 3) / 4)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) t[u][c] = ld4(cx + ((g >> 6) * a.C + c) * kBlkPts + 4 * (g & 63));
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int g = g0 + u * kBlock + threadIdx.x;
-      if (g < (nv + 3) / 4)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) *reinterpret_cast<float4*>(&s[c][4 * g]) = t[u][c];
-    }
-  }
-#else
-  for (int g = threadIdx.x; g < (nv + 3) / 4; g += kBlock)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      *reinterpret_cast<float4*>(&s[c][4 * g]) = ld4(cx + ((g >> 6) * a.C + c) * kBlkPts + 4 * (g & 63));
-#endif
-  __syncthreads();
-  for (int q = threadIdx.x; q < 2 * nv; q += kBlock) {
-    const int j = q >> 1, h = q & 1;
-    const v2d v = {(double)s[2 * h][j], (double)s[2 * h + 1][j]};
-    st_pol<MC_STAGE_ST>(reinterpret_cast<float*>(d2 + q), __builtin_bit_cast(float4, v));
-  }
-  __syncthreads();
-}
-
-// ---- 256-point stager units (MC_STAGE_QUAD) ---------------------------------------------------
-// A workgroup moves 256 points (64 float4 groups, one 256-point block of the batch) per unit, so
-// every lane issues ONE 16-byte load and two 16-byte stores (SoA -> AoS) or two loads and one store
-// (AoS -> SoA), each wave instruction covering 1 KB contiguous on both sides, transposed through a
-// 4 KB LDS tile.  Bare streams of these lane shapes: 6.11 TB/s (16 B in / 32 B out, 1 / 2 per
-// lane) vs 5.22-5.34 with the 2048-point tile's 8 / 16 per lane; 6.42 TB/s (32 B in / 16 B out,
-// 2 / 1) (tools/stage_probe.hip, profiles/round2/s07).  (A register-only version through DPP quad
-// transposes stored each row-side instruction with 16-byte holes: SoA -> AoS 721-777 vs 504 us,
-// profiles/round2/s11-s12.)
-#ifndef MC_STAGE_QUAD
-#define MC_STAGE_QUAD 1
-#endif
-constexpr int kStageQuarters = kTileGroups / kQuadGroups;   // 256-point units per tile
+constexpr int kStageSt = 1;                                // st_pol policy of the stager stores (nt)
+constexpr int kStageQuarters = kTileGroups / kQuadGroups;  // 256-point units per tile
 constexpr int kUnitRow = kQuadGroups * 4 + 4;              // LDS floats per column (+4: banks)
 
-// MC_STAGE_UNITS consecutive 256-point units (one tile's) per workgroup pass: every lane issues its
-// U column loads before the first LDS write, so a workgroup keeps U x 4 KB of reads in flight
-// through its barrier-separated store phase.
-#ifndef MC_STAGE_UNITS
-#define MC_STAGE_UNITS 1
-#endif
-constexpr int kStageU = MC_STAGE_UNITS;
-static_assert(kStageQuarters % kStageU == 0, "a pass stays inside one tile");
-
-template <int U>
-__device__ __forceinline__ void soa_to_aos_units(const LayoutArgs& a, double* __restrict__ aos) {
-  __shared__ float s[U][4 * kUnitRow];
-  const int64_t n_passes = (int64_t)a.n_tiles * (kStageQuarters / U);
-  const int t = threadIdx.x;
-  const int c = t >> 6, gi = t & 63;
-  for (int64_t it = blockIdx.x; it < n_passes; it += gridDim.x) {
-    const int64_t ps = gridDim.x >= n_passes ? xcd_unit<MC_XCD_STAGE>(it, n_passes) : it;
-    const Tile tl = ldu(a.tiles + ps / (kStageQuarters / U));
-    const int gb = (int)(ps % (kStageQuarters / U)) * U * kQuadGroups;   // first group of the pass
-    if (gb >= tl.ngroups) continue;   // uniform
-    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
-    float4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int g = gb + u * kQuadGroups + gi;
-      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (g < tl.ngroups) v[u] = ld4(a.cols + bidx(a.C, c, tl.pstart + 4 * (int64_t)g));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) *reinterpret_cast<float4*>(&s[u][c * kUnitRow + 4 * gi]) = v[u];
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t p0 = tl.pstart + 4 * (int64_t)(gb + u * kQuadGroups);
-      const int64_t loc0 = p0 - poff;
-      v2d* d = reinterpret_cast<v2d*>(aos + (doff - a.dbase + loc0) * 4);
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int i = t + h2 * kBlock, r = i >> 1, h = i & 1;
-        if (loc0 + r < cnt) {
-          const v2d w = {(double)s[u][(2 * h) * kUnitRow + r], (double)s[u][(2 * h + 1) * kUnitRow + r]};
-          st_pol<MC_STAGE_ST>(reinterpret_cast<float*>(d + i), __builtin_bit_cast(float4, w));
-        }
-      }
-    }
-    __syncthreads();   // s is rewritten by the next pass
-  }
-}
-
 __device__ __forceinline__ void soa_to_aos_unit(const LayoutArgs& a, double* __restrict__ aos) {
-  if constexpr (kStageU > 1) {
-    soa_to_aos_units<kStageU>(a, aos);
-    return;
-  }
   __shared__ float s[4 * kUnitRow];
   const int64_t n_units = (int64_t)a.n_tiles * kStageQuarters;
   const int t = threadIdx.x;
@@ -1945,7 +1596,7 @@ __device__ __forceinline__ void soa_to_aos_unit(const LayoutArgs& a, double* __r
       const int i = t + u * kBlock, r = i >> 1, h = i & 1;
       if (loc0 + r < cnt) {
         const v2d w = {(double)s[(2 * h) * kUnitRow + r], (double)s[(2 * h + 1) * kUnitRow + r]};
-        st_pol<MC_STAGE_ST>(reinterpret_cast<float*>(d + i), __builtin_bit_cast(float4, w));
+        st_pol<kStageSt>(reinterpret_cast<float*>(d + i), __builtin_bit_cast(float4, w));
       }
     }
     __syncthreads();   // s is rewritten by the next unit
@@ -1980,32 +1631,18 @@ __device__ __forceinline__ void aos_to_soa_unit(const LayoutArgs& a, const doubl
     __syncthreads();
     const int c = t >> 6, gi = t & 63;
     if (g0 + gi < tl.ngroups)
-      st_pol<MC_STAGE_ST>(a.cols + bidx(a.C, c, p0 + 4 * gi), *reinterpret_cast<const float4*>(&s[c * kUnitRow + 4 * gi]));
+      st_pol<kStageSt>(a.cols + bidx(a.C, c, p0 + 4 * gi), *reinterpret_cast<const float4*>(&s[c * kUnitRow + 4 * gi]));
     __syncthreads();
   }
 }
 
 // AoS f64 (dense, row stride ld) -> padded SoA f32 (padding slots zeroed)
 __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const double* __restrict__ aos, int64_t ld) {
-#if MC_STAGE_QUAD
   if (ld == 4) {
     aos_to_soa_unit(a, aos);
     return;
   }
-#endif
-#if MC_STAGE_LDS
-  __shared__ float s_t[4][kStageRow];
-  if (ld == 4) {
-    for (int64_t it = blockIdx.x; it < a.n_tiles; it += gridDim.x) {
-      const Tile tl = ldu(a.tiles + (gridDim.x >= a.n_tiles ? xcd_unit<MC_XCD_STAGE>(it, a.n_tiles) : it));
-      const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
-      const int64_t loc0 = tl.pstart - poff;
-      const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
-      stage_tile_lds_in(a, tl, reinterpret_cast<const v2d*>(aos + (doff + loc0) * 4), nv, s_t);
-    }
-    return;
-  }
-#endif
+  // wider rows (ld > 4: extra columns the reference carries along): one point per lane
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
@@ -2013,78 +1650,18 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
     const int np = 4 * tl.ngroups;                                      // padded points in the tile
     const int nv = (int)max<int64_t>(0, min<int64_t>(np, cnt - loc0)); // valid ones
     const double* src = aos + (doff + loc0) * ld;
-    if (ld == 4) {
-      const v2d* s2 = reinterpret_cast<const v2d*>(src);
-      for (int q0 = 0; q0 < 2 * np; q0 += kStageUnroll * kBlock) {
-        v2d v[kStageUnroll];
-#pragma unroll
-        for (int u = 0; u < kStageUnroll; ++u) {
-          const int q = q0 + u * kBlock + threadIdx.x;
-          if (q < 2 * nv) v[u] = __builtin_nontemporal_load(s2 + q);
-          else v[u] = v2d{0.0, 0.0};
-        }
-#pragma unroll
-        for (int u = 0; u < kStageUnroll; ++u) {
-          const int q = q0 + u * kBlock + threadIdx.x;
-          if (q < 2 * np) {
-            const int j = q >> 1, h = q & 1;               // point j, half h: (x,y) or (z,i)
-            a.col(2 * h, tl.pstart + j) = (float)v[u].x;
-            a.col(2 * h + 1, tl.pstart + j) = (float)v[u].y;
-          }
-        }
-      }
-    } else {
-      for (int j = threadIdx.x; j < np; j += kBlock) {
-        float r[4] = {0.f, 0.f, 0.f, 0.f};
-        if (j < nv)
-          for (int c = 0; c < 4; ++c) r[c] = (float)src[(int64_t)j * ld + c];
-        for (int c = 0; c < 4; ++c) a.col(c, tl.pstart + j) = r[c];
-      }
+    for (int j = threadIdx.x; j < np; j += kBlock) {
+      float r[4] = {0.f, 0.f, 0.f, 0.f};
+      if (j < nv)
+        for (int c = 0; c < 4; ++c) r[c] = (float)src[(int64_t)j * ld + c];
+      for (int c = 0; c < 4; ++c) a.col(c, tl.pstart + j) = r[c];
     }
   }
 }
 
 // padded SoA f32 -> dense AoS (N,4) f64  (the (N,4) float64 layout LMC:776 returns)
 __global__ __launch_bounds__(kBlock) void k_soa_to_aos(const LayoutArgs a, double* __restrict__ aos) {
-#if MC_STAGE_QUAD
   soa_to_aos_unit(a, aos);
-  return;
-#endif
-#if MC_STAGE_LDS
-  __shared__ float s_t[4][kStageRow];
-  for (int64_t it = blockIdx.x; it < a.n_tiles; it += gridDim.x) {
-    const Tile tl = ldu(a.tiles + (gridDim.x >= a.n_tiles ? xcd_unit<MC_XCD_STAGE>(it, a.n_tiles) : it));
-    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
-    const int64_t loc0 = tl.pstart - poff;
-    const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
-    stage_tile_lds_out(a, tl, reinterpret_cast<v2d*>(aos + (doff - a.dbase + loc0) * 4), nv, s_t);
-  }
-  return;
-#endif
-  for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-    const Tile tl = ldu(a.tiles + tile);
-    const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
-    const int64_t loc0 = tl.pstart - poff;
-    const int nv = (int)max<int64_t>(0, min<int64_t>(4 * tl.ngroups, cnt - loc0));
-    v2d* d2 = reinterpret_cast<v2d*>(aos + (doff - a.dbase + loc0) * 4);
-    for (int q0 = 0; q0 < 2 * nv; q0 += kStageUnroll * kBlock) {
-      v2d v[kStageUnroll];
-#pragma unroll
-      for (int u = 0; u < kStageUnroll; ++u) {
-        const int q = q0 + u * kBlock + threadIdx.x;
-        if (q < 2 * nv) {
-          const int j = q >> 1, h = q & 1;
-          v[u] = v2d{(double)__builtin_nontemporal_load(&a.col(2 * h, tl.pstart + j)),
-                     (double)__builtin_nontemporal_load(&a.col(2 * h + 1, tl.pstart + j))};
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kStageUnroll; ++u) {
-        const int q = q0 + u * kBlock + threadIdx.x;
-        if (q < 2 * nv) __builtin_nontemporal_store(v[u], d2 + q);
-      }
-    }
-  }
 }
 
 // dense column (N) <-> blocked column c; DIR 0: dense->blocked (padding zeroed), 1: blocked->dense

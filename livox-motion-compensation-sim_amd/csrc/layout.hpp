@@ -41,29 +41,11 @@ __device__ __forceinline__ int i4c(const int4& v, int c) {
 // [|v| >= 10] + [|v| >= 100] + [|v| >= 1000] bytes (a float32 never rounds across a power of ten at
 // six decimals: the float32 below 10 is 9.99999905).  Any value outside the packed path (NaN, inf,
 // |v| >= 4294) adds kPcdSlowValue: a block whose count reaches it holds a line for the exact
-// formatter (the measure pass).  Two ways to a wave total (MC_PCD_COUNT):
-//   0  per-lane sums (compares + adds), one wave reduction at the end
-//   1  one ballot per term (the i1 builtin: the compare writes its lane mask straight to an SGPR
-//      pair), population counts added up on the scalar unit, no reduction
-#ifndef MC_PCD_COUNT
-#define MC_PCD_COUNT 0
-#endif
+// formatter (the measure pass).  Per-lane sums (compares + adds) with one wave reduction at the end:
+// a ballot per term added up on the scalar unit was slower (+15 / +36 / +47 us: the 64-bit masks
+// spilled SGPRs into VGPR lanes, profiles/round3/s12).
 constexpr int kPcdSlowValue = 1 << 20;
 struct PcdCount {
-#if MC_PCD_COUNT
-  int n = 0;          // wave total
-  uint64_t slow = 0;
-  __device__ __forceinline__ void add(uint64_t valid, float v) {
-    const float a = fabsf(v);
-    n += 9 * __popcll(valid) + __popcll(valid & __builtin_amdgcn_ballot_w64(__float_as_int(v) < 0)) +
-         __popcll(valid & __builtin_amdgcn_ballot_w64(a >= 10.0f)) +
-         __popcll(valid & __builtin_amdgcn_ballot_w64(a >= 100.0f)) +
-         __popcll(valid & __builtin_amdgcn_ballot_w64(a >= 1000.0f));
-    slow |= valid & __builtin_amdgcn_ballot_w64(!(a < 4294.0f));
-  }
-  __device__ __forceinline__ static uint64_t lanes(bool valid) { return __builtin_amdgcn_ballot_w64(valid); }
-  __device__ __forceinline__ int bytes() const { return n + (slow ? kPcdSlowValue : 0); }
-#else
   int n = 0;          // this lane's sum
   uint32_t amax = 0;  // largest |v| bit pattern of the lane's valid values (NaN / inf above any finite)
   __device__ __forceinline__ void add(bool valid, float v) {
@@ -81,7 +63,6 @@ struct PcdCount {
     const bool slow = __builtin_amdgcn_ballot_w64(amax >= 0x45863000u) != 0;   // |v| >= 4294.0f
     return t + (slow ? kPcdSlowValue : 0);
   }
-#endif
 };
 
 // DPP quad exchange (quad_perm): lanes 4q .. 4q + 3 of a wave form a quad.

@@ -46,14 +46,10 @@ static int launch_grid(const mc_ctx* c, int32_t n_tiles) {
 
 static_assert(mcimpl::kBatchBlock == kBlkPts && mcplan::kBlk == kBlkPts, "batch block size");
 
-// workgroups of a stager launch over n_tiles tiles (the quad stager: 64-group units; ld: AoS columns)
-static int32_t stage_units(int32_t n_tiles, int64_t ld) {
-  return (MC_STAGE_QUAD && ld == 4) ? n_tiles * kStageQuarters : n_tiles;
-}
-// ... of the SoA -> AoS launch (kStageU units per workgroup pass)
-static int32_t fetch_units(int32_t n_tiles) {
-  return MC_STAGE_QUAD ? n_tiles * (kStageQuarters / kStageU) : n_tiles;
-}
+// workgroups of a stager launch over n_tiles tiles (256-point units; ld: AoS columns)
+static int32_t stage_units(int32_t n_tiles, int64_t ld) { return ld == 4 ? n_tiles * kStageQuarters : n_tiles; }
+// ... of the SoA -> AoS launch
+static int32_t fetch_units(int32_t n_tiles) { return n_tiles * kStageQuarters; }
 static_assert(sizeof(mcplan::TileRec) == sizeof(Tile) && offsetof(mcplan::TileRec, frame) == offsetof(Tile, frame) &&
                   offsetof(mcplan::TileRec, ngroups) == offsetof(Tile, ngroups),
               "host tile records are uploaded as mc::Tile");
@@ -296,10 +292,6 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
     if ((r = dev_alloc(&b->d_ftile, F + 1))) return bail(r);
     if ((r = dev_alloc(&b->d_strange, n_sub))) return bail(r);
     if ((r = dev_alloc(&b->d_swin, 2 * n_sub))) return bail(r);
-    if (!MC_IMU_SEGREC) {   // per-sub-tile IMU records (with MC_IMU_SEGREC the kernel reads the segment table)
-      b->srec_half = 2 * n_sub * std::max(sizeof(PoseWin), sizeof(ImuSeg));
-      if ((r = dev_alloc(reinterpret_cast<char**>(&b->d_srec), 2 * b->srec_half))) return bail(r);
-    }
   }
   if ((r = dev_alloc(&b->d_partial, 5 * (size_t)b->n_tiles))) return bail(r);
   hipStream_t s = c->stream;
@@ -380,7 +372,7 @@ int mc_batch_set_frame_start_ns(mc_batch* b, const int64_t* s) {
 }
 
 // Work this context queues on its stream and leaves running when the call returns must keep the next
-// mc_deskew's prep from being issued any-order (MC_PREP_ISSUE 2): that prep may only overtake this
+// mc_deskew's prep from being issued any-order: that prep may only overtake this
 // context's own deskew kernel.  Every API that returns with work in flight calls this.
 static inline void queued_async(mc_ctx* c) { c->prep_fence = true; }
 
@@ -599,33 +591,16 @@ int mc_batch_checksum(mc_batch* b, double* sums) {
 }
 
 // ---- the hot path ---------------------------------------------------------------------------
-// How mc_deskew issues a step's k_prep (tools/anyorder_probe.hip, tools/ab.py):
-//   0  on the side stream one step ahead, ordered by cross-queue events (round 1: ~7-10 us per step)
-//   1  on the main stream right before its kernel (serial; rejected in round 1: step wall +2 to +6 us)
-//   2  on the main stream as an any-order packet (hipExtAnyOrderLaunch: AQL barrier bit clear) right
-//      behind the previous step's deskew kernel, so it runs beside that kernel's tail without a
-//      second queue; the deskew kernel after it is an ordinary packet and waits for both
-#ifndef MC_PREP_ISSUE
-#define MC_PREP_ISSUE 2
-#endif
-#ifndef MC_SPEC_PREP
-#define MC_SPEC_PREP 1       // per-call speculation of the next identical call's prep (mc_ctx::PrepKey)
-#endif
-// Whether a mode's steps carry the next step's prep in their own launch (k_deskew_points<MODE, true>
-// / k_deskew_frame_next; mc_deskew's speculation and mc_deskew_steps' pipeline).  MC_FUSE_SLERP=0
-// issues SLERP's prep as an any-order packet before the plain kernel instead: the round-3 float64 prep
-// spilled the fused kernel to scratch (345.1 vs 317.2 us, profiles/round3/s15); with the slimmed
-// prep (78 VGPRs, no scratch) the fused launch is ahead again, step wall 320.2-328.3 vs 329.5-329.6 us
-// (profiles/round3/s19/ab_fuse.log); in the final tree's bench, step 317.5-320.8 vs 324.9-325.5 us
-// (profiles/round3/s64).
-#ifndef MC_FUSE_SLERP
-#define MC_FUSE_SLERP 1
-#endif
-#ifndef MC_DIAG_NO_PREP
-#define MC_DIAG_NO_PREP 0    // diagnostic timing build: after 4 calls, no k_prep (tables of earlier calls)
-#endif
+// How mc_deskew issues a step's k_prep (tools/anyorder_probe.hip, tools/ab.py): on the main stream as
+// an any-order packet (hipExtAnyOrderLaunch: AQL barrier bit clear) right behind the previous step's
+// deskew kernel, so it runs beside that kernel's tail without a second queue; the deskew kernel after
+// it is an ordinary packet and waits for both.  (Rejected in rounds 1-2: the prep on a side stream one
+// step ahead with cross-queue events, ~7-10 us per step; serial on the main stream, +2 to +6 us.)
+// Identical consecutive calls are speculated (mc_ctx::PrepKey): a call's launch also runs the next
+// identical call's prep in its first workgroups (k_deskew_points<MODE, true> / k_deskew_frame_next,
+// the same fused launch mc_deskew_steps' pipeline issues; for SLERP step wall 320.2-328.3 vs
+// 329.5-329.6 us with the prep as a separate packet, profiles/round3/s19).
 namespace {
-bool fuse_next(int mode) { return mode != MC_MODE_POSE_SLERP || MC_FUSE_SLERP; }
 
 // Table halves written outside mc_deskew's key bookkeeping: no speculated tables stay valid, and the
 // next mc_deskew does not speculate from a key seen before this call.
@@ -668,31 +643,16 @@ struct StepPlan {
   uint32_t prep_blocks;
   uint32_t grid;
   int32_t kernel;   // -1: no deskew launch (no tiles); else the mode
-  uint32_t lds;     // dynamic LDS reserved by the per-point launches (an occupancy cap; 0: none)
 };
 
 constexpr int64_t kSlerpXcdMinPoints = 200000000;
-#ifndef MC_SLERP_ALT
-#define MC_SLERP_ALT 0       // experiment (with MC_XCD_SLERP=0): odd table halves = odd steps take the XCD order
-#endif
 
-// Diagnostic occupancy cap for the per-point kernels: $MCDESKEW_POINTS_LDS bytes of dynamic LDS
-// per workgroup (160 KB per CU), read once.
-static uint32_t points_lds_reserve() {
-  static const uint32_t v = [] {
-    const char* e = std::getenv("MCDESKEW_POINTS_LDS");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
-  }();
-  return v;
-}
-
-// sub-tile order of a mode's kernel without a tuned choice: XCD-contiguous for the frame and IMU
-// kernels (rounds 1-2), and for SLERP since round 3 (MC_XCD_SLERP; a MC_XCD_SLERP=0 build keeps the
-// round-2 rule: dealt below kSlerpXcdMinPoints)
-int32_t default_order(int mode, int64_t P, int h) {
+// sub-tile order of a mode's kernel without a tuned choice (MC_XCD_*, kernels.hpp): XCD-contiguous
+// for the frame kernel; dealt for IMU and for SLERP below kSlerpXcdMinPoints padded points
+int32_t default_order(int mode, int64_t P) {
   if (mode == MC_MODE_FRAME) return MC_XCD_FRAME;
   if (mode == MC_MODE_IMU) return MC_XCD_IMU;
-  return (MC_XCD_SLERP || P >= kSlerpXcdMinPoints || (MC_SLERP_ALT && h == 1)) ? 1 : 0;
+  return (MC_XCD_SLERP || P >= kSlerpXcdMinPoints) ? 1 : 0;
 }
 
 void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int h, StepPlan* sp) {
@@ -742,20 +702,16 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (mode == MC_MODE_IMU) { da.nseg = c->M; da.ntab = c->M; }
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
-  int32_t units = mode == MC_MODE_FRAME && !MC_FRAME_SUB ? in->n_tiles : in->n_tiles * kSub;
-  if (mode != MC_MODE_FRAME && ((MC_POINTS_PAIR >> mode) & 1)) units = in->n_tiles;   // a workgroup per tile (both sub-tiles)
-  if (mode == MC_MODE_FRAME && MC_FRAME_QUAD) units = in->n_tiles * kSub * kQuadUnitsPerSub;
+  int32_t units = in->n_tiles * kSub;
+  if (mode == MC_MODE_FRAME) units = in->n_tiles * kSub * kQuadUnitsPerSub;   // the quad decomposition
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
   // sub-tile order: default_order, or mc_tune_order's measured choice
-  da.xcd_order = default_order(mode, in->P, h);
+  da.xcd_order = default_order(mode, in->P);
   // a device-measured choice for this mode and batch size (mc_tune_order) overrides the default
   const mc_ctx::OrderTune& ot = c->order_tune[mode];
   if (ot.order >= 0 && ot.P == in->P) da.xcd_order = ot.order;
-  // the prep writes the sub-tile windows in the layout this order reads them in
   pa.n_sub = (int64_t)in->n_tiles * kSub;
-  pa.swin_perm = da.xcd_order == 0 ? 1 : 0;
-  sp->lds = mode == MC_MODE_FRAME ? 0u : points_lds_reserve();
 }
 
 // Launches with optional hipExtLaunchKernel timing events (e0/e1 null: untimed) and AQL flags.
@@ -771,20 +727,20 @@ void launch_main(const StepPlan& sp, hipStream_t s, hipEvent_t e0 = nullptr, hip
   if (sp.da.pcd_len) {   // mc_deskew_pcd (never graph-captured)
     if (sp.kernel == MC_MODE_FRAME) hipExtLaunchKernelGGL(k_deskew_frame_pcd, grid, block, 0, s, e0, e1, 0u, sp.da);
     else if (sp.kernel == MC_MODE_POSE_SLERP)
-      hipExtLaunchKernelGGL((k_deskew_points<1, false, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
-    else hipExtLaunchKernelGGL((k_deskew_points<2, false, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+      hipExtLaunchKernelGGL((k_deskew_points<1, false, true>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+    else hipExtLaunchKernelGGL((k_deskew_points<2, false, true>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
     return;
   }
   if (!e0) {
     if (sp.kernel == MC_MODE_FRAME) hipLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, sp.da);
-    else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, sp.lds, s, sp.da, sp.pa, 0u);
-    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, sp.lds, s, sp.da, sp.pa, 0u);
+    else if (sp.kernel == MC_MODE_POSE_SLERP) hipLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, sp.da, sp.pa, 0u);
+    else hipLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, sp.da, sp.pa, 0u);
     return;
   }
   if (sp.kernel == MC_MODE_FRAME) hipExtLaunchKernelGGL(k_deskew_frame, grid, block, 0, s, e0, e1, 0u, sp.da);
   else if (sp.kernel == MC_MODE_POSE_SLERP)
-    hipExtLaunchKernelGGL((k_deskew_points<1>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
-  else hipExtLaunchKernelGGL((k_deskew_points<2>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+    hipExtLaunchKernelGGL((k_deskew_points<1>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
+  else hipExtLaunchKernelGGL((k_deskew_points<2>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
 }
 
 // This step's deskew (sp) with the NEXT step's prep (nx) in the first workgroups of the same launch
@@ -796,8 +752,8 @@ void launch_fused(const StepPlan& sp, const StepPlan& nx, hipStream_t s, hipEven
   if (sp.kernel == MC_MODE_FRAME)
     hipExtLaunchKernelGGL(k_deskew_frame_next, grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
   else if (sp.kernel == MC_MODE_POSE_SLERP)
-    hipExtLaunchKernelGGL((k_deskew_points<1, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, nx.pa, pre);
-  else hipExtLaunchKernelGGL((k_deskew_points<2, true>), grid, block, sp.lds, s, e0, e1, 0u, sp.da, nx.pa, pre);
+    hipExtLaunchKernelGGL((k_deskew_points<1, true>), grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
+  else hipExtLaunchKernelGGL((k_deskew_points<2, true>), grid, block, 0, s, e0, e1, 0u, sp.da, nx.pa, pre);
 }
 
 // frame time spans derived lazily from t_ns (queued on the main stream)
@@ -817,15 +773,10 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
   if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
   if (in->F == 0) return MC_OK;
   DeviceGuard g(c->device);
-  hipStream_t s = c->stream, sd = c->side;
-  (void)sd;
+  hipStream_t s = c->stream;
   if (mode != MC_MODE_FRAME && !in->trange_valid) {
     // the spans are queued on the main stream: order the prep after them
     if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
-#if MC_PREP_ISSUE == 0
-    HIPCHK(hipEventRecord(c->ev_order, s));
-    HIPCHK(hipStreamWaitEvent(sd, c->ev_order, 0));
-#endif
     c->prep_fence = true;
   }
   // Per-step tables come in two halves: this step's prep writes half h, which the deskew kernel
@@ -838,35 +789,16 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
   // a per-point deskew that carries t_ns into another batch rewrites that batch's time column:
   // its cached [min, max] spans no longer describe it
   if (sp.kernel >= 0 && sp.da.copy_t) out->trange_valid = false;
-#if MC_PREP_ISSUE == 0
-  // the prep on the side stream as soon as the kernel that last read half h has finished, i.e.
-  // concurrently with the previous call's kernel; the kernel waits for its own prep
-  c->spec_valid = false;
-  HIPCHK(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
-  {
-    TimedRegion tr(c, &c->prep_ev, sd);
-    launch_prep(sp, sd);
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev_prep_done[h], sd));
-  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
-  if (sp.kernel >= 0) {
-    TimedRegion tr(c, &c->main_ev, s);
-    launch_main(sp, s);
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev_main_done[h], s));
-#else
   // Speculation (see mc_ctx::PrepKey): h is the half the previous call's launch prepared for this
   // key, if it did; then this call needs no k_prep at all.
   const mc_ctx::PrepKey key{in->uid, c->traj_ver, c->imu_ver, in->prep_ver, mode, pose_select};
-  const bool hit = MC_SPEC_PREP && c->spec_valid && c->spec_half == h && c->spec_key == key;
+  const bool hit = c->spec_valid && c->spec_half == h && c->spec_key == key;
   // (the fused next-call launch has no PCD variant: a PCD call never speculates, it may hit)
-  const bool speculate = MC_SPEC_PREP && sp.kernel >= 0 && c->last_call == key && !pcd_len && fuse_next(mode);
+  const bool speculate = sp.kernel >= 0 && c->last_call == key && !pcd_len;
   c->last_call = key;
   c->spec_valid = false;
   if (!hit) {
-    // One queue.  Any-order prep (MC_PREP_ISSUE 2) only right behind this context's own deskew
+    // One queue.  Any-order prep only right behind this context's own deskew
     // kernel (prep_fence clear): the packets before it are then that kernel — still reading the
     // other half — and, before it, work the kernel's barrier already waited for.  Everything else
     // that could precede it either finished before its API call returned (trajectory / IMU / frame
@@ -874,11 +806,7 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
     // a speculative launch whose prep workgroups write this very half).  The deskew kernel's own
     // packet keeps the barrier bit, so it waits for this prep, and anything queued after it waits
     // for both.  With no kernel to follow (no tiles) the prep is ordinary.
-    const unsigned fl = (MC_PREP_ISSUE == 2 && !c->prep_fence && sp.kernel >= 0) ? hipExtAnyOrderLaunch : 0u;
-#if MC_DIAG_NO_PREP
-    static int diag_calls = 0;
-    if (++diag_calls <= 4)
-#endif
+    const unsigned fl = (!c->prep_fence && sp.kernel >= 0) ? hipExtAnyOrderLaunch : 0u;
     {
       LaunchEvents ev(c);
       launch_prep(sp, s, ev.e0, ev.e1, fl);
@@ -910,7 +838,6 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
   // No event records here: a marker packet between this kernel and the next step's any-order prep
   // would hold that prep until this kernel completes.  Everything is on one queue, so the stream
   // order is the only ordering the halves need (a graph replay forks its prep branch from s).
-#endif
   return MC_OK;
 }
 
@@ -985,23 +912,22 @@ int build_step_graph(mc_ctx* c, const StepPlan* plan, int32_t n_steps, int32_t e
 
 namespace {
 // The launches of n steps over the two table halves of `plan` (step i reads half i & 1 of plan):
-// fused modes (fuse_next) issue step 0's k_prep, then n deskew launches of which the first n - 1
-// carry the next step's prep; SLERP issues per step an any-order k_prep packet and the plain kernel.
+// step 0's k_prep, then n deskew launches of which the first n - 1 carry the next step's prep.
 // Every `every`-th step's kernel (and prep) is timed.
 void issue_steps(mc_ctx* c, const StepPlan* plan, int mode, int32_t n_steps, int32_t every) {
   hipStream_t s = c->stream;
-  const bool fuse = fuse_next(mode);
+  (void)mode;
   auto sampled = [&](int32_t i) { return every > 0 && i % every == every / 2; };
   for (int32_t i = 0; i < n_steps; ++i) {
-    if (i == 0 || !fuse) {
+    if (i == 0) {
       // any-order right behind this context's own deskew kernel, as in mc_deskew
-      const bool ao = MC_PREP_ISSUE == 2 && (i > 0 || !c->prep_fence);
+      const bool ao = !c->prep_fence;
       LaunchEvents ev(c, sampled(i));
       launch_prep(plan[i & 1], s, ev.e0, ev.e1, ao ? hipExtAnyOrderLaunch : 0u);
       ev.keep(&c->prep_ev);
     }
     LaunchEvents ev(c, sampled(i));
-    if (fuse && i + 1 < n_steps) launch_fused(plan[i & 1], plan[(i + 1) & 1], s, ev.e0, ev.e1);
+    if (i + 1 < n_steps) launch_fused(plan[i & 1], plan[(i + 1) & 1], s, ev.e0, ev.e1);
     else launch_main(plan[i & 1], s, ev.e0, ev.e1);
     ev.keep(&c->main_ev);
   }
@@ -1051,7 +977,7 @@ int mc_tune_order(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int po
   hipStream_t s = c->stream;
   if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
   forget_speculation(c);
-  // the candidates run as the steps of mc_deskew_steps do (issue_steps: prep packets or fused launches)
+  // the candidates run as the steps of mc_deskew_steps do (issue_steps: fused next-step launches)
   const int h0 = c->buf;
   StepPlan plan[2];
   deskew_plan(c, in, out, mode, pose_select, h0, &plan[0]);
@@ -1069,6 +995,9 @@ int mc_tune_order(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int po
     for (int k = 0; k < 2 && e == hipSuccess; ++k) {
       const int cand = (r & 1) ? 1 - k : k;
       plan[0].da.xcd_order = plan[1].da.xcd_order = cand;
+      // the previous round's last launch may read either half (odd `launches`): the warm-up's first
+      // prep is an ordinary packet, so it waits for that launch
+      c->prep_fence = true;
       issue_steps(c, plan, mode, 2, 0);   // untimed: this order's own steady state
       c->prep_fence = false;
       e = hipEventRecord(e0, s);
@@ -1367,9 +1296,6 @@ int mc_transform_affine(mc_ctx* c, const mc_batch* in, mc_batch* out, int32_t n_
     for (int r = 0; r < 3; ++r) tbl[3 * (size_t)f + r] = FrameRow{m[4 * r], m[4 * r + 1], m[4 * r + 2], m[4 * r + 3]};
   }
   FrameRow* frame_tbl = in->d_frame_tbl + 3 * (size_t)in->F * h;
-#if MC_PREP_ISSUE == 0
-  HIPCHK(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));   // the side-stream prep that last wrote half h
-#endif
   queued_async(c);
   HIPCHK(hipMemcpyAsync(frame_tbl, tbl.data(), tbl.size() * sizeof(FrameRow), hipMemcpyHostToDevice, s));
   if (in->n_tiles > 0) {

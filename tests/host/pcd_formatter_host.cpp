@@ -1,9 +1,10 @@
-// Host build of the device "%.6f" line writers in livox-motion-compensation-sim_amd/csrc/codecs.hpp
+// Host build of the device "%.6f" line writer in livox-motion-compensation-sim_amd/csrc/codecs.hpp
 // (the section from `struct PcdFast` to `kPcdSlowTile`, spliced in by tests/test_pcd_formatter_host.py
 // at FORMATTER_SECTION) with host stand-ins for the gfx950 intrinsics it uses.  Every line of a
-// 256-line tile is written in reverse lane order into a zeroed buffer at a tile offset modulo 16,
-// as the kernel's lanes may interleave, and the text is compared with the C library's correctly
-// rounded "%.6f" (the same digits as Python's formatting).  Exit status = number of bad tiles.
+// 256-line tile is written in reverse lane order into a buffer filled with a marker byte, at a tile
+// offset modulo 16, as the kernel's lanes may interleave; the text is compared with the C library's
+// correctly rounded "%.6f" (the same digits as Python's formatting) and no byte outside the text may
+// change.  Exit status = number of bad tiles.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -19,22 +20,6 @@
 #define __ATOMIC_RELAXED 0
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
 static inline uint32_t __umul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
-static inline uint32_t __hip_atomic_fetch_or(uint32_t* p, uint32_t v, int, int) { const uint32_t o = *p; *p |= v; return o; }
-// v_perm_b32: byte i of the result = byte sel[i] of {s0:s1} (0-3 = s1, 4-7 = s0), 12 -> 0x00
-static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
-  const uint64_t v = ((uint64_t)s0 << 32) | s1;
-  uint32_t r = 0;
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t c = (sel >> (8 * i)) & 0xffu;
-    const uint32_t b = c < 8 ? (uint32_t)(v >> (8 * c)) & 0xffu : (c == 12 ? 0u : 0xffu);
-    r |= b << (8 * i);
-  }
-  return r;
-}
-// v_alignbyte_b32: ({hi:lo} >> 8 * (k & 3))[31:0]
-static inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t k) {
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (k & 3)));
-}
 using std::fma;
 using std::signbit;
 using std::rint;
@@ -50,6 +35,7 @@ using namespace mc;
 
 int main(int argc, char** argv) {
   const int N = argc > 1 ? std::atoi(argv[1]) : 300000;
+  int bad = 0;
   std::mt19937_64 g(1);
   std::uniform_real_distribution<double> U(-90, 90);
   std::vector<double> pts(4 * (size_t)N);
@@ -66,7 +52,13 @@ int main(int argc, char** argv) {
   }
   const CodecFrames s{pts.data()};
   std::vector<uint32_t> buf(16400 / 4 + 4);
-  int bad = 0;
+  uint16_t tbl[kPcdPairs];
+  for (uint32_t i = 0; i < (uint32_t)kPcdPairs; ++i) tbl[i] = pcd_pair_entry(i);
+  // the multiply-shift divisions of pair_fields on their whole ranges
+  for (uint32_t fp = 0; fp < 1000000u; ++fp)
+    if ((uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32) != fp / 10000u) { ++bad; break; }
+  for (uint32_t x = 0; x < 10000u; ++x)
+    if ((__umul24(x, 5243u) >> 19) != x / 100u) { ++bad; break; }
   long lines = 0, fast = 0, f32_lines = 0;
   // every float32 in [0, 4294] at a stride, and every float32 within 4096 ulps of each digit-count
   // threshold (10, 100, 1000) and of 4294: the float32 path's N and length equal the float64 path's
@@ -95,11 +87,7 @@ int main(int argc, char** argv) {
     check(INFINITY);
   }
   for (int t = 0; t < N / 256; ++t) {
-#if MC_PCD_BYTES
-    std::memset(buf.data(), 0xA5, buf.size() * 4);   // the byte writer must not rely on zeros
-#else
-    std::memset(buf.data(), 0, buf.size() * 4);
-#endif
+    std::memset(buf.data(), 0xA5, buf.size() * 4);   // the writer must not rely on zeros
     const int shift = t % 16;
     int off = shift;
     std::string want;
@@ -139,17 +127,8 @@ int main(int argc, char** argv) {
       want += line;
     }
     for (int l = 255; l >= 0; --l)
-      if (P[l].ok) {
-#if MC_PCD_BYTES
-        pcd_emit_bytes(P[l], reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
-#elif MC_PCD_SWAR
-        pcd_emit_swar(P[l], buf.data(), offs[l]);
-#else
-        pcd_emit_fast(P[l], buf.data(), offs[l]);
-#endif
-      }
+      if (P[l].ok) pcd_emit_pairs(P[l], tbl, reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
     const std::string got(reinterpret_cast<const char*>(buf.data()) + shift, off - shift);
-#if MC_PCD_BYTES
     // nothing written outside the tile's text
     const unsigned char* bb = reinterpret_cast<const unsigned char*>(buf.data());
     for (size_t i = 0; i < buf.size() * 4; ++i)
@@ -158,7 +137,6 @@ int main(int argc, char** argv) {
         std::printf("tile %d: byte %zu outside the text [%d, %d) was written\n", t, i, shift, off);
         break;
       }
-#endif
     if (got != want) {
       ++bad;
       size_t i = 0;

@@ -42,7 +42,7 @@ def test_pcd_formatter_under_asan_ubsan(tmp_path):
     cpp = tmp_path / "fmt.cpp"
     cpp.write_text(code)
     exe = tmp_path / "fmt"
-    subprocess.run(["g++", *SAN, "-DMC_PCD_SWAR=1", "-DMC_PCD_DIAG=0", str(cpp), "-o", str(exe)],
+    subprocess.run(["g++", *SAN, str(cpp), "-o", str(exe)],
                    check=True, capture_output=True, text=True)
     r = subprocess.run([str(exe), "50000"], capture_output=True, text=True, timeout=300, env=ENV)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])

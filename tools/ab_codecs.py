@@ -2,7 +2,7 @@
 process, one device (GPU box only).  Each arm encodes the same device (N,4) f64 cloud; outputs of
 every arm are checked byte-identical to the first arm's.
 
-    make -C livox-motion-compensation-sim_amd/csrc variants VARIANTS="a:-DMC_KITERS=2 b:-DMC_XCD_CODEC=0"
+    make -C livox-motion-compensation-sim_amd/csrc variants VARIANTS="a:-DMC_XCD_CODEC=1 b:-DMC_XCD_CODEC=0"
     python tools/ab_codecs.py --libs build/variants/lib_a.so,build/variants/lib_b.so
 """
 from __future__ import annotations

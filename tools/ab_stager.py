@@ -1,7 +1,7 @@
 """Interleaved A/B of the device stager pair (SoA f32 <-> AoS f64) across library variants, one
 process, one device (GPU box only).  Also checks that every variant's round trip is bit-identical.
 
-    make -C livox-motion-compensation-sim_amd/csrc variants VARIANTS="base:-DMC_KITERS=2 lds:-DMC_STAGE_LDS=1"
+    make -C livox-motion-compensation-sim_amd/csrc variants VARIANTS="xcd:-DMC_XCD_STAGE=1 dealt:-DMC_XCD_STAGE=0"
     python tools/ab_stager.py --libs build/variants/lib_base.so,build/variants/lib_lds.so
 """
 from __future__ import annotations
