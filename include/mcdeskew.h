@@ -21,7 +21,9 @@
  *                                                              MC_POSE_SEARCHSORTED)
  *   save_results merge (np.vstack)             LMC:887-889     blocked-CSR batch layout;
  *                                                              mc_comm_gather_batch (multi-GPU)
- *   MotionCompensator.compensate_point_cloud   CSIM:1435-1480  mc_set_imu + mc_deskew(MC_MODE_IMU)
+ *   MotionCompensator.compensate_point_cloud   CSIM:1435-1480  mc_set_imu + mc_deskew_points_f64(MC_MODE_IMU)
+ *                                                              (host float64 rows), or mc_deskew(MC_MODE_IMU)
+ *                                                              on a device batch
  *     _interpolate_imu_data                    CSIM:1482-1516    (per-point gyro LERP in-kernel)
  *     _create_rotation_matrix                  CSIM:1518-1536    (R_xyz(theta)^T in-kernel)
  *   (build-added)                          mc_deskew(MC_MODE_POSE_SLERP)
@@ -238,6 +240,18 @@ int mc_deskew_steps(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, in
  * the latency path for the reference's one-frame-per-call use).  ld < 4 -> MC_ERR_INDEX. */
 int mc_transform_pointcloud_f64(mc_ctx* ctx, const double* points, int64_t n, int64_t ld, const double* rpy,
                                 const double* translation, double* out);
+
+/* The per-point modes on the reference's own float64 data (no float32 staging): MotionCompensator.
+ * compensate_point_cloud / apply_motion_compensation (CSIM:1435-1480, 2086-2105) for MC_MODE_IMU,
+ * the per-point SLERP deskew for MC_MODE_POSE_SLERP.  points (N, ld >= 3) float64 rows, frames back
+ * to back (counts[f] rows each); t_ns (N,) int64 = each point's time minus its frame's start (any
+ * int64: no int32 limit here); frame_times[F] (s, SLERP: t = frame_times[f] + t_ns * 1e-9) or
+ * frame_start_ns[F] (IMU: the point's timestamp = frame_start_ns[f] + t_ns, CSIM:1447, 1454).  out
+ * (N, 4) float64 = x', y', z' computed in float64 end to end, column 3 = points[:, 3] (0 when ld == 3).
+ * Pose / IMU tables from mc_set_trajectory / mc_set_imu.  ld < 3 -> MC_ERR_INDEX.  Synchronous. */
+int mc_deskew_points_f64(mc_ctx* ctx, int mode, int32_t n_frames, const int64_t* counts, const double* points,
+                         int64_t ld, const int64_t* t_ns, const double* frame_times, const int64_t* frame_start_ns,
+                         double* out);
 
 /* The frame loop (LMC:802-832) on host arrays: frames[f] (counts[f], lds[f] >= 4) float64 rows
  * -> outs[f] (counts[f], 4) float64, pose per frame from the uploaded trajectory (pose_select as

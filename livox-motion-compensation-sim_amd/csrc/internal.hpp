@@ -166,6 +166,12 @@ struct mc_ctx {
   // mc_deskew_pcd: ASCII PCD text bytes per 256-point output block, written by the deskew kernel
   int32_t* d_pcd_len = nullptr;
   int64_t pcd_len_cap = 0;
+  // segment table of the float64 per-point path (mc_deskew_points_f64): built by k_prep for one mode
+  // and the trajectory / IMU upload it came from (seg64_ver), rebuilt when either changes
+  void* d_seg64 = nullptr;
+  size_t seg64_bytes = 0;
+  int seg64_mode = -1;
+  uint64_t seg64_ver = 0;
   // pinned, device-mapped host buffer of the single-call drop-in path
   void* h_pin = nullptr;
   size_t pin_bytes = 0;

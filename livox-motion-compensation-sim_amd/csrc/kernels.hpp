@@ -1145,12 +1145,11 @@ __device__ __forceinline__ void sincos_tier(const P& poly, double x, double& s, 
   }
 }
 
-// quaternion SLERP + position LERP at the point's time, then p' = R(q) p + pos.
-// The time is formed as the reference forms it, t_frame + t_ns * 1e-9 (no contraction), and alpha
-// as the oracle's (t - t_k) / dt; TIER bounds alpha * Theta.
-template <typename P>
-__device__ __forceinline__ void slerp_point(const PoseWin& w, const P& poly, int t, float& x, float& y, float& z) {
-  const double tq = __dadd_rn(w.tf, __dmul_rn((double)t, 1e-9));
+// quaternion SLERP + position LERP at the point's time tq, then p' = R(q) p + pos;
+// alpha as the oracle's (t - t_k) / dt; the tier bounds alpha * Theta.  V: float (the batch's
+// columns, one rounding per output coordinate on the store) or double (host float64 rows).
+template <typename P, typename V>
+__device__ __forceinline__ void slerp_core(const PoseWin& w, const P& poly, double tq, V& x, V& y, V& z) {
   double al = (tq - w.t0) * w.inv_dt;
   al = fmin(fmax(al, 0.0), 1.0);
   double cs, sc;
@@ -1169,19 +1168,23 @@ __device__ __forceinline__ void slerp_point(const PoseWin& w, const P& poly, int
   const double cy = fma(qw, ty, fma(qz, tx, -qx * tz));
   const double cz = fma(qw, tz, fma(qx, ty, -qy * tx));
   // (p + alpha dp) + p0 + 2c: one SGPR operand per instruction (no copies of the record into VGPRs)
-  x = (float)fma(2.0, cx, fma(al, w.dp[0], X) + w.p0[0]);
-  y = (float)fma(2.0, cy, fma(al, w.dp[1], Y) + w.p0[1]);
-  z = (float)fma(2.0, cz, fma(al, w.dp[2], Z) + w.p0[2]);
+  x = (V)fma(2.0, cx, fma(al, w.dp[0], X) + w.p0[0]);
+  y = (V)fma(2.0, cy, fma(al, w.dp[1], Y) + w.p0[1]);
+  z = (V)fma(2.0, cz, fma(al, w.dp[2], Z) + w.p0[2]);
+}
+// the time formed as the reference forms it, t_frame + t_ns * 1e-9 (no contraction)
+__device__ __forceinline__ double slerp_time(double tf, double t_ns) { return __dadd_rn(tf, __dmul_rn(t_ns, 1e-9)); }
+template <typename P>
+__device__ __forceinline__ void slerp_point(const PoseWin& w, const P& poly, int t, float& x, float& y, float& z) {
+  slerp_core(w, poly, slerp_time(w.tf, (double)t), x, y, z);
 }
 
 // Path B body (CSIM:1447-1465): w = g + alpha*dg (alpha from the bracketing IMU samples, CSIM:1504-
-// 1511), theta = w * dt, dt = t_ns * 1e-9 (CSIM:1454), p' = Rx(-theta_x) Ry(-theta_y) Rz(-theta_z) p
-// (CSIM:1518-1536).  tsd = (double)w.ts: t - ts is exact in float64 (both integers below 2^53).
-template <typename P>
-__device__ __forceinline__ void imu_point(const ImuSeg& w, const P& poly, double tsd, int t, float& x, float& y,
-                                          float& z) {
-  const double td = (double)t;
-  double al = (td - tsd) * w.inv_dt;
+// 1511), theta = w * dt, dt = (t - frame start) * 1e-9 (CSIM:1454), p' = Rx(-theta_x) Ry(-theta_y)
+// Rz(-theta_z) p (CSIM:1518-1536).  dts = t - ts of the record (exact), td = t - frame start (ns).
+template <typename P, typename V>
+__device__ __forceinline__ void imu_core(const ImuSeg& w, const P& poly, double dts, double td, V& x, V& y, V& z) {
+  double al = dts * w.inv_dt;
   al = al > 0.0 ? al : 0.0;
   const double dt = td * 1e-9;
   double sa, ca, sb, cb, sc, cc;
@@ -1198,7 +1201,15 @@ __device__ __forceinline__ void imu_point(const ImuSeg& w, const P& poly, double
   // Rx(-a)
   const double y3 = fma(ca, y1, sa * z2);
   const double z3 = fma(-sa, y1, ca * z2);
-  x = (float)x2; y = (float)y3; z = (float)z3;
+  x = (V)x2; y = (V)y3; z = (V)z3;
+}
+// batch form: t = frame-relative int32 ns, tsd = (double)w.ts (frame-relative): t - ts is exact in
+// float64 (both integers below 2^53)
+template <typename P>
+__device__ __forceinline__ void imu_point(const ImuSeg& w, const P& poly, double tsd, int t, float& x, float& y,
+                                          float& z) {
+  const double td = (double)t;
+  imu_core(w, poly, td - tsd, td, x, y, z);
 }
 
 // window search: index of the window segment of frame-relative time t (bnd sorted, bnd[0] unused)
@@ -1531,6 +1542,59 @@ __global__ __launch_bounds__(kBlock, 4) void k_deskew_frame_next(const DeskewArg
     return;
   }
   deskew_frame_quad(a, pre);
+}
+
+// ---- per-point modes on float64 rows (the reference's own data, no float32 staging) --------------
+// The drop-in entry points (MotionCompensator.compensate_point_cloud / compensate_arrays /
+// apply_motion_compensation, CSIM:1435-1480 / 2086-2105; LiDARMotionSimulator.deskew_frames) hand
+// over float64 coordinates that float32 columns would round by up to 6e-8 |p| — enough to miss
+// 1e-5 relative on a coordinate that rotates to near zero.  Here every point is read, computed and
+// written in float64 (rows of pinned host memory for small calls, of a device staging buffer for
+// large ones): one thread per point, its frame by a binary search of the frame offsets, its
+// segment by a binary search of the pose / IMU time table as the oracle selects it (LMC:804-style
+// searchsorted 'right' - 1, clamped), the record from the segment table k_prep built (PoseSeg /
+// ImuSeg), and the batch kernels' own per-point math (slerp_core / imu_core) at the general tier.
+// PCIe-bound by construction (40-56 B of host traffic per point); never the bench's `value`.
+struct PointsF64Args {
+  const double* pts; int64_t ld; int64_t n;   // (n, ld) rows, ld >= 3: x, y, z [, intensity, ...]
+  const int64_t* t_ns;                        // per point, ns since its frame's start
+  const int64_t* doff; int32_t F;             // frame f = rows [doff[f], doff[f+1])
+  const double* ftime;                        // SLERP: frame time (s) per frame
+  const int64_t* fstart;                      // IMU: frame start (ns) per frame
+  const double* pose_time; const PoseSeg* pose_seg; int64_t nseg;
+  const int64_t* imu_ts; const ImuSeg* imu_seg;
+  int64_t ntab;                               // T or M
+  double* out;                                // (n, 4): x', y', z', column 3 (0 when ld == 3)
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_points_f64(const PointsF64Args a) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kBlock) {
+    int32_t lo = 0, hi = a.F;                    // last f with doff[f] <= i
+    while (hi - lo > 1) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (a.doff[mid] <= i) lo = mid; else hi = mid;
+    }
+    const double* q = a.pts + i * a.ld;
+    double x = q[0], y = q[1], z = q[2];
+    const double w = a.ld > 3 ? q[3] : 0.0;
+    const int64_t t = a.t_ns[i];
+    if constexpr (MODE == 1) {
+      const double tf = a.ftime[lo];
+      const double tq = slerp_time(tf, (double)t);
+      int64_t k = upper_bound(a.pose_time, a.ntab, tq) - 1;
+      k = k > a.nseg - 1 ? a.nseg - 1 : (k < 0 ? 0 : k);
+      slerp_core(a.pose_seg[k], kPoly10, tq, x, y, z);
+    } else {
+      const int64_t ta = a.fstart[lo] + t;       // the point's absolute timestamp (CSIM:1447)
+      int64_t k = upper_bound(a.imu_ts, a.ntab, ta) - 1;
+      k = k < 0 ? 0 : k;                         // before the first sample: the first (CSIM:1496)
+      const ImuSeg sg = a.imu_seg[k];
+      imu_core(sg, NoPoly{}, (double)(ta - sg.ts), (double)t, x, y, z);
+    }
+    double* o = a.out + 4 * i;
+    o[0] = x; o[1] = y; o[2] = z; o[3] = w;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -161,6 +161,7 @@ int mc_destroy(mc_ctx* c) {
   if (c->d_codec) (void)hipFree(c->d_codec);
   dev_free(c->d_codec_err);
   dev_free(c->d_pcd_len);
+  if (c->d_seg64) (void)hipFree(c->d_seg64);
   if (c->h_pin) (void)hipHostFree(c->h_pin);
   if (c->h_pipe) (void)hipHostFree(c->h_pipe);
   if (c->d_pipe) (void)hipFree(c->d_pipe);
@@ -1122,6 +1123,122 @@ int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int6
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   std::memcpy(out, pin + off, out_b);
+  return MC_OK;
+}
+
+// ---- per-point modes on host float64 rows (k_points_f64) --------------------------------------
+// pinned, device-mapped host scratch of at least `bytes` (the zero-copy path of the single calls)
+static int ctx_pin(mc_ctx* c, size_t bytes, char** out) {
+  if (bytes > c->pin_bytes) {
+    if (c->h_pin) { (void)hipStreamSynchronize(c->stream); (void)hipHostFree(c->h_pin); c->h_pin = nullptr; }
+    c->pin_bytes = 0;
+    HIPCHK(hipHostMalloc(&c->h_pin, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    c->pin_bytes = bytes;
+  }
+  *out = static_cast<char*>(c->h_pin);
+  return MC_OK;
+}
+
+int mc_deskew_points_f64(mc_ctx* c, int mode, int32_t F, const int64_t* counts, const double* points, int64_t ld,
+                         const int64_t* t_ns, const double* frame_times, const int64_t* frame_start_ns, double* out) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(mode == MC_MODE_POSE_SLERP || mode == MC_MODE_IMU, "mode %d: MC_MODE_POSE_SLERP or MC_MODE_IMU expected",
+            mode);
+  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(F == 0 || counts, "counts is NULL");
+  if (ld < 3) return fail(MC_ERR_INDEX, "points need at least 3 columns (x, y, z); got %lld", (long long)ld);
+  std::vector<int64_t> doff((size_t)F + 1, 0);
+  for (int32_t f = 0; f < F; ++f) {
+    CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
+    doff[f + 1] = doff[f] + counts[f];
+  }
+  if (mode == MC_MODE_POSE_SLERP) {
+    if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
+    CHECK_ARG(F == 0 || frame_times, "frame times are NULL");
+  } else {
+    if (c->M < 1) return fail(MC_ERR_STATE, "no IMU samples uploaded (mc_set_imu)");
+    CHECK_ARG(F == 0 || frame_start_ns, "frame start times are NULL");
+  }
+  const int64_t n = doff[F];
+  if (n == 0) return MC_OK;
+  CHECK_ARG(points && t_ns && out, "NULL points / t_ns / out");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  hipStream_t s = c->stream;
+  // the segment table of the uploaded trajectory / IMU samples (k_prep's table lanes, no frames)
+  const uint64_t ver = mode == MC_MODE_POSE_SLERP ? c->traj_ver : c->imu_ver;
+  const int64_t nseg = mode == MC_MODE_POSE_SLERP ? std::max<int64_t>(c->T - 1, 1) : c->M;
+  const size_t seg_b = (size_t)nseg * (mode == MC_MODE_POSE_SLERP ? sizeof(PoseSeg) : sizeof(ImuSeg));
+  if (!(c->d_seg64 && c->seg64_mode == mode && c->seg64_ver == ver)) {
+    c->seg64_mode = -1;
+    if (seg_b > c->seg64_bytes) {
+      if (c->d_seg64) (void)hipFree(c->d_seg64);
+      c->d_seg64 = nullptr;
+      c->seg64_bytes = 0;
+      HIPCHK(hipMalloc(&c->d_seg64, seg_b));
+      c->seg64_bytes = seg_b;
+    }
+    PrepArgs pa;
+    std::memset(&pa, 0, sizeof(pa));
+    pa.mode = mode;
+    pa.n_frames = 0;
+    pa.time = c->d_time; pa.pos = c->d_pos; pa.rpy = c->d_rpy; pa.T = c->T;
+    pa.imu_ts = c->d_imu_ts; pa.gyro = c->d_gyro; pa.M = c->M;
+    pa.pose_seg = static_cast<PoseSeg*>(c->d_seg64);
+    pa.imu_seg = static_cast<ImuSeg*>(c->d_seg64);
+    pa.nseg = nseg;
+    const uint32_t blocks = (uint32_t)(((nseg + 63) / 64 + 3) / 4);
+    hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(kBlock), 0, s, pa);
+    HIPCHK(hipGetLastError());
+    c->seg64_mode = mode;
+    c->seg64_ver = ver;
+  }
+  // scratch: [doff (F+1) | per-frame value (F) | t_ns (n) | points (n, ld) | out (n, 4)], 8-byte words;
+  // pinned and device-mapped below kZeroCopyRows rows (the kernel reads and writes host memory: no
+  // DMA round trips for the reference's per-frame calls), a device staging buffer above
+  const size_t w_doff = 0, w_fv = (size_t)F + 1, w_t = w_fv + (size_t)F, w_pts = w_t + (size_t)n,
+               w_out = w_pts + (size_t)n * (size_t)ld, words = w_out + 4 * (size_t)n;
+  const bool zero_copy = n < kZeroCopyRows;
+  char* base = nullptr;
+  if (zero_copy) {
+    if (int r = ctx_pin(c, words * 8, &base)) return r;
+    std::memcpy(base + 8 * w_doff, doff.data(), doff.size() * 8);
+    std::memcpy(base + 8 * w_fv, mode == MC_MODE_POSE_SLERP ? static_cast<const void*>(frame_times)
+                                                            : static_cast<const void*>(frame_start_ns), (size_t)F * 8);
+    std::memcpy(base + 8 * w_t, t_ns, (size_t)n * 8);
+    std::memcpy(base + 8 * w_pts, points, (size_t)n * (size_t)ld * 8);
+  } else {
+    void* st = nullptr;
+    if (int r = ctx_stage(c, words * 8, &st)) return r;
+    base = static_cast<char*>(st);
+    HIPCHK(hipMemcpyAsync(base + 8 * w_doff, doff.data(), doff.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_fv, mode == MC_MODE_POSE_SLERP ? static_cast<const void*>(frame_times)
+                                                                      : static_cast<const void*>(frame_start_ns),
+                          (size_t)F * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_t, t_ns, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_pts, points, (size_t)n * (size_t)ld * 8, hipMemcpyHostToDevice, s));
+  }
+  PointsF64Args a;
+  std::memset(&a, 0, sizeof(a));
+  a.pts = reinterpret_cast<const double*>(base + 8 * w_pts); a.ld = ld; a.n = n;
+  a.t_ns = reinterpret_cast<const int64_t*>(base + 8 * w_t);
+  a.doff = reinterpret_cast<const int64_t*>(base + 8 * w_doff); a.F = F;
+  a.ftime = reinterpret_cast<const double*>(base + 8 * w_fv);
+  a.fstart = reinterpret_cast<const int64_t*>(base + 8 * w_fv);
+  a.pose_time = c->d_time; a.pose_seg = static_cast<const PoseSeg*>(c->d_seg64); a.nseg = nseg;
+  a.imu_ts = c->d_imu_ts; a.imu_seg = static_cast<const ImuSeg*>(c->d_seg64);
+  a.ntab = mode == MC_MODE_POSE_SLERP ? c->T : c->M;
+  a.out = reinterpret_cast<double*>(base + 8 * w_out);
+  const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, zero_copy ? 1024 : 65536);
+  {
+    TimedRegion tr(c, &c->main_ev, s);
+    if (mode == MC_MODE_POSE_SLERP) hipLaunchKernelGGL(k_points_f64<1>, dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_points_f64<2>, dim3(grid), dim3(kBlock), 0, s, a);
+  }
+  HIPCHK(hipGetLastError());
+  if (!zero_copy) HIPCHK(hipMemcpyAsync(out, a.out, (size_t)n * 32, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (zero_copy) std::memcpy(out, a.out, (size_t)n * 32);
   return MC_OK;
 }
 

@@ -347,6 +347,33 @@ class Batch:
         return [aos[self.offsets[f]:self.offsets[f + 1]] for f in range(self.n_frames)]
 
 
+def deskew_points_f64(ctx: Context, mode: str, counts, points, t_ns, frame_times=None, frame_start_ns=None) -> np.ndarray:
+    """The per-point modes on host float64 rows (mc_deskew_points_f64): frames back to back
+    (``counts``), ``points`` (N, >=3) float64, ``t_ns`` (N,) int64 ns since each point's frame start,
+    ``frame_times`` (SLERP, s) or ``frame_start_ns`` (IMU) per frame.  Returns (N, 4) float64:
+    x', y', z' in float64, column 3 = points[:, 3] (0 for 3-column input).  The pose / IMU table is
+    the one uploaded to ``ctx``."""
+    c = np.ascontiguousarray(np.atleast_1d(counts), dtype=np.int64)
+    p = np.asarray(points)
+    if p.ndim != 2:
+        raise IndexError(f"too many indices for array: array is {p.ndim}-dimensional, but 2 were indexed")
+    p = np.ascontiguousarray(p, dtype=np.float64)
+    t = np.ascontiguousarray(t_ns, dtype=np.int64).reshape(-1)
+    n = int(c.sum())
+    if p.shape[0] != n or t.shape[0] != n:
+        raise ValueError(f"counts add up to {n} points; got {p.shape[0]} rows and {t.shape[0]} timestamps")
+    ft = None if frame_times is None else np.ascontiguousarray(frame_times, dtype=np.float64)
+    fs = None if frame_start_ns is None else np.ascontiguousarray(frame_start_ns, dtype=np.int64)
+    for v, what in ((ft, "frame_times"), (fs, "frame_start_ns")):
+        if v is not None and v.shape != (len(c),):
+            raise ValueError(f"{what}: one value per frame expected ({len(c)}), got {v.shape}")
+    out = np.empty((n, 4), np.float64)
+    check(ctx.lib.mc_deskew_points_f64(ctx.handle, _lib.MODES[mode], len(c), ptr(c, c_int64), ptr(p, c_double),
+                                       p.shape[1], ptr(t, c_int64), ptr(ft, c_double),
+                                       ptr(fs, c_int64), ptr(out, c_double)), f"deskew_points_f64[{mode}]")
+    return out
+
+
 _default_ctx: Context | None = None
 
 

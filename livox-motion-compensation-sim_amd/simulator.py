@@ -20,7 +20,6 @@ not provided.
 from __future__ import annotations
 
 import os
-from collections import OrderedDict
 from ctypes import c_double, c_int64
 from typing import Dict, List, Optional
 
@@ -31,7 +30,7 @@ from . import codecs as _codecs
 from . import config as _config
 from . import trajectory as _traj
 from ._lib import check, ptr
-from .runtime import Context, default_context
+from .runtime import Context, default_context, deskew_points_f64
 
 
 class LiDARMotionSimulator:
@@ -46,7 +45,6 @@ class LiDARMotionSimulator:
         np.random.seed(self.config["random_seed"])
         self._performance_stats = {"scan_times": [], "transform_times": [], "total_points_processed": 0}
         self._context = context
-        self._batches: "OrderedDict[tuple, tuple]" = OrderedDict()
 
     # ---- config contract (LMC:297-359) ---------------------------------------------------
     def default_config(self):
@@ -71,18 +69,6 @@ class LiDARMotionSimulator:
         if self._context is None:
             self._context = default_context()
         return self._context
-
-    def _io_batches(self, counts, with_time=False):
-        """Cached (input, output) batch pair for a frame-size signature (LRU of 4)."""
-        key = (tuple(int(c) for c in counts), with_time)
-        hit = self._batches.pop(key, None)
-        if hit is None:
-            ctx = self.context
-            hit = (ctx.batch(counts, with_time), ctx.batch(counts, False))
-        self._batches[key] = hit
-        while len(self._batches) > 4:
-            self._batches.popitem(last=False)
-        return hit
 
     @staticmethod
     def _check_points(points):
@@ -166,7 +152,9 @@ class LiDARMotionSimulator:
                       times: Optional[np.ndarray] = None) -> List[np.ndarray]:
         """Per-point motion compensation into the global frame: every return at time
         t_frame + t_ns*1e-9 gets the SLERP/LERP-interpolated pose of the trajectory
-        (position_gps, orientation_imu), p' = R(q(t)) p + pos(t)."""
+        (position_gps, orientation_imu), p' = R(q(t)) p + pos(t).  Computed in float64 on the given
+        float64 rows, one launch for all frames (mc_deskew_points_f64); device-resident frames take
+        ``Context.deskew(mode="pose_slerp")`` instead."""
         if times is None:
             times = self.lidar_times()[: len(frames)]
         times = np.asarray(times, dtype=np.float64)
@@ -180,13 +168,11 @@ class LiDARMotionSimulator:
         if not frames or counts.sum() == 0:
             return [np.zeros((0, 4)) for _ in frames]
         ctx = self.context
-        bin_, bout = self._io_batches(counts, with_time=True)
         ctx.set_trajectory(trajectory["time"], trajectory["position_gps"], trajectory["orientation_imu"])
-        bin_.set_frame_times(times)
-        bin_.upload_aos(_stack_aos(frames))
-        bin_.upload_time(np.concatenate([np.asarray(t, np.int64) for t in t_ns]))
-        ctx.deskew(bin_, bout, mode="pose_slerp")
-        return bout.split(bout.download_aos())
+        out = deskew_points_f64(ctx, "pose_slerp", counts, _stack_aos(frames),
+                                np.concatenate([np.asarray(t, np.int64) for t in t_ns]), frame_times=times)
+        offs = np.concatenate([[0], np.cumsum(counts)])
+        return [out[offs[f]:offs[f + 1]] for f in range(len(frames))]
 
     # ---- scanning (LMC:701-770) and the frame loop (LMC:778-858) ----------------------------
     def _load_environment(self, environment) -> np.ndarray:

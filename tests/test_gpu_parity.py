@@ -331,6 +331,20 @@ def test_config3_parking_600x100k_all_points(mc, gpu_ctx, mode):
 # ---------------------------------------------------------------------------------------------
 # per-point SLERP mode
 # ---------------------------------------------------------------------------------------------
+def _batch_deskew(ctx, frames, t_ns, mode, times=None, starts=None):
+    """The device-batch path (float32 columns, k_deskew_points) over host frames: what the bench
+    runs; the drop-in methods take the float64 rows path (k_points_f64) instead."""
+    b = ctx.batch(np.array([len(f) for f in frames]), with_time=True)
+    b.upload_aos(np.concatenate([np.column_stack([f[:, :3], f[:, 3] if f.shape[1] > 3 else np.zeros(len(f))])
+                                 for f in frames]))
+    b.upload_time(np.concatenate([np.asarray(t, np.int64) for t in t_ns]))
+    if times is not None:
+        b.set_frame_times(times)
+    if starts is not None:
+        b.set_frame_starts(starts)
+    return b.split(ctx.deskew(b, mode=mode).download_aos())
+
+
 def test_slerp_matches_scipy_golden_across_yaw_wrap(mc, gpu_ctx):
     g = golden("slerp.npz")
     tr = {"time": g["time"], "position_gps": g["position_gps"], "orientation_imu": g["orientation_imu"]}
@@ -340,11 +354,16 @@ def test_slerp_matches_scipy_golden_across_yaw_wrap(mc, gpu_ctx):
     pts = np.column_stack([g["xyz"], np.linspace(0, 1, len(g["xyz"]))])
     out = sim.deskew_frames([pts], [t_ns], tr, times=[t_frame])[0]
     tq = t_frame + t_ns * 1e-9
-    ref = R.deskew_pose_slerp(f32(g["xyz"]), t_ns, t_frame, tr)   # the inputs the float32 columns hold
     _, pos = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], tq)
+    # the drop-in computes in float64 on the float64 points: strict against the oracle and the golden
+    ref = R.deskew_pose_slerp(g["xyz"], t_ns, t_frame, tr)
     assert_scaled_close(out[:, :3], ref, scale_of(g["xyz"], pos), what="slerp vs oracle")
-    # the golden was made on the float64 points: their float32 staging is the only difference
-    assert_scaled_close(out[:, :3], g["out"], scale_of(g["xyz"], pos), what="slerp vs scipy golden", strict=False)
+    assert_scaled_close(out[:, :3], g["out"], scale_of(g["xyz"], pos), what="slerp vs scipy golden")
+    assert np.array_equal(out[:, 3], pts[:, 3])
+    # the device-batch kernel holds float32 columns: strict against the oracle on those inputs
+    bo = _batch_deskew(gpu_ctx, [pts], [t_ns], "pose_slerp", times=[t_frame])[0]
+    assert_scaled_close(bo[:, :3], R.deskew_pose_slerp(f32(g["xyz"]), t_ns, t_frame, tr), scale_of(g["xyz"], pos),
+                        what="batch slerp vs oracle")
 
 
 def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
@@ -364,11 +383,12 @@ def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
             rng.integers(0, 100_000_000, 2500)]                                # unsorted
     times = np.array([1.0, 0.2, 20.0, 39.95])                                 # frame 3 runs off the end
     sim = mc.LiDARMotionSimulator(context=gpu_ctx)
-    out = sim.deskew_frames(frames, t_ns, tr, times)
-    for f in range(len(counts)):
-        ref = R.deskew_pose_slerp(frames[f][:, :3], t_ns[f], times[f], tr)
-        _, p = R.slerp_pose(time, pos, rpy, times[f] + np.asarray(t_ns[f]) * 1e-9)
-        assert_scaled_close(out[f][:, :3], ref, scale_of(frames[f][:, :3], p), what=f"frame {f}")
+    for path, out in (("float64 rows", sim.deskew_frames(frames, t_ns, tr, times)),
+                      ("batch", _batch_deskew(gpu_ctx, frames, t_ns, "pose_slerp", times=times))):
+        for f in range(len(counts)):
+            ref = R.deskew_pose_slerp(frames[f][:, :3], t_ns[f], times[f], tr)
+            _, p = R.slerp_pose(time, pos, rpy, times[f] + np.asarray(t_ns[f]) * 1e-9)
+            assert_scaled_close(out[f][:, :3], ref, scale_of(frames[f][:, :3], p), what=f"{path} frame {f}")
 
 
 @pytest.mark.parametrize("mode", ["pose_slerp", "imu"])
@@ -391,11 +411,13 @@ def test_wide_frames_take_subtile_windows(mc, gpu_ctx, mode):
     times = np.array([2.0, 10.005, 20.0, 30.0, 35.0])
     sim = mc.LiDARMotionSimulator(context=gpu_ctx)
     if mode == "pose_slerp":
-        out = sim.deskew_frames(frames, t_ns, tr, times)
+        out = _batch_deskew(gpu_ctx, frames, t_ns, "pose_slerp", times=times)
+        o64 = sim.deskew_frames(frames, t_ns, tr, times)
         for f in range(len(counts)):
             ref = R.deskew_pose_slerp(frames[f][:, :3], t_ns[f], times[f], tr)
             _, p = R.slerp_pose(time, tr["position_gps"], tr["orientation_imu"], times[f] + np.asarray(t_ns[f]) * 1e-9)
             assert_scaled_close(out[f][:, :3], ref, scale_of(frames[f][:, :3], p), what=f"frame {f}")
+            assert_scaled_close(o64[f][:, :3], ref, scale_of(frames[f][:, :3], p), what=f"float64 rows frame {f}")
     else:
         ts = np.arange(0, 40_000_000_000, 1_000_000, dtype=np.int64)            # 1 kHz
         gyro = rng.normal(0, 0.5, (len(ts), 3))
@@ -473,10 +495,9 @@ def test_compensate_point_cloud_matches_reference(mc, gpu_ctx, case):
         assert out is pts
         return
     got = np.array([[p.x, p.y, p.z] for p in out])
-    # the reference's float64 points are staged into float32 columns: scaled bar vs its output,
-    # strict vs the oracle on the float32-rounded points
-    assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(xyz), what=case, strict=False)
-    ref = R.compensate_arrays(f32(xyz), g[f"{case}/ts"], int(g[f"{case}/frame_start"]), g[f"{case}/imu_ts"],
+    # float64 arithmetic on the reference's own float64 points: strict against its output and the oracle
+    assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(xyz), what=case)
+    ref = R.compensate_arrays(xyz, g[f"{case}/ts"], int(g[f"{case}/frame_start"]), g[f"{case}/imu_ts"],
                               g[f"{case}/imu_gyro"])
     assert_scaled_close(got, ref, scale_of(xyz), what=case + " vs oracle")
     meta = np.array([[p.intensity, p.timestamp, p.ring, p.tag] for p in out])
@@ -501,7 +522,82 @@ def test_compensator_disabled_and_driver(mc, gpu_ctx):
     assert all(r["motion_compensated"] for r in res) and res[2]["points"] == []
     for case, r in zip(("mid", "spike"), res):
         got = np.array([[p.x, p.y, p.z] for p in r["points"]])
-        assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case, strict=False)
+        assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case)
+
+
+def test_apply_motion_compensation_reference_goldens_strict(mc, gpu_ctx):
+    """CSIM:2086-2105 over every CSIM Path-B golden case at once: each case is a frame of one
+    apply_motion_compensation call (one launch), checked strictly against the reference's own
+    float64 output; metadata and record types pass through (CSIM:1467-1475)."""
+    g = golden("csim_pathb.npz")
+    cases = ["mid", "before", "after", "dup", "spike"]
+    # every case shares the mid IMU list (the same table for all frames of a run)
+    imu = [mc.IMUData(int(t), *map(float, gy), *map(float, ac))
+           for t, gy, ac in zip(g["mid/imu_ts"], g["mid/imu_gyro"], g["mid/imu_accel"])]
+    frames = []
+    for case in cases:
+        if not np.array_equal(g[f"{case}/imu_ts"], g["mid/imu_ts"]) or not np.array_equal(g[f"{case}/imu_gyro"], g["mid/imu_gyro"]):
+            continue
+        frames.append((case, {"timestamp": int(g[f"{case}/frame_start"]), "frame_duration_ns": 100_000_000,
+                              "points": [mc.LiDARPoint(float(p[0]), float(p[1]), float(p[2]), int(i), int(t), int(r), int(tg))
+                                         for p, i, t, r, tg in zip(g[f"{case}/xyz"], g[f"{case}/intensity"], g[f"{case}/ts"],
+                                                                   g[f"{case}/ring"], g[f"{case}/tag"])]}))
+    assert len(frames) >= 2
+    comp = mc.MotionCompensator({}, context=gpu_ctx)
+    res = comp.apply_motion_compensation([fr for _, fr in frames], imu)
+    for (case, fr), r in zip(frames, res):
+        got = np.array([[p.x, p.y, p.z] for p in r["points"]])
+        assert_scaled_close(got, g[f"{case}/out_xyz"], scale_of(g[f"{case}/xyz"]), what=case)
+        assert all(type(p) is mc.LiDARPoint for p in r["points"])
+        meta = np.array([[p.intensity, p.timestamp, p.ring, p.tag] for p in r["points"]])
+        assert np.array_equal(meta, g[f"{case}/out_meta"])
+
+
+def test_points_f64_contract_and_edges(mc, gpu_ctx):
+    """mc_deskew_points_f64: 3- and 5-column rows, empty frames in the middle, point times beyond
+    int32 ns of their frame start (the batch path's limit), points before the first / after the last
+    sample, the segment table rebuilt on a new IMU / trajectory upload, errors as the reference's."""
+    rng = np.random.default_rng(21)
+    ts = np.arange(0, 10_000_000_000, 5_000_000, dtype=np.int64)
+    gyro = rng.normal(0, 0.8, (len(ts), 3))
+    counts = np.array([700, 0, 3, 0, 40_000])                 # the last frame takes the staged (DMA) path
+    starts = np.array([1, 2, 3, 4, 5], np.int64) * 1_000_000_000
+    n = int(counts.sum())
+    xyz = rng.uniform(-90, 90, (n, 3))
+    t_rel = rng.integers(-3_000_000_000, 6_000_000_000, n)   # outside int32 ns and outside the IMU span
+    gpu_ctx.set_imu(ts, gyro)
+    for cols in (3, 5):
+        pts = np.column_stack([xyz, rng.uniform(0, 1, (n, cols - 3))]) if cols > 3 else xyz
+        out = mc.runtime.deskew_points_f64(gpu_ctx, "imu", counts, pts, t_rel, frame_start_ns=starts)
+        offs = np.concatenate([[0], np.cumsum(counts)])
+        for f in range(len(counts)):
+            s = slice(offs[f], offs[f + 1])
+            ref = R.compensate_arrays(xyz[s], starts[f] + t_rel[s], starts[f], ts, gyro)
+            assert_scaled_close(out[s, :3], ref, scale_of(xyz[s]), what=f"cols {cols} frame {f}")
+        assert np.array_equal(out[:, 3], pts[:, 3] if cols > 3 else np.zeros(n))
+    gyro2 = gyro[::-1].copy()
+    gpu_ctx.set_imu(ts, gyro2)                                # same length: the table must be rebuilt
+    out = mc.runtime.deskew_points_f64(gpu_ctx, "imu", [n], xyz, t_rel, frame_start_ns=[starts[0]])
+    assert_scaled_close(out[:, :3], R.compensate_arrays(xyz, starts[0] + t_rel, starts[0], ts, gyro2), scale_of(xyz))
+    T = 300
+    tr = {"time": np.linspace(0, 30, T), "position_gps": np.cumsum(rng.normal(0, 0.5, (T, 3)), axis=0),
+          "orientation_imu": np.cumsum(rng.normal(0, 0.1, (T, 3)), axis=0)}
+    gpu_ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    times = np.array([0.5, 1.0, 2.0, 3.0, 29.9])
+    out = mc.runtime.deskew_points_f64(gpu_ctx, "pose_slerp", counts, xyz, t_rel, frame_times=times)
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    for f in range(len(counts)):
+        s = slice(offs[f], offs[f + 1])
+        ref = R.deskew_pose_slerp(xyz[s], t_rel[s], times[f], tr)
+        _, p = R.slerp_pose(tr["time"], tr["position_gps"], tr["orientation_imu"], times[f] + t_rel[s] * 1e-9)
+        assert_scaled_close(out[s, :3], ref, scale_of(xyz[s], p), what=f"slerp frame {f}")
+    with pytest.raises(IndexError):
+        mc.runtime.deskew_points_f64(gpu_ctx, "imu", [n], xyz[:, :2], t_rel, frame_start_ns=[0])
+    with pytest.raises(ValueError):
+        mc.runtime.deskew_points_f64(gpu_ctx, "imu", [n + 1], xyz, t_rel, frame_start_ns=[0])
+    with pytest.raises(ValueError):
+        mc.runtime.deskew_points_f64(gpu_ctx, "frame", [n], xyz, t_rel, frame_start_ns=[0])
+    assert mc.runtime.deskew_points_f64(gpu_ctx, "imu", [0, 0], np.zeros((0, 3)), [], frame_start_ns=[0, 0]).shape == (0, 4)
 
 
 def test_compensator_sees_in_place_imu_edits(mc, gpu_ctx):
@@ -546,9 +642,11 @@ def test_imu_polynomial_tiers_and_thresholds(mc, gpu_ctx, rate):
     start = 1_000_000_000
     t_abs = np.sort(start + rng.integers(-2_000_000, 100_000_000, n))
     comp = mc.MotionCompensator({}, context=gpu_ctx)
-    got = comp.compensate_arrays(xyz, t_abs, start, ts, gyro)
+    gpu_ctx.set_imu(ts, gyro)
+    got = _batch_deskew(gpu_ctx, [xyz], [t_abs - start], "imu", starts=[start])[0][:, :3]
     ref = R.compensate_arrays(xyz, t_abs, start, ts, gyro)
     assert_scaled_close(got, ref, scale_of(xyz), what=f"rate {rate}")
+    assert_scaled_close(comp.compensate_arrays(xyz, t_abs, start, ts, gyro), ref, scale_of(xyz), what="float64 rows")
 
 
 def test_imu_slow_path_wide_subtile(mc, gpu_ctx):
@@ -561,9 +659,11 @@ def test_imu_slow_path_wide_subtile(mc, gpu_ctx):
     start = 1_000_000_000
     t_abs = start + rng.integers(-500_000_000, 1_000_000_000, n)
     comp = mc.MotionCompensator({}, context=gpu_ctx)
-    got = comp.compensate_arrays(xyz, t_abs, start, ts, gyro)
+    gpu_ctx.set_imu(ts, gyro)
+    got = _batch_deskew(gpu_ctx, [xyz], [t_abs - start], "imu", starts=[start])[0][:, :3]
     ref = R.compensate_arrays(xyz, t_abs, start, ts, gyro)
     assert_scaled_close(got, ref, scale_of(xyz))
+    assert_scaled_close(comp.compensate_arrays(xyz, t_abs, start, ts, gyro), ref, scale_of(xyz), what="float64 rows")
 
 
 # ---------------------------------------------------------------------------------------------
