@@ -174,13 +174,19 @@ def check_frames(batch, mode, tr, times, imu, counts, local_frames, global_ids):
 # ---------------------------------------------------------------------------------------------
 # CPU baseline (before the GPU is touched; the all-cores legs spawn worker processes)
 # ---------------------------------------------------------------------------------------------
+CPU_CACHE_FRAMES = 48   # synthetic frames a CPU worker generates once and then cycles through
+
+
 def _cpu_frames(mode, tr, times, counts, frame_lo, budget_s, f_first=0, f_step=1, start_at=None):
-    """The oracle on frames f_first, f_first+f_step, ... until budget_s of compute, one BLAS
-    thread.  Returns (points, seconds, frames, late start s).  frame mode = the reference's own op
-    sequence (scipy from_euler, R @ P.T, + t, column_stack; LMC:772-776) after the pose selection
-    (804-812).  Untimed first: one whole frame (imports scipy, faults in the buffers) — VERDICT r2: a
-    fresh worker otherwise paid the cold scipy import inside its timed region.  ``start_at`` (wall
-    clock): every worker of an all-cores leg starts timing at the same moment, so they run together."""
+    """The oracle on frames f_first, f_first+f_step, ... (cycling through them again while compute
+    time remains) until budget_s of compute, one BLAS thread.  Returns (points, seconds, frames, late
+    start s).  frame mode = the reference's own op sequence (scipy from_euler, R @ P.T, + t,
+    column_stack; LMC:772-776) after the pose selection (804-812).  The worker's frames (at most
+    CPU_CACHE_FRAMES) are generated before timing starts, so the budget is compute only (VERDICT r3:
+    one pass over 600 frames gave a 16-process frame leg only 11-26 ms per worker).  Untimed first:
+    one whole frame (imports scipy, faults in the buffers) — VERDICT r2: a fresh worker otherwise paid
+    the cold scipy import inside its timed region.  ``start_at`` (wall clock): every worker of an
+    all-cores leg starts timing at the same moment, so they run together."""
     from threadpoolctl import threadpool_limits
     from oracle import restatement as R
     from oracle import synth
@@ -191,9 +197,14 @@ def _cpu_frames(mode, tr, times, counts, frame_lo, budget_s, f_first=0, f_step=1
     if mode == "imu":
         ts_imu, gyro = mc.trajectory.imu_from_trajectory(tr, 200.0)
 
-    def one(f):
+    mine = list(range(f_first, len(counts), f_step))[:CPU_CACHE_FRAMES]
+    cache = {}
+    for f in mine:
         x, y, z, i, t = synth.synth_frame(int(counts[f]), 0, 1000 + frame_lo + f)
-        pts = np.column_stack([x, y, z, i]).astype(np.float64)
+        cache[f] = (np.column_stack([x, y, z, i]).astype(np.float64), t)
+
+    def one(f):
+        pts, t = cache[f]
         t0 = time.perf_counter()
         if mode == "frame":
             k = int(R.select_pose_index(tr["time"], times[f]))
@@ -210,20 +221,21 @@ def _cpu_frames(mode, tr, times, counts, frame_lo, budget_s, f_first=0, f_step=1
 
     late = 0.0
     with threadpool_limits(limits=1):
-        if len(counts) > f_first:
-            one(f_first)                      # untimed warm-up frame
+        if mine:
+            one(mine[0])                      # untimed warm-up frame
         if start_at is not None:
             wait = start_at - time.time()
             if wait > 0:
                 time.sleep(wait)
             else:
                 late = -wait
-        for f in range(f_first, len(counts), f_step):
-            if t_total >= budget_s:
-                break
+        k = 0
+        while mine and t_total < budget_s:
+            f = mine[k % len(mine)]
             t_total += one(f)
             done += int(counts[f])
             nf += 1
+            k += 1
     return done, t_total, nf, late
 
 
@@ -236,8 +248,9 @@ def cpu_leg(mode, tr, times, counts, frame_lo, budget_s, procs, pool):
     if procs <= 1:
         done, secs, nf, _ = _cpu_frames(mode, tr, times, counts, frame_lo, budget_s)
         return {"value": done / secs / 1e6, "unit": "Mpoints/s", "cores": 1, "blas_threads": 1,
-                "sample": f"{nf} of {len(counts)} frames x {n0} pts, {secs:.1f} s of compute "
-                          f"(after one untimed warm-up frame)"}
+                "compute_s": round(secs, 3),
+                "sample": f"{nf} frame passes over {min(len(counts), CPU_CACHE_FRAMES)} of the {len(counts)} frames x "
+                          f"{n0} pts, {secs:.1f} s of compute (after one untimed warm-up frame)"}
     start_at = time.time() + 10.0         # the workers are spawned and warmed up by then
     jobs = [(mode, tr, times, counts, frame_lo, budget_s, p, procs, start_at) for p in range(procs)]
     res = pool.map(_cpu_worker, jobs)
@@ -247,17 +260,20 @@ def cpu_leg(mode, tr, times, counts, frame_lo, budget_s, procs, pool):
     return {"value": pts / wall / 1e6, "unit": "Mpoints/s", "cores": procs, "blas_threads": 1,
             "per_worker_compute_s": [round(r[1], 3) for r in res],
             "late_start_s": round(max(r[3] for r in res), 3),
-            "sample": f"{frames} of {len(counts)} frames x {n0} pts over {procs} processes (round-robin frames), "
-                      f"each after an untimed warm-up frame, all starting at one wall-clock moment; "
-                      f"rate = points / slowest worker's compute time"}
+            "sample": f"{frames} frame passes (frames x {n0} pts, round-robin over {procs} processes, each cycling "
+                      f"through its frames for {budget_s:.1f} s of compute) after an untimed warm-up frame each, "
+                      f"all starting at one wall-clock moment; rate = points / slowest worker's compute time"}
 
 
 def cpu_baselines(mode, tr, times, counts, frame_lo, budget_s, procs):
-    """The oracle (numpy restatement of the reference's op sequence) on the same synthetic frames,
-    generation excluded: the headline mode and the reference's own frame-mode op sequence
-    (LMC:772-776), each on one core and on ``procs`` processes (OPENBLAS threads = 1 everywhere)."""
+    """The oracle on the same synthetic frames, generation excluded, each leg on one core and on
+    ``procs`` processes (OPENBLAS threads = 1 everywhere).  The line's top-level value is the
+    all-cores FRAME leg: the reference's own op sequence (LMC:772-776 — from_euler, R @ P.T, + t,
+    column_stack per frame), the only CPU path the reference has for this hot path.
+    The headline GPU mode's own oracle leg (SLERP: a build-added mode with no reference function)
+    is reported beside it as ``legs[mode]``."""
     import multiprocessing as mp
-    legs = [mode] + (["frame"] if mode != "frame" else [])
+    legs = ["frame"] + ([mode] if mode != "frame" else [])
     out = {}
     with mp.get_context("spawn").Pool(procs) if procs > 1 else _NullPool() as pool:
         for m in legs:
@@ -269,13 +285,15 @@ def cpu_baselines(mode, tr, times, counts, frame_lo, budget_s, procs):
                 if multi["value"] < single["value"]:
                     print(f"warning: cpu baseline {m}: {procs} processes ({multi['value']:.1f} Mpoints/s) below one "
                           f"core ({single['value']:.1f})", file=sys.stderr)
-    head = out[mode]["all_cores"] or out[mode]["single_core"]
+    head = out["frame"]["all_cores"] or out["frame"]["single_core"]
     line = {"value": head["value"], "unit": "Mpoints/s", "cores": head["cores"], "kind": "port",
-            "sample": f"{mode} mode: " + head["sample"],
+            "path": "reference op sequence (LMC:772-776, per frame after the LMC:804-812 pose selection)",
+            "sample": "frame leg: " + head["sample"],
             "legs": out,
-            "note": "oracle = numpy restatement of the reference's op sequence (oracle/restatement.py), same "
+            "note": "oracle = numpy restatement of the reference's op sequence (oracle/restatement.py; "
+                    "profiles/cpu_calibration.json: within 5 % of the reference's own transform_pointcloud), same "
                     "synthetic frames as the GPU, generation excluded; frame leg = scipy from_euler -> R @ P.T -> "
-                    "+ t -> column_stack per frame (LMC:772-776, the reference's own per-frame sequence)"}
+                    f"+ t -> column_stack per frame; legs[{mode!r}] = the headline GPU mode's oracle"}
     return line
 
 
@@ -735,6 +753,82 @@ def single_gpu_same_job(ctx, args, tr, times_all, counts_all, steps, warmup):
         b_out.close()
 
 
+def assemble_line(args, cid, label, scen, lo, hi, world, n_devices, n_rank, n_total, counts_all, results, spinup_ms,
+                  every, tuned, stager, scan, codecs, parity, gather, hung, single) -> dict:
+    """Rank 0's JSON line.  ``value`` is the timed steps' points over the max-over-ranks wall time
+    (the kernels only: the merged-cloud gather runs after and outside the timed region and is
+    reported on its own under ``gather``); at N > 1 the same-job single-GPU run and the speedup over
+    it sit beside it (kernel scaling and gather reported separately)."""
+    F_all = len(counts_all)
+    r = results[args.mode]
+    per_gpu_frames = hi - lo
+    traffic, traffic_src = load_traffic(args.mode, per_gpu_frames, int(counts_all[0]) if F_all else 0)
+    shared = n_devices < world
+    scaling = "weak" if cid is None else "strong"
+    gather_ok = None if gather is None else bool("error" not in gather and gather.get("parity", {}).get("ok"))
+    ok = (gather_ok is not False) and (parity is None or parity["ok"]) and not hung
+    line = {
+        "metric": "Mpoints/s deskewed (100k-pt Mid-70 frames) + % HBM roofline",
+        "value": r["value"],
+        "unit": "Mpoints/s",
+        "n_gpus": n_devices,
+        "steps": r["steps"],
+        "warmup": args.warmup,
+        "spinup": {"ms": round(spinup_ms, 1), "what": "untimed, before the warmup steps: the same step "
+                   "repeated until the device reaches its sustained memory throughput (tens of ms from "
+                   "idle; 5 warmup steps are 1.7 ms) — profiles/round2/s51"},
+        "ms_per_step": r["wall_s"] / r["steps"] * 1e3,
+        "higher_is_better": True,
+        "scaling": scaling if not shared else f"{scaling} (NOT a scaling result: {world} ranks share "
+                                              f"{n_devices} device(s))",
+        "vs_baseline": None,
+        "dtype": "f64 arithmetic on f32 point columns (one f32 rounding per output coordinate)",
+        "data": f"synthetic Mid-70 frames (counter-hash generator, on device); reference {scen} pose table, "
+                "seed 42, GPS/IMU noise on",
+        "config": {"workload": f"{label}; {world} rank(s), frames {lo}..{hi - 1} on rank 0",
+                   "baseline_config": cid, "scenario": scen, "mode": args.mode,
+                   "global_frames": F_all, "points_per_frame": int(counts_all[0]) if F_all else 0,
+                   "total_points": n_total, "rank0_frames": per_gpu_frames,
+                   "parallelism": f"frame-shard x{world} (dist.plan_shards)", "ranks": world,
+                   "devices": n_devices},
+        "roofline": {"bound": "hbm", "achieved": r["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": r["achieved_GBs"] / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": KERNEL_OF[args.issue][args.mode], "kernel_avg_us": r["main_avg_us"],
+                     "bytes_per_point": BYTES_PER_POINT[args.mode], "points_per_launch": n_rank,
+                     "kernel_time": ("HIP events around every launch of a second, untimed pass"
+                                     if args.events_after else
+                                     f"wall-clock stamp nodes around the kernels of {r['timed_launches']} of the "
+                                     f"{r['steps']} steps of the step graph (every {every}th)"
+                                     if args.issue == "graph" else
+                                     f"HIP events (hipExtLaunchKernel start/stop, the dispatch's own timestamps) "
+                                     f"on the kernels of {r['timed_launches']} of the {r['steps']} timed steps "
+                                     f"(every {every}th), on the kernel's stream")},
+        "order_tune": tuned or None,
+        "step_over_kernel": (r["wall_s"] / r["steps"] * 1e6) / r["main_avg_us"] if r["main_avg_us"] else None,
+        "prep_avg_us": r["prep_avg_us"],
+        "step_issue": {"calls": "per-call launches; prep as an any-order packet on the kernel's queue",
+                       "graph": f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
+                       "pipeline": f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
+                                   "k_prep, then each step's deskew kernel with the next step's prep in its "
+                                   "first workgroups (every step runs its own prep, one launch ahead)"}[args.issue],
+        "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
+                      "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"],
+                      "ms_per_step": v["wall_s"] / v["steps"] * 1e3}
+                  for m, v in results.items()},
+        "stager": stager,
+        "scan_environment": scan,
+        "codecs": codecs,
+        "parity": parity,
+        "gather": gather,
+        "gather_ok": gather_ok,
+        "single_gpu_same_job": single,
+        "speedup_vs_1gpu": (r["value"] / single["value"]) if single and "value" in single else None,
+        "ok": ok,
+    }
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -878,72 +972,9 @@ def main():
 
     ok = True
     if rank == 0:
-        r = results[args.mode]
-        per_gpu_frames = hi - lo
-        traffic, traffic_src = load_traffic(args.mode, per_gpu_frames, int(counts_all[0]) if F_all else 0)
-        shared = n_devices < world
-        scaling = "weak" if cid is None else "strong"
-        gather_ok = None if gather is None else bool("error" not in gather and gather.get("parity", {}).get("ok"))
-        ok = (gather_ok is not False) and (parity is None or parity["ok"]) and not hung
-        line = {
-            "metric": "Mpoints/s deskewed (100k-pt Mid-70 frames) + % HBM roofline",
-            "value": r["value"],
-            "unit": "Mpoints/s",
-            "n_gpus": n_devices,
-            "steps": r["steps"],
-            "warmup": args.warmup,
-            "spinup": {"ms": round(spinup_ms, 1), "what": "untimed, before the warmup steps: the same step "
-                       "repeated until the device reaches its sustained memory throughput (tens of ms from "
-                       "idle; 5 warmup steps are 1.7 ms) — profiles/round2/s51"},
-            "ms_per_step": r["wall_s"] / r["steps"] * 1e3,
-            "higher_is_better": True,
-            "scaling": scaling if not shared else f"{scaling} (NOT a scaling result: {world} ranks share "
-                                                  f"{n_devices} device(s))",
-            "vs_baseline": None,
-            "dtype": "f64 arithmetic on f32 point columns (one f32 rounding per output coordinate)",
-            "data": f"synthetic Mid-70 frames (counter-hash generator, on device); reference {scen} pose table, "
-                    "seed 42, GPS/IMU noise on",
-            "config": {"workload": f"{label}; {world} rank(s), frames {lo}..{hi - 1} on rank 0",
-                       "baseline_config": cid, "scenario": scen, "mode": args.mode,
-                       "global_frames": F_all, "points_per_frame": int(counts_all[0]) if F_all else 0,
-                       "total_points": n_total, "rank0_frames": per_gpu_frames,
-                       "parallelism": f"frame-shard x{world} (dist.plan_shards)", "ranks": world,
-                       "devices": n_devices},
-            "roofline": {"bound": "hbm", "achieved": r["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": r["achieved_GBs"] / HBM_PEAK_GBS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": KERNEL_OF[args.issue][args.mode], "kernel_avg_us": r["main_avg_us"],
-                         "bytes_per_point": BYTES_PER_POINT[args.mode], "points_per_launch": n_rank,
-                         "kernel_time": ("HIP events around every launch of a second, untimed pass"
-                                         if args.events_after else
-                                         f"wall-clock stamp nodes around the kernels of {r['timed_launches']} of the "
-                                         f"{r['steps']} steps of the step graph (every {every}th)"
-                                         if args.issue == "graph" else
-                                         f"HIP events (hipExtLaunchKernel start/stop, the dispatch's own timestamps) "
-                                         f"on the kernels of {r['timed_launches']} of the {r['steps']} timed steps "
-                                         f"(every {every}th), on the kernel's stream")},
-            "order_tune": tuned or None,
-            "step_over_kernel": (r["wall_s"] / r["steps"] * 1e6) / r["main_avg_us"] if r["main_avg_us"] else None,
-            "prep_avg_us": r["prep_avg_us"],
-            "step_issue": {"calls": "per-call launches; prep as an any-order packet on the kernel's queue",
-                           "graph": f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
-                           "pipeline": f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
-                                       "k_prep, then each step's deskew kernel with the next step's prep in its "
-                                       "first workgroups (every step runs its own prep, one launch ahead)"}[args.issue],
-            "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
-                          "frac": v["achieved_GBs"] / HBM_PEAK_GBS, "kernel_avg_us": v["main_avg_us"],
-                          "ms_per_step": v["wall_s"] / v["steps"] * 1e3}
-                      for m, v in results.items()},
-            "stager": stager,
-            "scan_environment": scan,
-            "codecs": codecs,
-            "parity": parity,
-            "gather": gather,
-            "gather_ok": gather_ok,
-            "single_gpu_same_job": single,
-            "speedup_vs_1gpu": (r["value"] / single["value"]) if single and "value" in single else None,
-            "ok": ok,
-        }
+        line = assemble_line(args, cid, label, scen, lo, hi, world, n_devices, n_rank, n_total, counts_all,
+                             results, spinup_ms, every, tuned, stager, scan, codecs, parity, gather, hung, single)
+        ok = line["ok"]
         if cpu is not None:
             line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)

@@ -36,7 +36,11 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run \
   -- python3 "$ROOT/bench.py" --steps "$STEPS" --no-cpu > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err"
 stop_if_fault $? rocprof
-find "$OUT/prof_$TAG" -name "*kernel_stats*" -exec cat {} \; | head -20
+find "$OUT/prof_$TAG" -name "*kernel_stats*" -exec cp {} "$OUT/kernel_stats_$TAG.csv" \;
+# the bench line's roofline kernel time recomputed from the same run's kernel trace (timed window only)
+python3 "$ROOT/tools/roofline_from_trace.py" --trace "$OUT/prof_$TAG" --bench "$OUT/prof_bench_$TAG.json" \
+  --out "$OUT/roofline_trace_$TAG.json" > /dev/null 2>> "$OUT/prof_$TAG.err"
+echo "[roofline_from_trace] rc=$?" | tee -a "$OUT/steps_$TAG.log"
 
 cd "$ROOT"
 if [ "${PMC:-1}" = "0" ]; then exit 0; fi
