@@ -241,6 +241,14 @@ int mc_deskew_steps(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, in
 int mc_transform_pointcloud_f64(mc_ctx* ctx, const double* points, int64_t n, int64_t ld, const double* rpy,
                                 const double* translation, double* out);
 
+/* Opt-in latency server for the single calls of mc_transform_pointcloud_f64 up to 32768 rows (the
+ * reference's one-frame-per-call use, LMC:831): one workgroup stays resident on its own stream and
+ * polls a mailbox in pinned host memory, so a call pays no kernel launch and no completion signal.
+ * It returns after 50 ms without a request (relaunched on the next call), after 2 s in all, and on
+ * disable / mc_destroy.  info: enabled flag, server launches, requests served. */
+int mc_set_latency_server(mc_ctx* ctx, int enable);
+int mc_latency_server_info(mc_ctx* ctx, int* enabled, int64_t* launches, int64_t* requests);
+
 /* The per-point modes on the reference's own float64 data (no float32 staging): MotionCompensator.
  * compensate_point_cloud / apply_motion_compensation (CSIM:1435-1480, 2086-2105) for MC_MODE_IMU,
  * the per-point SLERP deskew for MC_MODE_POSE_SLERP.  points (N, ld >= 3) float64 rows, frames back

@@ -172,6 +172,14 @@ struct mc_ctx {
   size_t seg64_bytes = 0;
   int seg64_mode = -1;
   uint64_t seg64_ver = 0;
+  // latency server (mc_set_latency_server): k_lat_server resident on lat_stream, mailbox + rows in
+  // pinned, device-mapped host memory h_lat = [LatMailbox (256 B) | in (kLatRows, 4) | out (kLatRows, 4)]
+  hipStream_t lat_stream = nullptr;
+  void* h_lat = nullptr;
+  bool lat_on = false;
+  bool lat_launched = false;
+  uint32_t lat_seq = 0;
+  uint64_t lat_launches = 0;
   // pinned, device-mapped host buffer of the single-call drop-in path
   void* h_pin = nullptr;
   size_t pin_bytes = 0;

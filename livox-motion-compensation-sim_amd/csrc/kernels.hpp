@@ -1058,6 +1058,92 @@ __global__ __launch_bounds__(kBlock) void k_transform_host_f64(const double* __r
   }
 }
 
+// ---- latency server: transform_pointcloud (LMC:772-776) without a launch per call --------------
+// The reference transforms one ~1.6k-point frame per call (LMC:831).  A launched kernel pays the
+// launch and the completion signal (15-17 us beyond the kernel); this opt-in server is
+// ONE workgroup that stays resident on its own stream and polls a mailbox in pinned, device-mapped
+// host memory: the host writes a request (row count, rpy, t; the rows already in the pinned input
+// buffer) and bumps seq_req; the server computes R (LMC:774) on one lane, transforms the rows from
+// the pinned input straight into the pinned output in float64, makes its stores visible system-wide
+// and publishes seq_done; the host spins on seq_done.  Every exit is bounded: the server returns
+// after idle_ticks without a request, after life_ticks in all, or on quit (mc_set_latency_server /
+// mc_destroy); the host relaunches it on the next request (alive == 0).  Only vector memory
+// instructions touch the mailbox (atomic loads / stores at system scope).
+struct LatMailbox {
+  uint32_t seq_req;    // host: number of the posted request
+  uint32_t seq_done;   // server: number of the last finished request
+  uint32_t alive;      // host 2 at launch, server 1 while polling, 0 on exit
+  uint32_t quit;       // host: stop now
+  int64_t n;           // rows of the request (<= the buffers' capacity)
+  double rpy[3];
+  double t[3];
+};
+constexpr int kLatThreads = 1024;
+
+__global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, const double* __restrict__ in,
+                                                            double* __restrict__ out, uint32_t seen,
+                                                            uint64_t idle_ticks, uint64_t life_ticks) {
+  __shared__ int s_go;
+  __shared__ uint32_t s_seq;
+  __shared__ int64_t s_n;
+  __shared__ double s_R[12];
+  const uint64_t t0 = wall_clock64();
+  uint64_t t_last = t0;
+  if (threadIdx.x == 0) __hip_atomic_store(&mb->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int go = 0;
+      uint32_t r = seen;
+      // relaxed polls (uncached system-scope loads, no cache invalidation per poll), one acquire fence
+      // once a request is seen
+      for (;;) {
+        r = __hip_atomic_load(&mb->seq_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (r != seen) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          go = 1;
+          break;
+        }
+        if (__hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        const uint64_t now = wall_clock64();
+        if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (go) {
+        const double rr = __hip_atomic_load(&mb->rpy[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const double rp = __hip_atomic_load(&mb->rpy[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const double ry = __hip_atomic_load(&mb->rpy[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        euler_xyz_matrix(rr, rp, ry, s_R);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s_R[9 + k] = __hip_atomic_load(&mb->t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_n = __hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      s_seq = r;
+      s_go = go;
+    }
+    __syncthreads();
+    if (!s_go) break;
+    const int64_t n = s_n;
+    const double R0 = s_R[0], R1 = s_R[1], R2 = s_R[2], R3 = s_R[3], R4 = s_R[4], R5 = s_R[5], R6 = s_R[6],
+                 R7 = s_R[7], R8 = s_R[8], tx = s_R[9], ty = s_R[10], tz = s_R[11];
+    for (int64_t i = threadIdx.x; i < n; i += kLatThreads) {
+      const double2 p01 = *reinterpret_cast<const double2*>(in + 4 * i);
+      const double2 p23 = *reinterpret_cast<const double2*>(in + 4 * i + 2);
+      const double x = p01.x, y = p01.y, z = p23.x;
+      *reinterpret_cast<double2*>(out + 4 * i) = double2{R0 * x + R1 * y + R2 * z + tx, R3 * x + R4 * y + R5 * z + ty};
+      *reinterpret_cast<double2*>(out + 4 * i + 2) = double2{R6 * x + R7 * y + R8 * z + tz, p23.y};
+    }
+    __threadfence_system();   // this lane's rows are visible to the host before the flag below
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&mb->seq_done, s_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      seen = s_seq;
+    }
+    t_last = wall_clock64();
+    __syncthreads();          // s_* are rewritten by the next request
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // CoordinateTransformer.transform_points on homogeneous (N,4) input (CSIM:214-233)
 __global__ __launch_bounds__(kBlock) void k_affine_w(const DeskewArgs a) { deskew_frame_body<true>(a); }
 

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -153,6 +154,7 @@ int mc_create(int device, mc_ctx** out) {
 int mc_destroy(mc_ctx* c) {
   if (!c) return MC_OK;
   DeviceGuard g(c->device);
+  (void)mc_set_latency_server(c, 0);
   (void)sync_all(c);
   dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
   dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
@@ -1079,6 +1081,119 @@ constexpr int64_t kJobRows = 8192;                                     // rows p
 static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
                         const int64_t* d_doff, const double* d_pose, double* const* outs);
 
+// ---- the latency server (k_lat_server) --------------------------------------------------------
+constexpr int64_t kLatRows = 1 << 15;       // rows one request may carry (the zero-copy range)
+constexpr size_t kLatMailboxBytes = 256;
+constexpr double kLatIdleMs = 50.0;         // the server returns after this long without a request
+constexpr double kLatLifeMs = 2000.0;       // ... and after this long in all (relaunched on demand)
+constexpr double kLatAnswerS = 2.0;         // a request unanswered this long is an error
+
+static LatMailbox* lat_mailbox(mc_ctx* c) { return static_cast<LatMailbox*>(c->h_lat); }
+static double* lat_in(mc_ctx* c) { return reinterpret_cast<double*>(static_cast<char*>(c->h_lat) + kLatMailboxBytes); }
+static double* lat_out(mc_ctx* c) { return lat_in(c) + 4 * kLatRows; }
+
+// (re)launch the server: it takes requests numbered after the last finished one
+static int lat_launch(mc_ctx* c) {
+  LatMailbox* mb = lat_mailbox(c);
+  if (c->wall_khz <= 0.0) {
+    int khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    if (khz <= 0) return fail(MC_ERR_HIP, "wall clock rate unavailable");
+    c->wall_khz = khz;
+  }
+  if (c->lat_launched) HIPCHK(hipStreamSynchronize(c->lat_stream));   // the previous instance has returned
+  __atomic_store_n(&mb->alive, 2u, __ATOMIC_RELEASE);
+  const uint32_t seen = __atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE);
+  hipLaunchKernelGGL(k_lat_server, dim3(1), dim3(kLatThreads), 0, c->lat_stream, mb, lat_in(c), lat_out(c), seen,
+                     (uint64_t)(kLatIdleMs * c->wall_khz), (uint64_t)(kLatLifeMs * c->wall_khz));
+  HIPCHK(hipGetLastError());
+  c->lat_launched = true;
+  ++c->lat_launches;
+  return MC_OK;
+}
+
+// stop the server (quit flag; returns once the instance has exited)
+static int lat_stop(mc_ctx* c) {
+  if (!c->lat_on || !c->lat_launched) return MC_OK;
+  LatMailbox* mb = lat_mailbox(c);
+  __atomic_store_n(&mb->quit, 1u, __ATOMIC_RELEASE);
+  const hipError_t e = hipStreamSynchronize(c->lat_stream);
+  __atomic_store_n(&mb->quit, 0u, __ATOMIC_RELEASE);
+  c->lat_launched = false;
+  if (e != hipSuccess) return fail(MC_ERR_HIP, "latency server stop: %s", hipGetErrorString(e));
+  return MC_OK;
+}
+
+int mc_set_latency_server(mc_ctx* c, int enable) {
+  CHECK_ARG(c, "ctx is NULL");
+  DeviceGuard g(c->device);
+  if (enable && !c->lat_on) {
+    HIPCHK(hipStreamCreateWithFlags(&c->lat_stream, hipStreamNonBlocking));
+    const size_t bytes = kLatMailboxBytes + 2 * (size_t)kLatRows * 4 * sizeof(double);
+    const hipError_t e = hipHostMalloc(&c->h_lat, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) {
+      (void)hipStreamDestroy(c->lat_stream);
+      c->lat_stream = nullptr;
+      return fail(MC_ERR_NOMEM, "latency server buffers: %s", hipGetErrorString(e));
+    }
+    std::memset(c->h_lat, 0, kLatMailboxBytes);
+    c->lat_on = true;
+    c->lat_launched = false;
+    c->lat_seq = 0;
+  } else if (!enable && c->lat_on) {
+    const int r = lat_stop(c);
+    (void)hipHostFree(c->h_lat);
+    (void)hipStreamDestroy(c->lat_stream);
+    c->h_lat = nullptr;
+    c->lat_stream = nullptr;
+    c->lat_on = false;
+    if (r) return r;
+  }
+  return MC_OK;
+}
+
+int mc_latency_server_info(mc_ctx* c, int* enabled, int64_t* launches, int64_t* requests) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (enabled) *enabled = c->lat_on ? 1 : 0;
+  if (launches) *launches = (int64_t)c->lat_launches;
+  if (requests) *requests = (int64_t)c->lat_seq;
+  return MC_OK;
+}
+
+// one transform_pointcloud request through the server (n <= kLatRows)
+static int lat_transform(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
+                         const double* translation, double* out) {
+  LatMailbox* mb = lat_mailbox(c);
+  double* in = lat_in(c);
+  if (ld == 4) std::memcpy(in, points, (size_t)n * 32);
+  else for (int64_t i = 0; i < n; ++i) std::memcpy(in + 4 * i, points + i * ld, 32);
+  mb->n = n;
+  for (int k = 0; k < 3; ++k) { mb->rpy[k] = rpy[k]; mb->t[k] = translation[k]; }
+  // an instance that has returned (idle / lifetime) is relaunched before the request is posted
+  if (!c->lat_launched || __atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) == 0)
+    if (int r = lat_launch(c)) return r;
+  const uint32_t seq = ++c->lat_seq;
+  __atomic_store_n(&mb->seq_req, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spins = 0;; ++spins) {
+    if (__atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE) == seq) break;
+    if (__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) == 0) {
+      // it returned before taking this request (a race with its idle exit): relaunch, it takes it
+      if (__atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE) == seq) break;
+      if (int r = lat_launch(c)) return r;
+      continue;
+    }
+    __builtin_ia32_pause();
+    if ((spins & 1023) == 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kLatAnswerS) {
+      (void)lat_stop(c);
+      return fail(MC_ERR_HIP, "latency server did not answer request %u within %.1f s", seq, kLatAnswerS);
+    }
+  }
+  std::memcpy(out, lat_out(c), (size_t)n * 32);
+  return MC_OK;
+}
+
 int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
                                 const double* translation, double* out) {
   CHECK_ARG(c && rpy && translation, "NULL argument");
@@ -1087,6 +1202,7 @@ int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int6
   if (n == 0) return MC_OK;
   CHECK_ARG(points && out, "NULL points / out");
   DeviceGuard g(c->device);
+  if (c->lat_on && n <= kLatRows) return lat_transform(c, points, n, ld, rpy, translation, out);
   if (n >= kZeroCopyRows) {                     // large: the DMA row pipeline with one frame
     if (int r = sync_all(c)) return r;
     void* st = nullptr;

@@ -173,6 +173,18 @@ class Context:
               "scan_emit")
         return out
 
+    def latency_server(self, enable: bool = True) -> dict:
+        """Opt-in resident kernel for single transform_pointcloud calls up to 32768 rows
+        (mc_set_latency_server): no launch and no completion signal per call.  Returns its info."""
+        check(self.lib.mc_set_latency_server(self.handle, int(bool(enable))), "latency_server")
+        return self.latency_server_info()
+
+    def latency_server_info(self) -> dict:
+        e, la, rq = c_int(), c_int64(), c_int64()
+        check(self.lib.mc_latency_server_info(self.handle, ctypes.byref(e), ctypes.byref(la), ctypes.byref(rq)),
+              "latency_server_info")
+        return {"enabled": bool(e.value), "launches": la.value, "requests": rq.value}
+
     def set_max_grid(self, max_grid: int):
         check(self.lib.mc_set_launch(self.handle, int(max_grid)), "set_launch")
 
