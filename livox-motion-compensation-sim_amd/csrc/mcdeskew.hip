@@ -1652,8 +1652,9 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
     }
     {
       TimedRegion tr(c, &c->scan_ev, c->stream);
-      hipLaunchKernelGGL(k_scan_count, dim3(tiles, (F + kScanFrames - 1) / kScanFrames), dim3(kBlock), 0, c->stream,
-                         c->d_env, c->env_ld, c->E, c->d_scan_pose, F, sp, c->d_scan_tcount, c->d_scan_bits);
+      const uint32_t units = (uint32_t)tiles * (uint32_t)((F + kScanFrames - 1) / kScanFrames);
+      hipLaunchKernelGGL(k_scan_count, dim3(units), dim3(kBlock), 0, c->stream, c->d_env, c->env_ld, c->E, tiles,
+                         c->d_scan_pose, F, sp, c->d_scan_tcount, c->d_scan_bits);
     }
     HIPCHK(hipGetLastError());
     std::vector<int32_t> tc((size_t)F * tiles);
@@ -1698,15 +1699,15 @@ int mc_scan_emit(mc_ctx* c, mc_batch* out, const double* noise) {
     d_noise = static_cast<const double*>(st);
   }
   ScanEmitArgs ea;
-  ea.env = c->d_env; ea.ld = c->env_ld; ea.E = c->E;
+  ea.env = c->d_env; ea.ld = c->env_ld; ea.E = c->E; ea.n_tiles = c->scan_tiles;
   ea.pose = c->d_scan_pose; ea.F = out->F;
   ea.sp = make_scan_params(c->scan_par, c->scan_cap);
   ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.vis_bits = c->d_scan_bits; ea.noise = d_noise;
   ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.C = out->C;
   {
     TimedRegion tr(c, &c->scan_ev, c->stream);
-    hipLaunchKernelGGL(k_scan_emit, dim3(c->scan_tiles, (out->F + kScanFrames - 1) / kScanFrames), dim3(kBlock), 0,
-                       c->stream, ea);
+    const uint32_t units = (uint32_t)c->scan_tiles * (uint32_t)((out->F + kScanFrames - 1) / kScanFrames);
+    hipLaunchKernelGGL(k_scan_emit, dim3(units), dim3(kBlock), 0, c->stream, ea);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

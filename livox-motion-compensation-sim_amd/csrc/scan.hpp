@@ -9,7 +9,12 @@
 // by the host from numpy's global RNG in frame order and added here.
 //
 // A workgroup owns a tile of kScanTile scene points held in registers and tests it against
-// kScanFrames frames (scene re-reads from L2 drop by that factor).
+// kScanFrames frames (scene re-reads from L2 drop by that factor).  Units (tile, frame group) are
+// numbered tile-major and taken in the XCD-contiguous order (scan_unit): each XCD runs a contiguous
+// range of tiles with all their frame groups, so every scene tile is fetched into one XCD's L2 only
+// (with the units dealt over the 8 XCDs every L2 fetched the whole scene: 2.9x the algorithmic
+// bytes, profiles/pmc_traffic.json r3s65), and a frame's output runs of neighbouring tiles meet in
+// one L2 instead of being written as partial lines by two.
 #pragma once
 #include "kernels.hpp"
 
@@ -112,8 +117,9 @@ struct ScanTile {
   bool in[kScanRounds];
 };
 
-__device__ __forceinline__ void scan_load_tile(const double* __restrict__ env, int64_t ld, int64_t E, ScanTile& t) {
-  const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
+__device__ __forceinline__ void scan_load_tile(const double* __restrict__ env, int64_t ld, int64_t E, int64_t tile,
+                                               ScanTile& t) {
+  const int64_t t0 = tile * kScanTile;
 #pragma unroll
   for (int r = 0; r < kScanRounds; ++r) {
     const int64_t e = t0 + r * kBlock + threadIdx.x;
@@ -125,16 +131,29 @@ __device__ __forceinline__ void scan_load_tile(const double* __restrict__ env, i
 
 static_assert(kScanFrames * kScanRounds == 32, "one 32-bit visibility word per thread and workgroup");
 
+// workgroup -> (scene tile, frame group): tile-major units, XCD-contiguous (grid = n_tiles * n_groups)
+struct ScanUnit {
+  int64_t tile;
+  int fg;
+};
+__device__ __forceinline__ ScanUnit scan_unit(int32_t n_tiles) {
+  const int64_t n = (int64_t)gridDim.x;
+  const int64_t u = xcd_unit<1>(blockIdx.x, n);
+  const int64_t n_fg = n / n_tiles;
+  return ScanUnit{u / n_fg, (int)(u % n_fg)};
+}
+
 // pass 1: visible scene points per (frame, tile) -> tile_count[f * n_tiles + tile], and the
 // visibility bits (bit j*kScanRounds + r: frame f0+j, round r) that pass 2 consumes
 __global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict__ env, int64_t ld, int64_t E,
-                                                       const double* __restrict__ pose, int32_t F, ScanParams sp,
-                                                       int32_t* __restrict__ tile_count,
+                                                       int32_t n_tiles, const double* __restrict__ pose, int32_t F,
+                                                       ScanParams sp, int32_t* __restrict__ tile_count,
                                                        uint32_t* __restrict__ vis_bits) {
   __shared__ int s_cnt[kScanFrames][kBlock / 64];
+  const ScanUnit su = scan_unit(n_tiles);
   ScanTile t;
-  scan_load_tile(env, ld, E, t);
-  const int f0 = blockIdx.y * kScanFrames;
+  scan_load_tile(env, ld, E, su.tile, t);
+  const int f0 = su.fg * kScanFrames;
   const int nf = F - f0 < kScanFrames ? F - f0 : kScanFrames;
   uint32_t bits = 0;
   for (int j = 0; j < nf; ++j) {
@@ -151,18 +170,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict_
     for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
     if ((threadIdx.x & 63) == 0) s_cnt[j][threadIdx.x >> 6] = n;
   }
-  vis_bits[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x] = bits;
+  vis_bits[((int64_t)su.fg * n_tiles + su.tile) * kBlock + threadIdx.x] = bits;
   __syncthreads();
   if (threadIdx.x < nf) {
     int tot = 0;
     for (int w = 0; w < kBlock / 64; ++w) tot += s_cnt[threadIdx.x][w];
-    tile_count[(int64_t)(f0 + threadIdx.x) * gridDim.x + blockIdx.x] = tot;
+    tile_count[(int64_t)(f0 + threadIdx.x) * n_tiles + su.tile] = tot;
   }
 }
 
 // pass 2: in-order compaction + systematic subsample + noise, written into the output batch
 struct ScanEmitArgs {
-  const double* env; int64_t ld; int64_t E;
+  const double* env; int64_t ld; int64_t E; int32_t n_tiles;
   const double* pose; int32_t F; ScanParams sp;
   const int64_t* tile_off;   // [F][n_tiles] exclusive visible-point offset of the tile in its frame
   const int64_t* nvis;       // [F] visible points before subsampling
@@ -175,12 +194,13 @@ struct ScanEmitArgs {
 __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
   __shared__ int s_cnt[kScanRounds][kBlock / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const ScanUnit su = scan_unit(a.n_tiles);
   ScanTile t;
-  scan_load_tile(a.env, a.ld, a.E, t);
-  const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
-  const int f0 = blockIdx.y * kScanFrames;
+  scan_load_tile(a.env, a.ld, a.E, su.tile, t);
+  const int64_t t0 = su.tile * kScanTile;
+  const int f0 = su.fg * kScanFrames;
   const int nf = a.F - f0 < kScanFrames ? a.F - f0 : kScanFrames;
-  const uint32_t bits = a.vis_bits[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x];
+  const uint32_t bits = a.vis_bits[((int64_t)su.fg * a.n_tiles + su.tile) * kBlock + threadIdx.x];
   for (int j = 0; j < nf; ++j) {
     const int f = f0 + j;
     const double* P = a.pose + 12 * (int64_t)f;
@@ -207,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
     const int64_t nv = a.nvis[f];
     const int64_t step = nv > a.sp.cap ? nv / a.sp.cap : 1;    // LMC:757-760
     const int64_t poff = a.poff[f], doff = a.doff[f];
-    int64_t base = a.tile_off[(int64_t)f * gridDim.x + blockIdx.x];
+    int64_t base = a.tile_off[(int64_t)f * a.n_tiles + su.tile];
 #pragma unroll
     for (int r = 0; r < kScanRounds; ++r) {
       int before = 0, total = 0;
