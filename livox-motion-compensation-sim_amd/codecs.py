@@ -239,13 +239,16 @@ def deskew_pcd_batch(inp: Batch, out: Batch, mode: str = "frame", pose_select: s
     (mc_deskew_pcd: the deskew kernel sums each block's text bytes, so the writer needs no measure
     pass over ``out``) — LMC:831 -> 887-889 -> 932-948 on device-resident frames.  Returns
     (device text buffer, body_pos) with frame f's lines at [body_pos[f], body_pos[f+1]); ``text``: a
-    DeviceBuffer to reuse (grown when too small)."""
+    DeviceBuffer to reuse.  The buffer is sized for the longest packed line (52 bytes: four values of
+    "-dddd.dddddd" and their separators), so the packed path never needs a second pass; a ``text``
+    smaller than that, or text of lines beyond the packed path that still does not fit, is closed
+    and replaced by a new buffer (the returned one) of exactly the size the first pass reported."""
     ctx = inp.ctx
     if out is inp:
         raise ValueError("deskew_pcd needs an output batch other than the input")
     counts = np.ascontiguousarray(out.counts, np.int64)
     pos = np.zeros(len(counts) + 1, np.int64)
-    cap = max(int(counts.sum()) * 48, 64)
+    cap = max(int(counts.sum()) * 52, 64)     # the packed maximum: 4 x (1 + 4 + 7) + 4
     if text is None or text.nbytes < cap:
         if text is not None:
             text.close()
