@@ -409,7 +409,9 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipel
                 ctx.deskew(b_in, b_out, mode=mode)
             ctx.timing(False)
         ctx.sync()
+    each = ctx.read_timing_each()
     tm = ctx.read_timing()
+    tm["main_ms"], tm["main_launches"], tm["main_each_us"] = sum(each), len(each), [round(x * 1e3, 2) for x in each]
     return t1 - t0, tm, every
 
 
@@ -795,6 +797,7 @@ def assemble_line(args, cid, label, scen, lo, hi, world, n_devices, n_rank, n_to
                      "frac": r["achieved_GBs"] / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": KERNEL_OF[args.issue][args.mode], "kernel_avg_us": r["main_avg_us"],
+                     "kernel_each_us": r.get("main_each_us"),
                      "bytes_per_point": BYTES_PER_POINT[args.mode], "points_per_launch": n_rank,
                      "kernel_time": ("HIP events around every launch of a second, untimed pass"
                                      if args.events_after else
@@ -929,7 +932,7 @@ def main():
         prep_avg_s = tm["prep_ms"] / tm["prep_launches"] / 1e3 if tm["prep_launches"] else None
         achieved = BYTES_PER_POINT[mode] * n_rank / main_avg_s / 1e9 if main_avg_s > 0 else 0.0
         results[mode] = {"wall_s": wall_max, "steps": steps, "main_avg_us": main_avg_s * 1e6,
-                         "timed_launches": int(tm["main_launches"]),
+                         "timed_launches": int(tm["main_launches"]), "main_each_us": tm["main_each_us"],
                          "prep_avg_us": prep_avg_s * 1e6 if prep_avg_s is not None else None,
                          "achieved_GBs": achieved,
                          "value": n_total * steps / wall_max / 1e6}

@@ -280,6 +280,9 @@ int mc_transform_affine(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int32_t 
 int mc_timing_enable(mc_ctx* ctx, int enable);
 int mc_timing_read(mc_ctx* ctx, double* main_ms_total, int64_t* main_launches,
                    double* prep_ms_total, int64_t* prep_launches);
+/* the main kernels' event times one by one (ms, in launch order; up to cap of them, *n = how many
+ * were pending); those events are released (the prep / layout / codec ones stay for mc_timing_read) */
+int mc_timing_read_each(mc_ctx* ctx, double* main_ms, int64_t cap, int64_t* n);
 /* kernel tuning knobs: 0 keeps the default */
 int mc_set_launch(mc_ctx* ctx, int32_t max_grid);
 

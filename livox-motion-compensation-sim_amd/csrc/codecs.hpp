@@ -513,9 +513,20 @@ __device__ __forceinline__ int wave_scan_incl(int x) {
 }
 
 // block-wide inclusive sum over the kPcdBlock threads of a PCD workgroup
+#ifndef MC_PCD_SCAN
+#define MC_PCD_SCAN 1
+#endif
 __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#if MC_PCD_SCAN
   x = wave_scan_incl(x);
+#else
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+#endif
   if (lane == 63) s_wave[wid] = x;
   __syncthreads();
   int before = 0;
@@ -655,6 +666,78 @@ __device__ __forceinline__ void pair_fields(const uint16_t* tbl, uint32_t N, uin
   T = (uint64_t)A | ((uint64_t)B << 32);
 }
 
+#ifndef MC_PCD_DIGITS
+#define MC_PCD_DIGITS 1
+#endif
+#ifndef MC_PCD_EMIT
+#define MC_PCD_EMIT 1
+#endif
+// y * 41 as two shift-adds (y*9, then + y*32): the compiler folds the plain product into a
+// quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t mul41(uint32_t y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t y9, r;
+  asm("v_lshl_add_u32 %0, %1, 3, %1" : "=v"(y9) : "v"(y));
+  asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(y), "v"(y9));
+  return r;
+#else
+  return y * 41u;
+#endif
+}
+// the same fields by multiply-shift SWAR arithmetic (round 3's writer)
+__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t sep, uint32_t& D, uint64_t& T) {
+  const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
+  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32);   // fp / 1000, exact
+  const uint32_t y = fh | ((fp - fh * 1000u) << 16);
+  const uint32_t h = ((mul41(y)) >> 12) & 0x000F000Fu;
+  const uint32_t r = y - h * 100u;
+  const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;
+  const uint32_t ht = h | (t << 8);
+  const uint32_t u = r - t * 10u;
+  const uint32_t A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;
+  const uint32_t B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);
+  const uint32_t hi2 = __umul24(ip, 5243u) >> 19;
+  const uint32_t y2 = hi2 | ((ip - hi2 * 100u) << 16);
+  const uint32_t t2 = (__umul24(y2, 103u) >> 10) & 0x000F000Fu;
+  const uint32_t u2 = y2 - t2 * 10u;
+  D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;
+  T = (uint64_t)A | ((uint64_t)B << 32);
+}
+__device__ __forceinline__ void digit_fields(const uint16_t* tbl, uint32_t N, uint32_t sep, uint32_t& D, uint64_t& T) {
+#if MC_PCD_DIGITS
+  pair_fields(tbl, N, sep, D, T);
+#else
+  (void)tbl;
+  swar_fields(N, sep, D, T);
+#endif
+}
+__device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+// round 3's emission: values in reverse order, fields stored as bytes at their final offsets, every
+// value but the line's first with its 4 digit bytes and a '-' slot (stray bytes land in the previous
+// value, written afterwards), the first value's head byte by byte
+template <bool EXACT>
+__device__ __forceinline__ void bytes_value(const uint16_t* tbl, uint8_t* base, int o, uint32_t N, int nd, bool neg,
+                                            uint32_t sep) {
+  uint32_t D;
+  uint64_t T;
+  digit_fields(tbl, N, sep, D, T);
+  uint8_t* pa = base + o + nd + (neg ? 1 : 0);   // the '.'
+  put4(pa, (uint32_t)T);
+  put4(pa + 4, (uint32_t)(T >> 32));
+  if (EXACT) {
+    pa[-1] = (uint8_t)(D >> 24);
+    if (nd >= 2) pa[-2] = (uint8_t)(D >> 16);
+    if (nd >= 3) pa[-3] = (uint8_t)(D >> 8);
+    if (nd >= 4) pa[-4] = (uint8_t)D;
+    if (neg) pa[-nd - 1] = '-';
+  } else {
+    put4(pa - 4, D);
+    pa[-nd - 1] = '-';
+  }
+}
+
 // One packed line at byte `off` of the tile text.  Exactly the line's own bytes end up written, so
 // lanes never touch each other's text (no zeroing, no atomics, no ordering between lanes):
 //   1. the first value's head ([-] + nd digits, left-aligned) as 8 bytes from `off`: its stray bytes
@@ -664,13 +747,22 @@ __device__ __forceinline__ void pair_fields(const uint16_t* tbl, uint32_t N, uin
 //   3. the four fixed 8-byte fraction fields, which overwrite every stray byte.
 // A lane's LDS stores complete in program order.
 __device__ __forceinline__ void pcd_emit_pairs(const PcdFast& P, const uint16_t* tbl, uint8_t* base, int off) {
+#if !MC_PCD_EMIT
+  const int o1 = off + 8 + P.nd[0] + (int)(P.neg & 1u), o2 = o1 + 8 + P.nd[1] + (int)((P.neg >> 1) & 1u);
+  const int o3 = o2 + 8 + P.nd[2] + (int)((P.neg >> 2) & 1u);
+  bytes_value<false>(tbl, base, o3, P.n[3], P.nd[3], (P.neg >> 3) & 1u, '\n');
+  bytes_value<false>(tbl, base, o2, P.n[2], P.nd[2], (P.neg >> 2) & 1u, ' ');
+  bytes_value<false>(tbl, base, o1, P.n[1], P.nd[1], (P.neg >> 1) & 1u, ' ');
+  bytes_value<true>(tbl, base, off, P.n[0], P.nd[0], P.neg & 1u, ' ');
+  return;
+#endif
   uint64_t T[4];
   int pa[4];
   int o = off;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     uint32_t D;
-    pair_fields(tbl, P.n[k], k < 3 ? 0x20u : 0x0Au, D, T[k]);
+    digit_fields(tbl, P.n[k], k < 3 ? 0x20u : 0x0Au, D, T[k]);
     const int nd = P.nd[k];
     const bool neg = (P.neg >> k) & 1u;
     pa[k] = o + nd + (neg ? 1 : 0);   // the '.'

@@ -230,8 +230,6 @@ struct mc_batch {
   int32_t* d_ftile = nullptr;      // first tile of each frame (F+1)
   int2* d_strange = nullptr;       // per sub-tile [min, max] t_ns
   mc::FrameWin* d_swin = nullptr;  // per sub-tile window, double-buffered (2 * n_sub)
-  void* d_srec = nullptr;          // 2 records per sub-tile, double-buffered
-  size_t srec_half = 0;
   double* d_partial = nullptr;
   bool has_times = false, has_starts = false, trange_valid = false;
 };

@@ -120,7 +120,9 @@ struct DeskewArgs {
   const FrameWin* fwin;    // per-point modes
   const void* frec;        // 2 frame-specialised records per frame (PoseWin or ImuSeg)
   const FrameWin* swin;    // per sub-tile: the same, for frames whose window exceeds kFastMaxW
-  const void* srec;        // 2 frame-specialised IMU records per sub-tile (MC_IMU_SEGREC=0 only; else null)
+  const void* pad0;        // unused: keeps the kernel-argument layout the deskew kernels' register
+                           // allocation was measured with (without it the fused SLERP kernel spills
+                           // more SGPRs into VGPR lanes: 147 vs 118 writelane / readlane)
   const double* pose_time; // T
   const PoseSeg* pose_seg; // nseg
   const int64_t* imu_ts;   // M
@@ -457,9 +459,7 @@ struct PrepArgs {
   // per sub-tile windows for frames whose window is wider than kFastMaxW
   const int32_t* ftile;    // first tile of frame f (F+1 entries)
   const int2* strange;     // per sub-tile [min, max] t_ns (recorded with trange)
-  FrameWin* swin; void* srec;
-  int64_t n_sub;           // sub-tiles of the batch (the swin slot permutation's range)
-  int32_t swin_perm;       // 1: swin slot of sub-tile st is xcd_unit(st, n_sub) (MC_SWIN_PERM, dealt order)
+  FrameWin* swin;
 };
 
 // Wave-cooperative searches over a sorted table: 64 lanes probe evenly spaced entries per round,

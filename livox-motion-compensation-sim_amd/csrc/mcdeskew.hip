@@ -327,8 +327,6 @@ int mc_batch_destroy(mc_batch* b) {
   if (b->d_frec) (void)hipFree(b->d_frec);
   b->d_frec = nullptr;
   dev_free(b->d_ftile); dev_free(b->d_strange); dev_free(b->d_swin);
-  if (b->d_srec) (void)hipFree(b->d_srec);
-  b->d_srec = nullptr;
   delete b;
   return MC_OK;
 }
@@ -677,8 +675,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   pa.frame_tbl = frame_tbl; pa.pose_seg = pose_seg; pa.imu_seg = imu_seg;
   pa.fwin = fwin; pa.frec = frec;
   FrameWin* swin = pb->d_swin ? pb->d_swin + (size_t)in->n_tiles * kSub * h : nullptr;
-  void* srec = pb->d_srec ? static_cast<char*>(pb->d_srec) + pb->srec_half * h : nullptr;
-  pa.ftile = pb->d_ftile; pa.strange = pb->d_strange; pa.swin = swin; pa.srec = srec;
+  pa.ftile = pb->d_ftile; pa.strange = pb->d_strange; pa.swin = swin;
   // one wave per frame, then one lane per pose segment / IMU sample
   int64_t table = 0;
   if (mode == MC_MODE_POSE_SLERP) { pa.nseg = std::max<int64_t>(c->T - 1, 1); table = pa.nseg; }
@@ -698,7 +695,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   da.frame_tbl = frame_tbl;
   da.frame_time = pb->d_frame_time; da.frame_start = pb->d_frame_start;
   da.fwin = fwin; da.frec = frec;
-  da.swin = swin; da.srec = srec;
+  da.swin = swin;
   da.pose_time = c->d_time; da.pose_seg = pose_seg;
   da.imu_ts = c->d_imu_ts; da.imu_seg = imu_seg;
   if (mode == MC_MODE_POSE_SLERP) { da.nseg = pa.nseg; da.ntab = c->T; }
@@ -714,7 +711,6 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // a device-measured choice for this mode and batch size (mc_tune_order) overrides the default
   const mc_ctx::OrderTune& ot = c->order_tune[mode];
   if (ot.order >= 0 && ot.P == in->P) da.xcd_order = ot.order;
-  pa.n_sub = (int64_t)in->n_tiles * kSub;
 }
 
 // Launches with optional hipExtLaunchKernel timing events (e0/e1 null: untimed) and AQL flags.
@@ -1557,6 +1553,19 @@ int mc_timing_enable(mc_ctx* c, int enable) {
   return MC_OK;
 }
 
+
+int mc_timing_read_each(mc_ctx* c, double* ms, int64_t cap, int64_t* n) {
+  CHECK_ARG(c && n && (cap == 0 || ms), "NULL argument");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  *n = (int64_t)c->main_ev.size();
+  for (int64_t k = 0; k < *n && k < cap; ++k) {
+    float m = 0.f;
+    HIPCHK(hipEventElapsedTime(&m, c->main_ev[k].first, c->main_ev[k].second));
+    ms[k] = m;
+  }
+  return sum_events(c, c->main_ev, nullptr, nullptr);   // the main events only (the rest stays pending)
+}
 
 int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms, int64_t* prep_n) {
   CHECK_ARG(c, "ctx is NULL");

@@ -204,6 +204,14 @@ class Context:
                 "layout_ms": lm.value, "layout_launches": ln.value, "scan_ms": sm.value, "scan_launches": sn.value,
                 "codec_ms": cm.value, "codec_launches": cn.value}
 
+    def read_timing_each(self, cap: int = 4096) -> list:
+        """The main kernels' event times (ms) one by one, in launch order (released; the other timing
+        events stay pending for read_timing)."""
+        buf = np.zeros(cap, np.float64)
+        n = c_int64()
+        check(self.lib.mc_timing_read_each(self.handle, ptr(buf, c_double), cap, ctypes.byref(n)), "timing_read_each")
+        return buf[:min(n.value, cap)].tolist()
+
     def device_buffer(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
 

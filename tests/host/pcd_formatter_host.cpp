@@ -20,6 +20,17 @@
 #define __ATOMIC_RELAXED 0
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
 static inline uint32_t __umul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
+// v_perm_b32: byte i of the result = byte sel[i] of {s0:s1} (0-3 = s1, 4-7 = s0), 12 -> 0x00
+static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t v = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t c = (sel >> (8 * i)) & 0xffu;
+    const uint32_t b = c < 8 ? (uint32_t)(v >> (8 * c)) & 0xffu : (c == 12 ? 0u : 0xffu);
+    r |= b << (8 * i);
+  }
+  return r;
+}
 using std::fma;
 using std::signbit;
 using std::rint;

@@ -331,9 +331,12 @@ def test_config3_parking_600x100k_all_points(mc, gpu_ctx, mode):
 # ---------------------------------------------------------------------------------------------
 # per-point SLERP mode
 # ---------------------------------------------------------------------------------------------
-def _batch_deskew(ctx, frames, t_ns, mode, times=None, starts=None):
+def _batch_deskew(ctx, frames, t_ns, mode, times=None, starts=None, tr=None):
     """The device-batch path (float32 columns, k_deskew_points) over host frames: what the bench
-    runs; the drop-in methods take the float64 rows path (k_points_f64) instead."""
+    runs; the drop-in methods take the float64 rows path (k_points_f64) instead.  SLERP: ``tr`` is
+    uploaded here (the context keeps whatever table the last call set)."""
+    if tr is not None:
+        ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
     b = ctx.batch(np.array([len(f) for f in frames]), with_time=True)
     b.upload_aos(np.concatenate([np.column_stack([f[:, :3], f[:, 3] if f.shape[1] > 3 else np.zeros(len(f))])
                                  for f in frames]))
@@ -361,7 +364,7 @@ def test_slerp_matches_scipy_golden_across_yaw_wrap(mc, gpu_ctx):
     assert_scaled_close(out[:, :3], g["out"], scale_of(g["xyz"], pos), what="slerp vs scipy golden")
     assert np.array_equal(out[:, 3], pts[:, 3])
     # the device-batch kernel holds float32 columns: strict against the oracle on those inputs
-    bo = _batch_deskew(gpu_ctx, [pts], [t_ns], "pose_slerp", times=[t_frame])[0]
+    bo = _batch_deskew(gpu_ctx, [pts], [t_ns], "pose_slerp", times=[t_frame], tr=tr)[0]
     assert_scaled_close(bo[:, :3], R.deskew_pose_slerp(f32(g["xyz"]), t_ns, t_frame, tr), scale_of(g["xyz"], pos),
                         what="batch slerp vs oracle")
 
@@ -384,7 +387,7 @@ def test_slerp_edge_cases_and_slow_path(mc, gpu_ctx):
     times = np.array([1.0, 0.2, 20.0, 39.95])                                 # frame 3 runs off the end
     sim = mc.LiDARMotionSimulator(context=gpu_ctx)
     for path, out in (("float64 rows", sim.deskew_frames(frames, t_ns, tr, times)),
-                      ("batch", _batch_deskew(gpu_ctx, frames, t_ns, "pose_slerp", times=times))):
+                      ("batch", _batch_deskew(gpu_ctx, frames, t_ns, "pose_slerp", times=times, tr=tr))):
         for f in range(len(counts)):
             ref = R.deskew_pose_slerp(frames[f][:, :3], t_ns[f], times[f], tr)
             _, p = R.slerp_pose(time, pos, rpy, times[f] + np.asarray(t_ns[f]) * 1e-9)
@@ -411,7 +414,7 @@ def test_wide_frames_take_subtile_windows(mc, gpu_ctx, mode):
     times = np.array([2.0, 10.005, 20.0, 30.0, 35.0])
     sim = mc.LiDARMotionSimulator(context=gpu_ctx)
     if mode == "pose_slerp":
-        out = _batch_deskew(gpu_ctx, frames, t_ns, "pose_slerp", times=times)
+        out = _batch_deskew(gpu_ctx, frames, t_ns, "pose_slerp", times=times, tr=tr)
         o64 = sim.deskew_frames(frames, t_ns, tr, times)
         for f in range(len(counts)):
             ref = R.deskew_pose_slerp(frames[f][:, :3], t_ns[f], times[f], tr)

@@ -20,12 +20,15 @@ def formatter_section() -> str:
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
-def test_line_writer_matches_printf(tmp_path):
+@pytest.mark.parametrize("digits,emit", [(1, 1), (0, 1), (1, 0), (0, 0)])
+def test_line_writer_matches_printf(tmp_path, digits, emit):
     code = open(HARNESS).read().replace("// FORMATTER_SECTION", formatter_section())
     cpp = tmp_path / "fmt.cpp"
     cpp.write_text(code)
     exe = tmp_path / "fmt"
-    subprocess.run(["g++", "-O2", "-std=c++17", str(cpp), "-o", str(exe)], check=True, capture_output=True, text=True)
+    r = subprocess.run(["g++", "-O2", "-std=c++17", f"-DMC_PCD_DIGITS={digits}", f"-DMC_PCD_EMIT={emit}", str(cpp),
+                        "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
     r = subprocess.run([str(exe), "200000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
     assert "bad 0" in r.stdout

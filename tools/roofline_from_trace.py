@@ -96,6 +96,9 @@ def main():
         "trace_all_timed_steps_avg_us": sum(dur) / len(dur),
         "bench_line_kernel_avg_us": bench_us,
         "trace_vs_bench": trace_us / bench_us - 1.0,
+        "bench_events_each_us": line["roofline"].get("kernel_each_us"),
+        "events_minus_trace_each_us": ([round(e - t, 2) for e, t in zip(line["roofline"]["kernel_each_us"], sampled)]
+                                       if line["roofline"].get("kernel_each_us") else None),
         "frac_from_trace": bpp * n / (trace_us * 1e-6) / 1e9 / line["roofline"]["peak"],
         "frac_bench_line": line["roofline"]["frac"],
         "all_launches_of_kernel_avg_us": sum(fused_all) / len(fused_all),
