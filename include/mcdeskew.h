@@ -245,9 +245,11 @@ int mc_transform_pointcloud_f64(mc_ctx* ctx, const double* points, int64_t n, in
  * reference's one-frame-per-call use, LMC:831): one workgroup stays resident on its own stream and
  * polls a mailbox in pinned host memory, so a call pays no kernel launch and no completion signal.
  * It returns after 50 ms without a request (relaunched on the next call), after 2 s in all, and on
- * disable / mc_destroy.  info: enabled flag, server launches, requests served. */
+ * disable / mc_destroy.  info: enabled flag, server launches, requests served, and the mean
+ * microseconds per request of {host copy in, post -> done, host copy out, the server's own time from
+ * seeing the request to publishing it} (phase_us[4], may be NULL). */
 int mc_set_latency_server(mc_ctx* ctx, int enable);
-int mc_latency_server_info(mc_ctx* ctx, int* enabled, int64_t* launches, int64_t* requests);
+int mc_latency_server_info(mc_ctx* ctx, int* enabled, int64_t* launches, int64_t* requests, double* phase_us);
 
 /* The per-point modes on the reference's own float64 data (no float32 staging): MotionCompensator.
  * compensate_point_cloud / apply_motion_compensation (CSIM:1435-1480, 2086-2105) for MC_MODE_IMU,

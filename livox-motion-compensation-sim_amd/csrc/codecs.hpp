@@ -513,20 +513,10 @@ __device__ __forceinline__ int wave_scan_incl(int x) {
 }
 
 // block-wide inclusive sum over the kPcdBlock threads of a PCD workgroup
-#ifndef MC_PCD_SCAN
-#define MC_PCD_SCAN 1
-#endif
+// (DPP instead of round 3's __shfl_up loop: measure + write 872.6 vs 892.7 us, profiles/round4/s07)
 __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#if MC_PCD_SCAN
   x = wave_scan_incl(x);
-#else
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-#endif
   if (lane == 63) s_wave[wid] = x;
   __syncthreads();
   int before = 0;
@@ -542,12 +532,13 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
 
 // ---- packed line path (every value of the line |v| < 4294, ties included) ----------------------
 // The common LiDAR line is formatted from four 32-bit integers N = round(|v| * 10^6): the digits come
-// out of a 200-byte "00".."99" pair table in LDS (five 2-digit groups per value: three of the six
-// fraction digits' pairs, two of the integer part's), and each value goes to the tile's LDS text as an
-// 8-byte ". dddddd sep" field plus its [-] + 1..4 digit head (pcd_emit_pairs).  Tiles holding a line
-// with any other value (NaN, inf, |v| >= 4294) take the byte path (fmt6_prepare / pcd_emit,
-// k_pcd_write_bytes).  (Round 3's writer built the digits with multiply-shift SWAR arithmetic and
-// byte stores: 368 VALU wave-instructions per 64 lines, profiles/r16/pmc_pcd_instructions.csv.)
+// out of multiply-shift SWAR arithmetic on two 3-digit halves at once (swar_fields), and each value
+// goes to the tile's LDS text at its final byte offset (pcd_emit_line).  Tiles holding a line with
+// any other value (NaN, inf, |v| >= 4294) take the byte path (fmt6_prepare / pcd_emit,
+// k_pcd_write_bytes).  Rejected in round 4 (tools/ab_codecs.py --source batch, profiles/round4/s07,
+// measure + write): digits from a 200-byte "00".."99" LDS pair table, 909.4 vs 872.6 us (fewer VALU
+// instructions, but five dependent LDS reads per value with bank conflicts); each value's text as
+// unaligned 8-byte LDS stores with exact line boundaries, 1084.2 us.
 struct PcdFast {
   uint32_t n[4];   // round-half-even(|v| * 10^6)
   uint32_t neg;    // bit k: value k is negative (signbit)
@@ -633,45 +624,6 @@ __device__ __forceinline__ int pcd_fast_len_f32(const float c[4]) {
   return ok ? len : -1;
 }
 
-// The pair table: entry x < 100 = the two ASCII digits of x, tens in the low byte.
-constexpr int kPcdPairs = 100;
-__device__ __forceinline__ uint16_t pcd_pair_entry(uint32_t x) {
-  const uint32_t t = x / 10u;
-  return (uint16_t)((0x30u + t) | ((0x30u + x - 10u * t) << 8));
-}
-
-// unaligned LDS stores (ds_write_b32 / b64 at any byte address: the HSA runtime runs the LDS in its
-// unaligned access mode, and the compiler emits them for these 1-aligned types)
-typedef uint32_t pcd_u32_ua __attribute__((aligned(1)));
-typedef uint64_t pcd_u64_ua __attribute__((aligned(1)));
-__device__ __forceinline__ void pcd_st32(uint8_t* p, uint32_t v) { *reinterpret_cast<pcd_u32_ua*>(p) = v; }
-__device__ __forceinline__ void pcd_st64(uint8_t* p, uint64_t v) { *reinterpret_cast<pcd_u64_ua*>(p) = v; }
-
-// Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
-// zeros (byte 0 = thousands), T = ". d1 d2 d3 d4 d5 d6 sep" (bytes in text order).  Divisions by
-// constants as multiply-shifts, exact on their ranges: fp / 10^4 = (fp * 429497) >> 32 for fp < 10^6
-// (error < 6.3e-5 < 10^-4), x / 100 = (x * 5243) >> 19 for x < 43699.
-__device__ __forceinline__ void pair_fields(const uint16_t* tbl, uint32_t N, uint32_t sep, uint32_t& D, uint64_t& T) {
-  const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
-  const uint32_t p0 = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32);
-  const uint32_t r = fp - p0 * 10000u;
-  const uint32_t p1 = __umul24(r, 5243u) >> 19;
-  const uint32_t p2 = r - p1 * 100u;
-  const uint32_t q0 = __umul24(ip, 5243u) >> 19;
-  const uint32_t q1 = ip - q0 * 100u;
-  const uint32_t P0 = tbl[p0], P1 = tbl[p1], P2 = tbl[p2];
-  D = (uint32_t)tbl[q0] | ((uint32_t)tbl[q1] << 16);
-  const uint32_t A = 0x2Eu | (P0 << 8) | (P1 << 24);       // . d1 d2 d3
-  const uint32_t B = (P1 >> 8) | (P2 << 8) | (sep << 24);   // d4 d5 d6 sep
-  T = (uint64_t)A | ((uint64_t)B << 32);
-}
-
-#ifndef MC_PCD_DIGITS
-#define MC_PCD_DIGITS 1
-#endif
-#ifndef MC_PCD_EMIT
-#define MC_PCD_EMIT 1
-#endif
 // y * 41 as two shift-adds (y*9, then + y*32): the compiler folds the plain product into a
 // quarter-rate v_mul_lo_u32
 __device__ __forceinline__ uint32_t mul41(uint32_t y) {
@@ -684,8 +636,12 @@ __device__ __forceinline__ uint32_t mul41(uint32_t y) {
   return y * 41u;
 #endif
 }
-// the same fields by multiply-shift SWAR arithmetic (round 3's writer)
-__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t sep, uint32_t& D, uint64_t& T) {
+// Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
+// zeros (byte 0 = thousands), A = ". d1 d2 d3", B = "d4 d5 d6 sep" (bytes in text order).  The six
+// fraction digits come from one word holding the two 3-digit halves (multiply-shift division on both
+// 16-bit halves at once), the integer digits likewise from two 2-digit halves; bytes placed with
+// v_perm_b32.  fh = (fp * 4294968) >> 32 is fp / 1000 exactly for fp < 10^6 (error < 1.7e-4).
+__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t sep, uint32_t& D, uint32_t& A, uint32_t& B) {
   const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
   const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32);   // fp / 1000, exact
   const uint32_t y = fh | ((fp - fh * 1000u) << 16);
@@ -694,38 +650,31 @@ __device__ __forceinline__ void swar_fields(uint32_t N, uint32_t sep, uint32_t& 
   const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;
   const uint32_t ht = h | (t << 8);
   const uint32_t u = r - t * 10u;
-  const uint32_t A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;
-  const uint32_t B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);
+  A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;
+  B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);
   const uint32_t hi2 = __umul24(ip, 5243u) >> 19;
   const uint32_t y2 = hi2 | ((ip - hi2 * 100u) << 16);
   const uint32_t t2 = (__umul24(y2, 103u) >> 10) & 0x000F000Fu;
   const uint32_t u2 = y2 - t2 * 10u;
   D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;
-  T = (uint64_t)A | ((uint64_t)B << 32);
-}
-__device__ __forceinline__ void digit_fields(const uint16_t* tbl, uint32_t N, uint32_t sep, uint32_t& D, uint64_t& T) {
-#if MC_PCD_DIGITS
-  pair_fields(tbl, N, sep, D, T);
-#else
-  (void)tbl;
-  swar_fields(N, sep, D, T);
-#endif
 }
 __device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
-// round 3's emission: values in reverse order, fields stored as bytes at their final offsets, every
-// value but the line's first with its 4 digit bytes and a '-' slot (stray bytes land in the previous
-// value, written afterwards), the first value's head byte by byte
+// One value whose text starts at byte o of the tile text; EXACT: the line's first value.  The
+// fields go to LDS as bytes at their final offsets (the compiler merges a value's 12 bytes into one
+// unaligned ds_write_b96).  Values are written in reverse order, and every value but the line's first
+// stores its 4-digit field and a '-' unconditionally (at most 5 bytes before its '.'): bytes left of
+// its own head fall inside the previous value of the same line, which is written afterwards and
+// overwrites them.  The line's first value stores exactly its own bytes, so no lane ever writes
+// another line's text: no zeroing, no atomics.
 template <bool EXACT>
-__device__ __forceinline__ void bytes_value(const uint16_t* tbl, uint8_t* base, int o, uint32_t N, int nd, bool neg,
-                                            uint32_t sep) {
-  uint32_t D;
-  uint64_t T;
-  digit_fields(tbl, N, sep, D, T);
+__device__ __forceinline__ void bytes_value(uint8_t* base, int o, uint32_t N, int nd, bool neg, uint32_t sep) {
+  uint32_t D, A, B;
+  swar_fields(N, sep, D, A, B);
   uint8_t* pa = base + o + nd + (neg ? 1 : 0);   // the '.'
-  put4(pa, (uint32_t)T);
-  put4(pa + 4, (uint32_t)(T >> 32));
+  put4(pa, A);
+  put4(pa + 4, B);
   if (EXACT) {
     pa[-1] = (uint8_t)(D >> 24);
     if (nd >= 2) pa[-2] = (uint8_t)(D >> 16);
@@ -738,45 +687,14 @@ __device__ __forceinline__ void bytes_value(const uint16_t* tbl, uint8_t* base, 
   }
 }
 
-// One packed line at byte `off` of the tile text.  Exactly the line's own bytes end up written, so
-// lanes never touch each other's text (no zeroing, no atomics, no ordering between lanes):
-//   1. the first value's head ([-] + nd digits, left-aligned) as 8 bytes from `off`: its stray bytes
-//      land inside value 0's fraction field;
-//   2. values 1-3: the 4 digit bytes (leading zeros) right against the value's '.' and a '-' in the
-//      sign slot: stray bytes (<= 3) land inside the previous value's fraction field;
-//   3. the four fixed 8-byte fraction fields, which overwrite every stray byte.
-// A lane's LDS stores complete in program order.
-__device__ __forceinline__ void pcd_emit_pairs(const PcdFast& P, const uint16_t* tbl, uint8_t* base, int off) {
-#if !MC_PCD_EMIT
+// one packed line at byte `off` of the tile text
+__device__ __forceinline__ void pcd_emit_line(const PcdFast& P, uint8_t* base, int off) {
   const int o1 = off + 8 + P.nd[0] + (int)(P.neg & 1u), o2 = o1 + 8 + P.nd[1] + (int)((P.neg >> 1) & 1u);
   const int o3 = o2 + 8 + P.nd[2] + (int)((P.neg >> 2) & 1u);
-  bytes_value<false>(tbl, base, o3, P.n[3], P.nd[3], (P.neg >> 3) & 1u, '\n');
-  bytes_value<false>(tbl, base, o2, P.n[2], P.nd[2], (P.neg >> 2) & 1u, ' ');
-  bytes_value<false>(tbl, base, o1, P.n[1], P.nd[1], (P.neg >> 1) & 1u, ' ');
-  bytes_value<true>(tbl, base, off, P.n[0], P.nd[0], P.neg & 1u, ' ');
-  return;
-#endif
-  uint64_t T[4];
-  int pa[4];
-  int o = off;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t D;
-    digit_fields(tbl, P.n[k], k < 3 ? 0x20u : 0x0Au, D, T[k]);
-    const int nd = P.nd[k];
-    const bool neg = (P.neg >> k) & 1u;
-    pa[k] = o + nd + (neg ? 1 : 0);   // the '.'
-    if (k == 0) {
-      const uint64_t H = (uint64_t)(D >> (8 * (4 - nd)));   // the nd digits, left-aligned
-      pcd_st64(base + o, neg ? (H << 8) | 0x2Du : H);
-    } else {
-      pcd_st32(base + pa[k] - 4, D);
-      base[pa[k] - nd - 1] = 0x2D;    // '-': the sign slot, or a stray byte
-    }
-    o = pa[k] + 8;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pcd_st64(base + pa[k], T[k]);
+  bytes_value<false>(base, o3, P.n[3], P.nd[3], (P.neg >> 3) & 1u, '\n');
+  bytes_value<false>(base, o2, P.n[2], P.nd[2], (P.neg >> 2) & 1u, ' ');
+  bytes_value<false>(base, o1, P.n[1], P.nd[1], (P.neg >> 1) & 1u, ' ');
+  bytes_value<true>(base, off, P.n[0], P.nd[0], P.neg & 1u, ' ');
 }
 
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
@@ -908,11 +826,11 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 // modulo 16), then stored with codec_store_piece.  Tiles flagged slow are skipped
 // (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text always fits.
 __device__ __forceinline__ void pcd_tile_out(const PcdArgs& a, const PcdFast& P, bool valid, int64_t G, int* s_wave,
-                                             const uint16_t* s_pairs, uint4* s_text4) {
+                                             uint4* s_text4) {
   int total;
   const int excl = block_scan(P.len, s_wave, total) - P.len;
   const int shift = (int)(G & 15);
-  if (valid) pcd_emit_pairs(P, s_pairs, reinterpret_cast<uint8_t*>(s_text4), shift + excl);
+  if (valid) pcd_emit_line(P, reinterpret_cast<uint8_t*>(s_text4), shift + excl);
   __syncthreads();
   codec_store_piece<kPcdBlock>(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
   __syncthreads();   // s_wave / s_text are reused by the next tile
@@ -921,9 +839,7 @@ __device__ __forceinline__ void pcd_tile_out(const PcdArgs& a, const PcdFast& P,
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
-  __shared__ uint16_t s_pairs[kPcdPairs];
   __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
-  if (threadIdx.x < kPcdPairs) s_pairs[threadIdx.x] = pcd_pair_entry(threadIdx.x);   // read after block_scan's barrier
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {
@@ -951,7 +867,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       PcdFast P;
       P.len = 0;
       if (valid) pcd_fast_vals_f32(c, P);
-      pcd_tile_out(a, P, valid, G, s_wave, s_pairs, s_text4);
+      pcd_tile_out(a, P, valid, G, s_wave, s_text4);
     }
   } else {
     for (int j = 0; j < kPcdTilesPerWG; ++j) {
@@ -964,7 +880,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       P.len = 0;
       if (valid) pcd_fast(a.src, f, row, P);
       const int64_t G = a.tile_pos[u];   // issued before the scan's barrier
-      pcd_tile_out(a, P, valid, G, s_wave, s_pairs, s_text4);
+      pcd_tile_out(a, P, valid, G, s_wave, s_text4);
     }
   }
 }

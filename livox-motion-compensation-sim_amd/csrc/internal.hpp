@@ -180,6 +180,8 @@ struct mc_ctx {
   bool lat_launched = false;
   uint32_t lat_seq = 0;
   uint64_t lat_launches = 0;
+  double lat_ns[4] = {0, 0, 0, 0};   // host phases summed over requests: copy in, post -> done, copy out, device
+                                    // (server detection -> flag, from its wall clock)
   // pinned, device-mapped host buffer of the single-call drop-in path
   void* h_pin = nullptr;
   size_t pin_bytes = 0;

@@ -1077,6 +1077,7 @@ struct LatMailbox {
   int64_t n;           // rows of the request (<= the buffers' capacity)
   double rpy[3];
   double t[3];
+  uint64_t dev_ticks[2];   // server: wall clock when it saw the request / when it published seq_done
 };
 constexpr int kLatThreads = 1024;
 
@@ -1109,6 +1110,7 @@ __global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, cons
         __builtin_amdgcn_s_sleep(1);
       }
       if (go) {
+        __hip_atomic_store(&mb->dev_ticks[0], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const double rr = __hip_atomic_load(&mb->rpy[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const double rp = __hip_atomic_load(&mb->rpy[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const double ry = __hip_atomic_load(&mb->rpy[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1132,9 +1134,12 @@ __global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, cons
       *reinterpret_cast<double2*>(out + 4 * i) = double2{R0 * x + R1 * y + R2 * z + tx, R3 * x + R4 * y + R5 * z + ty};
       *reinterpret_cast<double2*>(out + 4 * i + 2) = double2{R6 * x + R7 * y + R8 * z + tz, p23.y};
     }
-    __threadfence_system();   // this lane's rows are visible to the host before the flag below
+    // every lane's row stores acknowledged, then one system-scope release (one L2 write-back for the
+    // workgroup instead of one per wave) before the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
+      __hip_atomic_store(&mb->dev_ticks[1], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&mb->seq_done, s_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       seen = s_seq;
     }

@@ -1148,17 +1148,21 @@ int mc_set_latency_server(mc_ctx* c, int enable) {
   return MC_OK;
 }
 
-int mc_latency_server_info(mc_ctx* c, int* enabled, int64_t* launches, int64_t* requests) {
+int mc_latency_server_info(mc_ctx* c, int* enabled, int64_t* launches, int64_t* requests, double* phase_us) {
   CHECK_ARG(c, "ctx is NULL");
   if (enabled) *enabled = c->lat_on ? 1 : 0;
   if (launches) *launches = (int64_t)c->lat_launches;
   if (requests) *requests = (int64_t)c->lat_seq;
+  if (phase_us)
+    for (int k = 0; k < 4; ++k) phase_us[k] = c->lat_seq ? c->lat_ns[k] / 1e3 / (double)c->lat_seq : 0.0;
   return MC_OK;
 }
 
 // one transform_pointcloud request through the server (n <= kLatRows)
 static int lat_transform(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
                          const double* translation, double* out) {
+  using clk = std::chrono::steady_clock;
+  const auto h0 = clk::now();
   LatMailbox* mb = lat_mailbox(c);
   double* in = lat_in(c);
   if (ld == 4) std::memcpy(in, points, (size_t)n * 32);
@@ -1169,6 +1173,7 @@ static int lat_transform(mc_ctx* c, const double* points, int64_t n, int64_t ld,
   if (!c->lat_launched || __atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) == 0)
     if (int r = lat_launch(c)) return r;
   const uint32_t seq = ++c->lat_seq;
+  const auto h1 = clk::now();
   __atomic_store_n(&mb->seq_req, seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spins = 0;; ++spins) {
@@ -1186,7 +1191,15 @@ static int lat_transform(mc_ctx* c, const double* points, int64_t n, int64_t ld,
       return fail(MC_ERR_HIP, "latency server did not answer request %u within %.1f s", seq, kLatAnswerS);
     }
   }
+  const auto h2 = clk::now();
   std::memcpy(out, lat_out(c), (size_t)n * 32);
+  const auto h3 = clk::now();
+  auto ns = [](clk::duration d) { return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
+  c->lat_ns[0] += ns(h1 - h0);
+  c->lat_ns[1] += ns(h2 - h1);
+  c->lat_ns[2] += ns(h3 - h2);
+  c->lat_ns[3] += (double)(__atomic_load_n(&mb->dev_ticks[1], __ATOMIC_RELAXED) -
+                           __atomic_load_n(&mb->dev_ticks[0], __ATOMIC_RELAXED)) * 1e6 / c->wall_khz;
   return MC_OK;
 }
 

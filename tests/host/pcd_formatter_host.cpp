@@ -63,11 +63,9 @@ int main(int argc, char** argv) {
   }
   const CodecFrames s{pts.data()};
   std::vector<uint32_t> buf(16400 / 4 + 4);
-  uint16_t tbl[kPcdPairs];
-  for (uint32_t i = 0; i < (uint32_t)kPcdPairs; ++i) tbl[i] = pcd_pair_entry(i);
-  // the multiply-shift divisions of pair_fields on their whole ranges
+  // the multiply-shift divisions of swar_fields on their whole ranges
   for (uint32_t fp = 0; fp < 1000000u; ++fp)
-    if ((uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32) != fp / 10000u) { ++bad; break; }
+    if ((uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32) != fp / 1000u) { ++bad; break; }
   for (uint32_t x = 0; x < 10000u; ++x)
     if ((__umul24(x, 5243u) >> 19) != x / 100u) { ++bad; break; }
   long lines = 0, fast = 0, f32_lines = 0;
@@ -138,7 +136,7 @@ int main(int argc, char** argv) {
       want += line;
     }
     for (int l = 255; l >= 0; --l)
-      if (P[l].ok) pcd_emit_pairs(P[l], tbl, reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
+      if (P[l].ok) pcd_emit_line(P[l], reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
     const std::string got(reinterpret_cast<const char*>(buf.data()) + shift, off - shift);
     // nothing written outside the tile's text
     const unsigned char* bb = reinterpret_cast<const unsigned char*>(buf.data());
