@@ -1099,25 +1099,35 @@ __global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, cons
       // once a request is seen
       for (;;) {
         r = __hip_atomic_load(&mb->seq_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t q = __hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // same trip
         if (r != seen) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
           go = 1;
           break;
         }
-        if (__hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        if (q) break;
         const uint64_t now = wall_clock64();
         if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
         __builtin_amdgcn_s_sleep(1);
       }
       if (go) {
         __hip_atomic_store(&mb->dev_ticks[0], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const double rr = __hip_atomic_load(&mb->rpy[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const double rp = __hip_atomic_load(&mb->rpy[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const double ry = __hip_atomic_load(&mb->rpy[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        euler_xyz_matrix(rr, rp, ry, s_R);
+        // the request's parameters: all seven loads in flight together (one PCIe round trip), then
+        // R (LMC:774) with the prep's short-latency sincos
+        double v[7];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) s_R[9 + k] = __hip_atomic_load(&mb->t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        s_n = __hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 0; k < 3; ++k) {
+          v[k] = __hip_atomic_load(&mb->rpy[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          v[3 + k] = __hip_atomic_load(&mb->t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        const int64_t n = __hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        double R[9];
+        euler_xyz_matrix_prep(v[0], v[1], v[2], R);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) s_R[k] = R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s_R[9 + k] = v[3 + k];
+        s_n = n;
       }
       s_seq = r;
       s_go = go;
