@@ -246,8 +246,9 @@ int mc_transform_pointcloud_f64(mc_ctx* ctx, const double* points, int64_t n, in
  * polls a mailbox in pinned host memory, so a call pays no kernel launch and no completion signal.
  * It returns after 50 ms without a request (relaunched on the next call), after 2 s in all, and on
  * disable / mc_destroy.  info: enabled flag, server launches, requests served, and the mean
- * microseconds per request of {host copy in, post -> done, host copy out, the server's own time from
- * seeing the request to publishing it} (phase_us[4], may be NULL). */
+ * microseconds per request of {host copy in, post -> done, host copy out (host clock); the server's
+ * time from seeing the request to rows + parameters loaded and R formed, and from there to every row
+ * stored and acknowledged (device clock)} (phase_us[5], may be NULL). */
 int mc_set_latency_server(mc_ctx* ctx, int enable);
 int mc_latency_server_info(mc_ctx* ctx, int* enabled, int64_t* launches, int64_t* requests, double* phase_us);
 

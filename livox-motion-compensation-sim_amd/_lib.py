@@ -167,3 +167,13 @@ def ptr(a, ctype):
     if a is None:
         return None
     return a.ctypes.data_as(POINTER(ctype))
+
+
+def fptr(a, ctype):
+    """ptr() for the per-call latency path: a ctype instance over a's buffer, which POINTER(ctype)
+    argtypes pass by reference (~0.7 us instead of ~2.7 us for data_as); read-only or empty arrays
+    take ptr()."""
+    try:
+        return ctype.from_buffer(a)
+    except (TypeError, ValueError):
+        return ptr(a, ctype)

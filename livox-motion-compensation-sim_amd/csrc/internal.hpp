@@ -180,7 +180,8 @@ struct mc_ctx {
   bool lat_launched = false;
   uint32_t lat_seq = 0;
   uint64_t lat_launches = 0;
-  double lat_ns[4] = {0, 0, 0, 0};   // host phases summed over requests: copy in, post -> done, copy out, device
+  double lat_ns[5] = {0, 0, 0, 0, 0};   // summed over requests: copy in, post -> done, copy out (host clock);
+                                        // server load (rows + parameters + R), server store (device clock)
                                     // (server detection -> flag, from its wall clock)
   // pinned, device-mapped host buffer of the single-call drop-in path
   void* h_pin = nullptr;

@@ -1070,16 +1070,25 @@ __global__ __launch_bounds__(kBlock) void k_transform_host_f64(const double* __r
 // mc_destroy); the host relaunches it on the next request (alive == 0).  Only vector memory
 // instructions touch the mailbox (atomic loads / stores at system scope).
 struct LatMailbox {
+  // line 0, written by the host and polled by the server: one poll fetches the request number, the
+  // stop flag and the row count together
   uint32_t seq_req;    // host: number of the posted request
-  uint32_t seq_done;   // server: number of the last finished request
-  uint32_t alive;      // host 2 at launch, server 1 while polling, 0 on exit
   uint32_t quit;       // host: stop now
-  int64_t n;           // rows of the request (<= the buffers' capacity)
+  int64_t n_tag;       // host: (seq_req << 32) | rows of the request (<= the buffers' capacity)
   double rpy[3];
   double t[3];
-  uint64_t dev_ticks[2];   // server: wall clock when it saw the request / when it published seq_done
+  // line 1, written by the server
+  alignas(64) uint32_t seq_done;   // number of the last finished request
+  uint32_t alive;                  // host 2 at launch, server 1 while polling, 0 on exit
+  uint64_t dev_ticks[4];           // wall clock: request seen / rows + parameters loaded / rows stored / done
 };
 constexpr int kLatThreads = 1024;
+constexpr int kLatRowsPerLane = 4;                       // rows in flight per lane
+constexpr int kLatChunk = kLatThreads * kLatRowsPerLane;
+
+__device__ __forceinline__ void lat_tick(LatMailbox* mb, int k) {
+  __hip_atomic_store(&mb->dev_ticks[k], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, const double* __restrict__ in,
                                                             double* __restrict__ out, uint32_t seen,
@@ -1095,11 +1104,13 @@ __global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, cons
     if (threadIdx.x == 0) {
       int go = 0;
       uint32_t r = seen;
+      int64_t nt = 0;
       // relaxed polls (uncached system-scope loads, no cache invalidation per poll), one acquire fence
       // once a request is seen
       for (;;) {
         r = __hip_atomic_load(&mb->seq_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t q = __hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // same trip
+        nt = __hip_atomic_load(&mb->n_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (r != seen) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
           go = 1;
@@ -1111,23 +1122,11 @@ __global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, cons
         __builtin_amdgcn_s_sleep(1);
       }
       if (go) {
-        __hip_atomic_store(&mb->dev_ticks[0], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // the request's parameters: all seven loads in flight together (one PCIe round trip), then
-        // R (LMC:774) with the prep's short-latency sincos
-        double v[7];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          v[k] = __hip_atomic_load(&mb->rpy[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          v[3 + k] = __hip_atomic_load(&mb->t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        const int64_t n = __hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        double R[9];
-        euler_xyz_matrix_prep(v[0], v[1], v[2], R);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) s_R[k] = R[k];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) s_R[9 + k] = v[3 + k];
-        s_n = n;
+        lat_tick(mb, 0);
+        // the row count came with the poll; a count tagged with an older request (the poll's loads
+        // are unordered) is read again after the acquire
+        if ((uint32_t)((uint64_t)nt >> 32) != r) nt = __hip_atomic_load(&mb->n_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_n = nt & 0xffffffffLL;
       }
       s_seq = r;
       s_go = go;
@@ -1135,21 +1134,56 @@ __global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, cons
     __syncthreads();
     if (!s_go) break;
     const int64_t n = s_n;
-    const double R0 = s_R[0], R1 = s_R[1], R2 = s_R[2], R3 = s_R[3], R4 = s_R[4], R5 = s_R[5], R6 = s_R[6],
-                 R7 = s_R[7], R8 = s_R[8], tx = s_R[9], ty = s_R[10], tz = s_R[11];
-    for (int64_t i = threadIdx.x; i < n; i += kLatThreads) {
-      const double2 p01 = *reinterpret_cast<const double2*>(in + 4 * i);
-      const double2 p23 = *reinterpret_cast<const double2*>(in + 4 * i + 2);
-      const double x = p01.x, y = p01.y, z = p23.x;
-      *reinterpret_cast<double2*>(out + 4 * i) = double2{R0 * x + R1 * y + R2 * z + tx, R3 * x + R4 * y + R5 * z + ty};
-      *reinterpret_cast<double2*>(out + 4 * i + 2) = double2{R6 * x + R7 * y + R8 * z + tz, p23.y};
+    // the parameters (lane 0) and every lane's first rows are in flight together: one PCIe round trip
+    double v[6];
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        v[k] = __hip_atomic_load(&mb->rpy[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        v[3 + k] = __hip_atomic_load(&mb->t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    double R0 = 0, R1 = 0, R2 = 0, R3 = 0, R4 = 0, R5 = 0, R6 = 0, R7 = 0, R8 = 0, tx = 0, ty = 0, tz = 0;
+    for (int64_t base = 0; base < n; base += kLatChunk) {
+      double2 a[kLatRowsPerLane], b[kLatRowsPerLane];
+#pragma unroll
+      for (int j = 0; j < kLatRowsPerLane; ++j) {
+        const int64_t i = base + j * kLatThreads + threadIdx.x;
+        if (i < n) {
+          a[j] = *reinterpret_cast<const double2*>(in + 4 * i);
+          b[j] = *reinterpret_cast<const double2*>(in + 4 * i + 2);
+        }
+      }
+      if (base == 0) {   // R (LMC:774) with the prep's short-latency sincos, shared through LDS
+        if (threadIdx.x == 0) {
+          double R[9];
+          euler_xyz_matrix_prep(v[0], v[1], v[2], R);
+#pragma unroll
+          for (int k = 0; k < 9; ++k) s_R[k] = R[k];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) s_R[9 + k] = v[3 + k];
+          lat_tick(mb, 1);
+        }
+        __syncthreads();
+        R0 = s_R[0], R1 = s_R[1], R2 = s_R[2], R3 = s_R[3], R4 = s_R[4], R5 = s_R[5], R6 = s_R[6], R7 = s_R[7];
+        R8 = s_R[8], tx = s_R[9], ty = s_R[10], tz = s_R[11];
+      }
+#pragma unroll
+      for (int j = 0; j < kLatRowsPerLane; ++j) {
+        const int64_t i = base + j * kLatThreads + threadIdx.x;
+        if (i < n) {
+          const double x = a[j].x, y = a[j].y, z = b[j].x;
+          *reinterpret_cast<double2*>(out + 4 * i) = double2{R0 * x + R1 * y + R2 * z + tx, R3 * x + R4 * y + R5 * z + ty};
+          *reinterpret_cast<double2*>(out + 4 * i + 2) = double2{R6 * x + R7 * y + R8 * z + tz, b[j].y};
+        }
+      }
     }
     // every lane's row stores acknowledged, then one system-scope release (one L2 write-back for the
     // workgroup instead of one per wave) before the flag
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      __hip_atomic_store(&mb->dev_ticks[1], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      lat_tick(mb, 2);
       __hip_atomic_store(&mb->seq_done, s_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       seen = s_seq;
     }

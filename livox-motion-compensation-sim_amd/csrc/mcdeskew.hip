@@ -1090,6 +1090,7 @@ static double* lat_out(mc_ctx* c) { return lat_in(c) + 4 * kLatRows; }
 
 // (re)launch the server: it takes requests numbered after the last finished one
 static int lat_launch(mc_ctx* c) {
+  DeviceGuard g(c->device);
   LatMailbox* mb = lat_mailbox(c);
   if (c->wall_khz <= 0.0) {
     int khz = 0;
@@ -1154,7 +1155,7 @@ int mc_latency_server_info(mc_ctx* c, int* enabled, int64_t* launches, int64_t* 
   if (launches) *launches = (int64_t)c->lat_launches;
   if (requests) *requests = (int64_t)c->lat_seq;
   if (phase_us)
-    for (int k = 0; k < 4; ++k) phase_us[k] = c->lat_seq ? c->lat_ns[k] / 1e3 / (double)c->lat_seq : 0.0;
+    for (int k = 0; k < 5; ++k) phase_us[k] = c->lat_seq ? c->lat_ns[k] / 1e3 / (double)c->lat_seq : 0.0;
   return MC_OK;
 }
 
@@ -1167,12 +1168,13 @@ static int lat_transform(mc_ctx* c, const double* points, int64_t n, int64_t ld,
   double* in = lat_in(c);
   if (ld == 4) std::memcpy(in, points, (size_t)n * 32);
   else for (int64_t i = 0; i < n; ++i) std::memcpy(in + 4 * i, points + i * ld, 32);
-  mb->n = n;
+  const uint32_t seq = (uint32_t)c->lat_seq + 1;
+  mb->n_tag = (int64_t)((uint64_t)seq << 32 | (uint64_t)n);
   for (int k = 0; k < 3; ++k) { mb->rpy[k] = rpy[k]; mb->t[k] = translation[k]; }
   // an instance that has returned (idle / lifetime) is relaunched before the request is posted
   if (!c->lat_launched || __atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) == 0)
     if (int r = lat_launch(c)) return r;
-  const uint32_t seq = ++c->lat_seq;
+  ++c->lat_seq;
   const auto h1 = clk::now();
   __atomic_store_n(&mb->seq_req, seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
@@ -1198,8 +1200,9 @@ static int lat_transform(mc_ctx* c, const double* points, int64_t n, int64_t ld,
   c->lat_ns[0] += ns(h1 - h0);
   c->lat_ns[1] += ns(h2 - h1);
   c->lat_ns[2] += ns(h3 - h2);
-  c->lat_ns[3] += (double)(__atomic_load_n(&mb->dev_ticks[1], __ATOMIC_RELAXED) -
-                           __atomic_load_n(&mb->dev_ticks[0], __ATOMIC_RELAXED)) * 1e6 / c->wall_khz;
+  for (int k = 0; k < 2; ++k)
+    c->lat_ns[3 + k] += (double)(__atomic_load_n(&mb->dev_ticks[k + 1], __ATOMIC_RELAXED) -
+                                 __atomic_load_n(&mb->dev_ticks[k], __ATOMIC_RELAXED)) * 1e6 / c->wall_khz;
   return MC_OK;
 }
 
@@ -1210,8 +1213,8 @@ int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int6
   if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 1 with size %lld", (long long)ld);
   if (n == 0) return MC_OK;
   CHECK_ARG(points && out, "NULL points / out");
+  if (c->lat_on && n <= kLatRows) return lat_transform(c, points, n, ld, rpy, translation, out);   // no HIP call
   DeviceGuard g(c->device);
-  if (c->lat_on && n <= kLatRows) return lat_transform(c, points, n, ld, rpy, translation, out);
   if (n >= kZeroCopyRows) {                     // large: the DMA row pipeline with one frame
     if (int r = sync_all(c)) return r;
     void* st = nullptr;

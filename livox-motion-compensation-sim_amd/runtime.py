@@ -181,11 +181,12 @@ class Context:
 
     def latency_server_info(self) -> dict:
         e, la, rq = c_int(), c_int64(), c_int64()
-        ph = np.zeros(4, np.float64)
+        ph = np.zeros(5, np.float64)
         check(self.lib.mc_latency_server_info(self.handle, ctypes.byref(e), ctypes.byref(la), ctypes.byref(rq),
                                               ptr(ph, c_double)), "latency_server_info")
         return {"enabled": bool(e.value), "launches": la.value, "requests": rq.value,
-                "mean_us": {"copy_in": ph[0], "post_to_done": ph[1], "copy_out": ph[2], "server": ph[3]}}
+                "mean_us": {"copy_in": ph[0], "post_to_done": ph[1], "copy_out": ph[2], "server_load": ph[3],
+                            "server_store": ph[4], "server": ph[3] + ph[4]}}
 
     def set_max_grid(self, max_grid: int):
         check(self.lib.mc_set_launch(self.handle, int(max_grid)), "set_launch")

@@ -29,7 +29,7 @@ from . import _lib
 from . import codecs as _codecs
 from . import config as _config
 from . import trajectory as _traj
-from ._lib import check, ptr
+from ._lib import check, fptr, ptr
 from .runtime import Context, default_context, deskew_points_f64
 
 
@@ -94,9 +94,10 @@ class LiDARMotionSimulator:
         p = np.ascontiguousarray(points, dtype=np.float64)
         out = np.empty((p.shape[0], 4))
         ctx = self.context
-        check(ctx.lib.mc_transform_pointcloud_f64(ctx.handle, ptr(p, c_double), p.shape[0], p.shape[1],
-                                                  ptr(rot, c_double), ptr(trans, c_double), ptr(out, c_double)),
-              "transform_pointcloud")
+        rc = ctx.lib.mc_transform_pointcloud_f64(ctx.handle, fptr(p, c_double), p.shape[0], p.shape[1],
+                                                 fptr(rot, c_double), fptr(trans, c_double), fptr(out, c_double))
+        if rc:
+            check(rc, "transform_pointcloud")
         return out
 
     def align_frames(self, frames: List[np.ndarray], transformations: List[dict]) -> List[np.ndarray]:

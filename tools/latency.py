@@ -119,6 +119,22 @@ def main():
             ctx0.lib.mc_transform_pointcloud_f64(ctx0.handle, pt0(pts, c_double), pts.shape[0], 4, pt0(rot, c_double),
                                                  pt0(tra, c_double), pt0(o, c_double))
         out["latency_server"]["c_call_only_us"] = timed(raw, args.calls) * 1e6
+        # the Python wrapper alone: the same call into a C no-op with the same argtypes
+        import ctypes
+        noop = ctypes.CDLL(None).labs
+        noop.argtypes = ctx0.lib.mc_transform_pointcloud_f64.argtypes
+        noop.restype = ctypes.c_int
+
+        class _Lib:
+            mc_transform_pointcloud_f64 = noop
+
+        class _Ctx:
+            lib, handle = _Lib(), None
+
+        fake = mc.LiDARMotionSimulator({"duration": 120.0, "trajectory_type": "figure_eight", "lidar_fps": 10},
+                                       context=_Ctx())
+        out["latency_server"]["python_wrapper_only_us"] = timed(lambda: fake.transform_pointcloud(pts, pose),
+                                                                args.calls) * 1e6
         lat = []
         for _ in range(5):   # after an idle gap past the server's 50 ms: one relaunch per call
             time.sleep(0.12)
