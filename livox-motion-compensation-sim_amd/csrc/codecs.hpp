@@ -70,12 +70,12 @@ __device__ __forceinline__ int32_t codec_frame_of(const CodecFrames& s, int64_t 
   if (s.n_units > 0) {
     int64_t g = u * s.F / s.n_units;   // u < 2^31 and F < 2^31: no overflow
     g = g < s.F - 1 ? g : s.F - 1;
-    if (unit_off[g] <= u && u < unit_off[g + 1]) return (int32_t)g;
+    if (ldu(unit_off + g) <= u && u < ldu(unit_off + g + 1)) return (int32_t)g;
   }
   int32_t lo = 0, hi = s.F + 1;
   while (lo < hi) {
     const int32_t mid = (lo + hi) >> 1;
-    if (unit_off[mid] <= u) lo = mid + 1; else hi = mid;
+    if (ldu(unit_off + mid) <= u) lo = mid + 1; else hi = mid;
   }
   return lo - 1;
 }
@@ -102,7 +102,7 @@ __device__ __forceinline__ void codec_point(const CodecFrames& s, int32_t f, int
 
 // advance a workgroup-uniform frame cursor to unit u (units of a workgroup are consecutive)
 __device__ __forceinline__ int32_t codec_advance(const int64_t* __restrict__ unit_off, int32_t f, int64_t u) {
-  while (unit_off[f + 1] <= u) ++f;
+  while (ldu(unit_off + f + 1) <= u) ++f;
   return f;
 }
 
@@ -494,8 +494,9 @@ __device__ __forceinline__ void pcd_emit(const PcdLine& L, char* p) {
 
 __device__ __forceinline__ int64_t pcd_row(const CodecFrames& s, int64_t u, int32_t& f, bool& valid) {
   f = codec_advance(s.unit_off, f, u);
-  const int64_t row = s.doff[f] + (u - s.unit_off[f]) * kPcdBlock + threadIdx.x;
-  valid = row < s.doff[f + 1];
+  const int64_t d0 = ldu(s.doff + f), d1 = ldu(s.doff + f + 1);
+  const int64_t row = d0 + (u - ldu(s.unit_off + f)) * kPcdBlock + threadIdx.x;
+  valid = row < d1;
   return row;
 }
 
@@ -723,7 +724,7 @@ constexpr int32_t kPcdSlowTile = 1 << 30;
 
 // columns 0..3 of dense row `row` of a batch source as float32 (codec_point widens them)
 __device__ __forceinline__ void codec_point_f32(const CodecFrames& s, int32_t f, int64_t row, float c[4]) {
-  const float* q = s.cols + bidx(s.C, 0, s.poff[f] + (row - s.doff[f]));
+  const float* q = s.cols + bidx(s.C, 0, ldu(s.poff + f) + (row - ldu(s.doff + f)));
   c[0] = q[0]; c[1] = q[kBlkPts]; c[2] = q[2 * kBlkPts]; c[3] = q[3 * kBlkPts];
 }
 
@@ -825,13 +826,16 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 // Packed tiles: every line is formatted into the tile's LDS text (which sits at its HBM offset
 // modulo 16), then stored with codec_store_piece.  Tiles flagged slow are skipped
 // (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text always fits.
-__device__ __forceinline__ void pcd_tile_out(const PcdArgs& a, const PcdFast& P, bool valid, int64_t G, int* s_wave,
-                                             uint4* s_text4) {
+// pcd_tile_text: the tile's lines in LDS, -> the tile's text bytes; pcd_tile_store: its stores.
+__device__ __forceinline__ int pcd_tile_text(const PcdFast& P, bool valid, int64_t G, int* s_wave, uint4* s_text4) {
   int total;
   const int excl = block_scan(P.len, s_wave, total) - P.len;
-  const int shift = (int)(G & 15);
-  if (valid) pcd_emit_line(P, reinterpret_cast<uint8_t*>(s_text4), shift + excl);
+  if (valid) pcd_emit_line(P, reinterpret_cast<uint8_t*>(s_text4), (int)(G & 15) + excl);
   __syncthreads();
+  return total;
+}
+__device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int total, const uint4* s_text4) {
+  const int shift = (int)(G & 15);
   codec_store_piece<kPcdBlock>(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
   __syncthreads();   // s_wave / s_text are reused by the next tile
 }
@@ -843,44 +847,55 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {
-    // tile j + 1's loads are in flight while tile j is formatted and stored: one HBM round trip
-    // per workgroup instead of one per tile
+    // Tile j + 1's loads are in flight while tile j is formatted, and converted (pcd_fast_vals_f32)
+    // between tile j's LDS text and its stores.  vmcnt counts stores as well as loads, and a load
+    // consumed with stores in flight waits for them too: consumed after tile j's stores, it would
+    // wait for their completion; consumed before them, it waits only for tile j - 1's, long done.
+    // One call site and no branch around it, so no path carries a load into the next iteration.
     const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
     float cn[4] = {0.f, 0.f, 0.f, 0.f};
     bool vn = false;
     int32_t flag_n = 0;
     int64_t gn = 0;
+    PcdFast Pn;
     auto fetch = [&](int64_t u) {
       const int64_t row = pcd_row(a.src, u, f, vn);
       if (vn) codec_point_f32(a.src, f, row, cn);
-      flag_n = a.tile_bytes[u];
-      gn = a.tile_pos[u];
+      flag_n = ldu(a.tile_bytes + u);
+      gn = ldu(a.tile_pos + u);
+    };
+    auto convert = [&]() {
+      pcd_fast_vals_f32(cn, Pn);   // (invalid lanes convert zeros / stale values: length zeroed)
+      if (!vn) Pn.len = 0;
+      // pins the conversion here: the compiler would otherwise sink it below the stores, to its use
+      asm volatile("" ::"v"(Pn.n[0]), "v"(Pn.n[1]), "v"(Pn.n[2]), "v"(Pn.n[3]), "v"(Pn.len), "v"(Pn.neg) : "memory");
     };
     if (u0 < u_end) fetch(u0);
+    convert();
     for (int64_t u = u0; u < u_end; ++u) {
-      const float c[4] = {cn[0], cn[1], cn[2], cn[3]};
+      const PcdFast P = Pn;
       const bool valid = vn;
-      const int32_t flag = flag_n;
+      const bool packed = !(flag_n & kPcdSlowTile);   // workgroup-uniform
       const int64_t G = gn;
       if (u + 1 < u_end) fetch(u + 1);
-      if (flag & kPcdSlowTile) continue;   // workgroup-uniform
-      PcdFast P;
-      P.len = 0;
-      if (valid) pcd_fast_vals_f32(c, P);
-      pcd_tile_out(a, P, valid, G, s_wave, s_text4);
+      int total = 0;
+      if (packed) total = pcd_tile_text(P, valid, G, s_wave, s_text4);
+      convert();
+      if (packed) pcd_tile_store(a, G, total, s_text4);
     }
   } else {
     for (int j = 0; j < kPcdTilesPerWG; ++j) {
       const int64_t u = u0 + j;
       if (u >= a.src.n_units) break;
-      if (a.tile_bytes[u] & kPcdSlowTile) continue;   // workgroup-uniform
+      if (ldu(a.tile_bytes + u) & kPcdSlowTile) continue;   // workgroup-uniform
       bool valid;
       const int64_t row = pcd_row(a.src, u, f, valid);
       PcdFast P;
       P.len = 0;
       if (valid) pcd_fast(a.src, f, row, P);
-      const int64_t G = a.tile_pos[u];   // issued before the scan's barrier
-      pcd_tile_out(a, P, valid, G, s_wave, s_text4);
+      const int64_t G = ldu(a.tile_pos + u);
+      const int total = pcd_tile_text(P, valid, G, s_wave, s_text4);
+      pcd_tile_store(a, G, total, s_text4);
     }
   }
 }
@@ -918,6 +933,200 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write_bytes(const PcdArgs a, 
       pcd_emit(L, a.out + G + excl);
     }
     __syncthreads();   // s_wave / s_text are reused by the next tile
+  }
+}
+
+
+// ---- single pass (batch source): measure, scan and write in one launch -------------------------
+// Workgroups take partitions of kPcdTilesPerWG consecutive tiles in ticket order (one atomic per
+// workgroup).  A partition loads all its values, forms its lines' lengths, publishes its text bytes
+// and finds its offset by decoupled look-back over the predecessors' published sums (Merrill &
+// Garland 2016, single-pass prefix scan), then formats and stores its tiles.  Ticket order is the
+// scan order, so every partition a workgroup waits on holds an earlier ticket: its workgroup is
+// already resident and never waits on a later one.  The text needs one read of the values instead of
+// the measure pass's read plus the write pass's (16 B/pt), and no host round trip for the offsets.
+struct PcdScanArgs {
+  unsigned long long* status;   // [n_parts] flag << 62 | bytes (zeroed before the launch)
+  unsigned int* ticket;         // zeroed before the launch
+  int64_t* body_pos;            // [F + 1]: first byte of each frame with tiles; [F] = total bytes
+  int64_t cap;                  // text buffer bytes: a tile that would end beyond it is not stored
+};
+constexpr unsigned long long kScanAgg = 1ull << 62;    // the partition's own bytes
+constexpr unsigned long long kScanIncl = 2ull << 62;   // bytes of partitions 0 .. p
+constexpr unsigned long long kScanVal = kScanAgg - 1;
+
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Wave 0 of partition p: publishes agg, returns the bytes of partitions 0 .. p - 1 (every lane).
+// Waits are bounded (the predecessors publish right after their loads, so a correct launch waits
+// microseconds): past ~2^22 polls the launch is reported broken through *err instead of hanging.
+__device__ __forceinline__ int64_t pcd_lookback(unsigned long long* status, int64_t p, int64_t agg, int* err) {
+  const int lane = threadIdx.x & 63;
+  if (p == 0) {
+    if (lane == 0) __hip_atomic_store(status, kScanIncl | (unsigned long long)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(status + p, kScanAgg | (unsigned long long)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int64_t excl = 0;
+  uint32_t polls = 0;
+  for (int64_t end = p - 1;; end -= 64) {   // window: partitions end, end - 1, .., end - 63 (lane order)
+    const int64_t idx = end - lane;
+    unsigned long long v = idx >= 0 ? 0ull : kScanIncl;   // before partition 0: an inclusive zero
+    for (;;) {
+      if ((v >> 62) == 0) v = __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t nr = __builtin_amdgcn_ballot_w64((v >> 62) == 0);
+      const uint64_t inc = __builtin_amdgcn_ballot_w64((v >> 62) == 2);
+      const uint64_t low = inc & (~inc + 1);                 // the nearest inclusive predecessor
+      const uint64_t upto = inc ? (low | (low - 1)) : ~0ull;  // lanes that count
+      if ((nr & upto) == 0) {
+        const int64_t val = (upto >> lane) & 1 ? (int64_t)(v & kScanVal) : 0;
+        excl += wave_sum64(val);
+        if (inc) {
+          if (lane == 0)
+            __hip_atomic_store(status + p, kScanIncl | (unsigned long long)(excl + agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          return excl;
+        }
+        break;   // no inclusive sum in this window: the next 64 predecessors
+      }
+      if (++polls > (1u << 22)) {
+        if (lane == 0) *err = 2;
+        return excl;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
+// byte-path line of (float32) values c: pcd_line's formatting on the widened values
+__device__ __forceinline__ void pcd_line_vals(const float c[4], PcdLine& L, int* err) {
+  L.len = 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    L.v[k] = fmt6_prepare((double)c[k]);
+    if (L.v[k].kind == 3) *err = 1;
+    L.len += L.v[k].len;
+  }
+}
+
+__global__ __launch_bounds__(kPcdBlock) void k_pcd_encode(const PcdArgs a, const PcdScanArgs sc) {
+  constexpr int T = kPcdTilesPerWG;
+  __shared__ int s_wave[T][kPcdBlock / 64];
+  __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
+  __shared__ unsigned int s_ticket;
+  __shared__ int64_t s_base;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_ticket = atomicAdd(sc.ticket, 1u);
+  __syncthreads();
+  const int64_t p = s_ticket;
+  const int64_t u0 = p * T;
+  // all of the partition's values first: one HBM round trip
+  int32_t f = codec_frame_of(a.src, u0);
+  int32_t fr[T];
+  float c[T][4];
+  bool valid[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const int64_t u = u0 + j;
+    valid[j] = false;
+    fr[j] = -1;
+    c[j][0] = c[j][1] = c[j][2] = c[j][3] = 0.f;
+    if (u < a.src.n_units) {
+      const int64_t row = pcd_row(a.src, u, f, valid[j]);
+      fr[j] = f;
+      if (valid[j]) codec_point_f32(a.src, f, row, c[j]);
+    }
+  }
+  // line lengths (packed path), -1 outside it
+  int len[T];
+  bool slow = false;
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    len[j] = valid[j] ? pcd_fast_len_f32(c[j]) : 0;
+    slow = slow || len[j] < 0;
+  }
+  slow = __syncthreads_or(slow) != 0;   // workgroup-uniform: the whole partition takes the byte path
+  if (slow) {
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      PcdLine L;
+      L.len = 0;
+      if (valid[j]) pcd_line_vals(c[j], L, a.err);
+      len[j] = L.len;
+    }
+  }
+  // the T tiles' in-tile offsets: T block scans side by side
+  int excl[T], tot[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const int x = wave_scan_incl(len[j]);
+    excl[j] = x - len[j];
+    if (lane == 63) s_wave[j][wid] = x;
+  }
+  __syncthreads();
+  int64_t agg = 0;
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    int before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kPcdBlock / 64; ++w) {
+      const int cw = s_wave[j][w];
+      before += w < wid ? cw : 0;
+      total += cw;
+    }
+    excl[j] += before;
+    tot[j] = total;
+    agg += total;
+  }
+  if (wid == 0) {
+    const int64_t base = pcd_lookback(sc.status, p, agg, a.err);
+    if (lane == 0) s_base = base;
+  }
+  __syncthreads();
+  int64_t G = s_base;
+  if (threadIdx.x == 0) {
+    // frame offsets: a frame's first tile writes its start; the last partition the total
+    int64_t g = G;
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+      const int64_t u = u0 + j;
+      if (u < a.src.n_units && ldu(a.src.unit_off + fr[j]) == u) sc.body_pos[fr[j]] = g;
+      g += tot[j];
+    }
+    if (u0 + T >= a.src.n_units) sc.body_pos[a.src.F] = g;
+  }
+  char* const s_text = reinterpret_cast<char*>(s_text4);
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    if (u0 + j >= a.src.n_units) break;   // workgroup-uniform
+    const int shift = (int)(G & 15);
+    const bool fits = G + tot[j] <= sc.cap;
+    if (!slow) {
+      PcdFast P;
+      if (valid[j]) {
+        pcd_fast_vals_f32(c[j], P);
+        pcd_emit_line(P, reinterpret_cast<uint8_t*>(s_text4), shift + excl[j]);
+      }
+      __syncthreads();
+      if (fits) codec_store_piece<kPcdBlock>(a.out + (G - shift), s_text, shift, shift + tot[j]);
+    } else {
+      PcdLine L;
+      L.len = 0;
+      if (valid[j]) pcd_line_vals(c[j], L, a.err);
+      if (tot[j] + shift <= kPcdTileText) {
+        if (valid[j]) pcd_emit(L, s_text + shift + excl[j]);
+        __syncthreads();
+        if (fits) codec_store_piece<kPcdBlock>(a.out + (G - shift), s_text, shift, shift + tot[j]);
+      } else if (valid[j] && fits) {
+        pcd_emit(L, a.out + G + excl[j]);
+      }
+    }
+    __syncthreads();   // s_text is reused by the next tile
+    G += tot[j];
   }
 }
 

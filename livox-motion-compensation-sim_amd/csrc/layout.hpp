@@ -25,6 +25,19 @@ __device__ __forceinline__ int64_t xcd_unit(int64_t b, int64_t n) {
   return x * per + (x < rem ? x : rem) + i;
 }
 
+// wave-uniform load (memory the kernel never writes) through the constant address space -> s_load_dword* into SGPRs
+template <typename T>
+__device__ __forceinline__ T ldu(const T* p) {
+  static_assert(sizeof(T) % 4 == 0, "ldu needs a dword-multiple type");
+  struct Raw { int v[sizeof(T) / 4]; };
+  typedef __attribute__((address_space(4))) const int CI;
+  CI* q = (CI*)(p);
+  Raw r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) r.v[i] = q[i];
+  return __builtin_bit_cast(T, r);
+}
+
 // component c of a float4 / int4 (c a compile-time constant after unrolling)
 __device__ __forceinline__ float& f4c(float4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));

@@ -266,3 +266,39 @@ def test_deskew_pcd_space_and_errors(mc, gpu_ctx):
         mc.codecs.deskew_pcd_batch(b, b, mode="frame")
     with pytest.raises(ValueError):
         mc.codecs.deskew_pcd_batch(b, gpu_ctx.batch([300, 1, 1000]), mode="frame")
+
+
+def test_pcd_single_pass_lookback_space_and_sizes(mc, gpu_ctx):
+    """k_pcd_encode (batch source, one launch: lengths, decoupled look-back scan, text): hundreds of
+    partitions (look-back windows of 64 and beyond), empty frames between full ones, a partition
+    holding byte-path lines among packed ones, against the f64-AoS two-pass encoder and the oracle;
+    a buffer one byte short returns MC_ERR_SPACE with the exact size, a NULL buffer only the sizes."""
+    from ctypes import c_int64
+    rng = np.random.default_rng(77)
+    counts = np.array([1000] * 150 + [0, 0] + [300, 1, 0, 4096] * 20 + [777], np.int64)
+    n = int(counts.sum())
+    pts = np.column_stack([rng.normal(0, 300, (n, 3)), rng.uniform(0, 1, n)])
+    pts[50_000:50_003, 1] = [5000.0, -1e9, np.inf]                      # one partition takes the byte path
+    b = gpu_ctx.batch(counts)
+    b.upload_aos(pts)
+    host = b.split(b.download_aos())
+    got = mc.codecs.encode_pcd_batch(b)
+    assert got == mc.codecs.encode_pcd_frames(host, gpu_ctx)
+    for f in (0, 49, 50, 150, 151, 152, 153, len(counts) - 1):
+        assert got[f] == C.pcd_ascii_bytes(host[f])
+    lib, ptr = gpu_ctx.lib, mc._lib.ptr
+    pos = np.zeros(len(counts) + 1, np.int64)
+    assert lib.mc_pcd_encode_batch(gpu_ctx.handle, b.handle, None, 0, ptr(pos, c_int64)) == mc._lib.MC_ERR_SPACE
+    total = int(pos[-1])
+    assert total == sum(len(g) - len(mc.codecs.pcd_header(int(c))) for g, c in zip(got, counts))
+    buf = gpu_ctx.device_buffer(total)
+    try:
+        assert lib.mc_pcd_encode_batch(gpu_ctx.handle, b.handle, buf.ptr, total - 1, ptr(pos, c_int64)) == \
+            mc._lib.MC_ERR_SPACE
+        assert int(pos[-1]) == total
+        assert lib.mc_pcd_encode_batch(gpu_ctx.handle, b.handle, buf.ptr, total, ptr(pos, c_int64)) == 0
+        text = buf.to_host(np.uint8, count=total).tobytes()
+    finally:
+        buf.close()
+    for f, c in enumerate(counts):
+        assert mc.codecs.pcd_header(int(c)) + text[pos[f]:pos[f + 1]] == got[f]

@@ -5,6 +5,8 @@
 #   smoke   __graft_entry__.smoke()
 #   ab      tools/ab.py $AB_ARGS (interleaved A/B of build/variants/lib_*.so)
 #   bench   bench.py with the driver's flags ($BENCH_ARGS)
+#   abc     tools/ab_codecs.py $ABC_ARGS (interleaved A/B of the codec kernels across libraries)
+#   latency tools/latency.py ($LAT_ARGS)
 #   prof    rocprofv3 --kernel-trace --stats of the same bench command
 # Usage (repo root, on the GPU box):  STEPS="tests ab" bash tools/gpu_session.sh <tag>
 set -u
@@ -43,6 +45,14 @@ for step in $STEPS; do
       timeout -k 10 600 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
       stop_if_fault $? bench
       cat "$OUT/bench.json"; tail -3 "$OUT/bench.err" ;;
+    abc)
+      timeout -k 10 600 python -u tools/ab_codecs.py ${ABC_ARGS:-} > "$OUT/ab_codecs.log" 2>&1
+      stop_if_fault $? abc
+      cat "$OUT/ab_codecs.log" ;;
+    latency)
+      timeout -k 10 300 python -u tools/latency.py ${LAT_ARGS:-} > "$OUT/latency.json" 2> "$OUT/latency.err"
+      stop_if_fault $? latency
+      python -c "import json,sys; d=json.load(open(sys.argv[1])); print({k: d[k] for k in d if k != 'mc_deskew_per_call'})" "$OUT/latency.json" ;;
     prof)
       ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu ${BENCH_ARGS:-} \
