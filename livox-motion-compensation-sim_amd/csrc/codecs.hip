@@ -10,10 +10,6 @@
 
 using namespace mc;
 
-#ifndef MC_PCD_ONEPASS
-#define MC_PCD_ONEPASS 1   // batch source: k_pcd_encode (one pass) instead of k_pcd_measure + k_pcd_write
-#endif
-
 namespace {
 
 int codec_scratch(mc_ctx* c, size_t bytes, char** out) {
@@ -88,8 +84,6 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
                const uint64_t* ts_ns, const uint8_t* has_int, void* d_out, int64_t out_bytes);
 int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, void* d_out, int64_t out_bytes,
                int64_t* body_pos, const int32_t* d_measured = nullptr);
-int pcd_encode_onepass(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, const std::vector<int64_t>& doff,
-                       const std::vector<int64_t>& units, void* d_out, int64_t out_bytes, int64_t* body_pos);
 
 }  // namespace
 
@@ -234,57 +228,6 @@ int mc_deskew_pcd(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int po
 
 namespace {
 
-// Batch source: k_pcd_encode measures, scans (decoupled look-back) and writes in one launch; the
-// host reads back only the frame offsets.  Frames without points take the next frame's offset.
-int pcd_encode_onepass(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, const std::vector<int64_t>& doff,
-                       const std::vector<int64_t>& units, void* d_out, int64_t out_bytes, int64_t* body_pos) {
-  const int64_t n_tiles = units[F];
-  const int64_t n_parts = (n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG;
-  std::vector<uint8_t> blob;
-  const size_t o_doff = put(blob, doff.data(), doff.size());
-  const size_t o_unit = put(blob, units.data(), units.size());
-  const size_t o_zero = put(blob, (const uint64_t*)nullptr, 0);   // status words + ticket, zeroed
-  blob.resize(o_zero + ((size_t)n_parts + 1) * sizeof(uint64_t));
-  const size_t o_body = put(blob, (const int64_t*)nullptr, 0);
-  blob.resize(o_body + ((size_t)F + 1) * sizeof(int64_t));
-  char* d = nullptr;
-  if (int r = codec_scratch(c, blob.size(), &d)) return r;
-  HIPCHK(hipMemcpyAsync(d, blob.data(), o_zero, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(d + o_zero, 0, ((size_t)n_parts + 1) * sizeof(uint64_t), c->stream));
-  HIPCHK(hipMemsetAsync(c->d_codec_err, 0, sizeof(int), c->stream));
-  PcdArgs a;
-  a.src = frames_of(src, reinterpret_cast<const int64_t*>(d + o_doff), reinterpret_cast<const int64_t*>(d + o_unit),
-                    F, n_tiles);
-  a.tile_bytes = nullptr;
-  a.tile_pos = nullptr;
-  a.out = static_cast<char*>(d_out);
-  a.err = c->d_codec_err;
-  PcdScanArgs sc;
-  sc.status = reinterpret_cast<unsigned long long*>(d + o_zero);
-  sc.ticket = reinterpret_cast<unsigned int*>(d + o_zero + (size_t)n_parts * sizeof(uint64_t));
-  sc.body_pos = reinterpret_cast<int64_t*>(d + o_body);
-  sc.cap = d_out ? out_bytes : 0;   // no buffer: sizes only
-  {
-    TimedRegion tr(c, &c->codec_ev, c->stream);
-    hipLaunchKernelGGL(k_pcd_encode, dim3((uint32_t)n_parts), dim3(kPcdBlock), 0, c->stream, a, sc);
-  }
-  HIPCHK(hipGetLastError());
-  std::vector<int64_t> body((size_t)F + 1);
-  int err = 0;
-  HIPCHK(hipMemcpyAsync(body.data(), sc.body_pos, body.size() * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(&err, c->d_codec_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (err == 2) return fail(MC_ERR_HIP, "k_pcd_encode: look-back wait exceeded its bound");
-  if (err) return fail(MC_ERR_INVALID, "a value has |v| >= 2^107, beyond the device %%.6f formatter");
-  for (int32_t f = F - 1; f >= 0; --f)
-    if (units[f + 1] == units[f]) body[f] = body[f + 1];
-  std::copy(body.begin(), body.end(), body_pos);
-  if (out_bytes < body[F])
-    return fail(MC_ERR_SPACE, "PCD text needs %lld bytes, buffer has %lld", (long long)body[F], (long long)out_bytes);
-  CHECK_ARG(d_out, "d_out is NULL");
-  return MC_OK;
-}
-
 // d_measured (mc_deskew_pcd): the tiles' text bytes already written by the deskew kernel that
 // produced the batch (pcd_value_len sums per 256-point block = per tile); the measure pass is then
 // skipped unless a tile holds a value outside the packed path, whose exact length only the measure
@@ -303,8 +246,6 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
     return MC_OK;
   }
   DeviceGuard g(c->device);
-  if (src.batch && !d_measured && MC_PCD_ONEPASS) return pcd_encode_onepass(c, src, F, counts, doff, units, d_out,
-                                                                          out_bytes, body_pos);
   std::vector<uint8_t> blob;
   const size_t o_doff = put(blob, doff.data(), doff.size());
   const size_t o_unit = put(blob, units.data(), units.size());

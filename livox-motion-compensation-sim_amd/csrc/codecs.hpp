@@ -108,18 +108,24 @@ __device__ __forceinline__ int32_t codec_advance(const int64_t* __restrict__ uni
 
 // Store LDS bytes [lo, hi) to g + [lo, hi), where lds and g agree modulo 16: whole 16-byte chunks
 // with dwordx4 stores, the partial chunks at either end byte by byte.  All threads participate.
+// The LDS buffer extends to the 16-byte chunk holding hi.
 template <int NT = kCodecBlock>   // NT: threads of the workgroup
 __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const char* lds, int lo, int hi) {
   const int c0 = lo >> 4, c1 = (hi + 15) >> 4;
   for (int c = c0 + threadIdx.x; c < c1; c += NT) {
     const int b0 = c << 4;
+    const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
     if (b0 >= lo && b0 + 16 <= hi) {
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-      const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
       __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));
     } else {
-      const int e = b0 + 16 < hi ? b0 + 16 : hi;
-      for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];
+      // a partial chunk (at most two per piece): its bytes inside [lo, hi) from the chunk's 16
+      // bytes in registers (a copy loop here gets vectorised into a wide unrolled copy whose
+      // registers the whole kernel pays for)
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (b0 + k >= lo && b0 + k < hi) g[b0 + k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
 }
@@ -936,198 +942,5 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write_bytes(const PcdArgs a, 
   }
 }
 
-
-// ---- single pass (batch source): measure, scan and write in one launch -------------------------
-// Workgroups take partitions of kPcdTilesPerWG consecutive tiles in ticket order (one atomic per
-// workgroup).  A partition loads all its values, forms its lines' lengths, publishes its text bytes
-// and finds its offset by decoupled look-back over the predecessors' published sums (Merrill &
-// Garland 2016, single-pass prefix scan), then formats and stores its tiles.  Ticket order is the
-// scan order, so every partition a workgroup waits on holds an earlier ticket: its workgroup is
-// already resident and never waits on a later one.  The text needs one read of the values instead of
-// the measure pass's read plus the write pass's (16 B/pt), and no host round trip for the offsets.
-struct PcdScanArgs {
-  unsigned long long* status;   // [n_parts] flag << 62 | bytes (zeroed before the launch)
-  unsigned int* ticket;         // zeroed before the launch
-  int64_t* body_pos;            // [F + 1]: first byte of each frame with tiles; [F] = total bytes
-  int64_t cap;                  // text buffer bytes: a tile that would end beyond it is not stored
-};
-constexpr unsigned long long kScanAgg = 1ull << 62;    // the partition's own bytes
-constexpr unsigned long long kScanIncl = 2ull << 62;   // bytes of partitions 0 .. p
-constexpr unsigned long long kScanVal = kScanAgg - 1;
-
-__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Wave 0 of partition p: publishes agg, returns the bytes of partitions 0 .. p - 1 (every lane).
-// Waits are bounded (the predecessors publish right after their loads, so a correct launch waits
-// microseconds): past ~2^22 polls the launch is reported broken through *err instead of hanging.
-__device__ __forceinline__ int64_t pcd_lookback(unsigned long long* status, int64_t p, int64_t agg, int* err) {
-  const int lane = threadIdx.x & 63;
-  if (p == 0) {
-    if (lane == 0) __hip_atomic_store(status, kScanIncl | (unsigned long long)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return 0;
-  }
-  if (lane == 0) __hip_atomic_store(status + p, kScanAgg | (unsigned long long)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int64_t excl = 0;
-  uint32_t polls = 0;
-  for (int64_t end = p - 1;; end -= 64) {   // window: partitions end, end - 1, .., end - 63 (lane order)
-    const int64_t idx = end - lane;
-    unsigned long long v = idx >= 0 ? 0ull : kScanIncl;   // before partition 0: an inclusive zero
-    for (;;) {
-      if ((v >> 62) == 0) v = __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t nr = __builtin_amdgcn_ballot_w64((v >> 62) == 0);
-      const uint64_t inc = __builtin_amdgcn_ballot_w64((v >> 62) == 2);
-      const uint64_t low = inc & (~inc + 1);                 // the nearest inclusive predecessor
-      const uint64_t upto = inc ? (low | (low - 1)) : ~0ull;  // lanes that count
-      if ((nr & upto) == 0) {
-        const int64_t val = (upto >> lane) & 1 ? (int64_t)(v & kScanVal) : 0;
-        excl += wave_sum64(val);
-        if (inc) {
-          if (lane == 0)
-            __hip_atomic_store(status + p, kScanIncl | (unsigned long long)(excl + agg), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          return excl;
-        }
-        break;   // no inclusive sum in this window: the next 64 predecessors
-      }
-      if (++polls > (1u << 22)) {
-        if (lane == 0) *err = 2;
-        return excl;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-}
-
-// byte-path line of (float32) values c: pcd_line's formatting on the widened values
-__device__ __forceinline__ void pcd_line_vals(const float c[4], PcdLine& L, int* err) {
-  L.len = 4;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    L.v[k] = fmt6_prepare((double)c[k]);
-    if (L.v[k].kind == 3) *err = 1;
-    L.len += L.v[k].len;
-  }
-}
-
-__global__ __launch_bounds__(kPcdBlock) void k_pcd_encode(const PcdArgs a, const PcdScanArgs sc) {
-  constexpr int T = kPcdTilesPerWG;
-  __shared__ int s_wave[T][kPcdBlock / 64];
-  __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
-  __shared__ unsigned int s_ticket;
-  __shared__ int64_t s_base;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_ticket = atomicAdd(sc.ticket, 1u);
-  __syncthreads();
-  const int64_t p = s_ticket;
-  const int64_t u0 = p * T;
-  // all of the partition's values first: one HBM round trip
-  int32_t f = codec_frame_of(a.src, u0);
-  int32_t fr[T];
-  float c[T][4];
-  bool valid[T];
-#pragma unroll
-  for (int j = 0; j < T; ++j) {
-    const int64_t u = u0 + j;
-    valid[j] = false;
-    fr[j] = -1;
-    c[j][0] = c[j][1] = c[j][2] = c[j][3] = 0.f;
-    if (u < a.src.n_units) {
-      const int64_t row = pcd_row(a.src, u, f, valid[j]);
-      fr[j] = f;
-      if (valid[j]) codec_point_f32(a.src, f, row, c[j]);
-    }
-  }
-  // line lengths (packed path), -1 outside it
-  int len[T];
-  bool slow = false;
-#pragma unroll
-  for (int j = 0; j < T; ++j) {
-    len[j] = valid[j] ? pcd_fast_len_f32(c[j]) : 0;
-    slow = slow || len[j] < 0;
-  }
-  slow = __syncthreads_or(slow) != 0;   // workgroup-uniform: the whole partition takes the byte path
-  if (slow) {
-#pragma unroll
-    for (int j = 0; j < T; ++j) {
-      PcdLine L;
-      L.len = 0;
-      if (valid[j]) pcd_line_vals(c[j], L, a.err);
-      len[j] = L.len;
-    }
-  }
-  // the T tiles' in-tile offsets: T block scans side by side
-  int excl[T], tot[T];
-#pragma unroll
-  for (int j = 0; j < T; ++j) {
-    const int x = wave_scan_incl(len[j]);
-    excl[j] = x - len[j];
-    if (lane == 63) s_wave[j][wid] = x;
-  }
-  __syncthreads();
-  int64_t agg = 0;
-#pragma unroll
-  for (int j = 0; j < T; ++j) {
-    int before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < kPcdBlock / 64; ++w) {
-      const int cw = s_wave[j][w];
-      before += w < wid ? cw : 0;
-      total += cw;
-    }
-    excl[j] += before;
-    tot[j] = total;
-    agg += total;
-  }
-  if (wid == 0) {
-    const int64_t base = pcd_lookback(sc.status, p, agg, a.err);
-    if (lane == 0) s_base = base;
-  }
-  __syncthreads();
-  int64_t G = s_base;
-  if (threadIdx.x == 0) {
-    // frame offsets: a frame's first tile writes its start; the last partition the total
-    int64_t g = G;
-#pragma unroll
-    for (int j = 0; j < T; ++j) {
-      const int64_t u = u0 + j;
-      if (u < a.src.n_units && ldu(a.src.unit_off + fr[j]) == u) sc.body_pos[fr[j]] = g;
-      g += tot[j];
-    }
-    if (u0 + T >= a.src.n_units) sc.body_pos[a.src.F] = g;
-  }
-  char* const s_text = reinterpret_cast<char*>(s_text4);
-#pragma unroll
-  for (int j = 0; j < T; ++j) {
-    if (u0 + j >= a.src.n_units) break;   // workgroup-uniform
-    const int shift = (int)(G & 15);
-    const bool fits = G + tot[j] <= sc.cap;
-    if (!slow) {
-      PcdFast P;
-      if (valid[j]) {
-        pcd_fast_vals_f32(c[j], P);
-        pcd_emit_line(P, reinterpret_cast<uint8_t*>(s_text4), shift + excl[j]);
-      }
-      __syncthreads();
-      if (fits) codec_store_piece<kPcdBlock>(a.out + (G - shift), s_text, shift, shift + tot[j]);
-    } else {
-      PcdLine L;
-      L.len = 0;
-      if (valid[j]) pcd_line_vals(c[j], L, a.err);
-      if (tot[j] + shift <= kPcdTileText) {
-        if (valid[j]) pcd_emit(L, s_text + shift + excl[j]);
-        __syncthreads();
-        if (fits) codec_store_piece<kPcdBlock>(a.out + (G - shift), s_text, shift, shift + tot[j]);
-      } else if (valid[j] && fits) {
-        pcd_emit(L, a.out + G + excl[j]);
-      }
-    }
-    __syncthreads();   // s_text is reused by the next tile
-    G += tot[j];
-  }
-}
 
 }  // namespace mc

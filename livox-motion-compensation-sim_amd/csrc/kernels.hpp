@@ -29,7 +29,7 @@ namespace mc {
 
 // Shipping configuration.  The A/B history of every choice below (and of the arms that lost) is in
 // DESIGN.md §4 / §9 and profiles/; the kernels carry only the configuration that ships.
-//   * output stores: sc1 write-through (OutBuf) in the frame, SLERP and IMU kernels — SLERP +7 %
+//   * output stores: sc1 write-through (st_pol<2>) in the frame, SLERP and IMU kernels — SLERP +7 %
 //     vs nt; IMU 327.8-330.1 vs 337.9-343.9 us with sc1 nt (profiles/round3/s46); frame 298.2-298.9
 //     vs 300.3-301.3 us with sc1 nt (s48);
 //   * non-temporal input loads: SLERP 318.4-322.5 vs 351.7-358.9 us without (profiles/round3/s54);
@@ -165,44 +165,32 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 //   0 plain, 1 nt (builtin), 2 sc1 write-through.
 // The per-point kernels run 10-12% faster with sc1 write-through stores (the line leaves L2 at
 // once instead of being retained dirty); the frame kernel is 2% faster with nt.
-// sc1 has no C-level store builtin other than the buffer store's cache-policy operand, so policy 2
-// is a raw buffer store (OutBuf below) issued by the compiler, never inline asm: a store of more than
-// 8 bytes reads its data VGPRs after issue and on gfx940+ a VALU write to them needs 2 wait states
-// behind it, which the compiler's hazard recognizer inserts only around stores it can see (round 3's
-// inline-asm stores needed a hand-placed `s_nop 1`; without it the stager's sc1 build lost x and z,
-// profiles/round3/s08, s24).
+// sc1 alone has no C-level store builtin, so policy 2 is an inline-asm global_store_dwordx4.  What
+// the compiler cannot see about it, and why that is safe:
+//   * the store reads its data VGPRs after issue, and on gfx940+ a VALU write to them needs 2 wait
+//     states behind the store; the compiler inserts them only after stores it can see, so the asm
+//     ends in `s_nop 1` (without it the stager's sc1 build lost the first 8 bytes of chunks,
+//     profiles/round3/s08, s24; tests/test_asm_stores.py checks every asm store of the built
+//     library's ISA for it);
+//   * the compiler's vmcnt bookkeeping does not count the store; on gfx9 vector loads and stores
+//     retire from vmcnt in issue order, so an uncounted younger store only makes a wait the
+//     compiler places for an older load stricter, never looser.
+// The alternative the compiler sees, __builtin_amdgcn_raw_buffer_store_b128 with the SC1 aux bit,
+// measured IMU -1.3 %, frame -0.2 %, but SLERP bimodal at 316 / 380-390 us (median +20 %) in two
+// interleaved A/Bs (profiles/round4/s10, s11), so the asm store stays.
 template <int POL>
 __device__ __forceinline__ void st_pol(float* p, const float4& v) {
-  static_assert(POL == 0 || POL == 1, "policy 2 (sc1) goes through OutBuf");
+  static_assert(POL >= 0 && POL <= 2, "store policy 0 / 1 / 2");
   v4f t = {v.x, v.y, v.z, v.w};
-  if constexpr (POL == 1) {
+  if constexpr (POL == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
+  } else if constexpr (POL == 1) {
     __builtin_nontemporal_store(t, reinterpret_cast<v4f*>(p));
   } else {
     *reinterpret_cast<v4f*>(p) = t;
   }
 }
-
-// The output column block of one tile as a buffer resource: base = the 256-point block holding the
-// tile's first point (wave-uniform, built in SGPRs once per tile), each lane's store a 32-bit byte
-// offset from it (< 64 KB: a tile spans 2048 points x out_C columns).  The resource's record count
-// covers the offsets only; the stores themselves stay behind the callers' point guards.
-constexpr int kBufSc1 = 16;            // buffer-store aux bits: SC1 (gfx940+ cache-policy encoding)
-constexpr int kBufWord3 = 0x00020000;  // raw dword buffer descriptor word 3 on gfx942 / gfx950
-struct OutBuf {
-  float* base;
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ OutBuf(float* out, int C, int64_t pstart)
-      : base(out + (pstart >> 8) * C * kBlkPts),
-        r(__builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, kBufWord3)) {}
-  __device__ __forceinline__ void st(float* p, const float4& v) const {
-    if constexpr (kStorePol == 2) {
-      const v4i t = __builtin_bit_cast(v4i, v);
-      __builtin_amdgcn_raw_buffer_store_b128(t, r, (int)((p - base) * sizeof(float)), 0, kBufSc1);
-    } else {
-      st_pol<kStorePol == 2 ? 0 : kStorePol>(p, v);
-    }
-  }
-};
+__device__ __forceinline__ void st_out(float* p, const float4& v) { st_pol<kStorePol>(p, v); }
 
 // 16-byte streaming loads of the input columns
 __device__ __forceinline__ float4 ld4(const float* p) {
@@ -865,7 +853,6 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
     // group g of the tile: block pstart/256 + g/64, offset 4 (g % 64) inside it
     const float* ix = a.in + bidx((int)a.in_C, 0, tl.pstart);
     float* ox = a.out + bidx((int)a.out_C, 0, tl.pstart);
-    const OutBuf ob(a.out, (int)a.out_C, tl.pstart);
     float4 vx[kIters], vy[kIters], vz[kIters], vi[kIters];
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
@@ -891,10 +878,10 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
         MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
 #undef MC_XF
         float* o = ox + (int64_t)(g >> 6) * a.out_C * kBlkPts + 4 * (g & 63);
-        ob.st(o, ox4);
-        ob.st(o + kBlkPts, oy4);
-        ob.st(o + 2 * kBlkPts, oz4);
-        ob.st(o + 3 * kBlkPts, vi[it]);
+        st_out(o, ox4);
+        st_out(o + kBlkPts, oy4);
+        st_out(o + 2 * kBlkPts, oz4);
+        st_out(o + 3 * kBlkPts, vi[it]);
       }
     }
   }
@@ -934,7 +921,6 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
     // 96-byte table row set is L2-resident, and a per-lane select of three SGPR rows would cost 32
     // VALU instructions (two SGPR sources cannot meet in one v_cndmask)
     const FrameRow r = *(a.frame_tbl + 3 * tl.frame + (c < 2 ? c : 2));
-    const OutBuf ob(a.out, (int)a.out_C, tl.pstart);
     float4 v[kQuadU];
     bool act[kQuadU];
     int64_t p[kQuadU];
@@ -959,7 +945,7 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
       o.y = xf_row(r, X.y, Y.y, Z.y);
       o.z = xf_row(r, X.z, Y.z, Z.z);
       o.w = xf_row(r, X.w, Y.w, Z.w);
-      if (act[u]) ob.st(a.out + bidx((int)a.out_C, c, p[u]), c == 3 ? w : o);
+      if (act[u]) st_out(a.out + bidx((int)a.out_C, c, p[u]), c == 3 ? w : o);
       if constexpr (PCD) {
         // lane c's column of its group's four points (a whole line is the quad's four lanes)
         const float4 val = c == 3 ? w : o;
@@ -1628,13 +1614,12 @@ __global__ __launch_bounds__(kBlock, kPointsWaves) void k_deskew_points(const De
       }
     }
     if (act) {
-      const OutBuf ob(a.out, (int)a.out_C, tl.pstart);
       float* o = a.out + bidx((int)a.out_C, 0, p);
-      ob.st(o, X);
-      ob.st(o + kBlkPts, Y);
-      ob.st(o + 2 * kBlkPts, Z);
-      ob.st(o + 3 * kBlkPts, I);
-      if (a.copy_t) ob.st(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
+      st_out(o, X);
+      st_out(o + kBlkPts, Y);
+      st_out(o + 2 * kBlkPts, Z);
+      st_out(o + 3 * kBlkPts, I);
+      if (a.copy_t) st_out(o + 4 * kBlkPts, __builtin_bit_cast(float4, Tq));
     }
     if constexpr (PCD) {
       const int64_t i0 = p - ldu(a.fpoff + f), n = ldu(a.fcount + f);

@@ -268,11 +268,11 @@ def test_deskew_pcd_space_and_errors(mc, gpu_ctx):
         mc.codecs.deskew_pcd_batch(b, gpu_ctx.batch([300, 1, 1000]), mode="frame")
 
 
-def test_pcd_single_pass_lookback_space_and_sizes(mc, gpu_ctx):
-    """k_pcd_encode (batch source, one launch: lengths, decoupled look-back scan, text): hundreds of
-    partitions (look-back windows of 64 and beyond), empty frames between full ones, a partition
-    holding byte-path lines among packed ones, against the f64-AoS two-pass encoder and the oracle;
-    a buffer one byte short returns MC_ERR_SPACE with the exact size, a NULL buffer only the sizes."""
+def test_pcd_batch_many_tiles_space_and_sizes(mc, gpu_ctx):
+    """mc_pcd_encode_batch over thousands of tiles (several tiles per write workgroup, the next
+    tile's values converted before the current tile's stores), empty frames between full ones, a
+    tile holding byte-path lines among packed ones, against the f64-AoS encoder and the oracle; a
+    buffer one byte short returns MC_ERR_SPACE with the exact size, a NULL buffer only the sizes."""
     from ctypes import c_int64
     rng = np.random.default_rng(77)
     counts = np.array([1000] * 150 + [0, 0] + [300, 1, 0, 4096] * 20 + [777], np.int64)

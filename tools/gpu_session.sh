@@ -58,7 +58,12 @@ for step in $STEPS; do
           -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu ${BENCH_ARGS:-} \
           > "$OUT/prof_bench.json" 2> "$OUT/prof.err" )
       stop_if_fault $? prof
-      find "$OUT/prof" -name "*kernel_stats*" -exec head -12 {} \; ;;
+      find "$OUT/prof" -name "*kernel_stats*" -exec cp {} "$OUT/kernel_stats.csv" \;
+      head -12 "$OUT/kernel_stats.csv"
+      # the bench line's roofline kernel time recomputed from the same run's kernel trace (timed window)
+      python3 tools/roofline_from_trace.py --trace "$OUT/prof" --bench "$OUT/prof_bench.json" \
+        --out "$OUT/roofline_trace.json" > /dev/null 2>> "$OUT/prof.err"
+      echo "[roofline_from_trace] rc=$?" | tee -a "$OUT/steps.log" ;;
     *) echo "unknown step $step" ;;
   esac
 done
