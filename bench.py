@@ -384,6 +384,7 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipel
     ctx.sync()
     ctx.timing(False)
     ctx.read_timing()          # drop the warmup events (back to the pool)
+    ctx.read_timing_spans()    # and the warmup launches' spans
     rdv.barrier()
     t0 = time.perf_counter()
     if graph or issue == "pipeline":
@@ -410,8 +411,13 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipel
             ctx.timing(False)
         ctx.sync()
     each = ctx.read_timing_each()
+    spans = ctx.read_timing_spans()
     tm = ctx.read_timing()
     tm["main_ms"], tm["main_launches"], tm["main_each_us"] = sum(each), len(each), [round(x * 1e3, 2) for x in each]
+    # the same launches' own execution spans (first workgroup start to last workgroup end): the
+    # kernel time rocprofv3's kernel trace reports; the events also hold the dispatch gap ahead of
+    # each launch (~5 us, profiles/round4/s12/roofline_trace.json)
+    tm["main_span_us"] = [round(x, 2) for x in spans] if len(spans) == len(each) else None
     return t1 - t0, tm, every
 
 
@@ -797,16 +803,22 @@ def assemble_line(args, cid, label, scen, lo, hi, world, n_devices, n_rank, n_to
                      "frac": r["achieved_GBs"] / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": KERNEL_OF[args.issue][args.mode], "kernel_avg_us": r["main_avg_us"],
-                     "kernel_each_us": r.get("main_each_us"),
+                     "kernel_each_us": r.get("main_span_us") or r.get("main_each_us"),
+                     "events_avg_us": r.get("events_avg_us"), "events_each_us": r.get("main_each_us"),
                      "bytes_per_point": BYTES_PER_POINT[args.mode], "points_per_launch": n_rank,
                      "kernel_time": ("HIP events around every launch of a second, untimed pass"
                                      if args.events_after else
                                      f"wall-clock stamp nodes around the kernels of {r['timed_launches']} of the "
                                      f"{r['steps']} steps of the step graph (every {every}th)"
                                      if args.issue == "graph" else
-                                     f"HIP events (hipExtLaunchKernel start/stop, the dispatch's own timestamps) "
-                                     f"on the kernels of {r['timed_launches']} of the {r['steps']} timed steps "
-                                     f"(every {every}th), on the kernel's stream")},
+                                     (f"the kernels' own workgroup spans (first workgroup start to last "
+                                      f"workgroup end, device wall clock) of {r['timed_launches']} of the "
+                                      f"{r['steps']} timed steps (every {every}th); HIP events on the same "
+                                      f"launches in events_* (they also hold the dispatch gap ahead of a launch)"
+                                      if r.get("main_span_us") else
+                                      f"HIP events (hipExtLaunchKernel start/stop) on the kernels of "
+                                      f"{r['timed_launches']} of the {r['steps']} timed steps (every {every}th), "
+                                      f"on the kernel's stream"))},
         "order_tune": tuned or None,
         "step_over_kernel": (r["wall_s"] / r["steps"] * 1e6) / r["main_avg_us"] if r["main_avg_us"] else None,
         "prep_avg_us": r["prep_avg_us"],
@@ -928,11 +940,14 @@ def main():
         if mode == args.mode:
             every = ev
         wall_max = rdv.max(wall)
-        main_avg_s = tm["main_ms"] / max(tm["main_launches"], 1) / 1e3
+        events_avg_s = tm["main_ms"] / max(tm["main_launches"], 1) / 1e3
+        spans = tm.get("main_span_us")
+        main_avg_s = sum(spans) / len(spans) / 1e6 if spans else events_avg_s
         prep_avg_s = tm["prep_ms"] / tm["prep_launches"] / 1e3 if tm["prep_launches"] else None
         achieved = BYTES_PER_POINT[mode] * n_rank / main_avg_s / 1e9 if main_avg_s > 0 else 0.0
         results[mode] = {"wall_s": wall_max, "steps": steps, "main_avg_us": main_avg_s * 1e6,
                          "timed_launches": int(tm["main_launches"]), "main_each_us": tm["main_each_us"],
+                         "main_span_us": spans, "events_avg_us": events_avg_s * 1e6,
                          "prep_avg_us": prep_avg_s * 1e6 if prep_avg_s is not None else None,
                          "achieved_GBs": achieved,
                          "value": n_total * steps / wall_max / 1e6}

@@ -286,6 +286,10 @@ int mc_timing_read(mc_ctx* ctx, double* main_ms_total, int64_t* main_launches,
 /* the main kernels' event times one by one (ms, in launch order; up to cap of them, *n = how many
  * were pending); those events are released (the prep / layout / codec ones stay for mc_timing_read) */
 int mc_timing_read_each(mc_ctx* ctx, double* main_ms, int64_t cap, int64_t* n);
+/* the same timed deskew launches' own execution spans (us, launch order; up to cap, *n = how many):
+ * first workgroup start to last workgroup end on the wall clock, without the dispatch gap a start
+ * event ahead of a launch includes; released */
+int mc_timing_read_spans(mc_ctx* ctx, double* us, int64_t cap, int64_t* n);
 /* kernel tuning knobs: 0 keeps the default */
 int mc_set_launch(mc_ctx* ctx, int32_t max_grid);
 

@@ -106,6 +106,7 @@ _SIGS = {
     "mc_timing_enable": (c_int, [c_void_p, c_int]),
     "mc_timing_read": (c_int, [c_void_p, _pd, _pi64, _pd, _pi64]),
     "mc_timing_read_each": (c_int, [c_void_p, _pd, c_int64, _pi64]),
+    "mc_timing_read_spans": (c_int, [c_void_p, _pd, c_int64, _pi64]),
     "mc_set_launch": (c_int, [c_void_p, c_int32]),
     "mc_comm_unique_id": (c_int, [POINTER(c_char)]),
     "mc_comm_init": (c_int, [c_void_p, c_int, c_int, POINTER(c_char), POINTER(c_void_p)]),

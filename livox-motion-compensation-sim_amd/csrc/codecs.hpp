@@ -108,24 +108,20 @@ __device__ __forceinline__ int32_t codec_advance(const int64_t* __restrict__ uni
 
 // Store LDS bytes [lo, hi) to g + [lo, hi), where lds and g agree modulo 16: whole 16-byte chunks
 // with dwordx4 stores, the partial chunks at either end byte by byte.  All threads participate.
-// The LDS buffer extends to the 16-byte chunk holding hi.
+// (Partial chunks from one 16-byte LDS read + predicated byte stores: 50 instead of 56 VGPRs in the
+// LVX kernel but LVX 310.4 vs 308.2, PCD 808.4 vs 803.3 us, profiles/round4/s12: not taken.)
 template <int NT = kCodecBlock>   // NT: threads of the workgroup
 __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const char* lds, int lo, int hi) {
   const int c0 = lo >> 4, c1 = (hi + 15) >> 4;
   for (int c = c0 + threadIdx.x; c < c1; c += NT) {
     const int b0 = c << 4;
-    const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
     if (b0 >= lo && b0 + 16 <= hi) {
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
       __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));
     } else {
-      // a partial chunk (at most two per piece): its bytes inside [lo, hi) from the chunk's 16
-      // bytes in registers (a copy loop here gets vectorised into a wide unrolled copy whose
-      // registers the whole kernel pays for)
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (b0 + k >= lo && b0 + k < hi) g[b0 + k] = (char)(w[k >> 2] >> (8 * (k & 3)));
+      const int e = b0 + 16 < hi ? b0 + 16 : hi;
+      for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];
     }
   }
 }

@@ -197,6 +197,10 @@ struct mc_ctx {
   int32_t max_grid = 0;
   bool timing = false;
   double wall_khz = 0.0;   // wall_clock64() rate
+  // workgroup spans of timed deskew launches (DeskewArgs::span): kSpanSlots slots of 1 + kSpanTail
+  // wall-clock stamps, zeroed, handed out in launch order until mc_timing_read_spans
+  unsigned long long* d_span = nullptr;
+  int32_t span_used = 0;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> main_ev, prep_ev, layout_ev;
   mcimpl::StepGraph* step_graph = nullptr;

@@ -120,9 +120,11 @@ struct DeskewArgs {
   const FrameWin* fwin;    // per-point modes
   const void* frec;        // 2 frame-specialised records per frame (PoseWin or ImuSeg)
   const FrameWin* swin;    // per sub-tile: the same, for frames whose window exceeds kFastMaxW
-  const void* pad0;        // unused: keeps the kernel-argument layout the deskew kernels' register
-                           // allocation was measured with (without it the fused SLERP kernel spills
-                           // more SGPRs into VGPR lanes: 147 vs 118 writelane / readlane)
+  unsigned long long* span; // timed launches only (else null): the launch's workgroup span on the wall
+                           // clock, [0] = the first workgroup's start, [1 + k] = the end of the k-th of
+                           // its last kSpanTail workgroups (launch_span; the slot also keeps the
+                           // kernel-argument layout the deskew kernels' register allocation was
+                           // measured with: without it the fused SLERP kernel spills more SGPRs)
   const double* pose_time; // T
   const PoseSeg* pose_seg; // nseg
   const int64_t* imu_ts;   // M
@@ -514,6 +516,23 @@ __device__ __forceinline__ void wave_count2(const T* a, int64_t n, T x0, T x1, i
 // (s_memrealtime, hipDeviceAttributeWallClockRate) when the stream reaches it.
 __global__ __launch_bounds__(64) void k_stamp(unsigned long long* dst) {
   if (threadIdx.x == 0) *dst = (unsigned long long)wall_clock64();
+}
+
+// A timed launch's workgroup span (DeskewArgs::span): the first workgroup stamps its start, the last
+// kSpanTail workgroups their ends (after their own barrier, so every wave is done).  Workgroups are
+// dispatched in order and take similar times, so the launch ends with one of its last ones; the span
+// is the kernel's own execution time, without the dispatch gap a start event before the launch
+// includes (~5 us, profiles/round4/s12/roofline_trace.json).
+constexpr int kSpanTail = 2048;
+__device__ __forceinline__ void span_start(unsigned long long* span) {
+  if (span && blockIdx.x == 0 && threadIdx.x == 0) span[0] = (unsigned long long)wall_clock64();
+}
+__device__ __forceinline__ void span_end(unsigned long long* span) {
+  if (span && blockIdx.x + kSpanTail >= gridDim.x) {
+    __syncthreads();
+    const int k = (int)(blockIdx.x + kSpanTail - gridDim.x);
+    if (threadIdx.x == 0) span[1 + k] = (unsigned long long)wall_clock64();
+  }
 }
 
 // ---- k_prep's searches: one load round from an interpolation guess ----------------------------
@@ -972,7 +991,11 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
 }
 
 
-__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) { deskew_frame_quad(a, 0u); }
+__global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
+  span_start(a.span);
+  deskew_frame_quad(a, 0u);
+  span_end(a.span);
+}
 
 // Path A with the ASCII PCD text bytes of every output block (mc_deskew_pcd)
 __global__ __launch_bounds__(kBlock) void k_deskew_frame_pcd(const DeskewArgs a) { deskew_frame_quad<true>(a, 0u); }
@@ -1505,6 +1528,7 @@ __device__ __forceinline__ void fast_path(const WinOf<MODE>* rec, const FrameWin
 template <int MODE, bool NEXT = false, bool PCD = false>
 __global__ __launch_bounds__(kBlock, kPointsWaves) void k_deskew_points(const DeskewArgs a, const PrepArgs pn,
                                                                          const uint32_t pre) {
+  span_start(a.span);
   if constexpr (NEXT) {
     if (blockIdx.x < pre) {
       prep_body<MODE>(pn, blockIdx.x);
@@ -1654,6 +1678,7 @@ __global__ __launch_bounds__(kBlock, kPointsWaves) void k_deskew_points(const De
     load_sub(st, tl, Tq, X, Y, Z, I);
     sub_tile(st, tl, w, Tq, X, Y, Z, I);
   }
+  span_end(a.span);
 }
 
 // ---- the next step's prep inside this step's launch (mc_deskew_steps, MC_STEPS_PIPELINE) ---------
@@ -1665,11 +1690,13 @@ __global__ __launch_bounds__(kBlock, kPointsWaves) void k_deskew_points(const De
 // the XCD count, so deskew workgroup b - pre sits on the XCD xcd_unit assumes.
 __global__ __launch_bounds__(kBlock, 4) void k_deskew_frame_next(const DeskewArgs a, const PrepArgs p,
                                                                  const uint32_t pre) {
+  span_start(a.span);
   if (blockIdx.x < pre) {
     prep_body<0>(p, blockIdx.x);
     return;
   }
   deskew_frame_quad(a, pre);
+  span_end(a.span);
 }
 
 // ---- per-point modes on float64 rows (the reference's own data, no float32 staging) --------------

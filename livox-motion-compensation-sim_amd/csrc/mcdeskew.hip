@@ -161,6 +161,7 @@ int mc_destroy(mc_ctx* c) {
   dev_free(c->d_env); dev_free(c->d_scan_ftime); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount);
   dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis); dev_free(c->d_scan_bits);
   if (c->d_codec) (void)hipFree(c->d_codec);
+  if (c->d_span) (void)hipFree(c->d_span);
   dev_free(c->d_codec_err);
   dev_free(c->d_pcd_len);
   if (c->d_seg64) (void)hipFree(c->d_seg64);
@@ -713,6 +714,22 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (ot.order >= 0 && ot.P == in->P) da.xcd_order = ot.order;
 }
 
+// A span slot for a timed deskew launch (null when the pool is spent: that launch has events only)
+constexpr int32_t kSpanSlots = 64;
+constexpr size_t kSpanWords = 1 + kSpanTail;
+unsigned long long* span_take(mc_ctx* c) {
+  if (!c->d_span) {
+    if (hipMalloc(&c->d_span, kSpanSlots * kSpanWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_span, 0, kSpanSlots * kSpanWords * sizeof(unsigned long long)) != hipSuccess) {
+      if (c->d_span) (void)hipFree(c->d_span);
+      c->d_span = nullptr;
+      return nullptr;
+    }
+  }
+  if (c->span_used >= kSpanSlots) return nullptr;
+  return c->d_span + (size_t)c->span_used++ * kSpanWords;
+}
+
 // Launches with optional hipExtLaunchKernel timing events (e0/e1 null: untimed) and AQL flags.
 // Inside a graph capture (build_step_graph) both events are null and flags 0.
 void launch_prep(const StepPlan& sp, hipStream_t sd, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
@@ -815,6 +832,7 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
   }
   if (sp.kernel >= 0) {
     LaunchEvents ev(c);
+    if (ev.e0) sp.da.span = span_take(c);
     if (speculate) {
       // this call's deskew with an identical next call's prep in the first workgroups (half h ^ 1,
       // which no queued work reads: the previous kernel read it and has finished before this launch)
@@ -926,8 +944,10 @@ void issue_steps(mc_ctx* c, const StepPlan* plan, int mode, int32_t n_steps, int
       ev.keep(&c->prep_ev);
     }
     LaunchEvents ev(c, sampled(i));
-    if (i + 1 < n_steps) launch_fused(plan[i & 1], plan[(i + 1) & 1], s, ev.e0, ev.e1);
-    else launch_main(plan[i & 1], s, ev.e0, ev.e1);
+    StepPlan sp = plan[i & 1];
+    if (ev.e0) sp.da.span = span_take(c);
+    if (i + 1 < n_steps) launch_fused(sp, plan[(i + 1) & 1], s, ev.e0, ev.e1);
+    else launch_main(sp, s, ev.e0, ev.e1);
     ev.keep(&c->main_ev);
   }
 }
@@ -1581,6 +1601,33 @@ int mc_timing_read_each(mc_ctx* c, double* ms, int64_t cap, int64_t* n) {
     ms[k] = m;
   }
   return sum_events(c, c->main_ev, nullptr, nullptr);   // the main events only (the rest stays pending)
+}
+
+int mc_timing_read_spans(mc_ctx* c, double* us, int64_t cap, int64_t* n) {
+  CHECK_ARG(c && n && (cap == 0 || us), "NULL argument");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  *n = 0;
+  if (!c->d_span || c->span_used == 0) return MC_OK;
+  if (c->wall_khz <= 0.0) {
+    int khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    if (khz <= 0) return fail(MC_ERR_HIP, "wall clock rate %d kHz", khz);
+    c->wall_khz = khz;
+  }
+  std::vector<unsigned long long> h((size_t)c->span_used * kSpanWords);
+  HIPCHK(hipMemcpy(h.data(), c->d_span, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  for (int32_t k = 0; k < c->span_used; ++k) {
+    const unsigned long long* w = h.data() + (size_t)k * kSpanWords;
+    unsigned long long end = 0;
+    for (size_t j = 1; j < kSpanWords; ++j) end = w[j] > end ? w[j] : end;
+    if (w[0] == 0 || end < w[0]) continue;   // a launch without deskew workgroups
+    if (*n < cap) us[*n] = (double)(end - w[0]) / c->wall_khz * 1e3;   // ticks / kHz = ms
+    ++*n;
+  }
+  HIPCHK(hipMemset(c->d_span, 0, (size_t)c->span_used * kSpanWords * sizeof(unsigned long long)));
+  c->span_used = 0;
+  return MC_OK;
 }
 
 int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms, int64_t* prep_n) {

@@ -215,6 +215,14 @@ class Context:
         check(self.lib.mc_timing_read_each(self.handle, ptr(buf, c_double), cap, ctypes.byref(n)), "timing_read_each")
         return buf[:min(n.value, cap)].tolist()
 
+    def read_timing_spans(self, cap: int = 4096) -> list:
+        """The timed deskew launches' own execution spans (us): first workgroup start to last
+        workgroup end on the device wall clock, in launch order (released)."""
+        buf = np.zeros(cap, np.float64)
+        n = c_int64()
+        check(self.lib.mc_timing_read_spans(self.handle, ptr(buf, c_double), cap, ctypes.byref(n)), "timing_read_spans")
+        return buf[:min(n.value, cap)].tolist()
+
     def device_buffer(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
 

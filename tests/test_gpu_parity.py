@@ -768,3 +768,33 @@ def test_host_array_paths_zero_copy_and_pipeline(mc, gpu_ctx):
     poses = [{"translation": rng.normal(0, 100, 3), "rotation": rng.uniform(-1, 1, 3)} for _ in small]
     for g, s, p in zip(sim.align_frames(small, poses), small, poses):
         np.testing.assert_allclose(g, R.transform_pointcloud(s, p), rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("mode", ["pose_slerp", "frame"])
+def test_launch_spans_match_events(mc, gpu_ctx, mode):
+    """mc_timing_read_spans: every timed deskew launch's own workgroup span (the bench line's
+    roofline kernel time) is positive and within its HIP-event time, which also holds the dispatch
+    gap ahead of the launch; untimed launches take no span."""
+    counts = np.full(64, 100_000, np.int64)
+    b_in = gpu_ctx.batch(counts, with_time=mode != "frame")
+    b_out = gpu_ctx.batch(counts)
+    b_in.synth(seed=5, frame_id_base=0)
+    times = np.arange(64) * 0.1 + 1.0
+    b_in.set_frame_times(times)
+    sim = mc.LiDARMotionSimulator({"duration": 60.0, "trajectory_type": "figure_eight", "lidar_fps": 10})
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    gpu_ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    gpu_ctx.read_timing_each()
+    gpu_ctx.read_timing_spans()
+    gpu_ctx.deskew_steps(b_in, b_out, 9, mode=mode, sample_every=3, pipeline=True)
+    gpu_ctx.sync()
+    each = gpu_ctx.read_timing_each()
+    spans = gpu_ctx.read_timing_spans()
+    assert len(each) == 3 and len(spans) == 3
+    for e, s in zip(each, spans):
+        assert 0.0 < s <= e * 1e3 + 0.5, (s, e)
+    gpu_ctx.timing(False)
+    gpu_ctx.deskew(b_in, b_out, mode=mode)          # untimed
+    gpu_ctx.sync()
+    assert gpu_ctx.read_timing_spans() == []
+    gpu_ctx.read_timing()

@@ -1,7 +1,9 @@
 """The bench line's roofline kernel time, recomputed from a rocprofv3 kernel trace of the same run.
 
-bench.py times its roofline kernel with HIP events on every `every`-th of the K timed steps
-(hipExtLaunchKernel start/stop: the dispatch's own timestamps).  rocprofv3's --stats average mixes
+bench.py times its roofline kernel on every `every`-th of the K timed steps: since round 4 by the
+launch's own workgroup span (first workgroup start to last workgroup end on the device wall clock,
+mc_timing_read_spans), with the HIP events of the same launches beside it (their start marker also
+holds the ~5 us dispatch gap ahead of the launch).  rocprofv3's --stats average mixes
 in every other launch of that kernel in the process (the 250 ms spin-up, mc_tune_order's candidate
 orders, the warmup steps), so it does not reproduce the line (What's weak 2).  This
 tool picks the timed window out of the kernel trace of the profiled bench command itself — in
@@ -96,9 +98,13 @@ def main():
         "trace_all_timed_steps_avg_us": sum(dur) / len(dur),
         "bench_line_kernel_avg_us": bench_us,
         "trace_vs_bench": trace_us / bench_us - 1.0,
-        "bench_events_each_us": line["roofline"].get("kernel_each_us"),
-        "events_minus_trace_each_us": ([round(e - t, 2) for e, t in zip(line["roofline"]["kernel_each_us"], sampled)]
-                                       if line["roofline"].get("kernel_each_us") else None),
+        "bench_kernel_each_us": line["roofline"].get("kernel_each_us"),
+        "bench_minus_trace_each_us": ([round(e - t, 2) for e, t in zip(line["roofline"]["kernel_each_us"], sampled)]
+                                      if line["roofline"].get("kernel_each_us") else None),
+        "bench_events_each_us": line["roofline"].get("events_each_us"),
+        "events_minus_trace_each_us": ([round(e - t, 2) for e, t in zip(line["roofline"]["events_each_us"], sampled)]
+                                       if line["roofline"].get("events_each_us") else None),
+        "bench_kernel_time": line["roofline"].get("kernel_time"),
         "frac_from_trace": bpp * n / (trace_us * 1e-6) / 1e9 / line["roofline"]["peak"],
         "frac_bench_line": line["roofline"]["frac"],
         "all_launches_of_kernel_avg_us": sum(fused_all) / len(fused_all),
