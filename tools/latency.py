@@ -158,7 +158,8 @@ def main():
     ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
     F = len(scans)
     outs = [np.empty((s.shape[0], 4)) for s in scans]
-    fp = np.array([s.ctypes.data for s in scans], np.uintp).ctypes.data
+    fp_arr = np.array([s.ctypes.data for s in scans], np.uintp)   # kept alive: the call reads it
+    fp = fp_arr.ctypes.data
     op_arr = np.array([o.ctypes.data for o in outs], np.uintp)
     op = op_arr.ctypes.data
     counts = np.array([s.shape[0] for s in scans], np.int64)
