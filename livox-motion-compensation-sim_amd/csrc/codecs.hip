@@ -275,7 +275,8 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   if (!measured) {
     {
       TimedRegion tr(c, &c->codec_ev, c->stream);
-      const dim3 mgrid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
+      const int per = a.src.cols ? kPcdMeasureTiles : kPcdTilesPerWG;   // tiles per measure workgroup
+      const dim3 mgrid((uint32_t)((n_tiles + per - 1) / per));
       if (a.src.cols) hipLaunchKernelGGL(k_pcd_measure<true>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
       else hipLaunchKernelGGL(k_pcd_measure<false>, mgrid, dim3(kPcdBlock), 0, c->stream, a);
     }

@@ -544,23 +544,26 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
 // unaligned 8-byte LDS stores with exact line boundaries, 1084.2 us.
 struct PcdFast {
   uint32_t n[4];   // round-half-even(|v| * 10^6)
+  uint32_t ip[4];  // n / 10^6 (the integer part)
   uint32_t neg;    // bit k: value k is negative (signbit)
   int nd[4];       // integer digits of value k (1 .. 4)
   int len;         // line length in bytes
   bool ok;         // all four values took the fast path
 };
 
-__device__ __forceinline__ int fast_nd(uint32_t n) {
-  const uint32_t ip = n / 1000000u;
-  return 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u);
-}
+__device__ __forceinline__ int fast_nd(uint32_t ip) { return 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u); }
+
+// floor(N / 10^6) for N < 2^32 given as an exact float64: N 10^-6 is within 5e-13 of N / 10^6,
+// whose fraction is 0 or at least 10^-6 from 1, so adding 10^-9 and truncating is exact (one
+// full-rate f64 FMA + convert instead of the quarter-rate 32-bit mul_hi of N / 10^6)
+__device__ __forceinline__ uint32_t fast_ip(double N) { return (uint32_t)fma(N, 1e-6, 1e-9); }
 
 // N = round-half-even(|v| * 10^6) exactly, for |v| < 4294 (NaN / larger values fail the test).
 // y = fl(a * 10^6) and e = fma(a, 10^6, -y) represent the exact product as y + e; fr = y - floor(y)
 // and fr - 0.5 are exact, so d = (fr - 0.5) + e has the sign of the exact fraction minus one half
 // (rounding preserves signs) and is zero only on an exact tie, which rounds to even.  Exact ties are
 // common in float32-valued clouds (any odd multiple of 1/128).
-__device__ __forceinline__ bool fmt6_fast(double v, uint32_t& n) {
+__device__ __forceinline__ bool fmt6_fast(double v, uint32_t& n, uint32_t& ip) {
   const double a = fmin(fabs(v), 4294.0);
   const double y = a * 1000000.0;
   const double e = fma(a, 1000000.0, -y);
@@ -568,6 +571,7 @@ __device__ __forceinline__ bool fmt6_fast(double v, uint32_t& n) {
   const double d = ((y - fl) - 0.5) + e;
   const uint32_t m = (uint32_t)fl;
   n = m + ((d > 0.0 || (d == 0.0 && (m & 1u))) ? 1u : 0u);
+  ip = fast_ip((double)n);
   return fabs(v) < 4294.0;
 }
 
@@ -579,10 +583,10 @@ __device__ __forceinline__ void pcd_fast(const CodecFrames& s, int32_t f, int64_
   P.len = 4 + 4 * 7;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    P.ok &= fmt6_fast(c[k], P.n[k]);
+    P.ok &= fmt6_fast(c[k], P.n[k], P.ip[k]);
     const uint32_t ng = signbit(c[k]) ? 1u : 0u;
     P.neg |= ng << k;
-    P.nd[k] = fast_nd(P.n[k]);
+    P.nd[k] = fast_nd(P.ip[k]);
     P.len += (int)ng + P.nd[k];
   }
 }
@@ -593,9 +597,11 @@ __device__ __forceinline__ void pcd_fast(const CodecFrames& s, int32_t f, int64_
 // digit count needs no arithmetic at all: N >= 10^k <=> |v| >= (10^k - 1/2) / 10^6, and the
 // smallest float32 at or above 9.9999995 / 99.9999995 / 999.9999995 is 10 / 100 / 1000 exactly
 // (the float32 below each is 1 ulp ~ 1e-6 .. 6e-5 under it, outside the half-unit band).
-__device__ __forceinline__ bool fmt6_fast_f32(float v, uint32_t& n) {
+__device__ __forceinline__ bool fmt6_fast_f32(float v, uint32_t& n, uint32_t& ip) {
   const float a = fminf(fabsf(v), 4294.0f);   // NaN -> 4294 (the line fails the test below)
-  n = (uint32_t)rint((double)a * 1000000.0);
+  const double y = rint((double)a * 1000000.0);
+  n = (uint32_t)y;
+  ip = fast_ip(y);
   return fabsf(v) < 4294.0f;
 }
 
@@ -605,7 +611,7 @@ __device__ __forceinline__ void pcd_fast_vals_f32(const float c[4], PcdFast& P) 
   P.len = 4 + 4 * 7;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    P.ok &= fmt6_fast_f32(c[k], P.n[k]);
+    P.ok &= fmt6_fast_f32(c[k], P.n[k], P.ip[k]);
     const float a = fabsf(c[k]);
     const uint32_t ng = signbit(c[k]) ? 1u : 0u;
     P.neg |= ng << k;
@@ -644,9 +650,13 @@ __device__ __forceinline__ uint32_t mul41(uint32_t y) {
 // fraction digits come from one word holding the two 3-digit halves (multiply-shift division on both
 // 16-bit halves at once), the integer digits likewise from two 2-digit halves; bytes placed with
 // v_perm_b32.  fh = (fp * 4294968) >> 32 is fp / 1000 exactly for fp < 10^6 (error < 1.7e-4).
-__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t sep, uint32_t& D, uint32_t& A, uint32_t& B) {
-  const uint32_t ip = N / 1000000u, fp = N - ip * 1000000u;
-  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32);   // fp / 1000, exact
+__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t ip, uint32_t sep, uint32_t& D, uint32_t& A,
+                                            uint32_t& B) {
+  // the masks state the ranges (ip < 8192, fh < 1024) so the products stay 24-bit multiply-adds
+  // (v_mad_i32_i24) instead of quarter-rate 64-bit ones
+  ip &= 0x1fffu;
+  const uint32_t fp = N - ip * 1000000u;
+  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32) & 0x3ffu;   // fp / 1000, exact
   const uint32_t y = fh | ((fp - fh * 1000u) << 16);
   const uint32_t h = ((mul41(y)) >> 12) & 0x000F000Fu;
   const uint32_t r = y - h * 100u;
@@ -672,9 +682,10 @@ __device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
 // overwrites them.  The line's first value stores exactly its own bytes, so no lane ever writes
 // another line's text: no zeroing, no atomics.
 template <bool EXACT>
-__device__ __forceinline__ void bytes_value(uint8_t* base, int o, uint32_t N, int nd, bool neg, uint32_t sep) {
+__device__ __forceinline__ void bytes_value(uint8_t* base, int o, uint32_t N, uint32_t ip, int nd, bool neg,
+                                            uint32_t sep) {
   uint32_t D, A, B;
-  swar_fields(N, sep, D, A, B);
+  swar_fields(N, ip, sep, D, A, B);
   uint8_t* pa = base + o + nd + (neg ? 1 : 0);   // the '.'
   put4(pa, A);
   put4(pa + 4, B);
@@ -694,10 +705,10 @@ __device__ __forceinline__ void bytes_value(uint8_t* base, int o, uint32_t N, in
 __device__ __forceinline__ void pcd_emit_line(const PcdFast& P, uint8_t* base, int off) {
   const int o1 = off + 8 + P.nd[0] + (int)(P.neg & 1u), o2 = o1 + 8 + P.nd[1] + (int)((P.neg >> 1) & 1u);
   const int o3 = o2 + 8 + P.nd[2] + (int)((P.neg >> 2) & 1u);
-  bytes_value<false>(base, o3, P.n[3], P.nd[3], (P.neg >> 3) & 1u, '\n');
-  bytes_value<false>(base, o2, P.n[2], P.nd[2], (P.neg >> 2) & 1u, ' ');
-  bytes_value<false>(base, o1, P.n[1], P.nd[1], (P.neg >> 1) & 1u, ' ');
-  bytes_value<true>(base, off, P.n[0], P.nd[0], P.neg & 1u, ' ');
+  bytes_value<false>(base, o3, P.n[3], P.ip[3], P.nd[3], (P.neg >> 3) & 1u, '\n');
+  bytes_value<false>(base, o2, P.n[2], P.ip[2], P.nd[2], (P.neg >> 2) & 1u, ' ');
+  bytes_value<false>(base, o1, P.n[1], P.ip[1], P.nd[1], (P.neg >> 1) & 1u, ' ');
+  bytes_value<true>(base, off, P.n[0], P.ip[0], P.nd[0], P.neg & 1u, ' ');
 }
 
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
@@ -739,10 +750,14 @@ __device__ __forceinline__ int32_t pcd_tile_word(int v) {   // scanned bytes (+ 
 // replaces the block scan: no LDS, no barrier (measure + write 893.5 / 939.0 vs 989.4 / 1022.2 us with
 // a block per tile, profiles/round3/s70).  A workgroup takes kPcdTilesPerWG tiles, each wave
 // kPcdTilesPerWG / 4 of them, all of whose loads are issued before the first is measured.
-constexpr int kPcdMeasureWaveTiles = kPcdTilesPerWG / (kPcdBlock / 64);
+#ifndef MC_PCD_MEASURE_TILES
+#define MC_PCD_MEASURE_TILES 4
+#endif
+constexpr int kPcdMeasureTiles = MC_PCD_MEASURE_TILES;                 // tiles per measure workgroup
+constexpr int kPcdMeasureWaveTiles = kPcdMeasureTiles / (kPcdBlock / 64);
 __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) {
   static_assert(kPcdBlock == kBlkPts, "a PCD tile is one batch block");
-  static_assert(kPcdTilesPerWG % (kPcdBlock / 64) == 0, "whole tiles per wave");
+  static_assert(kPcdMeasureTiles % (kPcdBlock / 64) == 0, "whole tiles per wave");
   constexpr int NT = kPcdMeasureWaveTiles;
   const int lane = threadIdx.x & 63;
   int32_t f = codec_frame_of(a.src, u0);
@@ -794,7 +809,7 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
   if constexpr (F32) {
-    pcd_measure_waves(a, xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG);
+    pcd_measure_waves(a, xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdMeasureTiles);
   } else {
     __shared__ int s_wave[kPcdBlock / 64];
     const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly

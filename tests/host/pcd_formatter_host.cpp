@@ -68,14 +68,25 @@ int main(int argc, char** argv) {
     if ((uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32) != fp / 1000u) { ++bad; break; }
   for (uint32_t x = 0; x < 10000u; ++x)
     if ((__umul24(x, 5243u) >> 19) != x / 100u) { ++bad; break; }
+  // fast_ip (the integer part from the float64 N) at every multiple of 10^6 and its neighbours,
+  // and at a stride over all of [0, 2^32)
+  for (uint64_t k = 0; k * 1000000ull < (1ull << 32); ++k)
+    for (int64_t d = -2; d <= 2; ++d) {
+      const int64_t N = (int64_t)(k * 1000000ull) + d;
+      if (N < 0 || N >= (1ll << 32)) continue;
+      if (fast_ip((double)N) != (uint32_t)(N / 1000000)) { if (++bad < 20) std::printf("fast_ip(%lld)\n", (long long)N); }
+    }
+  for (uint64_t N = 0; N < (1ull << 32); N += 997)
+    if (fast_ip((double)N) != (uint32_t)(N / 1000000u)) { if (++bad < 20) std::printf("fast_ip(%llu)\n", (unsigned long long)N); }
   long lines = 0, fast = 0, f32_lines = 0;
   // every float32 in [0, 4294] at a stride, and every float32 within 4096 ulps of each digit-count
   // threshold (10, 100, 1000) and of 4294: the float32 path's N and length equal the float64 path's
   {
     auto check = [&](float v) {
       for (float w : {v, -v}) {
-        uint32_t n32 = 0, n64 = 0;
-        const bool k32 = fmt6_fast_f32(w, n32), k64 = fmt6_fast((double)w, n64);
+        uint32_t n32 = 0, n64 = 0, i32 = 0, i64 = 0;
+        const bool k32 = fmt6_fast_f32(w, n32, i32), k64 = fmt6_fast((double)w, n64, i64);
+        if (k64 && (i32 != n32 / 1000000u || i64 != n64 / 1000000u)) ++bad;
         const float c4[4] = {w, w, w, w};
         const double d4[4] = {w, w, w, w};
         if (k32 != k64 || (k64 && n32 != n64) || pcd_fast_len_f32(c4) != pcd_fast_len(d4)) {
@@ -117,7 +128,8 @@ int main(int argc, char** argv) {
         pcd_fast_vals_f32(cf, Q);
         ++f32_lines;
         if (pcd_fast_len_f32(cf) != lf || Q.ok != P[l].ok ||
-            (Q.ok && (Q.len != P[l].len || Q.neg != P[l].neg || std::memcmp(Q.n, P[l].n, sizeof Q.n)))) {
+            (Q.ok && (Q.len != P[l].len || Q.neg != P[l].neg || std::memcmp(Q.n, P[l].n, sizeof Q.n) ||
+                      std::memcmp(Q.ip, P[l].ip, sizeof Q.ip)))) {
           ++bad;
           std::printf("float32 path differs (len %d/%d ok %d/%d) for %s", Q.len, P[l].len, Q.ok, P[l].ok, line);
         }
