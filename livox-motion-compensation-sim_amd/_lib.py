@@ -136,7 +136,12 @@ def load(path: str | None = None):
     except OSError as e:  # pragma: no cover - depends on the image
         raise McLibraryError(f"cannot load {p}: {e}") from e
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if path is None:   # the in-tree library must export every entry point
+                raise
+            continue           # an explicit older build (tools/ab*.py arms): its own entry points only
         fn.restype = res
         fn.argtypes = args
     if lib.mc_abi_version() != 1:

@@ -108,6 +108,8 @@ def main():
                 ctx.timing(False)
                 t = ctx.read_timing()
                 per[lib].append(t["main_ms"] / t["main_launches"] * 1e3)
+                if hasattr(ctx.lib, "mc_timing_read_spans"):   # free the span slots: every timed launch stamps
+                    ctx.read_timing_spans()
         if args.check:
             ref = None
             for lib in libs:
