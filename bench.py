@@ -384,7 +384,6 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipel
     ctx.sync()
     ctx.timing(False)
     ctx.read_timing()          # drop the warmup events (back to the pool)
-    ctx.read_timing_spans()    # and the warmup launches' spans
     rdv.barrier()
     t0 = time.perf_counter()
     if graph or issue == "pipeline":
@@ -411,7 +410,10 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipel
             ctx.timing(False)
         ctx.sync()
     each = ctx.read_timing_each()
-    spans = ctx.read_timing_spans()
+    # the warmup launches' spans come first (reading them before the timed steps would idle the
+    # device between warmup and timing: after ~1 ms idle the next tens of launches run through a
+    # power transient, 317 -> 375 us, profiles/round4/s13 kernel trace)
+    spans = ctx.read_timing_spans()[-len(each):] if each else []
     tm = ctx.read_timing()
     tm["main_ms"], tm["main_launches"], tm["main_each_us"] = sum(each), len(each), [round(x * 1e3, 2) for x in each]
     # the same launches' own execution spans (first workgroup start to last workgroup end): the
