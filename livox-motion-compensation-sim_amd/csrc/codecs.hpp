@@ -556,6 +556,8 @@ __device__ __forceinline__ int fast_nd(uint32_t ip) { return 1 + (ip >= 10u) + (
 // floor(N / 10^6) for N < 2^32 given as an exact float64: N 10^-6 is within 5e-13 of N / 10^6,
 // whose fraction is 0 or at least 10^-6 from 1, so adding 10^-9 and truncating is exact (one
 // full-rate f64 FMA + convert instead of the quarter-rate 32-bit mul_hi of N / 10^6)
+// (against N / 10^6 on the integers: measure + write 812.4 vs 818.0 us, profiles/round4/s15 — within
+// noise, kept for the four quarter-rate multiplies per line it removes)
 __device__ __forceinline__ uint32_t fast_ip(double N) { return (uint32_t)fma(N, 1e-6, 1e-9); }
 
 // N = round-half-even(|v| * 10^6) exactly, for |v| < 4294 (NaN / larger values fail the test).
@@ -750,10 +752,9 @@ __device__ __forceinline__ int32_t pcd_tile_word(int v) {   // scanned bytes (+ 
 // replaces the block scan: no LDS, no barrier (measure + write 893.5 / 939.0 vs 989.4 / 1022.2 us with
 // a block per tile, profiles/round3/s70).  A workgroup takes kPcdTilesPerWG tiles, each wave
 // kPcdTilesPerWG / 4 of them, all of whose loads are issued before the first is measured.
-#ifndef MC_PCD_MEASURE_TILES
-#define MC_PCD_MEASURE_TILES 4
-#endif
-constexpr int kPcdMeasureTiles = MC_PCD_MEASURE_TILES;                 // tiles per measure workgroup
+// (8 / 16 tiles per measure workgroup: 821.8-833.0 / 842.0 vs 812.4-827.5 us measure + write,
+// profiles/round4/s14, s15)
+constexpr int kPcdMeasureTiles = kPcdTilesPerWG;                       // tiles per measure workgroup
 constexpr int kPcdMeasureWaveTiles = kPcdMeasureTiles / (kPcdBlock / 64);
 __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) {
   static_assert(kPcdBlock == kBlkPts, "a PCD tile is one batch block");

@@ -123,6 +123,10 @@ int mc_device_pci_bus_id(int device, char* out, int len) {
   return MC_OK;
 }
 
+// launch-span pool (DeskewArgs::span): slots of 1 + kSpanTail wall-clock stamps
+constexpr int32_t kSpanSlots = 64;
+constexpr size_t kSpanWords = 1 + kSpanTail;
+
 int mc_create(int device, mc_ctx** out) {
   CHECK_ARG(out, "out is NULL");
   *out = nullptr;
@@ -146,7 +150,14 @@ int mc_create(int device, mc_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_prep_done[i], fl);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming | hipEventReleaseToDevice);
-  if (e != hipSuccess) { delete c; return fail(MC_ERR_HIP, "stream/event creation: %s", hipGetErrorString(e)); }
+  // the launch-span pool (span_take), zeroed
+  if (e == hipSuccess) e = hipMalloc(&c->d_span, kSpanSlots * kSpanWords * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->d_span, 0, kSpanSlots * kSpanWords * sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    if (c->d_span) (void)hipFree(c->d_span);
+    delete c;
+    return fail(MC_ERR_HIP, "stream/event creation: %s", hipGetErrorString(e));
+  }
   *out = c;
   return MC_OK;
 }
@@ -714,19 +725,12 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (ot.order >= 0 && ot.P == in->P) da.xcd_order = ot.order;
 }
 
-// A span slot for a timed deskew launch (null when the pool is spent: that launch has events only)
-constexpr int32_t kSpanSlots = 64;
-constexpr size_t kSpanWords = 1 + kSpanTail;
+// A span slot for a timed deskew launch (null when the pool is spent: that launch has events only).
+// The pool is allocated and zeroed by mc_create: allocating it at the first timed launch idled the
+// device for ~11 ms right before the timed steps, and the launches after such a pause run through a
+// power transient (SLERP 341 -> 353 -> 327 us, profiles/round4/s15 kernel trace).
 unsigned long long* span_take(mc_ctx* c) {
-  if (!c->d_span) {
-    if (hipMalloc(&c->d_span, kSpanSlots * kSpanWords * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_span, 0, kSpanSlots * kSpanWords * sizeof(unsigned long long)) != hipSuccess) {
-      if (c->d_span) (void)hipFree(c->d_span);
-      c->d_span = nullptr;
-      return nullptr;
-    }
-  }
-  if (c->span_used >= kSpanSlots) return nullptr;
+  if (!c->d_span || c->span_used >= kSpanSlots) return nullptr;
   return c->d_span + (size_t)c->span_used++ * kSpanWords;
 }
 
