@@ -6,6 +6,7 @@
 #   ab      tools/ab.py $AB_ARGS (interleaved A/B of build/variants/lib_*.so)
 #   bench   bench.py with the driver's flags ($BENCH_ARGS)
 #   abc     tools/ab_codecs.py $ABC_ARGS (interleaved A/B of the codec kernels across libraries)
+#   pmc     tools/pmc_traffic.py (deskew kernels, then --aux), profiles/pmc_traffic.json copied out
 #   latency tools/latency.py ($LAT_ARGS)
 #   prof    rocprofv3 --kernel-trace --stats of the same bench command
 # Usage (repo root, on the GPU box):  STEPS="tests ab" bash tools/gpu_session.sh <tag>
@@ -49,6 +50,13 @@ for step in $STEPS; do
       timeout -k 10 600 python -u tools/ab_codecs.py ${ABC_ARGS:-} > "$OUT/ab_codecs.log" 2>&1
       stop_if_fault $? abc
       cat "$OUT/ab_codecs.log" ;;
+    pmc)
+      timeout -k 10 900 python tools/pmc_traffic.py --tag "$TAG" > "$OUT/pmc.log" 2>&1
+      stop_if_fault $? pmc
+      timeout -k 10 900 python tools/pmc_traffic.py --aux --tag "$TAG" > "$OUT/pmc_aux.log" 2>&1
+      stop_if_fault $? pmc_aux
+      cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"
+      tail -8 "$OUT/pmc_aux.log" ;;
     latency)
       timeout -k 10 300 python -u tools/latency.py ${LAT_ARGS:-} > "$OUT/latency.json" 2> "$OUT/latency.err"
       stop_if_fault $? latency
