@@ -533,6 +533,17 @@ __device__ __forceinline__ int block_scan(int x, int* s_wave, int& total) {
   return x + before;
 }
 
+// tens and units of two 2-digit numbers held in the 16-bit lanes of v (each < 100): v_pk_mul_lo_u16,
+// v_pk_lshrrev_b16, v_pk_mad_u16 — two lanes per instruction ((x 103) >> 10 = x / 10 for x < 179)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pk_tens_units(uint32_t v, uint32_t& t, uint32_t& u) {
+  const u16x2 x = __builtin_bit_cast(u16x2, v);
+  const u16x2 q = (u16x2)((x * (unsigned short)103) >> (unsigned short)10);
+  const u16x2 r = x - q * (unsigned short)10;
+  t = __builtin_bit_cast(uint32_t, q);
+  u = __builtin_bit_cast(uint32_t, r);
+}
+
 // ---- packed line path (every value of the line |v| < 4294, ties included) ----------------------
 // The common LiDAR line is formatted from four 32-bit integers N = round(|v| * 10^6): the digits come
 // out of multiply-shift SWAR arithmetic on two 3-digit halves at once (swar_fields), and each value
@@ -647,6 +658,41 @@ __device__ __forceinline__ uint32_t mul41(uint32_t y) {
   return y * 41u;
 #endif
 }
+#ifndef MC_PCD_PK
+#define MC_PCD_PK 1
+#endif
+#if MC_PCD_PK
+// Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
+// zeros (byte 0 = thousands), A = ". d1 d2 d3", B = "d4 d5 d6 sep" (bytes in text order).  The ten
+// digits as five 2-digit groups (ip / 100, ip % 100, fp / 10^4, fp / 100 % 100, fp % 100), split into
+// tens and units two groups per instruction with packed 16-bit arithmetic (pk_tens_units); bytes
+// placed with v_perm_b32.  g2 = (fp 429497) >> 32 is fp / 10^4 exactly for fp < 10^6 (the
+// multiplier's excess adds < 6.3e-5 to a quotient whose fraction is at most 0.9999).
+__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t ip, uint32_t sep, uint32_t& D, uint32_t& A,
+                                            uint32_t& B) {
+  // the masks state the ranges (ip < 8192, g2 < 128) so the products stay 24-bit multiply-adds
+  // (v_mad_i32_i24) instead of quarter-rate 64-bit ones
+  ip &= 0x1fffu;
+  const uint32_t fp = N - ip * 1000000u;                                                  // < 10^6
+  uint32_t g2 = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32);               // fp / 10^4
+  // opaque to the optimiser: it recognises fp - (fp / 10^4) 10^4 as fp % 10^4 and lowers that
+  // through a quarter-rate 64-bit multiply-add
+  asm("" : "+v"(g2));
+  const uint32_t r4 = fp - (g2 & 0x7fu) * 10000u;                                         // < 10^4
+  const uint32_t g3 = __umul24(r4, 5243u) >> 19;                                          // r4 / 100
+  const uint32_t g4 = r4 - g3 * 100u;
+  const uint32_t g0 = __umul24(ip, 5243u) >> 19;                                          // ip / 100
+  const uint32_t g1 = ip - g0 * 100u;
+  uint32_t T1, U1, T2, U2;
+  pk_tens_units(g0 | (g1 << 16), T1, U1);
+  pk_tens_units(g2 | (g3 << 16), T2, U2);
+  const uint32_t t4 = __umul24(g4, 103u) >> 10;
+  const uint32_t tu4 = t4 | ((g4 - t4 * 10u) << 8);
+  D = __builtin_amdgcn_perm(T1, U1, 0x02060004u) + 0x30303030u;
+  A = __builtin_amdgcn_perm(T2, U2, 0x0600040Cu) + 0x3030302Eu;
+  B = __builtin_amdgcn_perm(U2, tu4, 0x0C010006u) + (0x00303030u | (sep << 24));
+}
+#else
 // Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
 // zeros (byte 0 = thousands), A = ". d1 d2 d3", B = "d4 d5 d6 sep" (bytes in text order).  The six
 // fraction digits come from one word holding the two 3-digit halves (multiply-shift division on both
@@ -673,6 +719,7 @@ __device__ __forceinline__ void swar_fields(uint32_t N, uint32_t ip, uint32_t se
   const uint32_t u2 = y2 - t2 * 10u;
   D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;
 }
+#endif
 __device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }

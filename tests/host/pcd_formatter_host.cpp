@@ -31,6 +31,16 @@ static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t 
   }
   return r;
 }
+// pk_tens_units (codecs.hpp, outside the spliced section): per 16-bit lane
+static inline void pk_tens_units(uint32_t v, uint32_t& t, uint32_t& u) {
+  t = u = 0;
+  for (int l = 0; l < 2; ++l) {
+    const uint32_t x = (v >> (16 * l)) & 0xffffu;
+    const uint32_t q = ((x * 103u) & 0xffffu) >> 10;
+    t |= q << (16 * l);
+    u |= ((x - q * 10u) & 0xffffu) << (16 * l);
+  }
+}
 using std::fma;
 using std::signbit;
 using std::rint;
@@ -65,7 +75,8 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> buf(16400 / 4 + 4);
   // the multiply-shift divisions of swar_fields on their whole ranges
   for (uint32_t fp = 0; fp < 1000000u; ++fp)
-    if ((uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32) != fp / 1000u) { ++bad; break; }
+    if ((uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32) != fp / 1000u ||
+        (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32) != fp / 10000u) { ++bad; break; }
   for (uint32_t x = 0; x < 10000u; ++x)
     if ((__umul24(x, 5243u) >> 19) != x / 100u) { ++bad; break; }
   // fast_ip (the integer part from the float64 N) at every multiple of 10^6 and its neighbours,
