@@ -646,28 +646,14 @@ __device__ __forceinline__ int pcd_fast_len_f32(const float c[4]) {
   return ok ? len : -1;
 }
 
-// y * 41 as two shift-adds (y*9, then + y*32): the compiler folds the plain product into a
-// quarter-rate v_mul_lo_u32
-__device__ __forceinline__ uint32_t mul41(uint32_t y) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t y9, r;
-  asm("v_lshl_add_u32 %0, %1, 3, %1" : "=v"(y9) : "v"(y));
-  asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(y), "v"(y9));
-  return r;
-#else
-  return y * 41u;
-#endif
-}
-#ifndef MC_PCD_PK
-#define MC_PCD_PK 1
-#endif
-#if MC_PCD_PK
 // Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
 // zeros (byte 0 = thousands), A = ". d1 d2 d3", B = "d4 d5 d6 sep" (bytes in text order).  The ten
 // digits as five 2-digit groups (ip / 100, ip % 100, fp / 10^4, fp / 100 % 100, fp % 100), split into
 // tens and units two groups per instruction with packed 16-bit arithmetic (pk_tens_units); bytes
 // placed with v_perm_b32.  g2 = (fp 429497) >> 32 is fp / 10^4 exactly for fp < 10^6 (the
-// multiplier's excess adds < 6.3e-5 to a quotient whose fraction is at most 0.9999).
+// multiplier's excess adds < 6.3e-5 to a quotient whose fraction is at most 0.9999).  Against the
+// two 3-digit halves in 32-bit SWAR: 802.8 vs 806.8 us measure + write, fused write 751.4 vs 752.3
+// (profiles/round4/s17): kept for its ~2 fewer VALU instructions per value.
 __device__ __forceinline__ void swar_fields(uint32_t N, uint32_t ip, uint32_t sep, uint32_t& D, uint32_t& A,
                                             uint32_t& B) {
   // the masks state the ranges (ip < 8192, g2 < 128) so the products stay 24-bit multiply-adds
@@ -692,34 +678,6 @@ __device__ __forceinline__ void swar_fields(uint32_t N, uint32_t ip, uint32_t se
   A = __builtin_amdgcn_perm(T2, U2, 0x0600040Cu) + 0x3030302Eu;
   B = __builtin_amdgcn_perm(U2, tu4, 0x0C010006u) + (0x00303030u | (sep << 24));
 }
-#else
-// Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
-// zeros (byte 0 = thousands), A = ". d1 d2 d3", B = "d4 d5 d6 sep" (bytes in text order).  The six
-// fraction digits come from one word holding the two 3-digit halves (multiply-shift division on both
-// 16-bit halves at once), the integer digits likewise from two 2-digit halves; bytes placed with
-// v_perm_b32.  fh = (fp * 4294968) >> 32 is fp / 1000 exactly for fp < 10^6 (error < 1.7e-4).
-__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t ip, uint32_t sep, uint32_t& D, uint32_t& A,
-                                            uint32_t& B) {
-  // the masks state the ranges (ip < 8192, fh < 1024) so the products stay 24-bit multiply-adds
-  // (v_mad_i32_i24) instead of quarter-rate 64-bit ones
-  ip &= 0x1fffu;
-  const uint32_t fp = N - ip * 1000000u;
-  const uint32_t fh = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32) & 0x3ffu;   // fp / 1000, exact
-  const uint32_t y = fh | ((fp - fh * 1000u) << 16);
-  const uint32_t h = ((mul41(y)) >> 12) & 0x000F000Fu;
-  const uint32_t r = y - h * 100u;
-  const uint32_t t = (__umul24(r, 103u) >> 10) & 0x000F000Fu;
-  const uint32_t ht = h | (t << 8);
-  const uint32_t u = r - t * 10u;
-  A = __builtin_amdgcn_perm(ht, u, 0x0005040Cu) + 0x3030302Eu;
-  B = __builtin_amdgcn_perm(ht, u, 0x0C020706u) + 0x00303030u + (sep << 24);
-  const uint32_t hi2 = __umul24(ip, 5243u) >> 19;
-  const uint32_t y2 = hi2 | ((ip - hi2 * 100u) << 16);
-  const uint32_t t2 = (__umul24(y2, 103u) >> 10) & 0x000F000Fu;
-  const uint32_t u2 = y2 - t2 * 10u;
-  D = __builtin_amdgcn_perm(t2, u2, 0x02060004u) + 0x30303030u;
-}
-#endif
 __device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
