@@ -633,6 +633,25 @@ __device__ __forceinline__ void pcd_fast_vals_f32(const float c[4], PcdFast& P) 
   }
 }
 
+// pcd_fast_vals_f32 for a tile the measure pass found packed (every value |v| < 4294): no clamp and
+// no path test (a NaN cannot reach here; it would convert to 0)
+__device__ __forceinline__ void pcd_fast_vals_packed(const float c[4], PcdFast& P) {
+  P.ok = true;
+  P.neg = 0;
+  P.len = 4 + 4 * 7;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = fabsf(c[k]);
+    const double y = rint((double)a * 1000000.0);
+    P.n[k] = (uint32_t)y;
+    P.ip[k] = fast_ip(y);
+    const uint32_t ng = signbit(c[k]) ? 1u : 0u;
+    P.neg |= ng << k;
+    P.nd[k] = 1 + (a >= 10.0f) + (a >= 100.0f) + (a >= 1000.0f);
+    P.len += (int)ng + P.nd[k];
+  }
+}
+
 // pcd_fast_len for float32 values: line length, or -1 outside the packed path
 __device__ __forceinline__ int pcd_fast_len_f32(const float c[4]) {
   int len = 4 + 4 * 8;
@@ -857,9 +876,29 @@ __device__ __forceinline__ int pcd_tile_text(const PcdFast& P, bool valid, int64
   __syncthreads();
   return total;
 }
+// codec_store_piece for a tile's text: the full 16-byte chunks in a loop without per-chunk tests,
+// the (at most two) partial end chunks by lanes 0 and 1
 __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int total, const uint4* s_text4) {
-  const int shift = (int)(G & 15);
-  codec_store_piece<kPcdBlock>(a.out + (G - shift), reinterpret_cast<const char*>(s_text4), shift, shift + total);
+  const int lo = (int)(G & 15), hi = lo + total;
+  char* const g = a.out + (G - lo);
+  const char* const lds = reinterpret_cast<const char*>(s_text4);
+  const int f0 = (lo + 15) >> 4, f1 = hi >> 4;   // full chunks [f0, f1)
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) {
+    const uint4 v = s_text4[c];
+    __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + 16 * c));
+  }
+  if (threadIdx.x < 2) {
+    int b = lo, e = hi;                                    // a piece inside one chunk: lane 0 alone
+    if (f0 <= f1) {
+      if (threadIdx.x == 0) e = 16 * f0;                   // head: [lo, 16 f0)
+      else b = 16 * f1;                                    // tail: [16 f1, hi)
+    } else if (threadIdx.x == 1) {
+      e = b;
+    }
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (; b < e; ++b) g[b] = lds[b];
+  }
   __syncthreads();   // s_wave / s_text are reused by the next tile
 }
 
@@ -881,14 +920,23 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
     int32_t flag_n = 0;
     int64_t gn = 0;
     PcdFast Pn;
+    // tile u is block (poff_f + 256 (u - unit_off_f)) / 256 of the batch: its columns start at a
+    // workgroup-uniform address (scalar arithmetic), a lane's line at + threadIdx.x
     auto fetch = [&](int64_t u) {
-      const int64_t row = pcd_row(a.src, u, f, vn);
-      if (vn) codec_point_f32(a.src, f, row, cn);
+      f = codec_advance(a.src.unit_off, f, u);
+      const int64_t k = u - ldu(a.src.unit_off + f);                       // tile of frame f
+      const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
+      const int left = (int)min<int64_t>(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock);
+      vn = (int)threadIdx.x < left;
+      const float* q = a.src.cols + blk * a.src.C * kBlkPts + threadIdx.x;
+      if (vn) {
+        cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
+      }
       flag_n = ldu(a.tile_bytes + u);
       gn = ldu(a.tile_pos + u);
     };
     auto convert = [&]() {
-      pcd_fast_vals_f32(cn, Pn);   // (invalid lanes convert zeros / stale values: length zeroed)
+      pcd_fast_vals_packed(cn, Pn);   // (invalid lanes convert zeros / stale values: length zeroed)
       if (!vn) Pn.len = 0;
       // pins the conversion here: the compiler would otherwise sink it below the stores, to its use
       asm volatile("" ::"v"(Pn.n[0]), "v"(Pn.n[1]), "v"(Pn.n[2]), "v"(Pn.n[3]), "v"(Pn.len), "v"(Pn.neg) : "memory");
