@@ -282,6 +282,27 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(tb.data(), a.tile_bytes, tb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    if (a.src.cols) {
+      // the float32 measure pass only flags tiles with lines outside the packed path: their exact
+      // bytes from k_pcd_measure_list (the list rides in the tile-position slots, not yet written)
+      HIPCHK(hipStreamSynchronize(c->stream));
+      std::vector<int32_t> flagged;
+      for (int64_t t = 0; t < n_tiles; ++t)
+        if (tb[t] & kPcdSlowTile) flagged.push_back((int32_t)t);
+      if (!flagged.empty()) {
+        int32_t* d_list = reinterpret_cast<int32_t*>(d + o_tp);
+        HIPCHK(hipMemcpyAsync(d_list, flagged.data(), flagged.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                              c->stream));
+        {
+          TimedRegion tr(c, &c->codec_ev, c->stream);
+          hipLaunchKernelGGL(k_pcd_measure_list, dim3((uint32_t)flagged.size()), dim3(kPcdBlock), 0, c->stream, a,
+                             (const int32_t*)d_list);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(tb.data(), a.tile_bytes, tb.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                              c->stream));
+      }
+    }
   }
   int err = 0;
   HIPCHK(hipMemcpyAsync(&err, c->d_codec_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));

@@ -121,6 +121,7 @@ __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const ch
       __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));
     } else {
       const int e = b0 + 16 < hi ? b0 + 16 : hi;
+#pragma clang loop vectorize(disable) unroll(disable)
       for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];
     }
   }
@@ -786,25 +787,23 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
   constexpr int NT = kPcdMeasureWaveTiles;
   const int lane = threadIdx.x & 63;
   int32_t f = codec_frame_of(a.src, u0);
-  int32_t fr[NT];
-  int64_t r0[NT], cnt[NT];
+  int left[NT];   // lines of the tile at and after this lane's first (frame-relative, may be <= 0)
   float4 V[NT][4];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int64_t u = u0 + (threadIdx.x >> 6) * NT + j;   // a wave's tiles are consecutive
-    cnt[j] = 0;
-    r0[j] = 0;
-    fr[j] = f;
+    left[j] = 0;
     if (u < a.src.n_units) {
+      // tile u = block (poff_f + 256 (u - unit_off_f)) / 256: a wave-uniform base (scalar arithmetic)
       f = codec_advance(a.src.unit_off, f, u);
-      fr[j] = f;
-      r0[j] = (u - a.src.unit_off[f]) * kPcdBlock + 4 * lane;   // frame-relative line of .x
-      cnt[j] = a.src.doff[f + 1] - a.src.doff[f];
-    }
-    const float* q = a.src.cols + bidx(a.src.C, 0, a.src.poff[f] + r0[j]);
-    if (r0[j] < cnt[j]) {
+      const int64_t k = u - ldu(a.src.unit_off + f);
+      const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
+      left[j] = (int)min<int64_t>(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock) - 4 * lane;
+      const float* q = a.src.cols + blk * a.src.C * kBlkPts + 4 * lane;
+      if (left[j] > 0) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) V[j][c] = *reinterpret_cast<const float4*>(q + c * kBlkPts);
+        for (int c = 0; c < 4; ++c) V[j][c] = *reinterpret_cast<const float4*>(q + c * kBlkPts);
+      }
     }
   }
 #pragma unroll
@@ -814,21 +813,37 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
     int v = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (r0[j] + i < cnt[j]) {
+      if (i < left[j]) {
         const float c[4] = {f4g(V[j][0], i), f4g(V[j][1], i), f4g(V[j][2], i), f4g(V[j][3], i)};
-        int l = pcd_fast_len_f32(c);
-        if (l < 0) {
-          PcdLine L;
-          pcd_line(a.src, fr[j], a.src.doff[fr[j]] + r0[j] + i, L, a.err);
-          l = L.len + (1 << 20);
-        }
-        v += l;
+        const int l = pcd_fast_len_f32(c);
+        // a line outside the packed path flags the tile; its exact bytes come from
+        // k_pcd_measure_list (the byte formatter would double this kernel's registers)
+        v += l < 0 ? (1 << 20) : l;
       }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) a.tile_bytes[u] = pcd_tile_word(v);
   }
+}
+
+// The exact text bytes of the listed tiles (those k_pcd_measure<true> flagged): byte-path lengths
+// of every line, block scan; the flag stays (k_pcd_write_bytes writes these tiles).
+__global__ __launch_bounds__(kPcdBlock) void k_pcd_measure_list(const PcdArgs a, const int32_t* list) {
+  __shared__ int s_wave[kPcdBlock / 64];
+  const int64_t u = list[blockIdx.x];
+  int32_t f = codec_frame_of(a.src, u);
+  bool valid;
+  const int64_t row = pcd_row(a.src, u, f, valid);
+  int v = 0;
+  if (valid) {
+    PcdLine L;
+    pcd_line(a.src, f, row, L, a.err);
+    v = L.len;
+  }
+  int total;
+  block_scan(v, s_wave, total);
+  if (threadIdx.x == 0) a.tile_bytes[u] = total | kPcdSlowTile;
 }
 
 template <bool F32>
