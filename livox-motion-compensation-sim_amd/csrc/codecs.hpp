@@ -121,7 +121,6 @@ __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const ch
       __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));
     } else {
       const int e = b0 + 16 < hi ? b0 + 16 : hi;
-#pragma clang loop vectorize(disable) unroll(disable)
       for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];
     }
   }
