@@ -546,8 +546,8 @@ __device__ __forceinline__ void pk_tens_units(uint32_t v, uint32_t& t, uint32_t&
 
 // ---- packed line path (every value of the line |v| < 4294, ties included) ----------------------
 // The common LiDAR line is formatted from four 32-bit integers N = round(|v| * 10^6): the digits come
-// out of multiply-shift SWAR arithmetic on two 3-digit halves at once (swar_fields), and each value
-// goes to the tile's LDS text at its final byte offset (pcd_emit_line).  Tiles holding a line with
+// out of 2-digit groups split with packed 16-bit arithmetic (digit_groups, value_fields), and each value
+// goes to the tile's LDS text at its final byte offset (pcd_text, pcd_emit_line).  Tiles holding a line with
 // any other value (NaN, inf, |v| >= 4294) take the byte path (fmt6_prepare / pcd_emit,
 // k_pcd_write_bytes).  Rejected in round 4 (tools/ab_codecs.py --source batch, profiles/round4/s07,
 // measure + write): digits from a 200-byte "00".."99" LDS pair table, 909.4 vs 872.6 us (fewer VALU
@@ -557,12 +557,8 @@ struct PcdFast {
   uint32_t n[4];   // round-half-even(|v| * 10^6)
   uint32_t ip[4];  // n / 10^6 (the integer part)
   uint32_t neg;    // bit k: value k is negative (signbit)
-  int nd[4];       // integer digits of value k (1 .. 4)
-  int len;         // line length in bytes
   bool ok;         // all four values took the fast path
 };
-
-__device__ __forceinline__ int fast_nd(uint32_t ip) { return 1 + (ip >= 10u) + (ip >= 100u) + (ip >= 1000u); }
 
 // floor(N / 10^6) for N < 2^32 given as an exact float64: N 10^-6 is within 5e-13 of N / 10^6,
 // whose fraction is 0 or at least 10^-6 from 1, so adding 10^-9 and truncating is exact (one
@@ -593,23 +589,16 @@ __device__ __forceinline__ void pcd_fast(const CodecFrames& s, int32_t f, int64_
   codec_point(s, f, row, c);
   P.ok = true;
   P.neg = 0;
-  P.len = 4 + 4 * 7;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     P.ok &= fmt6_fast(c[k], P.n[k], P.ip[k]);
-    const uint32_t ng = signbit(c[k]) ? 1u : 0u;
-    P.neg |= ng << k;
-    P.nd[k] = fast_nd(P.ip[k]);
-    P.len += (int)ng + P.nd[k];
+    P.neg |= (signbit(c[k]) ? 1u : 0u) << k;
   }
 }
 
 // ---- float32 source (a batch's own columns) ----------------------------------------------------
 // v = m 2^e with a 24-bit m: |v| 10^6 = m 10^6 2^e has a significand below 2^44, so the float64
-// product is exact and N = rint(|v| 10^6) (round half to even) is exact with no error term.  The
-// digit count needs no arithmetic at all: N >= 10^k <=> |v| >= (10^k - 1/2) / 10^6, and the
-// smallest float32 at or above 9.9999995 / 99.9999995 / 999.9999995 is 10 / 100 / 1000 exactly
-// (the float32 below each is 1 ulp ~ 1e-6 .. 6e-5 under it, outside the half-unit band).
+// product is exact and N = rint(|v| 10^6) (round half to even) is exact with no error term.
 __device__ __forceinline__ bool fmt6_fast_f32(float v, uint32_t& n, uint32_t& ip) {
   const float a = fminf(fabsf(v), 4294.0f);   // NaN -> 4294 (the line fails the test below)
   const double y = rint((double)a * 1000000.0);
@@ -621,15 +610,10 @@ __device__ __forceinline__ bool fmt6_fast_f32(float v, uint32_t& n, uint32_t& ip
 __device__ __forceinline__ void pcd_fast_vals_f32(const float c[4], PcdFast& P) {
   P.ok = true;
   P.neg = 0;
-  P.len = 4 + 4 * 7;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     P.ok &= fmt6_fast_f32(c[k], P.n[k], P.ip[k]);
-    const float a = fabsf(c[k]);
-    const uint32_t ng = signbit(c[k]) ? 1u : 0u;
-    P.neg |= ng << k;
-    P.nd[k] = 1 + (a >= 10.0f) + (a >= 100.0f) + (a >= 1000.0f);
-    P.len += (int)ng + P.nd[k];
+    P.neg |= (signbit(c[k]) ? 1u : 0u) << k;
   }
 }
 
@@ -638,17 +622,12 @@ __device__ __forceinline__ void pcd_fast_vals_f32(const float c[4], PcdFast& P) 
 __device__ __forceinline__ void pcd_fast_vals_packed(const float c[4], PcdFast& P) {
   P.ok = true;
   P.neg = 0;
-  P.len = 4 + 4 * 7;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float a = fabsf(c[k]);
-    const double y = rint((double)a * 1000000.0);
+    const double y = rint((double)fabsf(c[k]) * 1000000.0);
     P.n[k] = (uint32_t)y;
     P.ip[k] = fast_ip(y);
-    const uint32_t ng = signbit(c[k]) ? 1u : 0u;
-    P.neg |= ng << k;
-    P.nd[k] = 1 + (a >= 10.0f) + (a >= 100.0f) + (a >= 1000.0f);
-    P.len += (int)ng + P.nd[k];
+    P.neg |= (signbit(c[k]) ? 1u : 0u) << k;
   }
 }
 
@@ -665,76 +644,106 @@ __device__ __forceinline__ int pcd_fast_len_f32(const float c[4]) {
   return ok ? len : -1;
 }
 
-// Digit fields of N = round(|v| 10^6) < 2^32 (|v| < 4294): D = the 4 integer digits with leading
-// zeros (byte 0 = thousands), A = ". d1 d2 d3", B = "d4 d5 d6 sep" (bytes in text order).  The ten
-// digits as five 2-digit groups (ip / 100, ip % 100, fp / 10^4, fp / 100 % 100, fp % 100), split into
-// tens and units two groups per instruction with packed 16-bit arithmetic (pk_tens_units); bytes
-// placed with v_perm_b32.  g2 = (fp 429497) >> 32 is fp / 10^4 exactly for fp < 10^6 (the
-// multiplier's excess adds < 6.3e-5 to a quotient whose fraction is at most 0.9999).  Against the
-// two 3-digit halves in 32-bit SWAR: 802.8 vs 806.8 us measure + write, fused write 751.4 vs 752.3
-// (profiles/round4/s17): kept for its ~2 fewer VALU instructions per value.
-__device__ __forceinline__ void swar_fields(uint32_t N, uint32_t ip, uint32_t sep, uint32_t& D, uint32_t& A,
-                                            uint32_t& B) {
-  // the masks state the ranges (ip < 8192, g2 < 128) so the products stay 24-bit multiply-adds
-  // (v_mad_i32_i24) instead of quarter-rate 64-bit ones
-  ip &= 0x1fffu;
-  const uint32_t fp = N - ip * 1000000u;                                                  // < 10^6
-  uint32_t g2 = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32);               // fp / 10^4
+// Digit groups of N = round(|v| 10^6) < 2^32 (|v| < 4294, so ip = N / 10^6 < 2^13): the ten digits
+// as five 2-digit groups, g0 = ip / 100, g1 = ip % 100, g2 = fp / 10^4, g3 = fp / 100 % 100 and
+// g4 = fp % 100 (fp = N - 10^6 ip), returned as g01 = g0 | g1 << 16, g23 = g2 | g3 << 16 and g4 (two
+// values' g4 are split together, pair_tu4).  g2 = (fp 429497) >> 32 is fp / 10^4 exactly for
+// fp < 10^6 (the multiplier's excess adds < 6.3e-5 to a quotient whose fraction is at most 0.9999).
+// The products are 24-bit multiply-adds (v_mad_i32_i24 by __mul24 with a negative constant, no
+// range masks).  Against the two 3-digit halves in 32-bit SWAR: 802.8 vs 806.8 us measure + write
+// (profiles/round4/s17).
+__device__ __forceinline__ void digit_groups(uint32_t N, uint32_t ip, uint32_t& g01, uint32_t& g23, uint32_t& g4) {
+  const uint32_t fp = N + (uint32_t)__mul24((int)ip, -1000000);                         // < 10^6
+  uint32_t g2 = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32);             // fp / 10^4
   // opaque to the optimiser: it recognises fp - (fp / 10^4) 10^4 as fp % 10^4 and lowers that
   // through a quarter-rate 64-bit multiply-add
   asm("" : "+v"(g2));
-  const uint32_t r4 = fp - (g2 & 0x7fu) * 10000u;                                         // < 10^4
-  const uint32_t g3 = __umul24(r4, 5243u) >> 19;                                          // r4 / 100
-  const uint32_t g4 = r4 - g3 * 100u;
-  const uint32_t g0 = __umul24(ip, 5243u) >> 19;                                          // ip / 100
+  const uint32_t r4 = fp + (uint32_t)__mul24((int)g2, -10000);                          // < 10^4
+  const uint32_t g3 = __umul24(r4, 5243u) >> 19;                                        // r4 / 100
+  g4 = r4 - g3 * 100u;
+  const uint32_t g0 = __umul24(ip, 5243u) >> 19;                                        // ip / 100
   const uint32_t g1 = ip - g0 * 100u;
+  g01 = g0 | (g1 << 16);
+  g23 = g2 | (g3 << 16);
+}
+// tens | units << 8 of two values' g4 at once (one packed split for both)
+__device__ __forceinline__ void pair_tu4(uint32_t ga, uint32_t gb, uint32_t& tua, uint32_t& tub) {
+  uint32_t T, U;
+  pk_tens_units(ga | (gb << 16), T, U);
+  tua = __builtin_amdgcn_perm(U, T, 0x0C0C0400u);
+  tub = __builtin_amdgcn_perm(U, T, 0x0C0C0602u);
+}
+// Text fields of one value (bytes in text order, v_perm_b32 placement): D = the 4 integer digits
+// with leading zeros as values 0..9 (byte 0 = thousands), A = ". d1 d2 d3", B = "d4 d5 d6 sep"
+__device__ __forceinline__ void value_fields(uint32_t g01, uint32_t g23, uint32_t tu4, uint32_t sep, uint32_t& D,
+                                             uint32_t& A, uint32_t& B) {
   uint32_t T1, U1, T2, U2;
-  pk_tens_units(g0 | (g1 << 16), T1, U1);
-  pk_tens_units(g2 | (g3 << 16), T2, U2);
-  const uint32_t t4 = __umul24(g4, 103u) >> 10;
-  const uint32_t tu4 = t4 | ((g4 - t4 * 10u) << 8);
-  D = __builtin_amdgcn_perm(T1, U1, 0x02060004u) + 0x30303030u;
+  pk_tens_units(g01, T1, U1);
+  pk_tens_units(g23, T2, U2);
+  D = __builtin_amdgcn_perm(T1, U1, 0x02060004u);
   A = __builtin_amdgcn_perm(T2, U2, 0x0600040Cu) + 0x3030302Eu;
   B = __builtin_amdgcn_perm(U2, tu4, 0x0C010006u) + (0x00303030u | (sep << 24));
 }
 __device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
-// One value whose text starts at byte o of the tile text; EXACT: the line's first value.  The
-// fields go to LDS as bytes at their final offsets (the compiler merges a value's 12 bytes into one
-// unaligned ds_write_b96).  Values are written in reverse order, and every value but the line's first
-// stores its 4-digit field and a '-' unconditionally (at most 5 bytes before its '.'): bytes left of
-// its own head fall inside the previous value of the same line, which is written afterwards and
-// overwrites them.  The line's first value stores exactly its own bytes, so no lane ever writes
-// another line's text: no zeroing, no atomics.
-template <bool EXACT>
-__device__ __forceinline__ void bytes_value(uint8_t* base, int o, uint32_t N, uint32_t ip, int nd, bool neg,
-                                            uint32_t sep) {
-  uint32_t D, A, B;
-  swar_fields(N, ip, sep, D, A, B);
-  uint8_t* pa = base + o + nd + (neg ? 1 : 0);   // the '.'
-  put4(pa, A);
-  put4(pa + 4, B);
-  if (EXACT) {
-    pa[-1] = (uint8_t)(D >> 24);
-    if (nd >= 2) pa[-2] = (uint8_t)(D >> 16);
-    if (nd >= 3) pa[-3] = (uint8_t)(D >> 8);
-    if (nd >= 4) pa[-4] = (uint8_t)D;
-    if (neg) pa[-nd - 1] = '-';
-  } else {
-    put4(pa - 4, D);
-    pa[-nd - 1] = '-';
+
+// A packed line's text: value k's fields D (ASCII), A, B, its count q of leading zero digits in D
+// (4 - its integer digit count: the index of D's first non-zero digit byte, one v_ffbl_b32), the sign
+// bits and the line length 4 (nd + [v < 0] + 8) summed = 48 + sum([v < 0] - q).  The digit count
+// comes out of the digits themselves, so it is N >= 10^7 / 10^8 / 10^9 exactly (no compares).
+struct PcdText {
+  uint32_t D[4], A[4], B[4];
+  int q[4];
+  uint32_t neg;
+  int len;
+};
+__device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
+  uint32_t g01[4], g23[4], g4[4], tu4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) digit_groups(P.n[k], P.ip[k], g01[k], g23[k], g4[k]);
+  pair_tu4(g4[0], g4[1], tu4[0], tu4[1]);
+  pair_tu4(g4[2], g4[3], tu4[2], tu4[3]);
+  int len = 48;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t D;
+    value_fields(g01[k], g23[k], tu4[k], k == 3 ? '\n' : ' ', D, T.A[k], T.B[k]);
+    T.q[k] = (int)(__builtin_ctz(D | 0x01000000u) >> 3);   // the units byte always counts
+    T.D[k] = D + 0x30303030u;
+    len += (int)((P.neg >> k) & 1u) - T.q[k];
   }
+  T.neg = P.neg;
+  T.len = len;
 }
 
-// one packed line at byte `off` of the tile text
-__device__ __forceinline__ void pcd_emit_line(const PcdFast& P, uint8_t* base, int off) {
-  const int o1 = off + 8 + P.nd[0] + (int)(P.neg & 1u), o2 = o1 + 8 + P.nd[1] + (int)((P.neg >> 1) & 1u);
-  const int o3 = o2 + 8 + P.nd[2] + (int)((P.neg >> 2) & 1u);
-  bytes_value<false>(base, o3, P.n[3], P.ip[3], P.nd[3], (P.neg >> 3) & 1u, '\n');
-  bytes_value<false>(base, o2, P.n[2], P.ip[2], P.nd[2], (P.neg >> 2) & 1u, ' ');
-  bytes_value<false>(base, o1, P.n[1], P.ip[1], P.nd[1], (P.neg >> 1) & 1u, ' ');
-  bytes_value<true>(base, off, P.n[0], P.ip[0], P.nd[0], P.neg & 1u, ' ');
+// One packed line at byte `off` of the tile text; the fields go to LDS as bytes at their final
+// offsets (the compiler merges them into unaligned ds_write_b64 / b96).  Values 3, 2, 1 are written
+// in that order, each storing its 4-digit field and a '-' unconditionally (at most 5 bytes before its
+// '.'): bytes left of its own head fall inside the previous value of the same line, which is written
+// afterwards and overwrites them.  Value 0 writes its integer text ('-' if negative, then its nd
+// digits) as one 8-byte store at the line start — the bytes past the integer text fall inside its
+// own fraction — and then its fraction.  No lane writes outside its own line: no zeroing, no atomics.
+__device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, int off) {
+  int pa[4];   // the '.' of each value
+  pa[0] = off + 4 - T.q[0] + (int)(T.neg & 1u);
+#pragma unroll
+  for (int k = 1; k < 4; ++k) pa[k] = pa[k - 1] + 12 - T.q[k] + (int)((T.neg >> k) & 1u);
+#pragma unroll
+  for (int k = 3; k >= 1; --k) {
+    uint8_t* const q = base + pa[k];
+    put4(q - 4, T.D[k]);
+    put4(q, T.A[k]);
+    put4(q + 4, T.B[k]);
+    q[T.q[k] - 5] = '-';
+  }
+  const uint32_t S = T.D[0] >> (8 * T.q[0]);   // the integer digits in the low bytes
+  const bool neg = T.neg & 1u;
+  const uint32_t lo = neg ? ((S << 8) | '-') : S, hi = S >> 24;   // hi: the 5th byte ("-dddd")
+  put4(base + off, lo);
+  put4(base + off + 4, hi);
+  put4(base + pa[0], T.A[0]);
+  put4(base + pa[0] + 4, T.B[0]);
 }
 
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
@@ -883,10 +892,10 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 // modulo 16), then stored with codec_store_piece.  Tiles flagged slow are skipped
 // (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text always fits.
 // pcd_tile_text: the tile's lines in LDS, -> the tile's text bytes; pcd_tile_store: its stores.
-__device__ __forceinline__ int pcd_tile_text(const PcdFast& P, bool valid, int64_t G, int* s_wave, uint4* s_text4) {
+__device__ __forceinline__ int pcd_tile_text(const PcdText& T, bool valid, int64_t G, int* s_wave, uint4* s_text4) {
   int total;
-  const int excl = block_scan(P.len, s_wave, total) - P.len;
-  if (valid) pcd_emit_line(P, reinterpret_cast<uint8_t*>(s_text4), (int)(G & 15) + excl);
+  const int excl = block_scan(T.len, s_wave, total) - T.len;
+  if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text4), (int)(G & 15) + excl);
   __syncthreads();
   return total;
 }
@@ -923,7 +932,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {
-    // Tile j + 1's loads are in flight while tile j is formatted, and converted (pcd_fast_vals_f32)
+    // Tile j + 1's loads are in flight while tile j is formatted, and converted (pcd_text)
     // between tile j's LDS text and its stores.  vmcnt counts stores as well as loads, and a load
     // consumed with stores in flight waits for them too: consumed after tile j's stores, it would
     // wait for their completion; consumed before them, it waits only for tile j - 1's, long done.
@@ -933,7 +942,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
     bool vn = false;
     int32_t flag_n = 0;
     int64_t gn = 0;
-    PcdFast Pn;
+    PcdText Tn;
     // tile u is block (poff_f + 256 (u - unit_off_f)) / 256 of the batch: its columns start at a
     // workgroup-uniform address (scalar arithmetic), a lane's line at + threadIdx.x
     auto fetch = [&](int64_t u) {
@@ -950,21 +959,25 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       gn = ldu(a.tile_pos + u);
     };
     auto convert = [&]() {
-      pcd_fast_vals_packed(cn, Pn);   // (invalid lanes convert zeros / stale values: length zeroed)
-      if (!vn) Pn.len = 0;
+      PcdFast P;
+      pcd_fast_vals_packed(cn, P);   // (invalid lanes convert zeros / stale values: length zeroed)
+      pcd_text(P, Tn);
+      if (!vn) Tn.len = 0;
       // pins the conversion here: the compiler would otherwise sink it below the stores, to its use
-      asm volatile("" ::"v"(Pn.n[0]), "v"(Pn.n[1]), "v"(Pn.n[2]), "v"(Pn.n[3]), "v"(Pn.len), "v"(Pn.neg) : "memory");
+      asm volatile("" ::"v"(Tn.D[0]), "v"(Tn.D[1]), "v"(Tn.D[2]), "v"(Tn.D[3]), "v"(Tn.A[0]), "v"(Tn.A[1]),
+                   "v"(Tn.A[2]), "v"(Tn.A[3]), "v"(Tn.B[0]), "v"(Tn.B[1]), "v"(Tn.B[2]), "v"(Tn.B[3]), "v"(Tn.len)
+                   : "memory");
     };
     if (u0 < u_end) fetch(u0);
     convert();
     for (int64_t u = u0; u < u_end; ++u) {
-      const PcdFast P = Pn;
+      const PcdText T = Tn;
       const bool valid = vn;
       const bool packed = !(flag_n & kPcdSlowTile);   // workgroup-uniform
       const int64_t G = gn;
       if (u + 1 < u_end) fetch(u + 1);
       int total = 0;
-      if (packed) total = pcd_tile_text(P, valid, G, s_wave, s_text4);
+      if (packed) total = pcd_tile_text(T, valid, G, s_wave, s_text4);
       convert();
       if (packed) pcd_tile_store(a, G, total, s_text4);
     }
@@ -975,11 +988,15 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       if (ldu(a.tile_bytes + u) & kPcdSlowTile) continue;   // workgroup-uniform
       bool valid;
       const int64_t row = pcd_row(a.src, u, f, valid);
-      PcdFast P;
-      P.len = 0;
-      if (valid) pcd_fast(a.src, f, row, P);
+      PcdText T;
+      T.len = 0;
+      if (valid) {
+        PcdFast P;
+        pcd_fast(a.src, f, row, P);
+        pcd_text(P, T);
+      }
       const int64_t G = ldu(a.tile_pos + u);
-      const int total = pcd_tile_text(P, valid, G, s_wave, s_text4);
+      const int total = pcd_tile_text(T, valid, G, s_wave, s_text4);
       pcd_tile_store(a, G, total, s_text4);
     }
   }

@@ -144,8 +144,8 @@ struct mc_ctx {
   double* d_gyro = nullptr;
   mc::ImuSeg* d_imu_seg = nullptr;     // 2 * M_cap (double buffer)
   // scan_environment state (LMC:701-770): scene, per-frame f64 poses, per-(frame, tile) counts
-  int64_t E = 0, env_ld = 4;
-  double* d_env = nullptr;
+  int64_t E = 0;
+  double* d_env = nullptr;   // the scene as columns (scan.hpp scene_cols)
   int32_t scan_F = 0, scan_tiles = 0;
   double* d_scan_ftime = nullptr;
   double* d_scan_pose = nullptr;

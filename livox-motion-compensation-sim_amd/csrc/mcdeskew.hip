@@ -1671,13 +1671,22 @@ int mc_set_environment(mc_ctx* c, int64_t n, const double* env, int64_t ld) {
   if (int r = sync_all(c)) return r;
   dev_free(c->d_env);
   c->E = 0;
-  if (int r = dev_alloc(&c->d_env, (size_t)std::max<int64_t>(n, 1) * ld)) return r;
+  // scan.hpp's column layout: x, y, z float64 and the intensity as float32 (the value k_scan_emit
+  // writes, (float) of the reference's float64), transposed here once per scene
+  const size_t words = scene_words(n);
+  if (int r = dev_alloc(&c->d_env, std::max<size_t>(words, 1))) return r;
   if (n > 0) {
-    HIPCHK(hipMemcpyAsync(c->d_env, env, (size_t)n * ld * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    std::vector<double> h(words);
+    float* w = reinterpret_cast<float*>(h.data() + 3 * n);
+    for (int64_t i = 0; i < n; ++i) {
+      const double* q = env + i * ld;
+      h[i] = q[0]; h[n + i] = q[1]; h[2 * n + i] = q[2];
+      w[i] = (float)q[3];
+    }
+    HIPCHK(hipMemcpyAsync(c->d_env, h.data(), words * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }
   c->E = n;
-  c->env_ld = ld;
   return MC_OK;
 }
 
@@ -1699,8 +1708,9 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   c->scan_F = 0;
   if (int r = dev_alloc(&c->d_scan_ftime, std::max(F, 1))) return r;
   if (int r = dev_alloc(&c->d_scan_pose, 12 * (size_t)std::max(F, 1))) return r;
-  if (int r = dev_alloc(&c->d_scan_tcount, (size_t)std::max(F, 1) * std::max(tiles, 1))) return r;
-  if (int r = dev_alloc(&c->d_scan_toff, (size_t)std::max(F, 1) * std::max(tiles, 1))) return r;
+  const int32_t Fp = scan_fpad(F);   // per-tile rows of counts / offsets, frames padded to kScanFrames
+  if (int r = dev_alloc(&c->d_scan_tcount, (size_t)std::max(Fp, 1) * std::max(tiles, 1))) return r;
+  if (int r = dev_alloc(&c->d_scan_toff, (size_t)std::max(Fp, 1) * std::max(tiles, 1))) return r;
   if (int r = dev_alloc(&c->d_scan_nvis, std::max(F, 1))) return r;
   c->scan_par[0] = params[0];
   c->scan_par[1] = params[1] * params[1];   // LMC:715 max_range_sq
@@ -1716,7 +1726,7 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   hipLaunchKernelGGL(k_scan_pose, dim3((F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->d_time, c->d_pos,
                      c->d_rpy, c->T, c->d_scan_ftime, F, pose_select, c->d_scan_pose);
   HIPCHK(hipGetLastError());
-  std::vector<int64_t> nvis(F, 0), toff((size_t)F * std::max(tiles, 1), 0);
+  std::vector<int64_t> nvis(F, 0), toff((size_t)Fp * std::max(tiles, 1), 0);
   if (tiles > 0) {
     const ScanParams sp = make_scan_params(c->scan_par, cap);
     const size_t words = (size_t)tiles * ((F + kScanFrames - 1) / kScanFrames) * kBlock;
@@ -1729,19 +1739,18 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
     {
       TimedRegion tr(c, &c->scan_ev, c->stream);
       const uint32_t units = (uint32_t)tiles * (uint32_t)((F + kScanFrames - 1) / kScanFrames);
-      hipLaunchKernelGGL(k_scan_count, dim3(units), dim3(kBlock), 0, c->stream, c->d_env, c->env_ld, c->E, tiles,
+      hipLaunchKernelGGL(k_scan_count, dim3(units), dim3(kBlock), 0, c->stream, c->d_env, c->E, tiles,
                          c->d_scan_pose, F, sp, c->d_scan_tcount, c->d_scan_bits);
     }
     HIPCHK(hipGetLastError());
-    std::vector<int32_t> tc((size_t)F * tiles);
+    std::vector<int32_t> tc((size_t)Fp * tiles);
     HIPCHK(hipMemcpyAsync(tc.data(), c->d_scan_tcount, tc.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    for (int32_t f = 0; f < F; ++f) {
-      int64_t run = 0;
-      for (int32_t t = 0; t < tiles; ++t) { toff[(size_t)f * tiles + t] = run; run += tc[(size_t)f * tiles + t]; }
-      nvis[f] = run;
+    for (int32_t t = 0; t < tiles; ++t) {   // tile-major rows: the frames' running sums side by side
+      const size_t row = (size_t)t * Fp;
+      for (int32_t f = 0; f < F; ++f) { toff[row + f] = nvis[f]; nvis[f] += tc[row + f]; }
     }
-    HIPCHK(hipMemcpyAsync(c->d_scan_toff, toff.data(), (size_t)F * tiles * sizeof(int64_t), hipMemcpyHostToDevice,
+    HIPCHK(hipMemcpyAsync(c->d_scan_toff, toff.data(), toff.size() * sizeof(int64_t), hipMemcpyHostToDevice,
                           c->stream));
   }
   HIPCHK(hipMemcpyAsync(c->d_scan_nvis, nvis.data(), F * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
@@ -1775,7 +1784,7 @@ int mc_scan_emit(mc_ctx* c, mc_batch* out, const double* noise) {
     d_noise = static_cast<const double*>(st);
   }
   ScanEmitArgs ea;
-  ea.env = c->d_env; ea.ld = c->env_ld; ea.E = c->E; ea.n_tiles = c->scan_tiles;
+  ea.env = c->d_env; ea.E = c->E; ea.n_tiles = c->scan_tiles;
   ea.pose = c->d_scan_pose; ea.F = out->F;
   ea.sp = make_scan_params(c->scan_par, c->scan_cap);
   ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.vis_bits = c->d_scan_bits; ea.noise = d_noise;

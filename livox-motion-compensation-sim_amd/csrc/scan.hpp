@@ -15,6 +15,12 @@
 // (with the units dealt over the 8 XCDs every L2 fetched the whole scene: 2.9x the algorithmic
 // bytes, profiles/pmc_traffic.json r3s65), and a frame's output runs of neighbouring tiles meet in
 // one L2 instead of being written as partial lines by two.
+//
+// Device layout (mc_set_environment / mc_scan_count): the scene as columns — x, y, z float64 (the
+// 24 bytes the visibility test needs, one coalesced 8-byte load per lane each; the reference's (E,4)
+// rows would fetch 32) and the intensity as float32 (the output's own rounding of the float64 value,
+// read only for emitted points); per-(tile, frame) counts and offsets tile-major with the frames
+// padded to kScanFrames, so a workgroup's 8 frames are one 32 / 64-byte run.
 #pragma once
 #include "kernels.hpp"
 
@@ -111,21 +117,30 @@ __device__ __forceinline__ bool scan_visible(const double* __restrict__ P, doubl
   return scan_fov_exact(lx, ly, s, az_in, el_in, sp.half_fov_h, sp.half_fov_v);
 }
 
+// the scene columns in one allocation of scene_words(E) doubles
+inline size_t scene_words(int64_t E) { return 3 * (size_t)E + ((size_t)E + 1) / 2; }
+struct SceneCols {
+  const double* x; const double* y; const double* z; const float* w;
+};
+__host__ __device__ inline SceneCols scene_cols(const double* env, int64_t E) {
+  return SceneCols{env, env + E, env + 2 * E, reinterpret_cast<const float*>(env + 3 * E)};
+}
+__host__ __device__ inline int32_t scan_fpad(int32_t F) { return (F + kScanFrames - 1) / kScanFrames * kScanFrames; }
+
 // the workgroup's scene tile, kScanRounds points per thread, in registers
 struct ScanTile {
   double x[kScanRounds], y[kScanRounds], z[kScanRounds];
   bool in[kScanRounds];
 };
 
-__device__ __forceinline__ void scan_load_tile(const double* __restrict__ env, int64_t ld, int64_t E, int64_t tile,
-                                               ScanTile& t) {
+__device__ __forceinline__ void scan_load_tile(const SceneCols& sc, int64_t E, int64_t tile, ScanTile& t) {
   const int64_t t0 = tile * kScanTile;
 #pragma unroll
   for (int r = 0; r < kScanRounds; ++r) {
     const int64_t e = t0 + r * kBlock + threadIdx.x;
     t.in[r] = e < E;
-    const double* q = env + (t.in[r] ? e : 0) * ld;
-    t.x[r] = q[0]; t.y[r] = q[1]; t.z[r] = q[2];
+    const int64_t i = t.in[r] ? e : 0;
+    t.x[r] = sc.x[i]; t.y[r] = sc.y[i]; t.z[r] = sc.z[i];
   }
 }
 
@@ -143,16 +158,16 @@ __device__ __forceinline__ ScanUnit scan_unit(int32_t n_tiles) {
   return ScanUnit{u / n_fg, (int)(u % n_fg)};
 }
 
-// pass 1: visible scene points per (frame, tile) -> tile_count[f * n_tiles + tile], and the
+// pass 1: visible scene points per (frame, tile) -> tile_count[tile * scan_fpad(F) + f], and the
 // visibility bits (bit j*kScanRounds + r: frame f0+j, round r) that pass 2 consumes
-__global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict__ env, int64_t ld, int64_t E,
-                                                       int32_t n_tiles, const double* __restrict__ pose, int32_t F,
-                                                       ScanParams sp, int32_t* __restrict__ tile_count,
+__global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict__ env, int64_t E, int32_t n_tiles,
+                                                       const double* __restrict__ pose, int32_t F, ScanParams sp,
+                                                       int32_t* __restrict__ tile_count,
                                                        uint32_t* __restrict__ vis_bits) {
   __shared__ int s_cnt[kScanFrames][kBlock / 64];
   const ScanUnit su = scan_unit(n_tiles);
   ScanTile t;
-  scan_load_tile(env, ld, E, su.tile, t);
+  scan_load_tile(scene_cols(env, E), E, su.tile, t);
   const int f0 = su.fg * kScanFrames;
   const int nf = F - f0 < kScanFrames ? F - f0 : kScanFrames;
   uint32_t bits = 0;
@@ -175,15 +190,15 @@ __global__ __launch_bounds__(kBlock) void k_scan_count(const double* __restrict_
   if (threadIdx.x < nf) {
     int tot = 0;
     for (int w = 0; w < kBlock / 64; ++w) tot += s_cnt[threadIdx.x][w];
-    tile_count[(int64_t)(f0 + threadIdx.x) * n_tiles + su.tile] = tot;
+    tile_count[su.tile * scan_fpad(F) + f0 + threadIdx.x] = tot;
   }
 }
 
 // pass 2: in-order compaction + systematic subsample + noise, written into the output batch
 struct ScanEmitArgs {
-  const double* env; int64_t ld; int64_t E; int32_t n_tiles;
+  const double* env; int64_t E; int32_t n_tiles;   // env: the scene columns (scene_cols)
   const double* pose; int32_t F; ScanParams sp;
-  const int64_t* tile_off;   // [F][n_tiles] exclusive visible-point offset of the tile in its frame
+  const int64_t* tile_off;   // [n_tiles][scan_fpad(F)] exclusive visible-point offset of the tile in its frame
   const int64_t* nvis;       // [F] visible points before subsampling
   const uint32_t* vis_bits;  // pass 1's visibility words
   const double* noise;       // (N_out, 3) in the batch's dense order, or nullptr
@@ -195,8 +210,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
   __shared__ int s_cnt[kScanRounds][kBlock / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const ScanUnit su = scan_unit(a.n_tiles);
+  const SceneCols sc = scene_cols(a.env, a.E);
   ScanTile t;
-  scan_load_tile(a.env, a.ld, a.E, su.tile, t);
+  scan_load_tile(sc, a.E, su.tile, t);
   const int64_t t0 = su.tile * kScanTile;
   const int f0 = su.fg * kScanFrames;
   const int nf = a.F - f0 < kScanFrames ? a.F - f0 : kScanFrames;
@@ -227,7 +243,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
     const int64_t nv = a.nvis[f];
     const int64_t step = nv > a.sp.cap ? nv / a.sp.cap : 1;    // LMC:757-760
     const int64_t poff = a.poff[f], doff = a.doff[f];
-    int64_t base = a.tile_off[(int64_t)f * a.n_tiles + su.tile];
+    int64_t base = a.tile_off[su.tile * scan_fpad(a.F) + f];
 #pragma unroll
     for (int r = 0; r < kScanRounds; ++r) {
       int before = 0, total = 0;
@@ -249,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
           q[0] = (float)(lx[r] + nx);
           q[kBlkPts] = (float)(ly[r] + ny);
           q[2 * kBlkPts] = (float)(lz[r] + nz);
-          q[3 * kBlkPts] = (float)a.env[e * a.ld + 3];
+          q[3 * kBlkPts] = sc.w[e];
         }
       }
       base += total;

@@ -20,6 +20,11 @@
 #define __ATOMIC_RELAXED 0
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
 static inline uint32_t __umul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
+// v_mul_i32_i24: the low 24 bits of each operand as signed integers
+static inline int __mul24(int a, int b) {
+  const int64_t x = (int64_t)(int32_t)((uint32_t)a << 8) >> 8, y = (int64_t)(int32_t)((uint32_t)b << 8) >> 8;
+  return (int)(uint32_t)(uint64_t)(x * y);
+}
 // v_perm_b32: byte i of the result = byte sel[i] of {s0:s1} (0-3 = s1, 4-7 = s0), 12 -> 0x00
 static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
   const uint64_t v = ((uint64_t)s0 << 32) | s1;
@@ -73,7 +78,7 @@ int main(int argc, char** argv) {
   }
   const CodecFrames s{pts.data()};
   std::vector<uint32_t> buf(16400 / 4 + 4);
-  // the multiply-shift divisions of swar_fields on their whole ranges
+  // the multiply-shift divisions of digit_groups on their whole ranges
   for (uint32_t fp = 0; fp < 1000000u; ++fp)
     if ((uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 4294968ull) >> 32) != fp / 1000u ||
         (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32) != fp / 10000u) { ++bad; break; }
@@ -123,10 +128,12 @@ int main(int argc, char** argv) {
     int off = shift;
     std::string want;
     std::vector<PcdFast> P(256);
+    std::vector<PcdText> T(256);
     std::vector<int> offs(256);
     for (int l = 0; l < 256; ++l) {
       const double* c = &pts[4 * ((size_t)t * 256 + l)];
       pcd_fast(s, 0, (int64_t)t * 256 + l, P[l]);
+      pcd_text(P[l], T[l]);
       char line[160];
       std::snprintf(line, sizeof line, "%.6f %.6f %.6f %.6f\n", c[0], c[1], c[2], c[3]);
       const double cc[4] = {c[0], c[1], c[2], c[3]};
@@ -139,10 +146,18 @@ int main(int argc, char** argv) {
         pcd_fast_vals_f32(cf, Q);
         ++f32_lines;
         if (pcd_fast_len_f32(cf) != lf || Q.ok != P[l].ok ||
-            (Q.ok && (Q.len != P[l].len || Q.neg != P[l].neg || std::memcmp(Q.n, P[l].n, sizeof Q.n) ||
+            (Q.ok && (Q.neg != P[l].neg || std::memcmp(Q.n, P[l].n, sizeof Q.n) ||
                       std::memcmp(Q.ip, P[l].ip, sizeof Q.ip)))) {
           ++bad;
-          std::printf("float32 path differs (len %d/%d ok %d/%d) for %s", Q.len, P[l].len, Q.ok, P[l].ok, line);
+          std::printf("float32 path differs (ok %d/%d) for %s", Q.ok, P[l].ok, line);
+        }
+        if (Q.ok) {   // the write pass's packed conversion of a measured-packed line: the same numbers
+          PcdFast R;
+          pcd_fast_vals_packed(cf, R);
+          if (R.neg != Q.neg || std::memcmp(R.n, Q.n, sizeof R.n) || std::memcmp(R.ip, Q.ip, sizeof R.ip)) {
+            ++bad;
+            std::printf("packed conversion differs for %s", line);
+          }
         }
       }
       if (!P[l].ok) {
@@ -150,16 +165,16 @@ int main(int argc, char** argv) {
         continue;
       }
       ++fast;
-      if ((int)std::strlen(line) != P[l].len || lf != P[l].len) {
+      if ((int)std::strlen(line) != T[l].len || lf != T[l].len) {
         ++bad;
-        std::printf("length %d / %d for %s", P[l].len, lf, line);
+        std::printf("length %d / %d for %s", T[l].len, lf, line);
       }
       offs[l] = off;
-      off += P[l].len;
+      off += T[l].len;
       want += line;
     }
     for (int l = 255; l >= 0; --l)
-      if (P[l].ok) pcd_emit_line(P[l], reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
+      if (P[l].ok) pcd_emit_line(T[l], reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
     const std::string got(reinterpret_cast<const char*>(buf.data()) + shift, off - shift);
     // nothing written outside the tile's text
     const unsigned char* bb = reinterpret_cast<const unsigned char*>(buf.data());

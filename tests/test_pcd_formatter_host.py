@@ -1,4 +1,4 @@
-"""The device "%.6f" line writer (codecs.hpp: pcd_fast / pcd_fast_len / swar_fields / pcd_emit_line)
+"""The device "%.6f" line writer (codecs.hpp: pcd_fast / pcd_fast_len / digit_groups / pcd_emit_line)
 compiled for the host with g++ and checked against the C library's correctly rounded
 formatting — the kernel's own source, spliced into tests/host/pcd_formatter_host.cpp, exercised
 on this CPU (no GPU): float32 / float64 values, exact ties, digit carries, -0.0, values near the

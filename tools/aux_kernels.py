@@ -65,16 +65,24 @@ def main():
         scans = ctx.scan(times, dict(cfg, lidar_range_noise=0.0), out=scans)
     ctx.sync()
     F = len(times)
-    bits = ((E + 1023) // 1024) * ((F + 7) // 8) * 256 * 4      # pass-1 visibility words
+    tiles, Fp = (E + 1023) // 1024, (F + 7) // 8 * 8
+    bits = tiles * (Fp // 8) * 256 * 4                         # pass-1 visibility words
+    poses = 96 * F                                             # R (9) + t (3) float64 per frame
+    n_out = int(scans.n_points)
     alg = {
         "k_soa_to_aos": 48 * n, "k_aos_to_soa": 48 * n,
         "k_lvx_packages": 16 * n + int(pos[-1]) - 88 - 24 * args.frames,
         "k_pcd_measure": 16 * n, "k_pcd_write": 16 * n + int(bpos[-1]),
-        "k_scan_count": 24 * E + bits, "k_scan_emit": 24 * E + bits + 16 * int(scans.n_points),
+        # scene x, y, z once + the poses once + the visibility words + the per-(tile, frame) counts
+        "k_scan_count": 24 * E + poses + bits + 4 * tiles * Fp,
+        # ... + the offsets (8 B) + per-frame visible counts, and per emitted point its float32
+        # intensity (4 B) and its output row (16 B)
+        "k_scan_emit": 24 * E + poses + bits + 8 * tiles * Fp + 8 * F + 20 * n_out,
     }
     print(json.dumps({"algorithmic_bytes_per_launch": alg, "points": n, "scene": E, "frames_scanned": len(times),
-                      "note": "scan kernels: the scene (24 B/pt of x,y,z) is read once from HBM and then "
-                              "re-read from L2 by every frame; algorithmic = scene + output"}))
+                      "note": "scan kernels: the scene (24 B/pt of x,y,z columns) and the frame poses (96 B) "
+                              "are read once from HBM and then re-read from L2; algorithmic = those + the "
+                              "visibility words, counts / offsets and output"}))
 
 
 if __name__ == "__main__":

@@ -6,6 +6,8 @@
 #   ab      tools/ab.py $AB_ARGS (interleaved A/B of build/variants/lib_*.so)
 #   bench   bench.py with the driver's flags ($BENCH_ARGS)
 #   abc     tools/ab_codecs.py $ABC_ARGS (interleaved A/B of the codec kernels across libraries)
+#   abf     tools/ab_pcd_fused.py $ABF_ARGS (interleaved A/B of the fused deskew -> PCD pipeline)
+#   pcdpmc  tools/pcd_pmc.sh (SQ instruction counters of the codec / stager kernels)
 #   pmc     tools/pmc_traffic.py (deskew kernels, then --aux), profiles/pmc_traffic.json copied out
 #   latency tools/latency.py ($LAT_ARGS)
 #   prof    rocprofv3 --kernel-trace --stats of the same bench command
@@ -50,6 +52,14 @@ for step in $STEPS; do
       timeout -k 10 600 python -u tools/ab_codecs.py ${ABC_ARGS:-} > "$OUT/ab_codecs.log" 2>&1
       stop_if_fault $? abc
       cat "$OUT/ab_codecs.log" ;;
+    abf)
+      timeout -k 10 600 python -u tools/ab_pcd_fused.py ${ABF_ARGS:-} > "$OUT/ab_fused.log" 2>&1
+      stop_if_fault $? abf
+      cat "$OUT/ab_fused.log" ;;
+    pcdpmc)
+      timeout -k 10 400 bash tools/pcd_pmc.sh > "$OUT/pcd_pmc.log" 2>&1
+      stop_if_fault $? pcdpmc
+      tail -8 "$OUT/pcd_pmc.log" ;;
     pmc)
       timeout -k 10 900 python tools/pmc_traffic.py --tag "$TAG" > "$OUT/pmc.log" 2>&1
       stop_if_fault $? pmc
