@@ -806,7 +806,7 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
       f = codec_advance(a.src.unit_off, f, u);
       const int64_t k = u - ldu(a.src.unit_off + f);
       const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
-      left[j] = (int)min<int64_t>(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock) - 4 * lane;
+      left[j] = (int)min_i64(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock) - 4 * lane;
       const float* q = a.src.cols + blk * a.src.C * kBlkPts + 4 * lane;
       if (left[j] > 0) {
 #pragma unroll
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       f = codec_advance(a.src.unit_off, f, u);
       const int64_t k = u - ldu(a.src.unit_off + f);                       // tile of frame f
       const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
-      const int left = (int)min<int64_t>(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock);
+      const int left = (int)min_i64(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock);
       vn = (int)threadIdx.x < left;
       const float* q = a.src.cols + blk * a.src.C * kBlkPts + threadIdx.x;
       if (vn) {

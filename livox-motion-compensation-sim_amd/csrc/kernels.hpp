@@ -1867,7 +1867,8 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
     const int64_t loc0 = tl.pstart - poff;
     const int np = 4 * tl.ngroups;                                      // padded points in the tile
-    const int nv = (int)max<int64_t>(0, min<int64_t>(np, cnt - loc0)); // valid ones
+    const int64_t rest = min_i64(np, cnt - loc0);
+    const int nv = rest > 0 ? (int)rest : 0;                          // valid ones
     const double* src = aos + (doff + loc0) * ld;
     for (int j = threadIdx.x; j < np; j += kBlock) {
       float r[4] = {0.f, 0.f, 0.f, 0.f};

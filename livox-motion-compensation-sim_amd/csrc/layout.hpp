@@ -25,6 +25,10 @@ __device__ __forceinline__ int64_t xcd_unit(int64_t b, int64_t n) {
   return x * per + (x < rem ? x : rem) + i;
 }
 
+// 64-bit integer minimum (HIP's min / max templates resolve int64_t arguments through float64
+// conversions on gfx950: six VALU instructions for a wave-uniform value)
+__device__ __forceinline__ int64_t min_i64(int64_t a, int64_t b) { return a < b ? a : b; }
+
 // wave-uniform load (memory the kernel never writes) through the constant address space -> s_load_dword* into SGPRs
 template <typename T>
 __device__ __forceinline__ T ldu(const T* p) {
