@@ -695,7 +695,7 @@ __device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
 struct PcdText {
   uint32_t D[4], A[4], B[4];
   int q[4];
-  uint32_t neg;
+  int ng[4];   // 1: value k is negative
   int len;
 };
 __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
@@ -711,9 +711,9 @@ __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
     value_fields(g01[k], g23[k], tu4[k], k == 3 ? '\n' : ' ', D, T.A[k], T.B[k]);
     T.q[k] = (int)(__builtin_ctz(D | 0x01000000u) >> 3);   // the units byte always counts
     T.D[k] = D + 0x30303030u;
-    len += (int)((P.neg >> k) & 1u) - T.q[k];
+    T.ng[k] = (int)((P.neg >> k) & 1u);
+    len += T.ng[k] - T.q[k];
   }
-  T.neg = P.neg;
   T.len = len;
 }
 
@@ -726,9 +726,9 @@ __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
 // own fraction — and then its fraction.  No lane writes outside its own line: no zeroing, no atomics.
 __device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, int off) {
   int pa[4];   // the '.' of each value
-  pa[0] = off + 4 - T.q[0] + (int)(T.neg & 1u);
+  pa[0] = off + 4 - T.q[0] + T.ng[0];
 #pragma unroll
-  for (int k = 1; k < 4; ++k) pa[k] = pa[k - 1] + 12 - T.q[k] + (int)((T.neg >> k) & 1u);
+  for (int k = 1; k < 4; ++k) pa[k] = pa[k - 1] + 12 - T.q[k] + T.ng[k];
 #pragma unroll
   for (int k = 3; k >= 1; --k) {
     uint8_t* const q = base + pa[k];
@@ -738,8 +738,7 @@ __device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, i
     q[T.q[k] - 5] = '-';
   }
   const uint32_t S = T.D[0] >> (8 * T.q[0]);   // the integer digits in the low bytes
-  const bool neg = T.neg & 1u;
-  const uint32_t lo = neg ? ((S << 8) | '-') : S, hi = S >> 24;   // hi: the 5th byte ("-dddd")
+  const uint32_t lo = T.ng[0] ? ((S << 8) | '-') : S, hi = S >> 24;   // hi: the 5th byte ("-dddd")
   put4(base + off, lo);
   put4(base + off + 4, hi);
   put4(base + pa[0], T.A[0]);
