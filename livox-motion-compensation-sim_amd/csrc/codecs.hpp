@@ -694,8 +694,9 @@ __device__ __forceinline__ void put4(uint8_t* p, uint32_t v) {
 // comes out of the digits themselves, so it is N >= 10^7 / 10^8 / 10^9 exactly (no compares).
 struct PcdText {
   uint32_t D[4], A[4], B[4];
-  int q[4];
+  int q0;      // q of value 0
   int ng[4];   // 1: value k is negative
+  int d[4];    // ng - q: value k's text is 12 + d[k] bytes with its separator
   int len;
 };
 __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
@@ -709,10 +710,12 @@ __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
   for (int k = 0; k < 4; ++k) {
     uint32_t D;
     value_fields(g01[k], g23[k], tu4[k], k == 3 ? '\n' : ' ', D, T.A[k], T.B[k]);
-    T.q[k] = (int)(__builtin_ctz(D | 0x01000000u) >> 3);   // the units byte always counts
+    const int q = (int)(__builtin_ctz(D | 0x01000000u) >> 3);   // the units byte always counts
+    if (k == 0) T.q0 = q;
     T.D[k] = D + 0x30303030u;
     T.ng[k] = (int)((P.neg >> k) & 1u);
-    len += T.ng[k] - T.q[k];
+    T.d[k] = T.ng[k] - q;
+    len += T.d[k];
   }
   T.len = len;
 }
@@ -726,18 +729,20 @@ __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
 // own fraction — and then its fraction.  No lane writes outside its own line: no zeroing, no atomics.
 __device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, int off) {
   int pa[4];   // the '.' of each value
-  pa[0] = off + 4 - T.q[0] + T.ng[0];
+  pa[0] = off + 4 + T.d[0];
 #pragma unroll
-  for (int k = 1; k < 4; ++k) pa[k] = pa[k - 1] + 12 - T.q[k] + T.ng[k];
+  for (int k = 1; k < 4; ++k) pa[k] = pa[k - 1] + 12 + T.d[k];
 #pragma unroll
   for (int k = 3; k >= 1; --k) {
     uint8_t* const q = base + pa[k];
     put4(q - 4, T.D[k]);
     put4(q, T.A[k]);
     put4(q + 4, T.B[k]);
-    q[T.q[k] - 5] = '-';
+    // value k starts at pa[k - 1] + 8: its '-', or (positive) the previous value's separator slot,
+    // which that value rewrites afterwards
+    base[pa[k - 1] + 7 + T.ng[k]] = '-';
   }
-  const uint32_t S = T.D[0] >> (8 * T.q[0]);   // the integer digits in the low bytes
+  const uint32_t S = T.D[0] >> (8 * T.q0);   // the integer digits in the low bytes
   const uint32_t lo = T.ng[0] ? ((S << 8) | '-') : S, hi = S >> 24;   // hi: the 5th byte ("-dddd")
   put4(base + off, lo);
   put4(base + off + 4, hi);
