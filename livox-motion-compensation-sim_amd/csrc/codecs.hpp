@@ -724,9 +724,10 @@ __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
 // offsets (the compiler merges them into unaligned ds_write_b64 / b96).  Values 3, 2, 1 are written
 // in that order, each storing its 4-digit field and a '-' unconditionally (at most 5 bytes before its
 // '.'): bytes left of its own head fall inside the previous value of the same line, which is written
-// afterwards and overwrites them.  Value 0 writes its integer text ('-' if negative, then its nd
-// digits) as one 8-byte store at the line start — the bytes past the integer text fall inside its
-// own fraction — and then its fraction.  No lane writes outside its own line: no zeroing, no atomics.
+// afterwards and overwrites them.  Value 0 stores exactly its own bytes, so no lane ever writes
+// another line's text: no zeroing, no atomics.  (Value 0's integer text as one unaligned 8-byte
+// store at the line start, spilling into its own fraction: 3 fewer VALU instructions per line but
+// +11 % LDS-active cycles, measure + write 817.8 vs 775.2 us, profiles/round4/s24 — not taken.)
 __device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, int off) {
   int pa[4];   // the '.' of each value
   pa[0] = off + 4 + T.d[0];
@@ -742,12 +743,15 @@ __device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, i
     // which that value rewrites afterwards
     base[pa[k - 1] + 7 + T.ng[k]] = '-';
   }
-  const uint32_t S = T.D[0] >> (8 * T.q0);   // the integer digits in the low bytes
-  const uint32_t lo = T.ng[0] ? ((S << 8) | '-') : S, hi = S >> 24;   // hi: the 5th byte ("-dddd")
-  put4(base + off, lo);
-  put4(base + off + 4, hi);
-  put4(base + pa[0], T.A[0]);
-  put4(base + pa[0] + 4, T.B[0]);
+  uint8_t* const q = base + pa[0];
+  put4(q, T.A[0]);
+  put4(q + 4, T.B[0]);
+  const uint32_t D = T.D[0];
+  q[-1] = (uint8_t)(D >> 24);
+  if (T.q0 <= 2) q[-2] = (uint8_t)(D >> 16);
+  if (T.q0 <= 1) q[-3] = (uint8_t)(D >> 8);
+  if (T.q0 == 0) q[-4] = (uint8_t)D;
+  if (T.ng[0]) base[off] = '-';
 }
 
 // The packed line's length without its digits: "%.6f" of |v| < 4294 has 1 + [v < 0] + nd + 7
