@@ -216,7 +216,8 @@ int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose
  * size.  Runs the kernel `launches` times per order and round (in -> out, out != in; the results do
  * not depend on the order), alternating the orders over `rounds`.  us_out[2] (may be NULL) receives
  * the median microseconds per launch of {dealt, XCD-contiguous}; *chosen (may be NULL) the order
- * kept (0 / 1; -1 for an empty batch).  Synchronous. */
+ * kept (0 / 1; -1 for an empty batch): the mode's default order unless the other one is at least
+ * 1 % faster.  Synchronous. */
 int mc_tune_order(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t launches,
                   int32_t rounds, double* us_out, int32_t* chosen);
 /* n_steps consecutive mc_deskew calls (same arguments), LMC:802-832 n times over one batch.
