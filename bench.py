@@ -55,7 +55,6 @@ KERNEL_OF = {"pipeline": {"pose_slerp": "k_deskew_points<1, true, false>", "imu"
                           "frame": "k_deskew_frame_next"},
              "calls": {"pose_slerp": "k_deskew_points<1, false, false>", "imu": "k_deskew_points<2, false, false>",
                        "frame": "k_deskew_frame"}}
-KERNEL_OF["graph"] = KERNEL_OF["calls"]
 REL_TOL = 1e-5                                                 # north_star, relative per coordinate
 
 SCENARIOS = {   # LMC:1182-1204
@@ -356,7 +355,7 @@ def spin_up(ctx, mode, b_in, b_out, ms, issue):
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < ms:
         if issue == "pipeline":
-            ctx.deskew_steps(b_in, b_out, 25, mode=mode, sample_every=0, pipeline=True)
+            ctx.deskew_steps(b_in, b_out, 25, mode=mode, sample_every=0)
         else:
             for _ in range(25):
                 ctx.deskew(b_in, b_out, mode=mode)
@@ -369,26 +368,22 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipel
     kernels themselves (hipExtLaunchKernel start/stop events: the dispatch's own timestamps, no
     marker packets between the steps) give the roofline's per-launch kernel time.  Otherwise a
     second, untimed pass carries events on every launch.  ``issue``: "pipeline" = one
-    Context.deskew_steps(pipeline=True) call, each step's launch also running the next step's prep
-    (the first step's prep is its own launch, inside the timed region); "graph" = one replay of a
-    HIP graph of the steps; "calls" = ``steps`` Context.deskew calls (prep + kernel each)."""
+    Context.deskew_steps call, each step's launch also running the next step's prep (the first
+    step's prep is its own launch, inside the timed region); "calls" = ``steps`` Context.deskew
+    calls (prep + kernel each)."""
     every = 10 if steps >= 50 else 5
-    graph = issue == "graph"
     ctx.timing(live)           # warmup steps fill the context's event pool for the sampled steps
     for _ in range(warmup):
         ctx.deskew(b_in, b_out, mode=mode)
     if issue == "pipeline" and warmup:
-        ctx.deskew_steps(b_in, b_out, warmup, mode=mode, sample_every=1 if live else 0, pipeline=True)
-    if graph:                  # capture + instantiate only (host work, untimed)
-        ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0, prepare=True)
+        ctx.deskew_steps(b_in, b_out, warmup, mode=mode, sample_every=1 if live else 0)
     ctx.sync()
     ctx.timing(False)
     ctx.read_timing()          # drop the warmup events (back to the pool)
     rdv.barrier()
     t0 = time.perf_counter()
-    if graph or issue == "pipeline":
-        ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0,
-                         pipeline=issue == "pipeline")
+    if issue == "pipeline":
+        ctx.deskew_steps(b_in, b_out, steps, mode=mode, sample_every=every if live else 0)
     else:
         for i in range(steps):
             sample = live and i % every == every // 2
@@ -402,7 +397,7 @@ def run_mode(ctx, rdv, mode, b_in, b_out, steps, warmup, live=True, issue="pipel
     rdv.barrier()
     if not live:
         if issue == "pipeline":
-            ctx.deskew_steps(b_in, b_out, min(steps, 50), mode=mode, sample_every=1, pipeline=True)
+            ctx.deskew_steps(b_in, b_out, min(steps, 50), mode=mode, sample_every=1)
         else:
             ctx.timing(True)
             for _ in range(min(steps, 50)):
@@ -810,9 +805,6 @@ def assemble_line(args, cid, label, scen, lo, hi, world, n_devices, n_rank, n_to
                      "bytes_per_point": BYTES_PER_POINT[args.mode], "points_per_launch": n_rank,
                      "kernel_time": ("HIP events around every launch of a second, untimed pass"
                                      if args.events_after else
-                                     f"wall-clock stamp nodes around the kernels of {r['timed_launches']} of the "
-                                     f"{r['steps']} steps of the step graph (every {every}th)"
-                                     if args.issue == "graph" else
                                      (f"the kernels' own workgroup spans (first workgroup start to last "
                                       f"workgroup end, device wall clock) of {r['timed_launches']} of the "
                                       f"{r['steps']} timed steps (every {every}th); HIP events on the same "
@@ -825,8 +817,7 @@ def assemble_line(args, cid, label, scen, lo, hi, world, n_devices, n_rank, n_to
         "step_over_kernel": (r["wall_s"] / r["steps"] * 1e6) / r["main_avg_us"] if r["main_avg_us"] else None,
         "prep_avg_us": r["prep_avg_us"],
         "step_issue": {"calls": "per-call launches; prep as an any-order packet on the kernel's queue",
-                       "graph": f"one HIP-graph replay of {r['steps']} steps (prep + kernel per step)",
-                       "pipeline": f"Context.deskew_steps(pipeline=True): {r['steps'] + 1} launches, step 0's "
+                       "pipeline": f"Context.deskew_steps: {r['steps'] + 1} launches, step 0's "
                                    "k_prep, then each step's deskew kernel with the next step's prep in its "
                                    "first workgroups (every step runs its own prep, one launch ahead)"}[args.issue],
         "modes": {m: {"Mpoints_s": v["value"], "kernel_GBs": v["achieved_GBs"],
@@ -869,11 +860,9 @@ def main():
     ap.add_argument("--events-after", action="store_true",
                     help="per-launch HIP events in a second, untimed pass instead of the timed steps")
     ap.add_argument("--gather-timeout", type=float, default=300.0)
-    ap.add_argument("--issue", choices=["pipeline", "calls", "graph"], default="pipeline",
-                    help="how the timed steps are issued: pipeline = one Context.deskew_steps(pipeline=True), each "
-                         "step's launch also running the next step's prep; calls = one Context.deskew per step "
-                         "(prep + kernel); graph = one HIP-graph replay (kernel time from wall-clock stamp nodes)")
-    ap.add_argument("--graph", action="store_true", help="same as --issue graph")
+    ap.add_argument("--issue", choices=["pipeline", "calls"], default="pipeline",
+                    help="how the timed steps are issued: pipeline = one Context.deskew_steps, each step's launch "
+                         "also running the next step's prep; calls = one Context.deskew per step (prep + kernel)")
     ap.add_argument("--control-plane-only", action="store_true",
                     help="no GPU: the ranks rendezvous, allgather, max and barrier only (CPU test of the launch)")
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
@@ -881,8 +870,6 @@ def main():
     ap.add_argument("--no-single-gpu", action="store_true", help="N > 1: skip rank 0's same-job 1-GPU run")
     ap.add_argument("--no-tune", action="store_true", help="keep each mode's default sub-tile order (no mc_tune_order)")
     args = ap.parse_args()
-    if args.graph:
-        args.issue = "graph"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
     if args.control_plane_only:

@@ -159,6 +159,13 @@ int mc_scan_count(mc_ctx* ctx, int32_t n_frames, const double* frame_times, int 
  * x,y,z + noise, intensity.  noise: (sum(counts), 3) float64 drawn by the caller in frame order
  * (LMC:767 np.random.normal), or NULL for noise-free scans. */
 int mc_scan_emit(mc_ctx* ctx, mc_batch* out, const double* noise);
+/* Pass 2 into the reference's own float64 arrays instead of a float32 batch: d_local receives every
+ * frame's scan_environment output (LMC:770: sensor-frame x, y, z + noise, intensity) and d_aligned
+ * (may be NULL) the frame loop's transform_pointcloud of it with the same pose (LMC:826-831), as
+ * device (N, 4) float64 rows, frames back to back (N = sum of counts_out).  Bit-identical to the
+ * reference's values: the pose's R is scipy's (mc_rotation_from_euler_xyz) and every product sum
+ * accumulates as numpy's matmul does.  Synchronous. */
+int mc_scan_emit_f64(mc_ctx* ctx, const double* noise, double* d_local, double* d_aligned);
 int mc_timing_read_scan(mc_ctx* ctx, double* ms_total, int64_t* launches);
 
 /* ---- output codecs, encoded from a device (N, ld) float64 AoS cloud whose
@@ -220,38 +227,27 @@ int mc_deskew(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose
  * 1 % faster.  Synchronous. */
 int mc_tune_order(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t launches,
                   int32_t rounds, double* us_out, int32_t* chosen);
-/* n_steps consecutive mc_deskew calls (same arguments), LMC:802-832 n times over one batch.
- * Default: one HIP graph: each step's pose prep and deskew kernel run exactly as in mc_deskew
- * (prep one step ahead on a second queue), the graph's edges replacing the per-call cross-queue
- * events.  The graph is captured on first use and replayed while the launch arguments (batches,
- * tables, sizes) are unchanged.
- * MC_STEPS_PIPELINE: no graph; n + 1 launches: step 0's prep, then n deskew launches of which the
- * first n - 1 also run the next step's prep in their first workgroups (every step still runs its
- * own prep, one launch ahead, into the other table half).
- * sample_every > 0 puts timing events around the kernels of every sample_every-th step (read by
- * mc_timing_read).  MC_STEPS_PREPARE: capture / instantiate only, launch nothing.  Asynchronous. */
-#define MC_STEPS_PREPARE 1
-#define MC_STEPS_PIPELINE 2
+/* n_steps consecutive mc_deskew calls (same arguments), LMC:802-832 n times over one batch, as
+ * n + 1 launches: step 0's pose prep, then n deskew launches of which the first n - 1 also run the
+ * next step's prep in their first workgroups (every step runs its own prep, one launch ahead, into
+ * the other table half).  sample_every > 0 puts timing events around the kernels of every
+ * sample_every-th step (read by mc_timing_read).  Asynchronous. */
 int mc_deskew_steps(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t n_steps,
-                    int32_t sample_every, int flags);
+                    int32_t sample_every);
 
 /* One call of transform_pointcloud (LMC:772-776) on host arrays: points (n, ld>=4) float64 rows,
- * rpy / translation (3,) float64 -> out (n, 4) float64 = [R_xyz(rpy) p + t, intensity], computed in
- * float64 by a kernel that reads and writes pinned, device-mapped host memory (no DMA round trips:
- * the latency path for the reference's one-frame-per-call use).  ld < 4 -> MC_ERR_INDEX. */
+ * rpy / translation (3,) float64 -> out (n, 4) float64 = [R p + t, intensity], bit-identical to the
+ * reference's float64 result (R as scipy's from_euler('xyz').as_matrix(), numpy's matmul
+ * accumulation).  Below 32768 rows the kernel reads and writes pinned, device-mapped host memory (no
+ * DMA round trips); a lone ~1.6k-row call still costs ~14 us against numpy's ~9.5 (INTEGRATION.md:
+ * batch the frames).  ld < 4 -> MC_ERR_INDEX. */
 int mc_transform_pointcloud_f64(mc_ctx* ctx, const double* points, int64_t n, int64_t ld, const double* rpy,
                                 const double* translation, double* out);
 
-/* Opt-in latency server for the single calls of mc_transform_pointcloud_f64 up to 32768 rows (the
- * reference's one-frame-per-call use, LMC:831): one workgroup stays resident on its own stream and
- * polls a mailbox in pinned host memory, so a call pays no kernel launch and no completion signal.
- * It returns after 50 ms without a request (relaunched on the next call), after 2 s in all, and on
- * disable / mc_destroy.  info: enabled flag, server launches, requests served, and the mean
- * microseconds per request of {host copy in, post -> done, host copy out (host clock); the server's
- * time from seeing the request to rows + parameters loaded and R formed, and from there to every row
- * stored and acknowledged (device clock)} (phase_us[5], may be NULL). */
-int mc_set_latency_server(mc_ctx* ctx, int enable);
-int mc_latency_server_info(mc_ctx* ctx, int* enabled, int64_t* launches, int64_t* requests, double* phase_us);
+/* Host only (no device): R (n, 3, 3) row-major of Rotation.from_euler('xyz', rpy[i]).as_matrix() for
+ * each rpy (n, 3) — scipy 1.15's arithmetic repeated operation for operation, equal bit for bit.  The
+ * per-frame rotation basis of every float64 path (LMC:726, 774). */
+int mc_rotation_from_euler_xyz(int64_t n, const double* rpy, double* R);
 
 /* The per-point modes on the reference's own float64 data (no float32 staging): MotionCompensator.
  * compensate_point_cloud / apply_motion_compensation (CSIM:1435-1480, 2086-2105) for MC_MODE_IMU,
@@ -279,6 +275,12 @@ int mc_align_frames_host_f64(mc_ctx* ctx, int32_t n_frames, const double* const*
  * Synchronous; timed with the deskew kernels (mc_timing_read main). */
 int mc_transform_affine(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int32_t n_mats, const double* mats,
                         int w_column);
+/* The same on the caller's float64 rows, bit-identical to the reference (numpy's accumulation of
+ * (T @ points_h.T).T, CSIM:230): rows (N, ld) with ld 3 (w = 1, CSIM:223-225) or 4 (the 4th column is
+ * w, CSIM:227), frames back to back (counts[f] rows); mats = 3x4 [A | b] row-major, 1 or n_frames of
+ * them; out (N, 3) float64 (CSIM:233).  Synchronous. */
+int mc_affine_rows_f64(mc_ctx* ctx, int32_t n_frames, const int64_t* counts, const double* rows, int64_t ld,
+                       int32_t n_mats, const double* mats, double* out);
 
 /* HIP-event timing of the hot kernels (main deskew kernel and the pose-prep kernel) */
 int mc_timing_enable(mc_ctx* ctx, int enable);

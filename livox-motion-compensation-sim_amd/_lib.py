@@ -27,8 +27,6 @@ MC_MODE_IMU = 2
 MC_POSE_SEARCHSORTED = 0
 MC_POSE_DIRECT = 1
 MC_BATCH_WITH_TIME = 1
-STEPS_PREPARE = 1    # MC_STEPS_PREPARE
-STEPS_PIPELINE = 2   # MC_STEPS_PIPELINE
 
 MODES = {"frame": MC_MODE_FRAME, "pose_slerp": MC_MODE_POSE_SLERP, "imu": MC_MODE_IMU}
 POSE_SELECT = {"searchsorted": MC_POSE_SEARCHSORTED, "direct": MC_POSE_DIRECT}
@@ -82,6 +80,7 @@ _SIGS = {
     "mc_set_environment": (c_int, [c_void_p, c_int64, _pd, c_int64]),
     "mc_scan_count": (c_int, [c_void_p, c_int32, _pd, c_int, _pd, c_int64, _pi64]),
     "mc_scan_emit": (c_int, [c_void_p, c_void_p, _pd]),
+    "mc_scan_emit_f64": (c_int, [c_void_p, _pd, c_void_p, c_void_p]),
     "mc_timing_read_scan": (c_int, [c_void_p, _pd, _pi64]),
     "mc_lvx_layout": (c_int, [c_int32, _pi64, _pi64]),
     "mc_lvx_encode": (c_int, [c_void_p, c_void_p, c_int64, c_int32, _pi64, POINTER(c_uint64), POINTER(c_uint64),
@@ -94,12 +93,12 @@ _SIGS = {
     "mc_batch_synth": (c_int, [c_void_p, c_uint64, c_int64]),
     "mc_batch_checksum": (c_int, [c_void_p, _pd]),
     "mc_deskew": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
-    "mc_deskew_steps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int32, c_int32, c_int]),
+    "mc_deskew_steps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int32, c_int32]),
     "mc_tune_order": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int32, c_int32, _pd, _pi32]),
     "mc_transform_affine": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, _pd, c_int]),
     "mc_transform_pointcloud_f64": (c_int, [c_void_p, _pd, c_int64, c_int64, _pd, _pd, _pd]),
-    "mc_set_latency_server": (c_int, [c_void_p, c_int]),
-    "mc_latency_server_info": (c_int, [c_void_p, POINTER(c_int), _pi64, _pi64, _pd]),
+    "mc_rotation_from_euler_xyz": (c_int, [c_int64, _pd, _pd]),
+    "mc_affine_rows_f64": (c_int, [c_void_p, c_int32, _pi64, _pd, c_int64, c_int32, _pd, _pd]),
     "mc_deskew_points_f64": (c_int, [c_void_p, c_int, c_int32, _pi64, _pd, c_int64, _pi64, _pd, _pi64, _pd]),
     # frames / outs: arrays of row pointers (passed as the address of a uintp array)
     "mc_align_frames_host_f64": (c_int, [c_void_p, c_int32, c_void_p, _pi64, _pi64, _pd, c_int, c_void_p]),

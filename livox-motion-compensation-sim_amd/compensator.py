@@ -81,10 +81,10 @@ class MotionCompensator:
             return points
         if not points:
             return []
-        ts, g = self._imu_arrays(imu_data)
+        self._imu_arrays(imu_data)          # built and uploaded once per call
         xyz = np.array([(p.x, p.y, p.z) for p in points], dtype=np.float64).reshape(-1, 3)
         t = np.fromiter((p.timestamp for p in points), dtype=np.int64, count=len(points))
-        out = self.compensate_arrays(xyz, t, frame_start_time, ts, g)
+        out = self._compensate_uploaded(xyz, t, frame_start_time)
         cls = type(points[0])
         return [cls(x=float(o[0]), y=float(o[1]), z=float(o[2]), intensity=p.intensity,
                     timestamp=p.timestamp, ring=p.ring, tag=p.tag) for o, p in zip(out, points)]
@@ -107,6 +107,11 @@ class MotionCompensator:
             return np.zeros((0, 3))
         imu_ts = np.ascontiguousarray(imu_ts, dtype=np.int64)
         self._upload_imu(imu_ts, np.ascontiguousarray(gyro, dtype=np.float64).reshape(-1, 3))
+        return self._compensate_uploaded(xyz, timestamp_ns, frame_start_ns, intensity)
+
+    def _compensate_uploaded(self, xyz, timestamp_ns, frame_start_ns: int, intensity=None) -> np.ndarray:
+        """The device call with the IMU table already on the context (one frame)."""
+        n = xyz.shape[0]
         t_rel = np.asarray(timestamp_ns, dtype=np.int64).reshape(-1) - int(frame_start_ns)
         if t_rel.shape != (n,):
             raise ValueError(f"one timestamp per point expected ({n}), got {t_rel.shape}")

@@ -2,9 +2,10 @@
 ``LiDARMotionSimulator._transform_coordinates`` (CSIM:2107-2180) — SURVEY §8f row 4.
 
 The 4x4 matrices are built on the host exactly as the reference does (Rz Ry Rx, ``np.linalg.inv``
-for the reverse direction); the per-point work ``T @ [p, 1]`` runs in the frame kernel of
-libmcdeskew.so (``mc_transform_affine``: the 3x4 [A | b] as a per-frame SGPR table), all frames of a
-run in one launch.  Homogeneous (N,4) input uses its 4th column as w, like CSIM:226-229.
+for the reverse direction); the per-point work ``T @ [p, 1]`` runs on the caller's float64 rows in
+libmcdeskew.so (``mc_affine_rows_f64``: numpy's accumulation order, so the outputs equal the
+reference's bit for bit), all frames of a run in one launch.  Homogeneous (N,4) input uses its 4th
+column as w, like CSIM:226-229.
 """
 from __future__ import annotations
 
@@ -109,7 +110,9 @@ class CoordinateTransformer:
 
 def transform_arrays(frames: Sequence[np.ndarray], T, context: Context | None = None) -> List[np.ndarray]:
     """T @ [p, 1] (or T @ p for (N,4) homogeneous rows) for every cloud; one matrix for all, or one
-    per cloud ((F,4,4) / (F,3,4)).  Returns (N_i, 3) float64 arrays."""
+    per cloud ((F,4,4) / (F,3,4)).  Returns (N_i, 3) float64 arrays, computed in float64 on the
+    device with numpy's accumulation order: equal to the reference's values bit for bit
+    (mc_affine_rows_f64)."""
     arrs = [np.asarray(f) for f in frames]
     if any(a.ndim != 2 for a in arrs):
         raise IndexError("tuple index out of range")     # points.shape[1] on a 1-D array (CSIM:223)
@@ -121,19 +124,9 @@ def transform_arrays(frames: Sequence[np.ndarray], T, context: Context | None = 
     counts = np.array([len(a) for a in arrs], np.int64)
     if not arrs or counts.sum() == 0:
         return [np.zeros((len(a), 3)) for a in arrs]
-    homog = widths == {4}
     ctx = context or default_context()
-    b = ctx.batch(counts)
-    try:
-        xyz = np.concatenate([a[:, :3] for a in arrs]).astype(np.float32)
-        w = np.concatenate([a[:, 3] for a in arrs]).astype(np.float32) if homog else None
-        b.upload_columns(np.ascontiguousarray(xyz[:, 0]), np.ascontiguousarray(xyz[:, 1]),
-                         np.ascontiguousarray(xyz[:, 2]), w)
-        ctx.transform_affine(b, b, T, w_column=homog)
-        x, y, z, _ = b.download_columns()
-    finally:
-        b.close()
-    out = np.column_stack([x, y, z]).astype(np.float64)
+    rows = arrs[0] if len(arrs) == 1 else np.concatenate(arrs)
+    out = ctx.affine_rows(counts, rows, T)
     return [out[o:o + n] for o, n in zip(np.concatenate([[0], np.cumsum(counts)[:-1]]), counts)]
 
 

@@ -72,27 +72,6 @@ class HostPool {
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
-// n deskew steps captured as one HIP graph (mc_deskew_steps), cached by its launch arguments
-struct StepGraph {
-  std::vector<char> key;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  // sampled steps: wall-clock stamps {prep start, prep end, kernel start, kernel end} per sample,
-  // written by one-lane stamp kernels inside the graph (captured event records are not timable)
-  int32_t samples = 0;
-  unsigned long long* d_stamps = nullptr;
-  int64_t pending = 0;   // sampled replays not yet read by mc_timing_read
-};
-inline void step_graph_destroy(StepGraph* g) {
-  if (!g) return;
-  if (g->exec) (void)hipGraphExecDestroy(g->exec);
-  if (g->graph) (void)hipGraphDestroy(g->graph);
-  if (g->d_stamps) (void)hipFree(g->d_stamps);
-  if (g->fork) (void)hipEventDestroy(g->fork);
-  if (g->join) (void)hipEventDestroy(g->join);
-  delete g;
-}
 }  // namespace mcimpl
 
 struct mc_ctx {
@@ -132,8 +111,10 @@ struct mc_ctx {
   hipEvent_t ev_main_done[2] = {nullptr, nullptr};
   hipEvent_t ev_prep_done[2] = {nullptr, nullptr};
   hipEvent_t ev_order = nullptr;  // orders side-stream prep after async main-stream staging
-  // trajectory (LMC:361-428): time, position_gps, orientation_imu
+  // trajectory (LMC:361-428): time, position_gps, orientation_imu; host copies for the float64
+  // paths' per-frame poses (rot.cpp frame_poses)
   int64_t T = 0, T_cap = 0;
+  std::vector<double> h_time, h_pos, h_rpy;
   double* d_time = nullptr;
   double* d_pos = nullptr;
   double* d_rpy = nullptr;
@@ -147,7 +128,6 @@ struct mc_ctx {
   int64_t E = 0;
   double* d_env = nullptr;   // the scene as columns (scan.hpp scene_cols)
   int32_t scan_F = 0, scan_tiles = 0;
-  double* d_scan_ftime = nullptr;
   double* d_scan_pose = nullptr;
   int32_t* d_scan_tcount = nullptr;
   int64_t* d_scan_toff = nullptr;
@@ -172,17 +152,6 @@ struct mc_ctx {
   size_t seg64_bytes = 0;
   int seg64_mode = -1;
   uint64_t seg64_ver = 0;
-  // latency server (mc_set_latency_server): k_lat_server resident on lat_stream, mailbox + rows in
-  // pinned, device-mapped host memory h_lat = [LatMailbox (256 B) | in (kLatRows, 4) | out (kLatRows, 4)]
-  hipStream_t lat_stream = nullptr;
-  void* h_lat = nullptr;
-  bool lat_on = false;
-  bool lat_launched = false;
-  uint32_t lat_seq = 0;
-  uint64_t lat_launches = 0;
-  double lat_ns[5] = {0, 0, 0, 0, 0};   // summed over requests: copy in, post -> done, copy out (host clock);
-                                        // server load (rows + parameters + R), server store (device clock)
-                                    // (server detection -> flag, from its wall clock)
   // pinned, device-mapped host buffer of the single-call drop-in path
   void* h_pin = nullptr;
   size_t pin_bytes = 0;
@@ -203,7 +172,6 @@ struct mc_ctx {
   int32_t span_used = 0;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> main_ev, prep_ev, layout_ev;
-  mcimpl::StepGraph* step_graph = nullptr;
 };
 
 struct mc_batch {

@@ -160,6 +160,10 @@ struct DeskewArgs {
 #ifndef MC_XCD_STAGE
 #define MC_XCD_STAGE 1       // the LDS stager pair's tile order
 #endif
+#ifndef MC_FRAME_GROUPS
+#define MC_FRAME_GROUPS 0    // frame kernel: 0 = quad decomposition, 1 = one float4 group per lane (the
+                             // per-point kernels' sub-tile structure, deskew_frame_groups)
+#endif
 // 16-byte non-temporal store (output is written once and never re-read by this kernel)
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -512,26 +516,18 @@ __device__ __forceinline__ void wave_count2(const T* a, int64_t n, T x0, T x1, i
   }
 }
 
-// Timestamp node of a graph-captured step (mc_deskew_steps): the constant-rate wall clock
-// (s_memrealtime, hipDeviceAttributeWallClockRate) when the stream reaches it.
-__global__ __launch_bounds__(64) void k_stamp(unsigned long long* dst) {
-  if (threadIdx.x == 0) *dst = (unsigned long long)wall_clock64();
-}
-
-// A timed launch's workgroup span (DeskewArgs::span): the first workgroup stamps its start, the last
-// kSpanTail workgroups their ends (after their own barrier, so every wave is done).  Workgroups are
-// dispatched in order and take similar times, so the launch ends with one of its last ones; the span
-// is the kernel's own execution time, without the dispatch gap a start event before the launch
-// includes (~5 us, profiles/round4/s12/roofline_trace.json).
+// A timed launch's workgroup span (DeskewArgs::span): the first workgroup stamps its start and every
+// wave its end, folded by atomicMax into one of kSpanTail slots (no wave is missed however the
+// workgroups are ordered over the XCDs); the span is the kernel's own execution time, without the
+// dispatch gap a start event before the launch includes (~5 us, profiles/round4/s12/roofline_trace.json).
 constexpr int kSpanTail = 2048;
 __device__ __forceinline__ void span_start(unsigned long long* span) {
   if (span && blockIdx.x == 0 && threadIdx.x == 0) span[0] = (unsigned long long)wall_clock64();
 }
 __device__ __forceinline__ void span_end(unsigned long long* span) {
-  if (span && blockIdx.x + kSpanTail >= gridDim.x) {
-    __syncthreads();
-    const int k = (int)(blockIdx.x + kSpanTail - gridDim.x);
-    if (threadIdx.x == 0) span[1 + k] = (unsigned long long)wall_clock64();
+  if (span && (threadIdx.x & 63) == 0) {
+    const unsigned slot = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kSpanTail - 1);
+    atomicMax(span + 1 + slot, (unsigned long long)wall_clock64());
   }
 }
 
@@ -991,225 +987,146 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
 }
 
 
+// Frame kernel in the per-point kernels' structure (MC_FRAME_GROUPS=1): one workgroup per 1024-point
+// sub-tile of one frame, every lane one float4 group of all four columns (4 loads, 4 stores), the
+// frame's [R | t] rows in SGPRs (scalar loads of a workgroup-uniform record), the sub-tile order and
+// sc1 stores of the SLERP kernel.  The same float64 arithmetic and rounding as the quad kernel, so the
+// output is byte-identical.
+template <bool PCD = false>
+__device__ __forceinline__ void deskew_frame_groups(const DeskewArgs& a, const uint32_t pre) {
+  const int64_t n_sub = (int64_t)a.n_tiles * kSub;
+  const uint32_t nb = gridDim.x - pre;
+  const int tid = threadIdx.x;
+  for (int64_t it = blockIdx.x - pre; it < n_sub; it += nb) {
+    const int64_t st = nb < n_sub ? it : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
+    const Tile tl = ldu(a.tiles + st / kSub);
+    const int g0 = (int)(st % kSub) * kBlock;
+    if (g0 >= tl.ngroups) continue;   // uniform: empty sub-tile of a short tile
+    const int g = g0 + tid;
+    const bool act = g < tl.ngroups;
+    const int64_t p = tl.pstart + 4 * (int64_t)(act ? g : g0);
+    const float* q = a.in + bidx((int)a.in_C, 0, p);
+    const float4 X = ld4(q), Y = ld4(q + kBlkPts), Z = ld4(q + 2 * kBlkPts), I = ld4(q + 3 * kBlkPts);
+    const FrameRow r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
+    const FrameRow r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
+    const FrameRow r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
+    float4 ox, oy, oz;
+#define MC_XF(c)                     \
+  ox.c = xf_row(r0, X.c, Y.c, Z.c);  \
+  oy.c = xf_row(r1, X.c, Y.c, Z.c);  \
+  oz.c = xf_row(r2, X.c, Y.c, Z.c);
+    MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
+#undef MC_XF
+    if (act) {
+      float* o = a.out + bidx((int)a.out_C, 0, p);
+      st_out(o, ox);
+      st_out(o + kBlkPts, oy);
+      st_out(o + 2 * kBlkPts, oz);
+      st_out(o + 3 * kBlkPts, I);
+    }
+    if constexpr (PCD) {
+      const int64_t i0 = p - ldu(a.fpoff + tl.frame), n = ldu(a.fcount + tl.frame);
+      PcdCount pc;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const auto v = PcdCount::lanes(act && i0 + c < n);
+        pc.add(v, f4g(ox, c));
+        pc.add(v, f4g(oy, c));
+        pc.add(v, f4g(oz, c));
+        pc.add(v, f4g(I, c));
+      }
+      const int bytes = pc.bytes();
+      const int wg = g0 + (tid & ~63);   // the wave's first group: one 256-point block of the output
+      if ((tid & 63) == 0 && wg < tl.ngroups) a.pcd_len[(tl.pstart + 4 * (int64_t)wg) >> 8] = bytes;
+    }
+  }
+}
+
+// workgroup units per sub-tile of the frame kernel (the launch grid, mcdeskew.hip deskew_plan)
+constexpr int kFrameUnitsPerSub = MC_FRAME_GROUPS ? 1 : kQuadUnitsPerSub;
+template <bool PCD = false>
+__device__ __forceinline__ void deskew_frame_any(const DeskewArgs& a, const uint32_t pre) {
+  if constexpr (MC_FRAME_GROUPS) deskew_frame_groups<PCD>(a, pre);
+  else deskew_frame_quad<PCD>(a, pre);
+}
+
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
   span_start(a.span);
-  deskew_frame_quad(a, 0u);
+  deskew_frame_any(a, 0u);
   span_end(a.span);
 }
 
 // Path A with the ASCII PCD text bytes of every output block (mc_deskew_pcd)
-__global__ __launch_bounds__(kBlock) void k_deskew_frame_pcd(const DeskewArgs a) { deskew_frame_quad<true>(a, 0u); }
+__global__ __launch_bounds__(kBlock) void k_deskew_frame_pcd(const DeskewArgs a) { deskew_frame_any<true>(a, 0u); }
 
-// Many frames on host-resident rows (LMC:802-832 on host arrays): frame f's rows [doff[f],
-// doff[f+1]) of the pinned input get pose[12 f ..] = R (row-major) | t (float64, from k_scan_pose).
-// Rows [r0, r0 + n) of the concatenated frames (a pipeline chunk); in / out hold (n, 4) rows.
-__global__ __launch_bounds__(kBlock) void k_align_rows_f64(const double* __restrict__ in, int64_t n, int64_t r0,
-                                                           const int64_t* __restrict__ doff, int32_t F,
+// ---- float64 rows: the reference's own arrays, bit for bit ---------------------------------------
+// R p + t (LMC:775: (R @ p.T).T + t) the way numpy's matmul accumulates it: per output an ascending
+// FMA chain over k, fma(R[i][2], z, fma(R[i][1], y, R[i][0] * x)), then + t[i] rounded on its own
+// (numpy's dgemm, measured on the reference's box: tools/fma_order.py).  P = {R row-major | t}; with
+// the host's scipy-faithful R (rot.cpp) the result equals the reference's float64 value exactly.
+__device__ __forceinline__ void frame_apply(const double* __restrict__ P, double x, double y, double z, double& ox,
+                                            double& oy, double& oz) {
+#pragma clang fp contract(off)
+  ox = __builtin_fma(P[2], z, __builtin_fma(P[1], y, P[0] * x)) + P[9];
+  oy = __builtin_fma(P[5], z, __builtin_fma(P[4], y, P[3] * x)) + P[10];
+  oz = __builtin_fma(P[8], z, __builtin_fma(P[7], y, P[6] * x)) + P[11];
+}
+
+// the frame of row `row`: last f with doff[f] <= row
+__device__ __forceinline__ int32_t row_frame(const int64_t* __restrict__ doff, int32_t F, int64_t row) {
+  int32_t lo = 0, hi = F;
+  while (hi - lo > 1) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (doff[mid] <= row) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// Many frames of (n, 4) float64 rows (LMC:802-832 on host arrays, the row pipeline's chunks and the
+// zero-copy path): frame f's rows [doff[f], doff[f+1]) get pose[12 f ..] (host frame_poses).  Rows
+// [r0, r0 + n) of the concatenated frames; in / out hold (n, ld_in) / (n, 4) rows.
+__global__ __launch_bounds__(kBlock) void k_align_rows_f64(const double* __restrict__ in, int64_t ld, int64_t n,
+                                                           int64_t r0, const int64_t* __restrict__ doff, int32_t F,
                                                            const double* __restrict__ pose, double* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const int64_t row = r0 + i;
-    int32_t lo = 0, hi = F;                      // last f with doff[f] <= row
-    while (hi - lo > 1) {
-      const int32_t mid = (lo + hi) >> 1;
-      if (doff[mid] <= row) lo = mid; else hi = mid;
-    }
-    const double* P = pose + 12 * (int64_t)lo;
-    const double2 p01 = *reinterpret_cast<const double2*>(in + 4 * i);
-    const double2 p23 = *reinterpret_cast<const double2*>(in + 4 * i + 2);
-    const double x = p01.x, y = p01.y, z = p23.x, w = p23.y;
-    double* o = out + 4 * i;
-    *reinterpret_cast<double2*>(o) = double2{P[0] * x + P[1] * y + P[2] * z + P[9], P[3] * x + P[4] * y + P[5] * z + P[10]};
-    *reinterpret_cast<double2*>(o + 2) = double2{P[6] * x + P[7] * y + P[8] * z + P[11], w};
-  }
-}
-
-// the 12-double pose (R row-major | t) of explicit Euler angles and translation
-__global__ void k_pose_from_rpy(double roll, double pitch, double yaw, double tx, double ty, double tz,
-                                double* __restrict__ pose) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    euler_xyz_matrix(roll, pitch, yaw, pose);
-    pose[9] = tx; pose[10] = ty; pose[11] = tz;
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_align_host_f64(const double* __restrict__ in, int64_t n, int64_t ld,
-                                                           const int64_t* __restrict__ doff, int32_t F,
-                                                           const double* __restrict__ pose, double* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    int32_t lo = 0, hi = F;                      // last f with doff[f] <= i
-    while (hi - lo > 1) {
-      const int32_t mid = (lo + hi) >> 1;
-      if (doff[mid] <= i) lo = mid; else hi = mid;
-    }
-    const double* P = pose + 12 * (int64_t)lo;
+    const double* P = pose + 12 * (int64_t)row_frame(doff, F, r0 + i);
     const double* q = in + i * ld;
-    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    double x, y, z, w;
+    if (ld == 4) {
+      const double2 p01 = *reinterpret_cast<const double2*>(q);
+      const double2 p23 = *reinterpret_cast<const double2*>(q + 2);
+      x = p01.x; y = p01.y; z = p23.x; w = p23.y;
+    } else {
+      x = q[0]; y = q[1]; z = q[2]; w = q[3];
+    }
+    double ox, oy, oz;
+    frame_apply(P, x, y, z, ox, oy, oz);
     double* o = out + 4 * i;
-    o[0] = P[0] * x + P[1] * y + P[2] * z + P[9];
-    o[1] = P[3] * x + P[4] * y + P[5] * z + P[10];
-    o[2] = P[6] * x + P[7] * y + P[8] * z + P[11];
-    o[3] = w;
+    *reinterpret_cast<double2*>(o) = double2{ox, oy};
+    *reinterpret_cast<double2*>(o + 2) = double2{oz, w};
   }
 }
 
-// Single-call drop-in of transform_pointcloud (LMC:772-776) on host-resident (n, ld) float64 rows:
-// reads and writes pinned, device-mapped host memory directly (no DMA round trips for the small
-// frames the reference transforms one call at a time), float64 math like the reference.
-__global__ __launch_bounds__(kBlock) void k_transform_host_f64(const double* __restrict__ in, int64_t n, int64_t ld,
-                                                               double roll, double pitch, double yaw, double tx,
-                                                               double ty, double tz, double* __restrict__ out) {
-  __shared__ double s_R[9];
-  if (threadIdx.x == 0) euler_xyz_matrix(roll, pitch, yaw, s_R);
-  __syncthreads();
-  const double R0 = s_R[0], R1 = s_R[1], R2 = s_R[2], R3 = s_R[3], R4 = s_R[4], R5 = s_R[5], R6 = s_R[6],
-               R7 = s_R[7], R8 = s_R[8];
+// CoordinateTransformer.transform_points (CSIM:214-233): (T @ [p, w].T).T[:, :3] per row with the
+// 4x4 T's top 3x4 [A | b] of the row's frame (mats + 12 * frame, or one matrix for all); w = the 4th
+// column of (n, 4) homogeneous rows, 1 for (n, 3) rows (CSIM:223-225's column of ones).  numpy's
+// accumulation over k = 0..3: fma(b_i, w, fma(A_i2, z, fma(A_i1, y, A_i0 * x))); out (n, 3).
+__global__ __launch_bounds__(kBlock) void k_affine_rows_f64(const double* __restrict__ in, int64_t ld, int64_t n,
+                                                            const int64_t* __restrict__ doff, int32_t F,
+                                                            const double* __restrict__ mats, int32_t n_mats,
+                                                            double* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double* M = mats + (n_mats == 1 ? 0 : 12 * (int64_t)row_frame(doff, F, i));
     const double* q = in + i * ld;
-    const double x = q[0], y = q[1], z = q[2], w = q[3];
-    double* o = out + 4 * i;
-    o[0] = R0 * x + R1 * y + R2 * z + tx;
-    o[1] = R3 * x + R4 * y + R5 * z + ty;
-    o[2] = R6 * x + R7 * y + R8 * z + tz;
-    o[3] = w;
+    const double x = q[0], y = q[1], z = q[2], w = ld == 4 ? q[3] : 1.0;
+    double* o = out + 3 * i;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      o[r] = __builtin_fma(M[4 * r + 3], w, __builtin_fma(M[4 * r + 2], z, __builtin_fma(M[4 * r + 1], y, M[4 * r] * x)));
   }
 }
 
-// ---- latency server: transform_pointcloud (LMC:772-776) without a launch per call --------------
-// The reference transforms one ~1.6k-point frame per call (LMC:831).  A launched kernel pays the
-// launch and the completion signal (15-17 us beyond the kernel); this opt-in server is
-// ONE workgroup that stays resident on its own stream and polls a mailbox in pinned, device-mapped
-// host memory: the host writes a request (row count, rpy, t; the rows already in the pinned input
-// buffer) and bumps seq_req; the server computes R (LMC:774) on one lane, transforms the rows from
-// the pinned input straight into the pinned output in float64, makes its stores visible system-wide
-// and publishes seq_done; the host spins on seq_done.  Every exit is bounded: the server returns
-// after idle_ticks without a request, after life_ticks in all, or on quit (mc_set_latency_server /
-// mc_destroy); the host relaunches it on the next request (alive == 0).  Only vector memory
-// instructions touch the mailbox (atomic loads / stores at system scope).
-struct LatMailbox {
-  // line 0, written by the host and polled by the server: one poll fetches the request number, the
-  // stop flag and the row count together
-  uint32_t seq_req;    // host: number of the posted request
-  uint32_t quit;       // host: stop now
-  int64_t n_tag;       // host: (seq_req << 32) | rows of the request (<= the buffers' capacity)
-  double rpy[3];
-  double t[3];
-  // line 1, written by the server
-  alignas(64) uint32_t seq_done;   // number of the last finished request
-  uint32_t alive;                  // host 2 at launch, server 1 while polling, 0 on exit
-  uint64_t dev_ticks[4];           // wall clock: request seen / rows + parameters loaded / rows stored / done
-};
-constexpr int kLatThreads = 1024;
-constexpr int kLatRowsPerLane = 4;                       // rows in flight per lane
-constexpr int kLatChunk = kLatThreads * kLatRowsPerLane;
-
-__device__ __forceinline__ void lat_tick(LatMailbox* mb, int k) {
-  __hip_atomic_store(&mb->dev_ticks[k], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__global__ __launch_bounds__(kLatThreads) void k_lat_server(LatMailbox* mb, const double* __restrict__ in,
-                                                            double* __restrict__ out, uint32_t seen,
-                                                            uint64_t idle_ticks, uint64_t life_ticks) {
-  __shared__ int s_go;
-  __shared__ uint32_t s_seq;
-  __shared__ int64_t s_n;
-  __shared__ double s_R[12];
-  const uint64_t t0 = wall_clock64();
-  uint64_t t_last = t0;
-  if (threadIdx.x == 0) __hip_atomic_store(&mb->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  for (;;) {
-    if (threadIdx.x == 0) {
-      int go = 0;
-      uint32_t r = seen;
-      int64_t nt = 0;
-      // relaxed polls (uncached system-scope loads, no cache invalidation per poll), one acquire fence
-      // once a request is seen
-      for (;;) {
-        r = __hip_atomic_load(&mb->seq_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t q = __hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // same trip
-        nt = __hip_atomic_load(&mb->n_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (r != seen) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-          go = 1;
-          break;
-        }
-        if (q) break;
-        const uint64_t now = wall_clock64();
-        if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (go) {
-        lat_tick(mb, 0);
-        // the row count came with the poll; a count tagged with an older request (the poll's loads
-        // are unordered) is read again after the acquire
-        if ((uint32_t)((uint64_t)nt >> 32) != r) nt = __hip_atomic_load(&mb->n_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        s_n = nt & 0xffffffffLL;
-      }
-      s_seq = r;
-      s_go = go;
-    }
-    __syncthreads();
-    if (!s_go) break;
-    const int64_t n = s_n;
-    // the parameters (lane 0) and every lane's first rows are in flight together: one PCIe round trip
-    double v[6];
-    if (threadIdx.x == 0) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        v[k] = __hip_atomic_load(&mb->rpy[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        v[3 + k] = __hip_atomic_load(&mb->t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-    double R0 = 0, R1 = 0, R2 = 0, R3 = 0, R4 = 0, R5 = 0, R6 = 0, R7 = 0, R8 = 0, tx = 0, ty = 0, tz = 0;
-    for (int64_t base = 0; base < n; base += kLatChunk) {
-      double2 a[kLatRowsPerLane], b[kLatRowsPerLane];
-#pragma unroll
-      for (int j = 0; j < kLatRowsPerLane; ++j) {
-        const int64_t i = base + j * kLatThreads + threadIdx.x;
-        if (i < n) {
-          a[j] = *reinterpret_cast<const double2*>(in + 4 * i);
-          b[j] = *reinterpret_cast<const double2*>(in + 4 * i + 2);
-        }
-      }
-      if (base == 0) {   // R (LMC:774) with the prep's short-latency sincos, shared through LDS
-        if (threadIdx.x == 0) {
-          double R[9];
-          euler_xyz_matrix_prep(v[0], v[1], v[2], R);
-#pragma unroll
-          for (int k = 0; k < 9; ++k) s_R[k] = R[k];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) s_R[9 + k] = v[3 + k];
-          lat_tick(mb, 1);
-        }
-        __syncthreads();
-        R0 = s_R[0], R1 = s_R[1], R2 = s_R[2], R3 = s_R[3], R4 = s_R[4], R5 = s_R[5], R6 = s_R[6], R7 = s_R[7];
-        R8 = s_R[8], tx = s_R[9], ty = s_R[10], tz = s_R[11];
-      }
-#pragma unroll
-      for (int j = 0; j < kLatRowsPerLane; ++j) {
-        const int64_t i = base + j * kLatThreads + threadIdx.x;
-        if (i < n) {
-          const double x = a[j].x, y = a[j].y, z = b[j].x;
-          *reinterpret_cast<double2*>(out + 4 * i) = double2{R0 * x + R1 * y + R2 * z + tx, R3 * x + R4 * y + R5 * z + ty};
-          *reinterpret_cast<double2*>(out + 4 * i + 2) = double2{R6 * x + R7 * y + R8 * z + tz, b[j].y};
-        }
-      }
-    }
-    // every lane's row stores acknowledged, then one system-scope release (one L2 write-back for the
-    // workgroup instead of one per wave) before the flag
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      lat_tick(mb, 2);
-      __hip_atomic_store(&mb->seq_done, s_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      seen = s_seq;
-    }
-    t_last = wall_clock64();
-    __syncthreads();          // s_* are rewritten by the next request
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// CoordinateTransformer.transform_points on homogeneous (N,4) input (CSIM:214-233)
+// CSIM coordinate transforms with matrices per frame on the f32 batch columns (mc_transform_affine)
 __global__ __launch_bounds__(kBlock) void k_affine_w(const DeskewArgs a) { deskew_frame_body<true>(a); }
 
 // ---------------------------------------------------------------------------------------------
@@ -1695,7 +1612,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_deskew_frame_next(const DeskewArg
     prep_body<0>(p, blockIdx.x);
     return;
   }
-  deskew_frame_quad(a, pre);
+  deskew_frame_any(a, pre);
   span_end(a.span);
 }
 

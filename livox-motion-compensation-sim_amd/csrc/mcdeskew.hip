@@ -10,6 +10,7 @@
 #include "internal.hpp"
 #include "hostutil.hpp"
 #include "plan.hpp"
+#include "rot.hpp"
 
 #include <algorithm>
 #include <array>
@@ -165,11 +166,10 @@ int mc_create(int device, mc_ctx** out) {
 int mc_destroy(mc_ctx* c) {
   if (!c) return MC_OK;
   DeviceGuard g(c->device);
-  (void)mc_set_latency_server(c, 0);
   (void)sync_all(c);
   dev_free(c->d_time); dev_free(c->d_pos); dev_free(c->d_rpy); dev_free(c->d_pose_seg);
   dev_free(c->d_imu_ts); dev_free(c->d_gyro); dev_free(c->d_imu_seg);
-  dev_free(c->d_env); dev_free(c->d_scan_ftime); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount);
+  dev_free(c->d_env); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount);
   dev_free(c->d_scan_toff); dev_free(c->d_scan_nvis); dev_free(c->d_scan_bits);
   if (c->d_codec) (void)hipFree(c->d_codec);
   if (c->d_span) (void)hipFree(c->d_span);
@@ -185,8 +185,6 @@ int mc_destroy(mc_ctx* c) {
   for (auto& p : c->scan_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->prep_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
   for (auto& p : c->layout_ev) { c->ev_pool.push_back(p.first); c->ev_pool.push_back(p.second); }
-  mcimpl::step_graph_destroy(c->step_graph);
-  c->step_graph = nullptr;
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) { (void)hipEventDestroy(c->ev_main_done[i]); (void)hipEventDestroy(c->ev_prep_done[i]); }
   (void)hipEventDestroy(c->ev_order);
@@ -232,6 +230,9 @@ int mc_set_trajectory(mc_ctx* c, int64_t T, const double* time, const double* po
   HIPCHK(hipMemcpyAsync(c->d_pos, pos, 3 * T * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_rpy, rpy, 3 * T * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  c->h_time.assign(time, time + T);
+  c->h_pos.assign(pos, pos + 3 * T);
+  c->h_rpy.assign(rpy, rpy + 3 * T);
   c->T = T;
   return MC_OK;
 }
@@ -715,7 +716,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
   int32_t units = in->n_tiles * kSub;
-  if (mode == MC_MODE_FRAME) units = in->n_tiles * kSub * kQuadUnitsPerSub;   // the quad decomposition
+  if (mode == MC_MODE_FRAME) units = in->n_tiles * kSub * kFrameUnitsPerSub;
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
   // sub-tile order: default_order, or mc_tune_order's measured choice
@@ -735,7 +736,6 @@ unsigned long long* span_take(mc_ctx* c) {
 }
 
 // Launches with optional hipExtLaunchKernel timing events (e0/e1 null: untimed) and AQL flags.
-// Inside a graph capture (build_step_graph) both events are null and flags 0.
 void launch_prep(const StepPlan& sp, hipStream_t sd, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
                  unsigned flags = 0) {
   if (!e0 && !flags) hipLaunchKernelGGL(k_prep, dim3(sp.prep_blocks), dim3(kBlock), 0, sd, sp.pa);
@@ -744,7 +744,7 @@ void launch_prep(const StepPlan& sp, hipStream_t sd, hipEvent_t e0 = nullptr, hi
 
 void launch_main(const StepPlan& sp, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
   const dim3 grid(sp.grid), block(kBlock);
-  if (sp.da.pcd_len) {   // mc_deskew_pcd (never graph-captured)
+  if (sp.da.pcd_len) {   // mc_deskew_pcd
     if (sp.kernel == MC_MODE_FRAME) hipExtLaunchKernelGGL(k_deskew_frame_pcd, grid, block, 0, s, e0, e1, 0u, sp.da);
     else if (sp.kernel == MC_MODE_POSE_SLERP)
       hipExtLaunchKernelGGL((k_deskew_points<1, false, true>), grid, block, 0, s, e0, e1, 0u, sp.da, sp.pa, 0u);
@@ -863,73 +863,6 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
 }
 
 extern "C" {
-
-// ---- n steps as one HIP graph ---------------------------------------------------------------
-// The step sequence of n mc_deskew calls (prep on the side stream one step ahead, kernel on the
-// main stream) captured once and replayed: the graph's edges replace the per-step cross-queue
-// event protocol (~6.5 us per step, tools/gap_probe.hip patterns 1 vs 4).  Every replay runs all
-// n preps and n kernels.  The graph is cached by its launch arguments (device pointers, sizes,
-// grids), which are all a launch bakes in: table and point contents are read when it runs.
-namespace {
-int build_step_graph(mc_ctx* c, const StepPlan* plan, int32_t n_steps, int32_t every, std::vector<char>&& key) {
-  mcimpl::step_graph_destroy(c->step_graph);
-  c->step_graph = nullptr;
-  auto* g = new mcimpl::StepGraph();
-  g->key = std::move(key);
-  auto bail = [&](hipError_t e, const char* what) {
-    mcimpl::step_graph_destroy(g);
-    return fail(MC_ERR_HIP, "step graph %s: %s", what, hipGetErrorString(e));
-  };
-  hipError_t e = hipEventCreateWithFlags(&g->fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&g->join, hipEventDisableTiming);
-  auto sampled = [&](int32_t i) { return every > 0 && i % every == every / 2; };
-  for (int32_t i = 0; i < n_steps; ++i) g->samples += sampled(i) ? 1 : 0;
-  if (e == hipSuccess && g->samples > 0)
-    e = hipMalloc(&g->d_stamps, 4 * sizeof(unsigned long long) * (size_t)g->samples);
-  if (e != hipSuccess) return bail(e, "events");
-  if (c->wall_khz <= 0.0) {
-    int khz = 0;
-    e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device);
-    if (e != hipSuccess || khz <= 0) return bail(e, "wall clock rate");
-    c->wall_khz = khz;
-  }
-  unsigned long long* st = g->d_stamps;
-  hipStream_t s = c->stream, sd = c->side;
-  e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
-  if (e != hipSuccess) return bail(e, "begin capture");
-  // capture: any error is remembered and the capture still ended, so the stream leaves capture mode
-  auto rec = [&](hipError_t r) { if (e == hipSuccess) e = r; };
-  rec(hipEventRecord(g->fork, s));
-  rec(hipStreamWaitEvent(sd, g->fork, 0));
-  size_t k = 0;
-  for (int32_t i = 0; i < n_steps && e == hipSuccess; ++i) {
-    const int h = i & 1;
-    const StepPlan& sp = plan[h];
-    const bool smp = sampled(i);
-    if (i >= 2) rec(hipStreamWaitEvent(sd, c->ev_main_done[h], 0));
-    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, sd, st + 4 * k + 0);
-    launch_prep(sp, sd);
-    rec(hipGetLastError());
-    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, sd, st + 4 * k + 1);
-    rec(hipEventRecord(c->ev_prep_done[h], sd));
-    rec(hipStreamWaitEvent(s, c->ev_prep_done[h], 0));
-    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, st + 4 * k + 2);
-    launch_main(sp, s);
-    rec(hipGetLastError());
-    if (smp) hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, st + 4 * k++ + 3);
-    rec(hipEventRecord(c->ev_main_done[h], s));
-  }
-  rec(hipEventRecord(g->join, sd));
-  rec(hipStreamWaitEvent(s, g->join, 0));
-  const hipError_t ec = hipStreamEndCapture(s, &g->graph);
-  if (e != hipSuccess) return bail(e, "capture");
-  if (ec != hipSuccess) return bail(ec, "end capture");
-  e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
-  if (e != hipSuccess) return bail(e, "instantiate");
-  c->step_graph = g;
-  return MC_OK;
-}
-}  // namespace
 
 namespace {
 // The launches of n steps over the two table halves of `plan` (step i reads half i & 1 of plan):
@@ -1055,48 +988,18 @@ int mc_tune_order(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int po
 }
 
 int mc_deskew_steps(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t n_steps,
-                    int32_t sample_every, int flags) {
+                    int32_t sample_every) {
   if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
   CHECK_ARG(n_steps >= 1 && n_steps <= (1 << 16), "n_steps %d outside [1, 65536]", n_steps);
   CHECK_ARG(sample_every >= 0, "sample_every %d < 0", sample_every);
-  CHECK_ARG((flags & ~(MC_STEPS_PREPARE | MC_STEPS_PIPELINE)) == 0, "unknown flags 0x%x", flags);
   if (in->F == 0 || in->n_tiles == 0) {
-    // nothing for a graph to carry (no points): the plain calls
-    if (flags & MC_STEPS_PREPARE) return MC_OK;
+    // no deskew launch to carry a prep: the plain calls
     for (int32_t i = 0; i < n_steps; ++i)
       if (int r = mc_deskew(c, in, out, mode, pose_select)) return r;
     return MC_OK;
   }
   DeviceGuard g(c->device);
-  hipStream_t s = c->stream;
-  forget_speculation(c);
-  if (flags & MC_STEPS_PIPELINE) {
-    if (flags & MC_STEPS_PREPARE) return MC_OK;   // nothing to capture
-    return deskew_steps_pipelined(c, in, out, mode, pose_select, n_steps, sample_every);
-  }
-  // queued on the main stream, ahead of the graph (whose prep branch forks from it)
-  if (int r = ensure_trange(const_cast<mc_batch*>(in), mode)) return r;
-  // the graph starts on half 0 whatever c->buf is: everything that last used either half precedes
-  // it on the main stream (a plain call's kernel waits for its own prep)
-  StepPlan plan[2];
-  deskew_plan(c, in, out, mode, pose_select, 0, &plan[0]);
-  deskew_plan(c, in, out, mode, pose_select, 1, &plan[1]);
-  std::vector<char> key(sizeof(plan) + 2 * sizeof(int32_t));
-  std::memcpy(key.data(), plan, sizeof(plan));
-  std::memcpy(key.data() + sizeof(plan), &n_steps, sizeof(int32_t));
-  std::memcpy(key.data() + sizeof(plan) + sizeof(int32_t), &sample_every, sizeof(int32_t));
-  if (!c->step_graph || c->step_graph->key != key) {
-    if (int r = build_step_graph(c, plan, n_steps, sample_every, std::move(key))) return r;
-  }
-  if (flags & MC_STEPS_PREPARE) return MC_OK;
-  HIPCHK(hipGraphLaunch(c->step_graph->exec, s));
-  c->prep_fence = true;   // the graph's last kernel reads a half the next any-order prep may write
-  // later plain calls order their side-stream prep after the whole graph
-  HIPCHK(hipEventRecord(c->ev_main_done[0], s));
-  HIPCHK(hipEventRecord(c->ev_main_done[1], s));
-  c->buf = 0;
-  if (sample_every > 0) c->step_graph->pending += 1;
-  return MC_OK;
+  return deskew_steps_pipelined(c, in, out, mode, pose_select, n_steps, sample_every);
 }
 
 constexpr int64_t kPipeRows = 1 << 20;                                 // 32 MB of (n,4) float64
@@ -1107,184 +1010,6 @@ constexpr int64_t kJobRows = 8192;                                     // rows p
 static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
                         const int64_t* d_doff, const double* d_pose, double* const* outs);
 
-// ---- the latency server (k_lat_server) --------------------------------------------------------
-constexpr int64_t kLatRows = 1 << 15;       // rows one request may carry (the zero-copy range)
-constexpr size_t kLatMailboxBytes = 256;
-constexpr double kLatIdleMs = 50.0;         // the server returns after this long without a request
-constexpr double kLatLifeMs = 2000.0;       // ... and after this long in all (relaunched on demand)
-constexpr double kLatAnswerS = 2.0;         // a request unanswered this long is an error
-
-static LatMailbox* lat_mailbox(mc_ctx* c) { return static_cast<LatMailbox*>(c->h_lat); }
-static double* lat_in(mc_ctx* c) { return reinterpret_cast<double*>(static_cast<char*>(c->h_lat) + kLatMailboxBytes); }
-static double* lat_out(mc_ctx* c) { return lat_in(c) + 4 * kLatRows; }
-
-// (re)launch the server: it takes requests numbered after the last finished one
-static int lat_launch(mc_ctx* c) {
-  DeviceGuard g(c->device);
-  LatMailbox* mb = lat_mailbox(c);
-  if (c->wall_khz <= 0.0) {
-    int khz = 0;
-    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
-    if (khz <= 0) return fail(MC_ERR_HIP, "wall clock rate unavailable");
-    c->wall_khz = khz;
-  }
-  if (c->lat_launched) HIPCHK(hipStreamSynchronize(c->lat_stream));   // the previous instance has returned
-  __atomic_store_n(&mb->alive, 2u, __ATOMIC_RELEASE);
-  const uint32_t seen = __atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE);
-  hipLaunchKernelGGL(k_lat_server, dim3(1), dim3(kLatThreads), 0, c->lat_stream, mb, lat_in(c), lat_out(c), seen,
-                     (uint64_t)(kLatIdleMs * c->wall_khz), (uint64_t)(kLatLifeMs * c->wall_khz));
-  HIPCHK(hipGetLastError());
-  c->lat_launched = true;
-  ++c->lat_launches;
-  return MC_OK;
-}
-
-// stop the server (quit flag; returns once the instance has exited)
-static int lat_stop(mc_ctx* c) {
-  if (!c->lat_on || !c->lat_launched) return MC_OK;
-  LatMailbox* mb = lat_mailbox(c);
-  __atomic_store_n(&mb->quit, 1u, __ATOMIC_RELEASE);
-  const hipError_t e = hipStreamSynchronize(c->lat_stream);
-  __atomic_store_n(&mb->quit, 0u, __ATOMIC_RELEASE);
-  c->lat_launched = false;
-  if (e != hipSuccess) return fail(MC_ERR_HIP, "latency server stop: %s", hipGetErrorString(e));
-  return MC_OK;
-}
-
-int mc_set_latency_server(mc_ctx* c, int enable) {
-  CHECK_ARG(c, "ctx is NULL");
-  DeviceGuard g(c->device);
-  if (enable && !c->lat_on) {
-    HIPCHK(hipStreamCreateWithFlags(&c->lat_stream, hipStreamNonBlocking));
-    const size_t bytes = kLatMailboxBytes + 2 * (size_t)kLatRows * 4 * sizeof(double);
-    const hipError_t e = hipHostMalloc(&c->h_lat, bytes, hipHostMallocMapped | hipHostMallocCoherent);
-    if (e != hipSuccess) {
-      (void)hipStreamDestroy(c->lat_stream);
-      c->lat_stream = nullptr;
-      return fail(MC_ERR_NOMEM, "latency server buffers: %s", hipGetErrorString(e));
-    }
-    std::memset(c->h_lat, 0, kLatMailboxBytes);
-    c->lat_on = true;
-    c->lat_launched = false;
-    c->lat_seq = 0;
-  } else if (!enable && c->lat_on) {
-    const int r = lat_stop(c);
-    (void)hipHostFree(c->h_lat);
-    (void)hipStreamDestroy(c->lat_stream);
-    c->h_lat = nullptr;
-    c->lat_stream = nullptr;
-    c->lat_on = false;
-    if (r) return r;
-  }
-  return MC_OK;
-}
-
-int mc_latency_server_info(mc_ctx* c, int* enabled, int64_t* launches, int64_t* requests, double* phase_us) {
-  CHECK_ARG(c, "ctx is NULL");
-  if (enabled) *enabled = c->lat_on ? 1 : 0;
-  if (launches) *launches = (int64_t)c->lat_launches;
-  if (requests) *requests = (int64_t)c->lat_seq;
-  if (phase_us)
-    for (int k = 0; k < 5; ++k) phase_us[k] = c->lat_seq ? c->lat_ns[k] / 1e3 / (double)c->lat_seq : 0.0;
-  return MC_OK;
-}
-
-// one transform_pointcloud request through the server (n <= kLatRows)
-static int lat_transform(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
-                         const double* translation, double* out) {
-  using clk = std::chrono::steady_clock;
-  const auto h0 = clk::now();
-  LatMailbox* mb = lat_mailbox(c);
-  double* in = lat_in(c);
-  if (ld == 4) std::memcpy(in, points, (size_t)n * 32);
-  else for (int64_t i = 0; i < n; ++i) std::memcpy(in + 4 * i, points + i * ld, 32);
-  const uint32_t seq = (uint32_t)c->lat_seq + 1;
-  mb->n_tag = (int64_t)((uint64_t)seq << 32 | (uint64_t)n);
-  for (int k = 0; k < 3; ++k) { mb->rpy[k] = rpy[k]; mb->t[k] = translation[k]; }
-  // an instance that has returned (idle / lifetime) is relaunched before the request is posted
-  if (!c->lat_launched || __atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) == 0)
-    if (int r = lat_launch(c)) return r;
-  ++c->lat_seq;
-  const auto h1 = clk::now();
-  __atomic_store_n(&mb->seq_req, seq, __ATOMIC_RELEASE);
-  const auto t0 = std::chrono::steady_clock::now();
-  for (uint64_t spins = 0;; ++spins) {
-    if (__atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE) == seq) break;
-    if (__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) == 0) {
-      // it returned before taking this request (a race with its idle exit): relaunch, it takes it
-      if (__atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE) == seq) break;
-      if (int r = lat_launch(c)) return r;
-      continue;
-    }
-    __builtin_ia32_pause();
-    if ((spins & 1023) == 0 &&
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kLatAnswerS) {
-      (void)lat_stop(c);
-      return fail(MC_ERR_HIP, "latency server did not answer request %u within %.1f s", seq, kLatAnswerS);
-    }
-  }
-  const auto h2 = clk::now();
-  std::memcpy(out, lat_out(c), (size_t)n * 32);
-  const auto h3 = clk::now();
-  auto ns = [](clk::duration d) { return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
-  c->lat_ns[0] += ns(h1 - h0);
-  c->lat_ns[1] += ns(h2 - h1);
-  c->lat_ns[2] += ns(h3 - h2);
-  for (int k = 0; k < 2; ++k)
-    c->lat_ns[3 + k] += (double)(__atomic_load_n(&mb->dev_ticks[k + 1], __ATOMIC_RELAXED) -
-                                 __atomic_load_n(&mb->dev_ticks[k], __ATOMIC_RELAXED)) * 1e6 / c->wall_khz;
-  return MC_OK;
-}
-
-int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
-                                const double* translation, double* out) {
-  CHECK_ARG(c && rpy && translation, "NULL argument");
-  CHECK_ARG(n >= 0, "negative point count");
-  if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 1 with size %lld", (long long)ld);
-  if (n == 0) return MC_OK;
-  CHECK_ARG(points && out, "NULL points / out");
-  if (c->lat_on && n <= kLatRows) return lat_transform(c, points, n, ld, rpy, translation, out);   // no HIP call
-  DeviceGuard g(c->device);
-  if (n >= kZeroCopyRows) {                     // large: the DMA row pipeline with one frame
-    if (int r = sync_all(c)) return r;
-    void* st = nullptr;
-    if (int r = ctx_stage(c, 2 * sizeof(int64_t) + 12 * sizeof(double), &st)) return r;
-    int64_t* d_doff = static_cast<int64_t*>(st);
-    double* d_pose = reinterpret_cast<double*>(d_doff + 2);
-    const std::vector<int64_t> doff{0, n};
-    HIPCHK(hipMemcpyAsync(d_doff, doff.data(), 2 * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_pose_from_rpy, dim3(1), dim3(64), 0, c->stream, rpy[0], rpy[1], rpy[2], translation[0],
-                       translation[1], translation[2], d_pose);
-    HIPCHK(hipGetLastError());
-    const double* fr[1] = {points};
-    const int64_t lds[1] = {ld};
-    double* const outs[1] = {out};
-    return row_pipeline(c, fr, lds, doff, d_doff, d_pose, outs);
-  }
-  const size_t in_b = (size_t)n * ld * sizeof(double), out_b = (size_t)n * 4 * sizeof(double);
-  const size_t off = (in_b + 255) & ~size_t(255);
-  if (off + out_b > c->pin_bytes) {
-    if (c->h_pin) { (void)hipStreamSynchronize(c->stream); (void)hipHostFree(c->h_pin); c->h_pin = nullptr; }
-    c->pin_bytes = 0;
-    HIPCHK(hipHostMalloc(&c->h_pin, off + out_b, hipHostMallocMapped | hipHostMallocCoherent));
-    c->pin_bytes = off + out_b;
-  }
-  char* pin = static_cast<char*>(c->h_pin);
-  std::memcpy(pin, points, in_b);
-  const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
-  {
-    TimedRegion tr(c, &c->main_ev, c->stream);
-    hipLaunchKernelGGL(k_transform_host_f64, dim3(grid), dim3(kBlock), 0, c->stream,
-                       reinterpret_cast<const double*>(pin), n, ld, rpy[0], rpy[1], rpy[2], translation[0],
-                       translation[1], translation[2], reinterpret_cast<double*>(pin + off));
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
-  std::memcpy(out, pin + off, out_b);
-  return MC_OK;
-}
-
-// ---- per-point modes on host float64 rows (k_points_f64) --------------------------------------
 // pinned, device-mapped host scratch of at least `bytes` (the zero-copy path of the single calls)
 static int ctx_pin(mc_ctx* c, size_t bytes, char** out) {
   if (bytes > c->pin_bytes) {
@@ -1296,6 +1021,72 @@ static int ctx_pin(mc_ctx* c, size_t bytes, char** out) {
   *out = static_cast<char*>(c->h_pin);
   return MC_OK;
 }
+
+// Frames of host float64 rows through k_align_rows_f64 with the per-frame poses pose12 (F x 12,
+// host): below kZeroCopyRows rows the kernel reads and writes pinned, device-mapped host memory
+// (no DMA round trips for the reference's per-frame calls); above, the DMA row pipeline.
+static int align_host_rows(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
+                           const std::vector<double>& pose12, double* const* outs) {
+  const int32_t F = (int32_t)doff.size() - 1;
+  const int64_t n = doff[F];
+  if (n >= kZeroCopyRows) {
+    void* st = nullptr;
+    const size_t tab_b = doff.size() * sizeof(int64_t) + pose12.size() * sizeof(double);
+    if (int r = ctx_stage(c, tab_b, &st)) return r;
+    int64_t* d_doff = static_cast<int64_t*>(st);
+    double* d_pose = reinterpret_cast<double*>(d_doff + doff.size());
+    HIPCHK(hipMemcpyAsync(d_doff, doff.data(), doff.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_pose, pose12.data(), pose12.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return row_pipeline(c, frames, lds, doff, d_doff, d_pose, outs);
+  }
+  // pinned [doff (F+1) | poses (12 F) | rows (n, 4) | out (n, 4)], 8-byte words
+  const size_t w_pose = doff.size(), w_rows = w_pose + pose12.size(), w_out = w_rows + 4 * (size_t)n;
+  char* base = nullptr;
+  if (int r = ctx_pin(c, (w_out + 4 * (size_t)n) * 8, &base)) return r;
+  double* pin = reinterpret_cast<double*>(base);
+  std::memcpy(pin, doff.data(), doff.size() * 8);
+  std::memcpy(pin + w_pose, pose12.data(), pose12.size() * 8);
+  for (int32_t f = 0; f < F; ++f) {
+    const int64_t m = doff[f + 1] - doff[f], ld = lds[f];
+    double* dst = pin + w_rows + 4 * doff[f];
+    if (ld == 4) std::memcpy(dst, frames[f], (size_t)m * 4 * sizeof(double));
+    else for (int64_t i = 0; i < m; ++i) std::memcpy(dst + 4 * i, frames[f] + i * ld, 4 * sizeof(double));
+  }
+  {
+    TimedRegion tr(c, &c->main_ev, c->stream);
+    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
+    hipLaunchKernelGGL(k_align_rows_f64, dim3(grid), dim3(kBlock), 0, c->stream, pin + w_rows, (int64_t)4, n,
+                       (int64_t)0, reinterpret_cast<const int64_t*>(pin), F, pin + w_pose, pin + w_out);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int32_t f = 0; f < F; ++f)
+    if (doff[f + 1] > doff[f])
+      std::memcpy(outs[f], pin + w_out + 4 * doff[f], (size_t)(doff[f + 1] - doff[f]) * 4 * sizeof(double));
+  return MC_OK;
+}
+
+int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
+                                const double* translation, double* out) {
+  CHECK_ARG(c && rpy && translation, "NULL argument");
+  CHECK_ARG(n >= 0, "negative point count");
+  if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 1 with size %lld", (long long)ld);
+  if (n == 0) return MC_OK;
+  CHECK_ARG(points && out, "NULL points / out");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  // LMC:774: R = Rotation.from_euler('xyz', rotation).as_matrix(), scipy's arithmetic (rot.cpp)
+  std::vector<double> pose(12);
+  mcrot::euler_xyz_scipy(rpy, pose.data());
+  for (int k = 0; k < 3; ++k) pose[9 + k] = translation[k];
+  const std::vector<int64_t> doff{0, n};
+  const double* fr[1] = {points};
+  const int64_t lds[1] = {ld};
+  double* const outs[1] = {out};
+  return align_host_rows(c, fr, lds, doff, pose, outs);
+}
+
+// ---- per-point modes on host float64 rows (k_points_f64) --------------------------------------
 
 int mc_deskew_points_f64(mc_ctx* c, int mode, int32_t F, const int64_t* counts, const double* points, int64_t ld,
                          const int64_t* t_ns, const double* frame_times, const int64_t* frame_start_ns, double* out) {
@@ -1464,7 +1255,7 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
     if (e == hipSuccess) {
       TimedRegion tr(c, &c->main_ev, s);
       hipLaunchKernelGGL(k_align_rows_f64, dim3((unsigned)std::min<int64_t>((m + kBlock - 1) / kBlock, 4096)),
-                         dim3(kBlock), 0, s, dev[b], m, r0, d_doff, F, d_pose, dev[2 + b]);
+                         dim3(kBlock), 0, s, dev[b], (int64_t)4, m, r0, d_doff, F, d_pose, dev[2 + b]);
     }
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess && k >= 1) {                                // chunk k-1's rows are back: copy out
@@ -1506,48 +1297,61 @@ int mc_align_frames_host_f64(mc_ctx* c, int32_t F, const double* const* frames, 
   if (n == 0) return MC_OK;
   DeviceGuard g(c->device);
   if (int r = sync_all(c)) return r;
-  // per-frame float64 pose (k_scan_pose: pose selection LMC:804-812 + Euler -> R) in device scratch
-  void* st = nullptr;
-  const size_t tab_b = ((size_t)F + 1) * sizeof(int64_t) + (size_t)F * sizeof(double) + 12 * (size_t)F * sizeof(double);
-  if (int r = ctx_stage(c, tab_b, &st)) return r;
-  int64_t* d_doff = static_cast<int64_t*>(st);
-  double* d_ft = reinterpret_cast<double*>(d_doff + F + 1);
-  double* d_pose = d_ft + F;
-  HIPCHK(hipMemcpyAsync(d_doff, doff.data(), doff.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-  if (pose_select == MC_POSE_SEARCHSORTED)
-    HIPCHK(hipMemcpyAsync(d_ft, frame_times, F * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_scan_pose, dim3((F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->d_time, c->d_pos,
-                     c->d_rpy, c->T, d_ft, F, pose_select, d_pose);
-  HIPCHK(hipGetLastError());
-  if (n >= kZeroCopyRows) return row_pipeline(c, frames, lds, doff, d_doff, d_pose, outs);
+  // per-frame float64 pose {R | t}: pose selection LMC:804-812 and scipy's R (LMC:774), host-side
+  std::vector<double> pose(12 * (size_t)F);
+  mcrot::frame_poses(c->h_time.data(), c->h_pos.data(), c->h_rpy.data(), c->T, frame_times, F, pose_select,
+                     pose.data());
+  return align_host_rows(c, frames, lds, doff, pose, outs);
+}
 
-  // small: the kernel reads and writes pinned, device-mapped host memory [rows (n,4) | out (n,4)]
-  const size_t rows_b = (size_t)n * 4 * sizeof(double);
-  if (2 * rows_b > c->pin_bytes) {
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->h_pin) { (void)hipHostFree(c->h_pin); c->h_pin = nullptr; }
-    c->pin_bytes = 0;
-    HIPCHK(hipHostMalloc(&c->h_pin, 2 * rows_b, hipHostMallocMapped | hipHostMallocCoherent));
-    c->pin_bytes = 2 * rows_b;
-  }
-  double* pin_in = static_cast<double*>(c->h_pin);
-  double* pin_out = pin_in + 4 * n;
+int mc_affine_rows_f64(mc_ctx* c, int32_t F, const int64_t* counts, const double* rows, int64_t ld, int32_t n_mats,
+                       const double* mats, double* out) {
+  CHECK_ARG(c && (F == 0 || counts) && mats, "NULL argument");
+  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(ld == 3 || ld == 4, "rows need 3 or 4 columns (got %lld)", (long long)ld);
+  CHECK_ARG(n_mats == 1 || n_mats == F, "need 1 or n_frames matrices (got %d for %d frames)", n_mats, F);
+  std::vector<int64_t> doff((size_t)F + 1, 0);
   for (int32_t f = 0; f < F; ++f) {
-    const int64_t m = counts[f], ld = lds[f];
-    double* dst = pin_in + 4 * doff[f];
-    if (ld == 4) std::memcpy(dst, frames[f], (size_t)m * 4 * sizeof(double));
-    else for (int64_t i = 0; i < m; ++i) std::memcpy(dst + 4 * i, frames[f] + i * ld, 4 * sizeof(double));
+    CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
+    doff[f + 1] = doff[f] + counts[f];
   }
+  const int64_t n = doff[F];
+  if (n == 0) return MC_OK;
+  CHECK_ARG(rows && out, "NULL rows / out");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  // [doff (F+1) | mats (12 n_mats) | rows (n, ld) | out (n, 3)] in 8-byte words: pinned and
+  // device-mapped below kZeroCopyRows rows, device staging with DMA above
+  const size_t w_mat = doff.size(), w_rows = w_mat + 12 * (size_t)n_mats, w_out = w_rows + (size_t)n * ld,
+               words = w_out + 3 * (size_t)n;
+  const bool zero_copy = n < kZeroCopyRows;
+  char* base = nullptr;
+  hipStream_t s = c->stream;
+  if (zero_copy) {
+    if (int r = ctx_pin(c, words * 8, &base)) return r;
+    std::memcpy(base, doff.data(), doff.size() * 8);
+    std::memcpy(base + 8 * w_mat, mats, 12 * (size_t)n_mats * 8);
+    std::memcpy(base + 8 * w_rows, rows, (size_t)n * ld * 8);
+  } else {
+    void* st = nullptr;
+    if (int r = ctx_stage(c, words * 8, &st)) return r;
+    base = static_cast<char*>(st);
+    HIPCHK(hipMemcpyAsync(base, doff.data(), doff.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_mat, mats, 12 * (size_t)n_mats * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_rows, rows, (size_t)n * ld * 8, hipMemcpyHostToDevice, s));
+  }
+  double* d_out = reinterpret_cast<double*>(base + 8 * w_out);
   {
-    TimedRegion tr(c, &c->main_ev, c->stream);
-    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
-    hipLaunchKernelGGL(k_align_host_f64, dim3(grid), dim3(kBlock), 0, c->stream, pin_in, n, (int64_t)4, d_doff, F,
-                       d_pose, pin_out);
+    TimedRegion tr(c, &c->main_ev, s);
+    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, zero_copy ? 1024 : 65536);
+    hipLaunchKernelGGL(k_affine_rows_f64, dim3(grid), dim3(kBlock), 0, s,
+                       reinterpret_cast<const double*>(base + 8 * w_rows), ld, n, reinterpret_cast<const int64_t*>(base),
+                       F, reinterpret_cast<const double*>(base + 8 * w_mat), n_mats, d_out);
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
-  for (int32_t f = 0; f < F; ++f)
-    if (counts[f]) std::memcpy(outs[f], pin_out + 4 * doff[f], (size_t)counts[f] * 4 * sizeof(double));
+  if (!zero_copy) HIPCHK(hipMemcpyAsync(out, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (zero_copy) std::memcpy(out, d_out, (size_t)n * 24);
   return MC_OK;
 }
 
@@ -1646,24 +1450,6 @@ int mc_timing_read(mc_ctx* c, double* main_ms, int64_t* main_n, double* prep_ms,
   if (int r = sync_all(c)) return r;
   if (int r = sum_events(c, c->main_ev, main_ms, main_n)) return r;
   if (int r = sum_events(c, c->prep_ev, prep_ms, prep_n)) return r;
-  // graph-captured steps: their sampled events hold the last replay; each replay since the last
-  // read counts with those times
-  if (mcimpl::StepGraph* g = c->step_graph) {
-    if (g->pending > 0 && g->samples > 0) {
-      std::vector<unsigned long long> h(4 * (size_t)g->samples);
-      HIPCHK(hipMemcpy(h.data(), g->d_stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      double m = 0.0, p = 0.0;
-      for (int32_t k = 0; k < g->samples; ++k) {
-        p += (double)(h[4 * k + 1] - h[4 * k + 0]) / c->wall_khz;   // ticks / kHz = ms
-        m += (double)(h[4 * k + 3] - h[4 * k + 2]) / c->wall_khz;
-      }
-      if (main_ms) *main_ms += m * g->pending;
-      if (main_n) *main_n += (int64_t)g->samples * g->pending;
-      if (prep_ms) *prep_ms += p * g->pending;
-      if (prep_n) *prep_n += (int64_t)g->samples * g->pending;
-    }
-    g->pending = 0;
-  }
   return MC_OK;
 }
 
@@ -1677,17 +1463,14 @@ int mc_set_environment(mc_ctx* c, int64_t n, const double* env, int64_t ld) {
   if (int r = sync_all(c)) return r;
   dev_free(c->d_env);
   c->E = 0;
-  // scan.hpp's column layout: x, y, z float64 and the intensity as float32 (the value k_scan_emit
-  // writes, (float) of the reference's float64), transposed here once per scene
+  // scan.hpp's column layout: x, y, z, intensity float64, transposed here once per scene
   const size_t words = scene_words(n);
   if (int r = dev_alloc(&c->d_env, std::max<size_t>(words, 1))) return r;
   if (n > 0) {
     std::vector<double> h(words);
-    float* w = reinterpret_cast<float*>(h.data() + 3 * n);
     for (int64_t i = 0; i < n; ++i) {
       const double* q = env + i * ld;
-      h[i] = q[0]; h[n + i] = q[1]; h[2 * n + i] = q[2];
-      w[i] = (float)q[3];
+      h[i] = q[0]; h[n + i] = q[1]; h[2 * n + i] = q[2]; h[3 * n + i] = q[3];
     }
     HIPCHK(hipMemcpyAsync(c->d_env, h.data(), words * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1709,10 +1492,9 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   DeviceGuard g(c->device);
   if (int r = sync_all(c)) return r;
   const int32_t tiles = (int32_t)((c->E + kScanTile - 1) / kScanTile);
-  dev_free(c->d_scan_ftime); dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount); dev_free(c->d_scan_toff);
+  dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount); dev_free(c->d_scan_toff);
   dev_free(c->d_scan_nvis);
   c->scan_F = 0;
-  if (int r = dev_alloc(&c->d_scan_ftime, std::max(F, 1))) return r;
   if (int r = dev_alloc(&c->d_scan_pose, 12 * (size_t)std::max(F, 1))) return r;
   const int32_t Fp = scan_fpad(F);   // per-tile rows of counts / offsets, frames padded to kScanFrames
   if (int r = dev_alloc(&c->d_scan_tcount, (size_t)std::max(Fp, 1) * std::max(tiles, 1))) return r;
@@ -1727,11 +1509,11 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   c->scan_F = F;
   c->scan_tiles = tiles;
   if (F == 0) return MC_OK;
-  if (pose_select == MC_POSE_SEARCHSORTED)
-    HIPCHK(hipMemcpyAsync(c->d_scan_ftime, frame_times, F * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_scan_pose, dim3((F + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->d_time, c->d_pos,
-                     c->d_rpy, c->T, c->d_scan_ftime, F, pose_select, c->d_scan_pose);
-  HIPCHK(hipGetLastError());
+  // per-frame sensor pose {R | t} (LMC:804-812; R as scipy computes it, LMC:726), host-side
+  std::vector<double> pose(12 * (size_t)F);
+  mcrot::frame_poses(c->h_time.data(), c->h_pos.data(), c->h_rpy.data(), c->T, frame_times, F, pose_select,
+                     pose.data());
+  HIPCHK(hipMemcpyAsync(c->d_scan_pose, pose.data(), pose.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
   std::vector<int64_t> nvis(F, 0), toff((size_t)Fp * std::max(tiles, 1), 0);
   if (tiles > 0) {
     const ScanParams sp = make_scan_params(c->scan_par, cap);
@@ -1775,34 +1557,56 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   return MC_OK;
 }
 
+// pass 2 of the last mc_scan_count: the batch's float32 columns (out != nullptr) or the reference's
+// float64 rows (local, aligned: device (N, 4) arrays, aligned may be nullptr)
+static int scan_emit(mc_ctx* c, mc_batch* out, const double* noise, double* d_local, double* d_aligned) {
+  int64_t N = 0;
+  for (int64_t k : c->scan_counts) N += k;
+  if (c->scan_F == 0 || N == 0 || c->scan_tiles == 0) return MC_OK;
+  DeviceGuard g(c->device);
+  // staging: [noise (N, 3) | doff (F + 1)] (the rows path has no batch offsets of its own)
+  const size_t noise_w = noise ? 3 * (size_t)N : 0;
+  void* st = nullptr;
+  if (int r = ctx_stage(c, (noise_w + (size_t)c->scan_F + 1) * 8, &st)) return r;
+  double* d_noise = noise ? static_cast<double*>(st) : nullptr;
+  int64_t* d_doff = reinterpret_cast<int64_t*>(static_cast<double*>(st) + noise_w);
+  if (noise) HIPCHK(hipMemcpyAsync(d_noise, noise, noise_w * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  std::vector<int64_t> doff((size_t)c->scan_F + 1, 0);
+  for (int32_t f = 0; f < c->scan_F; ++f) doff[f + 1] = doff[f] + c->scan_counts[f];
+  if (!out) HIPCHK(hipMemcpyAsync(d_doff, doff.data(), doff.size() * 8, hipMemcpyHostToDevice, c->stream));
+  ScanEmitArgs ea;
+  std::memset(&ea, 0, sizeof(ea));
+  ea.env = c->d_env; ea.E = c->E; ea.n_tiles = c->scan_tiles;
+  ea.pose = c->d_scan_pose; ea.F = c->scan_F;
+  ea.sp = make_scan_params(c->scan_par, c->scan_cap);
+  ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.vis_bits = c->d_scan_bits; ea.noise = d_noise;
+  if (out) {
+    ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.C = out->C;
+  } else {
+    ea.doff = d_doff; ea.local = d_local; ea.aligned = d_aligned;
+  }
+  {
+    TimedRegion tr(c, &c->scan_ev, c->stream);
+    const uint32_t units = (uint32_t)c->scan_tiles * (uint32_t)((c->scan_F + kScanFrames - 1) / kScanFrames);
+    if (out) hipLaunchKernelGGL(k_scan_emit<false>, dim3(units), dim3(kBlock), 0, c->stream, ea);
+    else hipLaunchKernelGGL(k_scan_emit<true>, dim3(units), dim3(kBlock), 0, c->stream, ea);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
 int mc_scan_emit(mc_ctx* c, mc_batch* out, const double* noise) {
   CHECK_ARG(c && out, "NULL argument");
   CHECK_ARG(out->ctx == c, "batch belongs to another context");
   if (out->counts != c->scan_counts)
     return fail(MC_ERR_INVALID, "output batch frame counts differ from the last mc_scan_count");
-  if (out->F == 0 || out->N == 0 || c->scan_tiles == 0) return MC_OK;
-  DeviceGuard g(c->device);
-  const double* d_noise = nullptr;
-  if (noise) {
-    void* st = nullptr;
-    if (int r = ctx_stage(c, (size_t)out->N * 3 * sizeof(double), &st)) return r;
-    HIPCHK(hipMemcpyAsync(st, noise, (size_t)out->N * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    d_noise = static_cast<const double*>(st);
-  }
-  ScanEmitArgs ea;
-  ea.env = c->d_env; ea.E = c->E; ea.n_tiles = c->scan_tiles;
-  ea.pose = c->d_scan_pose; ea.F = out->F;
-  ea.sp = make_scan_params(c->scan_par, c->scan_cap);
-  ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.vis_bits = c->d_scan_bits; ea.noise = d_noise;
-  ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.C = out->C;
-  {
-    TimedRegion tr(c, &c->scan_ev, c->stream);
-    const uint32_t units = (uint32_t)c->scan_tiles * (uint32_t)((out->F + kScanFrames - 1) / kScanFrames);
-    hipLaunchKernelGGL(k_scan_emit, dim3(units), dim3(kBlock), 0, c->stream, ea);
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return MC_OK;
+  return scan_emit(c, out, noise, nullptr, nullptr);
+}
+
+int mc_scan_emit_f64(mc_ctx* c, const double* noise, double* d_local, double* d_aligned) {
+  CHECK_ARG(c && d_local, "NULL argument");
+  return scan_emit(c, nullptr, noise, d_local, d_aligned);
 }
 
 int mc_timing_read_scan(mc_ctx* c, double* ms, int64_t* n) {

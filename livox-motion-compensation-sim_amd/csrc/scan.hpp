@@ -3,10 +3,13 @@
 //
 // Per (frame, scene point): world distance prefilter, R^T (p - t) into the sensor frame, FOV mask
 // on atan2 / asin in degrees and range_min, then in-order stream compaction and the systematic
-// subsample (every (n // cap)-th visible point, at most cap).  Visibility is evaluated in f64
-// with the reference's operation order (no FMA contraction in the distance sum, the same degree
-// conversions), so the kept point sets are the reference's; the range noise (LMC:765-768) is drawn
-// by the host from numpy's global RNG in frame order and added here.
+// subsample (every (n // cap)-th visible point, at most cap).  Everything is evaluated in f64 with
+// the reference's operation order: the distance sum without contraction, the rotation as numpy's
+// matmul accumulates it (scan_rotate) with the pose's R from rot.cpp (scipy's, bit for bit), the
+// same degree conversions — so the kept point sets and their sensor-frame coordinates are the
+// reference's exactly.  The range noise (LMC:765-768) is drawn by the host from numpy's global RNG in
+// frame order and added here.  Output: float32 batch columns (k_scan_emit<false>) or the reference's
+// float64 rows, local and aligned in one pass (k_scan_emit<true>, mc_scan_emit_f64).
 //
 // A workgroup owns a tile of kScanTile scene points held in registers and tests it against
 // kScanFrames frames (scene re-reads from L2 drop by that factor).  Units (tile, frame group) are
@@ -16,11 +19,11 @@
 // bytes, profiles/pmc_traffic.json r3s65), and a frame's output runs of neighbouring tiles meet in
 // one L2 instead of being written as partial lines by two.
 //
-// Device layout (mc_set_environment / mc_scan_count): the scene as columns — x, y, z float64 (the
-// 24 bytes the visibility test needs, one coalesced 8-byte load per lane each; the reference's (E,4)
-// rows would fetch 32) and the intensity as float32 (the output's own rounding of the float64 value,
-// read only for emitted points); per-(tile, frame) counts and offsets tile-major with the frames
-// padded to kScanFrames, so a workgroup's 8 frames are one 32 / 64-byte run.
+// Device layout (mc_set_environment / mc_scan_count): the scene as float64 columns x, y, z (the 24
+// bytes the visibility test needs, one coalesced 8-byte load per lane each; the reference's (E,4)
+// rows would fetch 32) and intensity (read only for emitted points); per-frame poses {R | t} from the
+// host (rot.cpp frame_poses); per-(tile, frame) counts and offsets tile-major with the frames padded
+// to kScanFrames, so a workgroup's 8 frames are one 32 / 64-byte run.
 #pragma once
 #include "kernels.hpp"
 
@@ -53,23 +56,16 @@ inline ScanParams make_scan_params(const double par[4], int64_t cap) {
   return sp;
 }
 
-// f64 sensor pose per frame: R (row-major, 9) + position (3), pose selection as in LMC:804-812
-__global__ __launch_bounds__(kBlock) void k_scan_pose(const double* time, const double* pos, const double* rpy,
-                                                      int64_t T, const double* frame_time, int32_t F,
-                                                      int pose_select, double* pose) {
-  const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (f >= F) return;
-  int64_t idx;
-  if (pose_select == 1) {
-    idx = f;
-  } else {
-    idx = lower_bound_f64(time, T, frame_time[f]);
-    if (idx > T - 1) idx = T - 1;
-  }
-  double R[9];
-  euler_xyz_matrix(rpy[3 * idx], rpy[3 * idx + 1], rpy[3 * idx + 2], R);
-  for (int k = 0; k < 9; ++k) pose[12 * f + k] = R[k];
-  for (int k = 0; k < 3; ++k) pose[12 * f + 9 + k] = pos[3 * idx + k];
+// R^T d (LMC:728: (R.T @ d.T).T) the way numpy's matmul accumulates it: per output an ascending
+// FMA chain over k, fma(A[i][2], d2, fma(A[i][1], d1, A[i][0] * d0)) with A = R^T (numpy's dgemm on
+// the reference's box, tools/fma_order.py).  With the pose's R from rot.cpp the sensor-frame
+// coordinates equal the reference's bit for bit.
+__device__ __forceinline__ void scan_rotate(const double* __restrict__ P, double dx, double dy, double dz, double& lx,
+                                            double& ly, double& lz) {
+#pragma clang fp contract(off)
+  lx = __builtin_fma(P[6], dz, __builtin_fma(P[3], dy, P[0] * dx));
+  ly = __builtin_fma(P[7], dz, __builtin_fma(P[4], dy, P[1] * dx));
+  lz = __builtin_fma(P[8], dz, __builtin_fma(P[5], dy, P[2] * dx));
 }
 
 // the reference's degree comparisons (LMC:735-744), for points near an FOV edge only: kept out of
@@ -88,9 +84,7 @@ __device__ __forceinline__ bool scan_visible(const double* __restrict__ P, doubl
   const double dx = ex - P[9], dy = ey - P[10], dz = ez - P[11];
   const double d2 = dx * dx + dy * dy + dz * dz;              // np.sum(.., axis=1) order
   if (!(d2 <= sp.range_max_sq)) return false;                 // LMC:718
-  lx = P[0] * dx + P[3] * dy + P[6] * dz;                      // R^T (p - t), LMC:727-728
-  ly = P[1] * dx + P[4] * dy + P[7] * dz;
-  lz = P[2] * dx + P[5] * dy + P[8] * dz;
+  scan_rotate(P, dx, dy, dz, lx, ly, lz);                      // R^T (p - t), LMC:727-728
   // Away from the edges the tests of LMC:732-745 are decided without sqrt / division / atan2 /
   // asin: r >= range_min by d2 against range_min^2, |az| <= h by |ly| <= tan(h) lx (lx > 0),
   // |el| <= v by lz^2 <= sin(v)^2 d2 (both FOVs below 90 degrees, where atan2 / asin are
@@ -117,13 +111,13 @@ __device__ __forceinline__ bool scan_visible(const double* __restrict__ P, doubl
   return scan_fov_exact(lx, ly, s, az_in, el_in, sp.half_fov_h, sp.half_fov_v);
 }
 
-// the scene columns in one allocation of scene_words(E) doubles
-inline size_t scene_words(int64_t E) { return 3 * (size_t)E + ((size_t)E + 1) / 2; }
+// the scene columns x, y, z, intensity (float64) in one allocation of scene_words(E) doubles
+inline size_t scene_words(int64_t E) { return 4 * (size_t)E; }
 struct SceneCols {
-  const double* x; const double* y; const double* z; const float* w;
+  const double* x; const double* y; const double* z; const double* w;
 };
 __host__ __device__ inline SceneCols scene_cols(const double* env, int64_t E) {
-  return SceneCols{env, env + E, env + 2 * E, reinterpret_cast<const float*>(env + 3 * E)};
+  return SceneCols{env, env + E, env + 2 * E, env + 3 * E};
 }
 __host__ __device__ inline int32_t scan_fpad(int32_t F) { return (F + kScanFrames - 1) / kScanFrames * kScanFrames; }
 
@@ -204,8 +198,13 @@ struct ScanEmitArgs {
   const double* noise;       // (N_out, 3) in the batch's dense order, or nullptr
   const int64_t* poff; const int64_t* doff;
   float* cols; int32_t C;   // the output batch's blocked columns (kernels.hpp bidx)
+  double* local;            // ROWS: (N_out, 4) float64 sensor-frame rows (LMC:770), dense order
+  double* aligned;          // ROWS: (N_out, 4) float64 R p + t of those rows (LMC:831), or nullptr
 };
 
+// ROWS = false: float32 columns of a batch; ROWS = true: the reference's float64 rows (local and,
+// fused, the aligned cloud of the same frame pose, LMC:826-831) with no float32 rounding anywhere
+template <bool ROWS>
 __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
   __shared__ int s_cnt[kScanRounds][kBlock / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -231,9 +230,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
         // the sensor-frame point exactly as pass 1 (and LMC:727-728) computed it
 #pragma clang fp contract(off)
         const double dx = t.x[r] - P[9], dy = t.y[r] - P[10], dz = t.z[r] - P[11];
-        lx[r] = P[0] * dx + P[3] * dy + P[6] * dz;
-        ly[r] = P[1] * dx + P[4] * dy + P[7] * dz;
-        lz[r] = P[2] * dx + P[5] * dy + P[8] * dz;
+        scan_rotate(P, dx, dy, dz, lx[r], ly[r], lz[r]);
       }
       const unsigned long long m = __ballot(vis[r]);
       rank[r] = __popcll(m & ((1ull << lane) - 1ull));
@@ -242,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
     __syncthreads();
     const int64_t nv = a.nvis[f];
     const int64_t step = nv > a.sp.cap ? nv / a.sp.cap : 1;    // LMC:757-760
-    const int64_t poff = a.poff[f], doff = a.doff[f];
+    const int64_t poff = ROWS ? 0 : a.poff[f], doff = a.doff[f];
     int64_t base = a.tile_off[su.tile * scan_fpad(a.F) + f];
 #pragma unroll
     for (int r = 0; r < kScanRounds; ++r) {
@@ -259,13 +256,27 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
           const int64_t o = idx / step;
           double nx = 0, ny = 0, nz = 0;
           if (a.noise) { const double* q = a.noise + 3 * (doff + o); nx = q[0]; ny = q[1]; nz = q[2]; }
-          const int64_t p = poff + o;
           const int64_t e = t0 + r * kBlock + threadIdx.x;
-          float* q = a.cols + bidx(a.C, 0, p);
-          q[0] = (float)(lx[r] + nx);
-          q[kBlkPts] = (float)(ly[r] + ny);
-          q[2 * kBlkPts] = (float)(lz[r] + nz);
-          q[3 * kBlkPts] = sc.w[e];
+          // LMC:768 visible_points += noise (one rounding; 0 noise leaves the value unchanged)
+          const double px = __dadd_rn(lx[r], nx), py = __dadd_rn(ly[r], ny), pz = __dadd_rn(lz[r], nz);
+          if constexpr (ROWS) {
+            double* q = a.local + 4 * (doff + o);
+            *reinterpret_cast<double2*>(q) = double2{px, py};
+            *reinterpret_cast<double2*>(q + 2) = double2{pz, sc.w[e]};
+            if (a.aligned) {
+              double ax, ay, az;
+              frame_apply(P, px, py, pz, ax, ay, az);
+              double* w = a.aligned + 4 * (doff + o);
+              *reinterpret_cast<double2*>(w) = double2{ax, ay};
+              *reinterpret_cast<double2*>(w + 2) = double2{az, sc.w[e]};
+            }
+          } else {
+            float* q = a.cols + bidx(a.C, 0, poff + o);
+            q[0] = (float)px;
+            q[kBlkPts] = (float)py;
+            q[2 * kBlkPts] = (float)pz;
+            q[3 * kBlkPts] = (float)sc.w[e];
+          }
         }
       }
       base += total;

@@ -95,16 +95,13 @@ class Context:
         return out
 
     def deskew_steps(self, inp: "Batch", out: "Batch", n_steps: int, mode: str = "frame",
-                     pose_select: str = "searchsorted", sample_every: int = 0, prepare: bool = False,
-                     pipeline: bool = False) -> "Batch":
-        """``n_steps`` calls of :meth:`deskew` (asynchronous); every step runs its prep and kernel.
-        Default: replayed as one HIP graph (``prepare``: capture the graph only).  ``pipeline``: no
-        graph; each step's launch also runs the next step's prep (MC_STEPS_PIPELINE).
-        ``sample_every``: timing events around every n-th step's kernels (:meth:`read_timing`)."""
-        flags = (_lib.STEPS_PREPARE if prepare else 0) | (_lib.STEPS_PIPELINE if pipeline else 0)
+                     pose_select: str = "searchsorted", sample_every: int = 0) -> "Batch":
+        """``n_steps`` calls of :meth:`deskew` (asynchronous) as n + 1 launches: each step's launch
+        also runs the next step's prep (mc_deskew_steps).  ``sample_every``: timing events around
+        every n-th step's kernels (:meth:`read_timing`)."""
         check(self.lib.mc_deskew_steps(self.handle, inp.handle, out.handle, _lib.MODES[mode],
-                                       _lib.POSE_SELECT[pose_select], int(n_steps), int(sample_every),
-                                       flags), f"deskew_steps[{mode}]")
+                                       _lib.POSE_SELECT[pose_select], int(n_steps), int(sample_every)),
+              f"deskew_steps[{mode}]")
         return out
 
     def tune_order(self, inp: "Batch", out: "Batch", mode: str = "frame", pose_select: str = "searchsorted",
@@ -145,14 +142,7 @@ class Context:
         check(self.lib.mc_set_environment(self.handle, env.shape[0], ptr(env, c_double), env.shape[1]),
               "set_environment")
 
-    def scan(self, frame_times, config: dict, pose_select: str = "searchsorted", rng=np.random,
-             out: "Batch | None" = None) -> "Batch":
-        """All frames' local scans of the scene (LMC:701-770 once per frame of LMC:802-831) in two
-        launches: visibility counts per (frame, scene tile), then in-order compaction, the systematic
-        subsample and the range noise.  The trajectory must be set (pose per frame as in
-        ``deskew(mode='frame')``).  The noise is drawn here from ``rng`` (numpy's global RNG by
-        default) in frame order, exactly as the reference's per-frame ``np.random.normal`` calls
-        consume it (LMC:765-768), so seeded runs reproduce the reference's scans."""
+    def _scan_count(self, frame_times, config: dict, pose_select: str, rng):
         t = np.ascontiguousarray(np.atleast_1d(frame_times), dtype=np.float64)
         F = len(t)
         par = np.array([config["range_min"], config["range_max"], config["fov_horizontal"],
@@ -161,32 +151,65 @@ class Context:
         check(self.lib.mc_scan_count(self.handle, F, ptr(t, c_double), _lib.POSE_SELECT[pose_select],
                                      ptr(par, c_double), int(config["points_per_frame"]), ptr(counts, c_int64)),
               "scan_count")
-        if out is None or not np.array_equal(out.counts, counts):
-            out = Batch(self, counts)
         noise = None
         std = config["lidar_range_noise"]
         if std > 0 and counts.sum() > 0:
             # one draw of sum(n_f) x 3 consumes the legacy normal stream exactly like F per-frame
             # draws of n_f x 3 (frames with no visible point draw nothing in the reference either)
             noise = np.ascontiguousarray(rng.normal(0, std, (int(counts.sum()), 3)), dtype=np.float64)
-        check(self.lib.mc_scan_emit(self.handle, out.handle, ptr(noise, c_double) if noise is not None else None),
-              "scan_emit")
+        return counts, noise
+
+    def scan(self, frame_times, config: dict, pose_select: str = "searchsorted", rng=np.random,
+             out: "Batch | None" = None) -> "Batch":
+        """All frames' local scans of the scene (LMC:701-770 once per frame of LMC:802-831) in two
+        launches into a float32 batch: visibility counts per (frame, scene tile), then in-order
+        compaction, the systematic subsample and the range noise.  The trajectory must be set (pose
+        per frame as in ``deskew(mode='frame')``).  The noise is drawn here from ``rng`` (numpy's
+        global RNG by default) in frame order, exactly as the reference's per-frame
+        ``np.random.normal`` calls consume it (LMC:765-768), so seeded runs reproduce its scans."""
+        counts, noise = self._scan_count(frame_times, config, pose_select, rng)
+        if out is None or not np.array_equal(out.counts, counts):
+            out = Batch(self, counts)
+        check(self.lib.mc_scan_emit(self.handle, out.handle, ptr(noise, c_double)), "scan_emit")
         return out
 
-    def latency_server(self, enable: bool = True) -> dict:
-        """Opt-in resident kernel for single transform_pointcloud calls up to 32768 rows
-        (mc_set_latency_server): no launch and no completion signal per call.  Returns its info."""
-        check(self.lib.mc_set_latency_server(self.handle, int(bool(enable))), "latency_server")
-        return self.latency_server_info()
+    def scan_rows(self, frame_times, config: dict, pose_select: str = "searchsorted", rng=np.random,
+                  aligned: bool = True):
+        """:meth:`scan` into the reference's own float64 arrays (mc_scan_emit_f64): returns
+        (counts, local, aligned) with local / aligned (N, 4) float64 host arrays, frames back to back
+        — scan_environment's output and transform_pointcloud of it with the frame's pose (LMC:815,
+        831), equal to the reference's values bit for bit; ``aligned=False``: local only (None)."""
+        counts, noise = self._scan_count(frame_times, config, pose_select, rng)
+        n = int(counts.sum())
+        if n == 0:
+            return counts, np.zeros((0, 4)), (np.zeros((0, 4)) if aligned else None)
+        loc = DeviceBuffer(self, n * 32)
+        al = DeviceBuffer(self, n * 32) if aligned else None
+        try:
+            check(self.lib.mc_scan_emit_f64(self.handle, ptr(noise, c_double), loc.ptr, al.ptr if al else None),
+                  "scan_emit_f64")
+            return counts, loc.to_host(np.float64, (n, 4)), (al.to_host(np.float64, (n, 4)) if al else None)
+        finally:
+            loc.close()
+            if al:
+                al.close()
 
-    def latency_server_info(self) -> dict:
-        e, la, rq = c_int(), c_int64(), c_int64()
-        ph = np.zeros(5, np.float64)
-        check(self.lib.mc_latency_server_info(self.handle, ctypes.byref(e), ctypes.byref(la), ctypes.byref(rq),
-                                              ptr(ph, c_double)), "latency_server_info")
-        return {"enabled": bool(e.value), "launches": la.value, "requests": rq.value,
-                "mean_us": {"copy_in": ph[0], "post_to_done": ph[1], "copy_out": ph[2], "server_load": ph[3],
-                            "server_store": ph[4], "server": ph[3] + ph[4]}}
+    def affine_rows(self, counts, rows, mats) -> np.ndarray:
+        """(T @ [p, w].T).T[:, :3] on float64 rows (mc_affine_rows_f64): rows (N, 3) (w = 1) or
+        (N, 4) homogeneous, frames of ``counts`` rows back to back; one (3|4, 4) matrix or one per
+        frame.  Returns (N, 3) float64, bit-identical to numpy's (CSIM:230)."""
+        c = np.ascontiguousarray(np.atleast_1d(counts), dtype=np.int64)
+        r = np.ascontiguousarray(rows, dtype=np.float64)
+        m = np.ascontiguousarray(mats, dtype=np.float64)
+        if m.ndim == 2:
+            m = m[None]
+        if m.shape[1:] not in ((3, 4), (4, 4)):
+            raise ValueError(f"expected (3,4) / (4,4) matrices, got {np.shape(mats)}")
+        m = np.ascontiguousarray(m[:, :3, :4])
+        out = np.empty((r.shape[0], 3), np.float64)
+        check(self.lib.mc_affine_rows_f64(self.handle, len(c), ptr(c, c_int64), ptr(r, c_double), r.shape[1],
+                                          len(m), ptr(m, c_double), ptr(out, c_double)), "affine_rows")
+        return out
 
     def set_max_grid(self, max_grid: int):
         check(self.lib.mc_set_launch(self.handle, int(max_grid)), "set_launch")

@@ -195,12 +195,13 @@ class LiDARMotionSimulator:
         ctx = self.context
         ctx.set_trajectory([0.0], np.asarray(sensor_pose["position"], np.float64).reshape(1, 3),
                            np.asarray(sensor_pose["orientation"], np.float64).reshape(1, 3))
-        scans = ctx.scan([0.0], self.config, pose_select="direct")
-        return scans.download_aos() if scans.n_points else np.zeros((0, 4))
+        _, local, _ = ctx.scan_rows([0.0], self.config, pose_select="direct", aligned=False)
+        return local
 
     def scan_frames(self, environment, trajectory: dict, times: Optional[np.ndarray] = None):
-        """Every frame's scan (LMC:802-817 pose selection + 815 scan) as one device batch, noise
-        drawn in frame order from the global RNG.  Returns the device ``Batch`` of local scans."""
+        """Every frame's scan (LMC:802-817 pose selection + 815 scan) as one device batch of float32
+        columns (the hot path's input layout), noise drawn in frame order from the global RNG.
+        Returns the device ``Batch`` of local scans."""
         if times is None:
             times = self.lidar_times()
         self._load_environment(environment)
@@ -209,30 +210,32 @@ class LiDARMotionSimulator:
         return ctx.scan(np.asarray(times, np.float64), self.config, pose_select="searchsorted")
 
     def simulate_frames(self, environment, trajectory: dict, times: Optional[np.ndarray] = None) -> dict:
-        """The frame loop of run_simulation (LMC:802-850) with both point stages on the GPU: the
-        scans are produced into HBM and aligned there (MC_POSE_SEARCHSORTED) without a host round
-        trip in between.  Returns run_simulation's dict (LMC:852-858)."""
+        """The frame loop of run_simulation (LMC:802-850) with both point stages on the GPU in one
+        pass: every frame's scan (LMC:815) and its alignment with the same pose (LMC:826-831) are
+        written by one kernel as the reference's float64 arrays, bit-identical to the reference's
+        values (mc_scan_emit_f64).  Returns run_simulation's dict (LMC:852-858)."""
         if times is None:
             times = self.lidar_times()
         times = np.asarray(times, np.float64)
-        scans = self.scan_frames(environment, trajectory, times)
-        scans.set_frame_times(times)
-        aligned_b = self.context.deskew(scans, None, mode="frame", pose_select="searchsorted")
-        local = scans.split(scans.download_aos())
-        aligned = aligned_b.split(aligned_b.download_aos())
+        self._load_environment(environment)
+        ctx = self.context
+        ctx.set_trajectory(trajectory["time"], trajectory["position_gps"], trajectory["orientation_imu"])
+        counts, local, aligned = ctx.scan_rows(times, self.config, pose_select="searchsorted")
+        offs = np.concatenate([[0], np.cumsum(counts)])
         idx = np.clip(np.searchsorted(trajectory["time"], times), 0, len(trajectory["time"]) - 1)
-        raw, motion = [], []
+        raw, al, motion = [], [], []
         for i, (t, k) in enumerate(zip(times, idx)):
             pose = {"position": trajectory["position_gps"][k], "orientation": trajectory["orientation_imu"][k],
                     "velocity": trajectory["velocity"][k]}
-            raw.append({"frame_id": i, "timestamp": t, "points_local": local[i], "sensor_pose": pose})
+            raw.append({"frame_id": i, "timestamp": t, "points_local": local[offs[i]:offs[i + 1]], "sensor_pose": pose})
+            al.append(aligned[offs[i]:offs[i + 1]])
             p, o, v = pose["position"], pose["orientation"], pose["velocity"]
             motion.append({"frame_id": i, "timestamp": t,
                            "gps_lat": p[1] / 111320.0 + 40.0,
                            "gps_lon": p[0] / (111320.0 * np.cos(np.radians(40.0))) - 74.0,
                            "gps_alt": p[2], "imu_roll": o[0], "imu_pitch": o[1], "imu_yaw": o[2],
                            "vel_x": v[0], "vel_y": v[1], "vel_z": v[2]})
-        return {"raw_scans": raw, "aligned_pointclouds": aligned, "motion_data": motion,
+        return {"raw_scans": raw, "aligned_pointclouds": al, "motion_data": motion,
                 "trajectory": trajectory, "environment": environment}
 
     def run_simulation(self, environment):
@@ -292,7 +295,8 @@ class LiDARMotionSimulator:
             print("Warning: No raw point clouds to merge")
         try:
             if merged_aligned is None:
-                raise NameError("name 'merged_aligned' is not defined")   # LMC:903 on the skipped merge
+                # LMC:903 reads merged_aligned, unbound when LMC:887 skipped the merge
+                raise UnboundLocalError("local variable 'merged_aligned' referenced before assignment")
             self.save_las(merged_aligned, os.path.join(output_dir, "merged_aligned.las"))
             print("LAS format saved successfully")
         except Exception as e:

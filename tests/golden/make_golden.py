@@ -26,6 +26,11 @@ Fixtures:
   coords.npz          CoordinateTransformer matrices / transforms and _transform_coordinates
                       (CSIM:153-233, 2107-2163).
   save_results.npz    the whole output directory of LMC's save_results (LMC:860-931).
+  lmc_run_files.json  the reference's own end-to-end runs: for each scenario, run_simulation()
+                      (LMC:778-858) then save_results() (LMC:860-931); every file of the output
+                      directory by relative path -> [size, sha256], the printed log, and per-frame
+                      point counts.  The scene and the RNG state before the frame loop are
+                      lmc_env_<cfg>.npz (checked here to be the same run).
 """
 from __future__ import annotations
 
@@ -346,6 +351,14 @@ def make_coords(csim):
                 assert fr["coordinate_system"] == target
         out["tc/n_frames"] = np.int64(len(counts))
         out["utm_available"] = np.bool_(csim.UTM_AVAILABLE)
+        # a UTM-scale translation (easting / northing ~ 5e5 / 4.4e6 m): float32 would quantise it to 0.5 m
+        ct.set_transformation("sensor", "utm_grid", [512345.678, 4431234.567, 12.5], [0.01, -0.02, 1.2])
+        pb = rng.normal(0, 40, (300, 3))
+        out["big/p3"] = pb
+        out["big/T"] = ct.transformations[("sensor", "utm_grid")]
+        out["big/T_inv"] = ct.transformations[("utm_grid", "sensor")]
+        out["big/fwd"] = ct.transform_points(pb, "sensor", "utm_grid")
+        out["big/back"] = ct.transform_points(out["big/fwd"], "utm_grid", "sensor")
     np.savez_compressed(os.path.join(HERE, "coords.npz"), **out)
 
 
@@ -394,8 +407,46 @@ def make_save_results(lmc):
     np.savez_compressed(os.path.join(HERE, "save_results.npz"), **out)
 
 
+def make_run_files(lmc):
+    """Digest of every file the reference writes for a whole scenario (LMC:1176-1233 minus the
+    plots and report): run_simulation -> save_results into a temp dir."""
+    import hashlib
+    import shutil
+    import tempfile
+    out = {}
+    for name, cfg in SCENARIOS.items():
+        sim = lmc.LiDARMotionSimulator(dict(cfg))
+        with contextlib.redirect_stdout(io.StringIO()):
+            res = sim.run_simulation()
+        e = np.load(os.path.join(HERE, f"lmc_env_{name}.npz"))
+        assert np.array_equal(e["environment"], res["environment"]), name
+        d = tempfile.mkdtemp()
+        try:
+            log = io.StringIO()
+            with contextlib.redirect_stdout(log):
+                sim.save_results(res, d)
+            files = {}
+            for root, _, fs in os.walk(d):
+                for fn in sorted(fs):
+                    p = os.path.join(root, fn)
+                    with open(p, "rb") as fh:
+                        data = fh.read()
+                    files[os.path.relpath(p, d)] = [len(data), hashlib.sha256(data).hexdigest()]
+            out[name] = {"files": files, "log": log.getvalue().replace(d, "<out>"),
+                         "frame_counts": [int(len(s["points_local"])) for s in res["raw_scans"]]}
+        finally:
+            shutil.rmtree(d)
+        print(f"{name}: {len(out[name]['files'])} files, {sum(v[0] for v in out[name]['files'].values())} bytes")
+    with open(os.path.join(HERE, "lmc_run_files.json"), "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+
+
 def main():
     lmc, csim = import_reference()
+    one = {"run_files": lambda: make_run_files(lmc), "coords": lambda: make_coords(csim)}
+    if sys.argv[1:2] and sys.argv[1] in one:   # one fixture only (the others are unchanged by it)
+        one[sys.argv[1]]()
+        return
     make_save_results(lmc)
     make_coords(csim)
     make_codecs(lmc)
@@ -406,6 +457,7 @@ def main():
     make_pathb(csim)
     make_slerp(lmc)
     make_synth()
+    make_run_files(lmc)
     for f in sorted(os.listdir(HERE)):
         print(f"{f:24s} {os.path.getsize(os.path.join(HERE, f)):>9d} B")
 

@@ -1,7 +1,10 @@
-"""Multi-rank path on CPU: shard planning, the socket control plane, and a world-size-2
-``gloo`` run whose rank-ordered gather equals the reference's frame-ordered np.vstack
-(LMC:887-889).  The per-rank compute here is the oracle (test-only); on GPUs it is the HIP
-kernel and the gather is RCCL (tests/test_gpu_parity.py covers the single-rank RCCL path)."""
+"""Multi-rank path on CPU: shard planning, the socket control plane, and ``gloo`` runs of the
+merged-cloud gather (LMC:887-889 np.vstack).  Each rank holds its frame shard in the product's
+blocked-CSR batch layout; the root assembles the merged batch at the offsets of the library's own
+gather plan (mc_gather_plan, the host half of mc_comm_gather_batch) from point-to-point
+sends / receives — the transfers mc_comm_gather_batch issues as ncclSend / ncclRecv — including
+shards whose column count differs (t_ns carried) and is re-pitched.  On GPUs the same plan drives
+RCCL (tests/test_gpu_gather_issue.py covers the device copies / re-pitch in one process)."""
 import multiprocessing as mp
 import os
 import socket
@@ -71,53 +74,79 @@ def test_rendezvous_processes(world):
         assert blob == b"uid-" + bytes(range(124))
 
 
-def _gloo_worker(rank, world, port, q):
+def _gloo_worker(rank, world, root, port, q):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import importlib
+    import torch
     import torch.distributed as dist
-    from oracle import restatement as R
     from oracle import synth
     m = importlib.import_module("livox-motion-compensation-sim_amd")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sim = m.LiDARMotionSimulator({"duration": 12.0, "trajectory_type": "figure_eight", "max_speed": 12.0})
-    tr = sim.add_sensor_noise(sim.generate_trajectory())
-    times = sim.lidar_times()
-    counts = np.array([(997 * (f + 3)) % 4000 for f in range(len(times))], np.int64)
+    F = len(sim.lidar_times())
+    counts = np.array([(997 * (f + 3)) % 4000 for f in range(F)], np.int64)
+    counts[3] = 0                                     # an empty frame inside a shard
     b = m.dist.plan_shards(counts, world)
     lo, hi = int(b[rank]), int(b[rank + 1])
+    # this rank's frames: x, y, z, intensity (+ t_ns on odd ranks: a 5-column batch, re-pitched)
     x, y, z, i, t = synth.synth_batch(counts[lo:hi], seed=5, frame_id_base=lo)
-    pts = np.column_stack([x, y, z, i]).astype(np.float64)
-    offs = np.concatenate([[0], np.cumsum(counts[lo:hi])])
-    shard = [pts[offs[k]:offs[k + 1]] for k in range(hi - lo)]
-    aligned = R.align_frames(shard, tr, times[lo:hi])
-    local = R.merge_aligned(aligned) if aligned else np.zeros((0, 4))
-    parts = [None] * world
-    dist.all_gather_object(parts, local)
-    dist.destroy_process_group()
-    if rank == 0:
+    C = 5 if rank % 2 else 4
+    rows = np.column_stack([x, y, z, i, t.astype(np.float32)])[:, :C]
+    flat, P = _blocked(rows, counts[lo:hi], C)
+    # shard sizes to every rank (a gather of two int64 per rank, as mc_comm_gather_batch's all-gather)
+    meta = torch.tensor([P, C], dtype=torch.int64)
+    metas = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(metas, meta)
+    Ps = [int(v[0]) for v in metas]
+    Cs = [int(v[1]) for v in metas]
+    ok = True
+    if rank == root:
+        plan = m.dist.gather_plan(Ps, Cs, sum(Ps), 4, root=root)
+        merged = np.full(sum(Ps) * 4, np.nan, np.float32)
+        stage = np.full(max(plan["stage_values"], 1), np.nan, np.float32)
+        for src in range(world):
+            if src == root or Ps[src] == 0:
+                continue
+            n = Cs[src] * Ps[src]
+            so = plan["stage_offset"][src]
+            dst = stage[so:so + n] if so >= 0 else merged[plan["offset"][src] * 4:plan["offset"][src] * 4 + n]
+            dist.recv(torch.from_numpy(dst), src=src)       # into the plan's place
+        for r in range(world):                              # the root's own shard and the re-pitches
+            if Ps[r] == 0 or (r != root and plan["stage_offset"][r] < 0):
+                continue
+            so = plan["stage_offset"][r]
+            src_vals = flat if r == root else stage[so:so + Cs[r] * Ps[r]]
+            o = plan["offset"][r] * 4
+            merged[o:o + Ps[r] * 4] = src_vals.reshape(Ps[r] // 256, Cs[r], 256)[:, :4].reshape(-1)
+        got = _unblocked(merged, counts, 4)
         x, y, z, i, t = synth.synth_batch(counts, seed=5, frame_id_base=0)
-        allp = np.column_stack([x, y, z, i]).astype(np.float64)
+        frames = np.column_stack([x, y, z, i])
         offs = np.concatenate([[0], np.cumsum(counts)])
-        full = R.merge_aligned(R.align_frames([allp[offs[k]:offs[k + 1]] for k in range(len(counts))], tr, times))
-        q.put(bool(np.array_equal(np.vstack(parts), full)))
-    else:
-        q.put(True)
+        want = np.vstack([frames[offs[f]:offs[f + 1]] for f in range(F)])   # LMC:888, frame order
+        ok = bool(np.array_equal(got, want)) and not np.isnan(merged[:1]).any()
+        ok = ok and any(plan["stage_offset"][r] >= 0 for r in range(world) if Cs[r] != 4 and r != root)
+    elif P > 0:
+        dist.send(torch.from_numpy(flat), dst=root)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, ok))
 
 
-def test_gloo_world2_shard_and_gather_equals_vstack():
+@pytest.mark.parametrize("world,root", [(2, 0), (3, 2), (4, 1)])
+def test_gloo_gather_of_blocked_shards_equals_vstack(world, root):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_gloo_worker, args=(r, world, root, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=300) for _ in ps]
+    res = sorted(q.get(timeout=300) for _ in ps)
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert all(res)
+    assert all(ok for _, ok in res), res
 
 
 def _blocked(rows, counts, C):

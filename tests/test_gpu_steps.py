@@ -1,11 +1,11 @@
-"""GPU: n deskew steps (mc_deskew_steps) give the plain calls' bytes, replayed as one HIP graph or
-pipelined (MC_STEPS_PIPELINE: each step's launch also runs the next step's prep).
+"""GPU: n deskew steps (mc_deskew_steps: each step's launch also runs the next step's prep) give the
+plain calls' bytes.
 
-Every step of the graph recomputes its pose prep and reruns its kernel, so after any number of
-replays the output is bit-identical to one mc_deskew call on the same batch; the oracle check of
-that output is the parity tests' (test_gpu_parity.py).  Here: byte equality with mc_deskew over
-every mode, ragged batches, odd / even step counts, interleaving with plain calls, re-capture when
-the launch arguments change, and the sampled timing events.
+Every step recomputes its pose prep and reruns its kernel, so after any number of steps the output
+is bit-identical to one mc_deskew call on the same batch; the oracle check of that output is the
+parity tests' (test_gpu_parity.py).  Here: byte equality with mc_deskew over every mode, ragged
+batches, odd / even step counts, interleaving with plain calls, new tables between calls, and the
+sampled timing events.
 """
 import numpy as np
 import pytest
@@ -38,25 +38,24 @@ def _cols(b):
     return np.stack(b.download_columns())
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
 @pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
 @pytest.mark.parametrize("n_steps", [1, 2, 7])
-def test_steps_match_plain_calls(mc, gpu_ctx, mode, n_steps, pipeline):
+def test_steps_match_plain_calls(mc, gpu_ctx, mode, n_steps):
     counts = [3000, 0, 1, 257, 20_000, 1023, 4097]
     b, tr, times = _setup(mc, gpu_ctx, counts)
     ref = gpu_ctx.batch(b.counts)
     gpu_ctx.deskew(b, ref, mode=mode)
     want = _cols(ref)
     out = gpu_ctx.batch(b.counts)
-    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode, pipeline=pipeline)
+    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode)
     gpu_ctx.sync()
     assert np.array_equal(_cols(out), want)
-    # again (graph: replay of the cached graph), then interleaved with plain calls on the same tables
+    # again, then interleaved with plain calls on the same tables
     out2 = gpu_ctx.batch(b.counts)
     gpu_ctx.deskew(b, out2, mode=mode)
-    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode, pipeline=pipeline)
+    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode)
     gpu_ctx.deskew(b, out2, mode=mode)
-    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode, pipeline=pipeline)
+    gpu_ctx.deskew_steps(b, out, n_steps, mode=mode)
     gpu_ctx.sync()
     assert np.array_equal(_cols(out), want)
     assert np.array_equal(_cols(out2), want)
@@ -64,16 +63,13 @@ def test_steps_match_plain_calls(mc, gpu_ctx, mode, n_steps, pipeline):
         x.close()
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_steps_oracle_and_recapture_on_new_trajectory(mc, gpu_ctx, pipeline):
-    """A graph replayed after the trajectory grows (new table pointers and sizes) must be re-captured:
-    the output follows the new table (checked against the oracle), not the old graph's.  Pipelined:
-    every step's prep reads the tables current when it runs (nothing carried over from the last call)."""
+def test_steps_oracle_after_new_trajectory(mc, gpu_ctx):
+    """Steps after the trajectory grows (new table pointers and sizes): every step's prep reads the
+    tables current when it runs (nothing carried over from the last call); checked against the oracle."""
     counts = [5000, 5000, 5000]
     b, tr, times = _setup(mc, gpu_ctx, counts, seed=11)
     out = gpu_ctx.batch(b.counts)
-    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp", prepare=True, pipeline=pipeline)   # capture only
-    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp", pipeline=pipeline)
+    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp")
     gpu_ctx.sync()
     first = _cols(out)
     # a longer, shifted trajectory: every point's pose changes
@@ -83,7 +79,7 @@ def test_steps_oracle_and_recapture_on_new_trajectory(mc, gpu_ctx, pipeline):
     rpy2 = np.column_stack([np.interp(t2, tr["time"], tr["orientation_imu"][:, i]) for i in range(3)])
     tr2 = {"time": t2, "position_gps": pos2, "orientation_imu": rpy2}
     gpu_ctx.set_trajectory(t2, pos2, rpy2)
-    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp", pipeline=pipeline)
+    gpu_ctx.deskew_steps(b, out, 4, mode="pose_slerp")
     gpu_ctx.sync()
     got = _cols(out)
     assert not np.array_equal(got, first)
@@ -113,17 +109,17 @@ def test_pipelined_steps_in_place_and_new_frame_times(mc, gpu_ctx, mode):
     c.set_frame_starts((times * 1e9).astype(np.int64))
     for _ in range(3):
         gpu_ctx.deskew(c, c, mode=mode)
-    gpu_ctx.deskew_steps(b, b, 3, mode=mode, pipeline=True)
+    gpu_ctx.deskew_steps(b, b, 3, mode=mode)
     gpu_ctx.sync()
     assert np.array_equal(_cols(b), _cols(c))
     t2 = times + 0.037
     for x in (b, c):
         x.synth(seed=5, frame_id_base=1000)
     out, want = gpu_ctx.batch(b.counts), gpu_ctx.batch(b.counts)
-    gpu_ctx.deskew_steps(b, out, 2, mode=mode, pipeline=True)
+    gpu_ctx.deskew_steps(b, out, 2, mode=mode)
     b.set_frame_times(t2)
     b.set_frame_starts((t2 * 1e9).astype(np.int64))
-    gpu_ctx.deskew_steps(b, out, 2, mode=mode, pipeline=True)
+    gpu_ctx.deskew_steps(b, out, 2, mode=mode)
     gpu_ctx.deskew(b, want, mode=mode)
     gpu_ctx.sync()
     assert np.array_equal(_cols(out), _cols(want))
@@ -135,26 +131,9 @@ def test_pipelined_steps_sampled_timing(mc, gpu_ctx):
     b, _, _ = _setup(mc, gpu_ctx, [20_000] * 8)
     out = gpu_ctx.batch(b.counts)
     gpu_ctx.read_timing()
-    gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp", sample_every=5, pipeline=True)   # steps 2, 7, 12, 17
+    gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp", sample_every=5)   # steps 2, 7, 12, 17
     t = gpu_ctx.read_timing()
     assert t["main_launches"] == 4 and t["main_ms"] > 0
-    gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp", pipeline=True)
-    assert gpu_ctx.read_timing()["main_launches"] == 0
-    out.close()
-    b.close()
-
-
-def test_steps_sampled_timing(mc, gpu_ctx):
-    b, _, _ = _setup(mc, gpu_ctx, [20_000] * 8)
-    out = gpu_ctx.batch(b.counts)
-    gpu_ctx.read_timing()
-    gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp", sample_every=10)   # steps 5 and 15
-    gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp", sample_every=10)
-    t = gpu_ctx.read_timing()
-    assert t["main_launches"] == 4 and t["prep_launches"] == 4
-    assert t["main_ms"] > 0 and t["prep_ms"] > 0
-    assert gpu_ctx.read_timing()["main_launches"] == 0
-    # without sampling nothing is recorded
     gpu_ctx.deskew_steps(b, out, 20, mode="pose_slerp")
     assert gpu_ctx.read_timing()["main_launches"] == 0
     out.close()
@@ -237,7 +216,7 @@ def test_repeated_calls_speculate_and_every_input_change_misses(mc, gpu_ctx, mod
     o2 = ctx.batch(other.counts)
     for k in range(6):
         ctx.deskew(other if k % 2 else b, o2 if k % 2 else out, mode=mode)
-    ctx.deskew_steps(b, out, 3, mode=mode, pipeline=True)
+    ctx.deskew_steps(b, out, 3, mode=mode)
     ctx.deskew(b, out, mode=mode)
     assert np.array_equal(_cols(out), want)
 
@@ -265,7 +244,7 @@ def test_tune_order_keeps_bytes_and_applies_per_size(mc, gpu_ctx, mode):
     out2 = ctx.batch(b.counts)
     ctx.deskew(b, out2, mode=mode)
     assert np.array_equal(_cols(out2), ref)
-    ctx.deskew_steps(b, out2, 3, mode=mode, pipeline=True)
+    ctx.deskew_steps(b, out2, 3, mode=mode)
     assert np.array_equal(_cols(out2), ref)
     with pytest.raises(ValueError):               # in place: repeated launches would compound
         ctx.tune_order(b, b, mode=mode)

@@ -153,3 +153,28 @@ def test_pcd_header_matches_reference_files():
     for case in ("tricky", "random", "empty"):
         pts = g[f"pcd/{case}/points"]
         assert g[f"pcd/{case}/bytes"].tobytes().startswith(m.codecs.pcd_header(len(pts)))
+
+
+def test_rotation_basis_bitwise_equals_scipy():
+    """rot.cpp (mc_rotation_from_euler_xyz, host only) is scipy's Rotation.from_euler('xyz', rpy)
+    .as_matrix() bit for bit (LMC:726, 774): the basis every float64 path uses."""
+    import ctypes
+    from scipy.spatial.transform import Rotation
+    m = pkg()
+    lib = m._lib.load()
+    rng = np.random.default_rng(12)
+    for scale in (1e-6, 0.05, 1.0, np.pi, 40.0):
+        rpy = rng.uniform(-scale, scale, (100_000, 3))
+        rpy[:4] = [[0, 0, 0], [np.pi, 0, 0], [0, np.pi / 2, 0], [-np.pi, -np.pi / 2, np.pi]]
+        R = np.empty((len(rpy), 3, 3))
+        m._lib.check(lib.mc_rotation_from_euler_xyz(len(rpy), rpy.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                                    R.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        ref = Rotation.from_euler("xyz", rpy).as_matrix()
+        assert np.array_equal(R, ref), (scale, int(np.count_nonzero(R != ref)))
+    # the frames of the reference's recorded runs: their poses' orientations
+    for name in ("urban_complex", "parking_detailed", "highway_simple"):
+        rpy = np.ascontiguousarray(golden(f"lmc_traj_{name}.npz")["orientation_imu"])
+        R = np.empty((len(rpy), 3, 3))
+        lib.mc_rotation_from_euler_xyz(len(rpy), rpy.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                       R.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        assert np.array_equal(R, Rotation.from_euler("xyz", rpy).as_matrix()), name

@@ -1,0 +1,84 @@
+"""Which accumulation order numpy's matmul uses for the reference's 3x3 (and 4x4) transforms.
+
+The float64 row kernels (kernels.hpp frame_apply / k_affine_rows_f64, scan.hpp scan_rotate) repeat
+it so that their outputs equal the reference's values bit for bit.  Compiles a tiny C helper with
+gcc into a temp dir and compares, on random data, numpy's
+
+    (R.T @ d.T).T         LMC:728   (scan_environment)
+    (R @ p.T).T + t       LMC:775   (transform_pointcloud)
+    (T @ [p, w].T).T      CSIM:230  (CoordinateTransformer.transform_points)
+
+with three candidate orders per output: plain left-to-right sums, the ascending FMA chain
+fma(a2, x2, fma(a1, x1, a0 * x0)) and the descending one.  Measured in the build container
+(OpenBLAS 0.3.29 Haswell-family dgemm, the box the golden fixtures come from): the ascending chain
+matches every value, the others miss 25-45 %.
+
+    python tools/fma_order.py
+"""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+from scipy.spatial.transform import Rotation
+
+C_SRC = r"""
+#include <math.h>
+#include <stdint.h>
+void chain(const double* A, int K, const double* X, int64_t n, int order, double* o) {
+  for (int64_t r = 0; r < n; ++r)
+    for (int i = 0; i < 3; ++i) {
+      const double* a = A + K * i; const double* x = X + K * r; double s;
+      if (order == 0) { s = a[0] * x[0]; for (int k = 1; k < K; ++k) s = s + a[k] * x[k]; }
+      else if (order == 1) { s = a[0] * x[0]; for (int k = 1; k < K; ++k) s = fma(a[k], x[k], s); }
+      else { s = a[K - 1] * x[K - 1]; for (int k = K - 2; k >= 0; --k) s = fma(a[k], x[k], s); }
+      o[3 * r + i] = s;
+    }
+}
+"""
+
+
+def main():
+    d = tempfile.mkdtemp()
+    src, so = os.path.join(d, "c.c"), os.path.join(d, "c.so")
+    open(src, "w").write(C_SRC)
+    subprocess.run(["gcc", "-O2", "-mfma", "-ffp-contract=off", "-shared", "-fPIC", src, "-o", so, "-lm"], check=True)
+    lib = ctypes.CDLL(so)
+
+    def run(A, X, order):
+        A = np.ascontiguousarray(A)
+        X = np.ascontiguousarray(X)
+        o = np.empty((len(X), 3))
+        lib.chain(ctypes.c_void_p(A.ctypes.data), ctypes.c_int(A.shape[1]), ctypes.c_void_p(X.ctypes.data),
+                  ctypes.c_int64(len(X)), ctypes.c_int(order), ctypes.c_void_p(o.ctypes.data))
+        return o
+
+    rng = np.random.default_rng(0)
+    n = 200_000
+    R = Rotation.from_euler("xyz", rng.uniform(-3, 3, 3)).as_matrix()
+    t = rng.normal(0, 30, 3)
+    d3 = rng.uniform(-100, 100, (n, 3))
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = [5e5, 4.43e6, 3.0]
+    p4 = np.column_stack([d3, rng.uniform(0, 1, n)])
+    cases = {
+        "LMC:728 (R.T @ d.T).T": ((R.T @ d3.T).T, R.T, d3, None),
+        "LMC:775 (R @ p.T).T + t": ((R @ d3.T).T + t, R, d3, t),
+        "CSIM:230 T @ [p, 1]": ((T @ np.column_stack([d3, np.ones(n)]).T).T[:, :3], T[:3], np.column_stack([d3, np.ones(n)]), None),
+        "CSIM:230 T @ [p, w]": ((T @ p4.T).T[:, :3], T[:3], p4, None),
+    }
+    for name, (ref, A, X, add) in cases.items():
+        miss = []
+        for order in range(3):
+            o = run(A, X, order)
+            if add is not None:
+                o = o + add
+            miss.append(int(np.count_nonzero(o != ref)))
+        print(f"{name:28s} values {ref.size}: mismatches plain {miss[0]}, fma ascending {miss[1]}, "
+              f"fma descending {miss[2]}")
+
+
+if __name__ == "__main__":
+    main()

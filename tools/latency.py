@@ -100,51 +100,9 @@ def main():
     out["oracle_transform_pointcloud_us"] = timed(lambda: R.transform_pointcloud(pts, pose), args.calls) * 1e6
     out["reference_ops_transform_pointcloud_us"] = timed(lambda: R.transform_pointcloud_ref_ops(pts, pose),
                                                          args.calls) * 1e6
-    # the opt-in latency server (mc_set_latency_server): no launch / completion signal per call
-    base = sim.transform_pointcloud(pts, pose)
-    info0 = sim.context.latency_server(True)
-    out["latency_server"] = {}
-    try:
-        got = sim.transform_pointcloud(pts, pose)
-        out["latency_server"]["max_abs_diff_vs_launched_kernel"] = float(np.abs(got - base).max())
-        out["latency_server"]["transform_pointcloud_us"] = timed(lambda: sim.transform_pointcloud(pts, pose),
-                                                                 args.calls) * 1e6
-        from ctypes import c_double
-        rot, tra = np.ascontiguousarray(pose["rotation"]), np.ascontiguousarray(pose["translation"])
-        o = np.empty((pts.shape[0], 4))
-        ctx0 = sim.context
-        pt0 = mc._lib.ptr
-
-        def raw():
-            ctx0.lib.mc_transform_pointcloud_f64(ctx0.handle, pt0(pts, c_double), pts.shape[0], 4, pt0(rot, c_double),
-                                                 pt0(tra, c_double), pt0(o, c_double))
-        out["latency_server"]["c_call_only_us"] = timed(raw, args.calls) * 1e6
-        # the Python wrapper alone: the same call into a C no-op with the same argtypes
-        import ctypes
-        noop = ctypes.CDLL(None).labs
-        noop.argtypes = ctx0.lib.mc_transform_pointcloud_f64.argtypes
-        noop.restype = ctypes.c_int
-
-        class _Lib:
-            mc_transform_pointcloud_f64 = noop
-
-        class _Ctx:
-            lib, handle = _Lib(), None
-
-        fake = mc.LiDARMotionSimulator({"duration": 120.0, "trajectory_type": "figure_eight", "lidar_fps": 10},
-                                       context=_Ctx())
-        out["latency_server"]["python_wrapper_only_us"] = timed(lambda: fake.transform_pointcloud(pts, pose),
-                                                                args.calls) * 1e6
-        lat = []
-        for _ in range(5):   # after an idle gap past the server's 50 ms: one relaunch per call
-            time.sleep(0.12)
-            t0 = time.perf_counter()
-            sim.transform_pointcloud(pts, pose)
-            lat.append((time.perf_counter() - t0) * 1e6)
-        out["latency_server"]["after_idle_us"] = lat
-        out["latency_server"]["info"] = sim.context.latency_server_info()
-    finally:
-        sim.context.latency_server(False)
+    # bit-identical to the reference's operation sequence (scipy R, numpy matmul accumulation)
+    out["bitwise_equal_reference_ops"] = bool(np.array_equal(sim.transform_pointcloud(pts, pose),
+                                                              R.transform_pointcloud_ref_ops(pts, pose)))
     tr = sim.add_sensor_noise(sim.generate_trajectory())
     times = sim.lidar_times()[:args.frames]
     scans = [pts] * args.frames
