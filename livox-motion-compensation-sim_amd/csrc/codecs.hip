@@ -46,6 +46,8 @@ int check_frames(int32_t F, const int64_t* counts, std::vector<int64_t>& doff) {
   doff.assign((size_t)F + 1, 0);
   for (int32_t f = 0; f < F; ++f) {
     CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
+    CHECK_ARG(counts[f] < ((int64_t)1 << 31), "frame %d has %lld points (the encoders take < 2^31 per frame)", f,
+              (long long)counts[f]);
     doff[f + 1] = doff[f] + counts[f];
   }
   return MC_OK;
@@ -77,6 +79,7 @@ CodecFrames frames_of(const Source& src, const int64_t* d_doff, const int64_t* d
   cf.unit_off = d_units;
   cf.F = F;
   cf.n_units = n_units;
+  cf.frames_per_unit = n_units > 0 ? (double)F / (double)n_units : 0.0;
   return cf;
 }
 
@@ -168,7 +171,9 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
     if (F > 0)
       hipLaunchKernelGGL(k_lvx_frames, dim3((F + kCodecBlock - 1) / kCodecBlock), dim3(kCodecBlock), 0, c->stream,
                          a, (int64_t)0);
-    if (n_pkg > 0 && a.src.cols && kLvxUnitsPerWG > 1)
+    if (n_pkg > 0 && a.src.cols && MC_LVX_UNITS)
+      hipLaunchKernelGGL(k_lvx_units, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
+    else if (n_pkg > 0 && a.src.cols && kLvxUnitsPerWG > 1)
       hipLaunchKernelGGL(k_lvx_packages_cols, dim3((uint32_t)((n_pkg + kLvxUnitsPerWG - 1) / kLvxUnitsPerWG)),
                          dim3(kCodecBlock), 0, c->stream, a);
     else if (n_pkg > 0)

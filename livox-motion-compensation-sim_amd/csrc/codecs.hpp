@@ -42,6 +42,14 @@ constexpr int kLvxFileHdr = 88;
 constexpr int kLvxPkgPerWG = 8;                                 // one unit = up to this many packages of a frame
 constexpr int kLvxUnitPoints = kLvxPkgPerWG * kLvxPkgPoints;    // 768
 constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment shift
+constexpr int kLvxSlots = kLvxUnitPoints / kCodecBlock;         // 3 batch blocks per unit
+static_assert(kLvxUnitPoints % kCodecBlock == 0, "unit = whole blocks");
+#ifndef MC_LVX_UNITS
+#define MC_LVX_UNITS 1       // batch-source LVX: k_lvx_units (1) or the generic k_lvx_packages (0)
+#endif
+#ifndef MC_PCD_NOBAR
+#define MC_PCD_NOBAR 0       // packed PCD write pass: no barrier after a tile's stores (pcd_tile_store)
+#endif
 #ifndef MC_PCD_TILES_PER_WG
 #define MC_PCD_TILES_PER_WG 4   // 4 / 8 / 16 / 32: 1048.0 / 1023.5 / 1029.2 / 1054.9 us (profiles/round2/s26,
                                 // XCD unit order); in the dealt order 4 wins: write pass 788.0 / 741.0 vs
@@ -51,6 +59,7 @@ constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment s
 constexpr int kPcdTilesPerWG = MC_PCD_TILES_PER_WG;             // PCD tiles of kCodecBlock lines per workgroup
 constexpr int kPcdBlock = 256;   // PCD: threads per workgroup = lines per tile (512: 1088 / 1085 vs 1080 us, profiles/round2/s40)
 constexpr int kPcdTileText = kPcdBlock * 64;                     // LDS text buffer per tile (packed lines <= 52 B)
+constexpr int kPcdPackedText = kPcdBlock * 52 + 16;              // a packed tile's text + its HBM offset mod 16
 
 struct CodecFrames {
   const double* aos; int64_t ld;   // (N, ld) float64 AoS source, or
@@ -60,6 +69,7 @@ struct CodecFrames {
   const int64_t* unit_off;   // [F+1] prefix of per-frame units
   int32_t F;
   int64_t n_units;           // unit_off[F]
+  double frames_per_unit;    // F / n_units (the frame guess of codec_frame_guess without a division)
 };
 
 // frame owning unit u: last f with unit_off[f] <= u (frames without units are skipped over).
@@ -78,6 +88,15 @@ __device__ __forceinline__ int32_t codec_frame_of(const CodecFrames& s, int64_t 
     if (ldu(unit_off + mid) <= u) lo = mid + 1; else hi = mid;
   }
   return lo - 1;
+}
+
+// codec_frame_of with the interpolation guess from a host-computed ratio (one FMA-rate multiply
+// instead of a 64-bit integer division on the scalar unit), the binary search when it misses
+__device__ __forceinline__ int32_t codec_frame_guess(const CodecFrames& s, int64_t u) {
+  int64_t g = (int64_t)((double)u * s.frames_per_unit);
+  g = g < s.F - 1 ? g : s.F - 1;
+  if (ldu(s.unit_off + g) <= u && u < ldu(s.unit_off + g + 1)) return (int32_t)g;
+  return codec_frame_of(s, u);
 }
 
 // columns 0..3 of dense row `row` (frame f) as float64; ld == 3 leaves c[3] = 0.  A batch source
@@ -202,14 +221,82 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
 }
 
+// Batch source, one unit per workgroup (MC_LVX_UNITS=1): the unit's frame from codec_frame_guess and
+// every per-unit quantity in 32-bit scalar arithmetic (frames < 2^31 points, checked by the host); the
+// unit's 3 blocks loaded under workgroup-uniform guards (no divergent load branches), each lane's
+// records formed branch-free (a NaN only sets a flag, stored once per lane: the per-value error
+// branches and their stores were most of the old kernel's 689 scalar instructions); padding slots and
+// slots past the unit's packages are written too — as zero records inside the LDS buffer, outside
+// the stored piece where no package exists.
+__global__ __launch_bounds__(kCodecBlock) void k_lvx_units(const LvxArgs a) {
+  __shared__ uint4 s_buf[kLvxLds / 16 + 1];
+  uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
+  const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
+  const int32_t f = codec_frame_guess(a.src, u);
+  const uint32_t fcount = (uint32_t)(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f));
+  const uint32_t ui = (uint32_t)(u - ldu(a.src.unit_off + f));
+  const uint32_t pkg0 = ui * kLvxPkgPerWG;
+  const uint32_t fpkgs = (fcount + kLvxPkgPoints - 1) / kLvxPkgPoints;
+  const int k = (int)min(fpkgs - pkg0, (uint32_t)kLvxPkgPerWG);
+  const int n = (int)min(fcount - pkg0 * kLvxPkgPoints, (uint32_t)(k * kLvxPkgPoints));
+  const int64_t S = ldu(a.frame_pos + f) + kLvxFrameHdr + (int64_t)pkg0 * kLvxPkg;   // even
+  const int shift = (int)(S & 15);
+  const uint64_t ts = ldu(a.ts_ns + f);
+  const bool hi = a.has_int ? a.has_int[f] != 0 : true;
+  const float* q0 = a.src.cols + ((ldu(a.src.poff + f) >> 8) + 3 * (int64_t)ui) * a.src.C * kBlkPts + threadIdx.x;
+  // all 12 loads back to back: block j of a short unit re-reads the unit's last block (results unused)
+  const int jl = (n - 1) / kCodecBlock;
+  float v[kLvxSlots][4];
+#pragma unroll
+  for (int j = 0; j < kLvxSlots; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[j][c] = q0[((j < jl ? j : jl) * a.src.C + c) * kBlkPts];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < kLvxSlots; ++j) {
+    const int i = j * kCodecBlock + (int)threadIdx.x;
+    const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
+    uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
+    const bool ok = i < n;
+    // int(np.clip(v * 1000, ...)) (LMC:259-261): the float32 value times 1000 is exact in float64
+    uint32_t w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double sc = (double)v[j][c] * (c < 3 ? 1000.0 : 255.0);
+      bad |= ok && sc != sc;
+      w[c] = (uint32_t)(int32_t)(c < 3 ? fmin(fmax(sc, -2147483648.0), 2147483647.0) : fmin(fmax(sc, 0.0), 255.0));
+    }
+    const uint32_t refl = hi ? w[3] : 128u;   // tag byte 0 (LMC:268)
+    const uint32_t x = ok ? w[0] : 0u, y = ok ? w[1] : 0u, z = ok ? w[2] : 0u, rt = ok ? refl : 0u;
+    r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
+    r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
+    r[4] = (uint16_t)z; r[5] = (uint16_t)(z >> 16);
+    r[6] = (uint16_t)rt;
+  }
+  if ((int)threadIdx.x < k * (kLvxPkgHdr / 2)) {   // k * 11 <= 88 header halfwords
+    const int h = threadIdx.x, pk = h / (kLvxPkgHdr / 2), wd = h - pk * (kLvxPkgHdr / 2);
+    uint32_t hv;
+    switch (wd) {
+      case 0: hv = 0x0500u; break;
+      case 1: hv = 0x0100u; break;
+      case 4: hv = 0x0100u; break;
+      case 5: hv = 0x0002u; break;
+      case 7: case 8: case 9: case 10: hv = (uint32_t)(ts >> (16 * (wd - 7))) & 0xffffu; break;
+      default: hv = 0u;
+    }
+    s16[((shift + pk * kLvxPkg) >> 1) + wd] = (uint16_t)hv;
+  }
+  if (bad) *a.err = 1;
+  __syncthreads();
+  codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
+}
+
 // Batch source.  The loop takes kLvxUnitsPerWG consecutive units per workgroup, unit j + 1's meta
 // data and point values loaded while unit j is assembled and stored (two LDS buffers, one barrier per
 // unit); one unit per workgroup ships (2 / 4 / 8: 305.0 / 306.6 vs 333.9 / 338.5, 356.3 / 356.4 us in
 // the dealt order, profiles/round3/s69).  A unit's first row is a multiple of 768 = 3 blocks into its
 // frame, so thread t's slot j is row t of the unit's block j.
 constexpr int kLvxUnitsPerWG = 1;
-constexpr int kLvxSlots = kLvxUnitPoints / kCodecBlock;   // 3
-static_assert(kLvxUnitPoints % kCodecBlock == 0 && kCodecBlock == kBlkPts, "unit = whole blocks");
 
 struct LvxUnit {
   int64_t S;     // file offset of the unit's first package
@@ -930,13 +1017,16 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
 #pragma clang loop vectorize(disable) unroll(disable)
     for (; b < e; ++b) g[b] = lds[b];
   }
-  __syncthreads();   // s_wave / s_text are reused by the next tile
+  // s_wave / s_text are reused by the next tile, but only after its scan's barrier, which every lane
+  // reaches after these LDS reads (__syncthreads waits for them); s_wave was read before this tile's
+  // text barrier.  MC_PCD_NOBAR drops this barrier.
+  if (!MC_PCD_NOBAR) __syncthreads();
 }
 
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
-  __shared__ uint4 s_text4[kPcdTileText / 16 + 1];
+  __shared__ uint4 s_text4[kPcdPackedText / 16 + 1];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {

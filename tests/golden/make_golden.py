@@ -135,6 +135,14 @@ def make_kat(lmc):
         out[f"r{i}"] = np.array(r)
         out[f"out{i}"] = sim.transform_pointcloud(pts, {"translation": np.array(t), "rotation": np.array(r)})
     out["empty_out"] = sim.transform_pointcloud(np.zeros((0, 4)), {"translation": np.zeros(3), "rotation": np.zeros(3)})
+    # one frame above the zero-copy size (the library's DMA row pipeline path), highway-scale pose
+    # (points regenerated by the test from this seed; the output's sha256 and every 1000th row kept)
+    import hashlib
+    brng = np.random.default_rng(2024)
+    big = np.column_stack([brng.uniform(-90, 90, (40_000, 3)), brng.uniform(0, 1, 40_000)])
+    bo = sim.transform_pointcloud(big, {"translation": np.array(cases[3][0]), "rotation": np.array(cases[3][1])})
+    out["big/sha256"] = np.frombuffer(hashlib.sha256(np.ascontiguousarray(bo).tobytes()).digest(), np.uint8)
+    out["big/rows"] = bo[::1000]
     out["n_cases"] = np.int64(len(cases))
     np.savez_compressed(os.path.join(HERE, "lmc_kat.npz"), **out)
 
@@ -443,7 +451,7 @@ def make_run_files(lmc):
 
 def main():
     lmc, csim = import_reference()
-    one = {"run_files": lambda: make_run_files(lmc), "coords": lambda: make_coords(csim)}
+    one = {"run_files": lambda: make_run_files(lmc), "coords": lambda: make_coords(csim), "kat": lambda: make_kat(lmc)}
     if sys.argv[1:2] and sys.argv[1] in one:   # one fixture only (the others are unchanged by it)
         one[sys.argv[1]]()
         return

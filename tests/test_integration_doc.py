@@ -33,6 +33,7 @@ def test_stub_matches_reference_known_answers():
         out = ns["transform_pointcloud"](None, pts, {"translation": g[f"t{i}"], "rotation": g[f"r{i}"]})
         assert out.shape == (len(pts), 4) and out.dtype == np.float64
         assert_scaled_close(out[:, :3], g[f"out{i}"][:, :3], scale_of(pts[:, :3], g[f"t{i}"]))
+        assert np.array_equal(out, g[f"out{i}"])   # the reference's float64 values, bit for bit
     assert ns["transform_pointcloud"](None, np.zeros((0, 4)), {"translation": np.zeros(3),
                                                               "rotation": np.zeros(3)}).shape == (0, 4)
     with pytest.raises(IndexError):
