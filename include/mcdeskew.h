@@ -164,7 +164,7 @@ int mc_scan_emit(mc_ctx* ctx, mc_batch* out, const double* noise);
  * (may be NULL) the frame loop's transform_pointcloud of it with the same pose (LMC:826-831), as
  * device (N, 4) float64 rows, frames back to back (N = sum of counts_out).  Bit-identical to the
  * reference's values: the pose's R is scipy's (mc_rotation_from_euler_xyz) and every product sum
- * accumulates as numpy's matmul does (DESIGN.md §5).  Synchronous. */
+ * accumulates as numpy's matmul does (DESIGN.md §4).  Synchronous. */
 int mc_scan_emit_f64(mc_ctx* ctx, const double* noise, double* d_local, double* d_aligned);
 int mc_timing_read_scan(mc_ctx* ctx, double* ms_total, int64_t* launches);
 

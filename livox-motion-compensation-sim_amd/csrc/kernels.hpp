@@ -28,7 +28,7 @@
 namespace mc {
 
 // Shipping configuration.  The A/B history of every choice below (and of the arms that lost) is in
-// DESIGN.md §4 / §9 and profiles/; the kernels carry only the configuration that ships.
+// profiles/HISTORY_r1-r4.md and profiles/; the kernels carry only the configuration that ships.
 //   * output stores: sc1 write-through (st_pol<2>) in the frame, SLERP and IMU kernels — SLERP +7 %
 //     vs nt; IMU 327.8-330.1 vs 337.9-343.9 us with sc1 nt (profiles/round3/s46); frame 298.2-298.9
 //     vs 300.3-301.3 us with sc1 nt (s48);
@@ -1699,7 +1699,7 @@ __device__ __forceinline__ int64_t local_index(const LayoutArgs& a, const Tile& 
 // through a 4 KB LDS tile; non-temporal loads and stores (st_pol<1>).  Bare streams of these lane
 // shapes: 6.11 TB/s (16 B in / 32 B out, 1 / 2 per lane) vs 5.22-5.34 with a 2048-point tile's 8 / 16
 // per lane; 6.42 TB/s (32 B in / 16 B out, 2 / 1) (tools/stage_probe.hip, profiles/round2/s07).
-// Rejected: 2048-point LDS tiles (71 / 75 % of peak), register-only quad transposes
+// Rejected (profiles/HISTORY_r1-r4.md §4, §9): 2048-point LDS tiles (71 / 75 % of peak), register-only quad transposes
 // (16-byte holes in every row-side store, profiles/round2/s11-s12), 2 / 4 units per workgroup pass
 // (profiles/round3/s09), sc1 / sc1 nt stores (s31), the dealt unit order (s57).
 typedef double v2d __attribute__((ext_vector_type(2)));

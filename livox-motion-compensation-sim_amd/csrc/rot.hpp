@@ -11,7 +11,7 @@
 //
 // With that R, the float64 row kernels reproduce numpy's matmul accumulation (an ascending FMA
 // chain per output, then the translation added separately) and their outputs equal the
-// reference's float64 values exactly.
+// reference's float64 values exactly ("Float64 rows").
 #pragma once
 #include <cstdint>
 

@@ -241,7 +241,7 @@ class LiDARMotionSimulator:
     def run_simulation(self, environment):
         """LMC:778-858 given the scene: trajectory + sensor noise (LMC:784-785, global RNG), then
         simulate_frames over the lidar time grid.  Scene synthesis (LMC:430-699) is not provided
-        (DESIGN.md §6): pass the environment array."""
+        (DESIGN.md §1): pass the environment array."""
         trajectory = self.add_sensor_noise(self.generate_trajectory())
         return self.simulate_frames(environment, trajectory, self.lidar_times())
 

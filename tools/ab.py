@@ -64,7 +64,7 @@ def main():
                          "the first arm's (variants that must not change results)")
     ap.add_argument("--replicas", type=int, default=1,
                     help="independent allocations (contexts) per library: where a batch's pages land moves a "
-                         "kernel by up to ~10 %% (DESIGN.md section 8), so a variant is judged by the median "
+                         "kernel by up to ~10 %% (profiles/HISTORY_r1-r4.md section 8), so a variant is judged by the median "
                          "over its replicas")
     args = ap.parse_args()
     base_libs = [l for l in args.libs.split(",") if l]

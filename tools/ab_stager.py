@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--replicas", type=int, default=1,
                     help="independent buffer sets per library, allocated alternately (page placement "
-                         "moves streaming kernels by several percent, DESIGN.md section 8)")
+                         "moves streaming kernels by several percent, profiles/HISTORY_r1-r4.md section 8)")
     args = ap.parse_args()
     libs = [l for l in args.libs.split(",") if l]
     counts = np.full(args.frames, args.points, np.int64)

@@ -1,4 +1,4 @@
-"""Placement study: identical frame-mode kernels on R independent allocations of the
+"""Placement study (profiles/HISTORY_r1-r4.md §8): identical frame-mode kernels on R independent allocations of the
 same 600 x 100k workload ("replicas") run at two distinct speeds.  Each replica runs K kernels in
 turn (replica 0 x K, replica 1 x K, ...), so under ``rocprofv3 --pmc`` dispatch order maps a
 counter row to its replica; HIP events give each replica's kernel time in the same run.
