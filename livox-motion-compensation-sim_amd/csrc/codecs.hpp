@@ -69,16 +69,24 @@ struct CodecFrames {
   const int64_t* unit_off;   // [F+1] prefix of per-frame units
   int32_t F;
   int64_t n_units;           // unit_off[F]
-  double frames_per_unit;    // F / n_units (the frame guess of codec_frame_guess without a division)
+  double frames_per_unit;    // F / n_units (codec_frame_of's guess without an integer division)
 };
 
 // frame owning unit u: last f with unit_off[f] <= u (frames without units are skipped over).
 // First the interpolation guess u * F / n_units with its two bounds (one round of loads when the
-// frames are of similar size), the binary search (~log2 F dependent loads) otherwise.
+// frames are of similar size), the binary search (~log2 F dependent loads) otherwise.  The guess
+// multiplies by the host's F / n_units in float64 (MC_CODEC_GUESS_F64): the integer quotient was a
+// 64-bit division on the scalar unit, ~130 dependent instructions at the head of every workgroup.
+#ifndef MC_CODEC_GUESS_F64
+#define MC_CODEC_GUESS_F64 1
+#endif
 __device__ __forceinline__ int32_t codec_frame_of(const CodecFrames& s, int64_t u) {
   const int64_t* __restrict__ unit_off = s.unit_off;
   if (s.n_units > 0) {
-    int64_t g = u * s.F / s.n_units;   // u < 2^31 and F < 2^31: no overflow
+    // (+1e-6: u * ratio rounds to within 2^-21 of the exact quotient, which is an integer at every
+    // frame's first unit when the frames are equal)
+    int64_t g = MC_CODEC_GUESS_F64 ? (int64_t)((double)u * s.frames_per_unit + 1e-6)
+                                   : u * s.F / s.n_units;   // u < 2^31 and F < 2^31: no overflow
     g = g < s.F - 1 ? g : s.F - 1;
     if (ldu(unit_off + g) <= u && u < ldu(unit_off + g + 1)) return (int32_t)g;
   }
@@ -88,15 +96,6 @@ __device__ __forceinline__ int32_t codec_frame_of(const CodecFrames& s, int64_t 
     if (ldu(unit_off + mid) <= u) lo = mid + 1; else hi = mid;
   }
   return lo - 1;
-}
-
-// codec_frame_of with the interpolation guess from a host-computed ratio (one FMA-rate multiply
-// instead of a 64-bit integer division on the scalar unit), the binary search when it misses
-__device__ __forceinline__ int32_t codec_frame_guess(const CodecFrames& s, int64_t u) {
-  int64_t g = (int64_t)((double)u * s.frames_per_unit);
-  g = g < s.F - 1 ? g : s.F - 1;
-  if (ldu(s.unit_off + g) <= u && u < ldu(s.unit_off + g + 1)) return (int32_t)g;
-  return codec_frame_of(s, u);
 }
 
 // columns 0..3 of dense row `row` (frame f) as float64; ld == 3 leaves c[3] = 0.  A batch source
@@ -221,7 +220,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
 }
 
-// Batch source, one unit per workgroup (MC_LVX_UNITS=1): the unit's frame from codec_frame_guess and
+// Batch source, one unit per workgroup (MC_LVX_UNITS=1): the unit's frame from codec_frame_of and
 // every per-unit quantity in 32-bit scalar arithmetic (frames < 2^31 points, checked by the host); the
 // unit's 3 blocks loaded under workgroup-uniform guards (no divergent load branches), each lane's
 // records formed branch-free (a NaN only sets a flag, stored once per lane: the per-value error
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_units(const LvxArgs a) {
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
   const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
-  const int32_t f = codec_frame_guess(a.src, u);
+  const int32_t f = codec_frame_of(a.src, u);
   const uint32_t fcount = (uint32_t)(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f));
   const uint32_t ui = (uint32_t)(u - ldu(a.src.unit_off + f));
   const uint32_t pkg0 = ui * kLvxPkgPerWG;

@@ -144,10 +144,30 @@ def test_batch_source_encoders_match_f64_source(mc, gpu_ctx, with_time):
     lvx = mc.codecs.encode_lvx_batch(b2, ids, ts)
     assert lvx == mc.codecs.encode_lvx([{"frame_id": i, "timestamp": t, "points": h}
                                         for i, t, h in zip(ids, ts, h2)], gpu_ctx)
+    # clipping (LMC:259-261, 268): coordinates past +-2^31 mm, intensities outside [0, 1]; frames of
+    # 1 / 767 / 768 / 769 / 1537 points (k_lvx_units: a unit is 768 points = 3 blocks)
+    cc = np.array([767, 1, 768, 769, 1537], np.int64)
+    m = int(cc.sum())
+    clip = np.column_stack([rng.normal(0, 40, (m, 3)), rng.uniform(-0.3, 1.3, m)])
+    clip[::7, 0] = 3e6
+    clip[::11, 1] = -3e6
+    clip[::13, 2] = 2147483.5
+    b3 = gpu_ctx.batch(cc, with_time=with_time)
+    b3.upload_aos(clip)
+    h3 = b3.split(b3.download_aos())
+    ids3, ts3 = np.arange(5) + 7, np.arange(5) * 0.1 + 3.0
+    assert mc.codecs.encode_lvx_batch(b3, ids3, ts3) == mc.codecs.encode_lvx(
+        [{"frame_id": i, "timestamp": t, "points": h} for i, t, h in zip(ids3, ts3, h3)], gpu_ctx)
     nan = gpu_ctx.batch([3])
     nan.upload_aos(np.array([[1.0, np.nan, 0, 0.5], [0, 0, 0, 0], [1, 1, 1, 1]]))
     with pytest.raises(ValueError):                 # the reference's int(nan) (LMC:259)
         mc.codecs.encode_lvx_batch(nan, [0], [0.0])
+    nan2 = gpu_ctx.batch([800])                     # a NaN intensity in the second unit
+    v = np.column_stack([rng.normal(0, 10, (800, 3)), rng.uniform(0, 1, 800)])
+    v[790, 3] = np.nan
+    nan2.upload_aos(v)
+    with pytest.raises(ValueError):
+        mc.codecs.encode_lvx_batch(nan2, [0], [0.0])
 
 
 def test_simulator_save_lvx_and_pcd(mc, gpu_ctx, tmp_path):

@@ -72,12 +72,13 @@ def main():
     alg = {
         "k_soa_to_aos": 48 * n, "k_aos_to_soa": 48 * n,
         "k_lvx_packages": 16 * n + int(pos[-1]) - 88 - 24 * args.frames,
+        "k_lvx_units": 16 * n + int(pos[-1]) - 88 - 24 * args.frames,
         "k_pcd_measure": 16 * n, "k_pcd_write": 16 * n + int(bpos[-1]),
         # scene x, y, z once + the poses once + the visibility words + the per-(tile, frame) counts
         "k_scan_count": 24 * E + poses + bits + 4 * tiles * Fp,
-        # ... + the offsets (8 B) + per-frame visible counts, and per emitted point its float32
-        # intensity (4 B) and its output row (16 B)
-        "k_scan_emit": 24 * E + poses + bits + 8 * tiles * Fp + 8 * F + 20 * n_out,
+        # ... + the offsets (8 B) + per-frame visible counts, and per emitted point its float64
+        # intensity (8 B) and its float32 output row (16 B)
+        "k_scan_emit": 24 * E + poses + bits + 8 * tiles * Fp + 8 * F + 24 * n_out,
     }
     print(json.dumps({"algorithmic_bytes_per_launch": alg, "points": n, "scene": E, "frames_scanned": len(times),
                       "note": "scan kernels: the scene (24 B/pt of x,y,z columns) and the frame poses (96 B) "
