@@ -333,7 +333,10 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   const dim3 grid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
+    if (a.src.cols && MC_PCD_PC)
+      hipLaunchKernelGGL(k_pcd_write_pc, dim3((uint32_t)((n_tiles + kPcdPcTiles - 1) / kPcdPcTiles)),
+                         dim3(2 * kPcdBlock), 0, c->stream, a);
+    else if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
     else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kPcdBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());

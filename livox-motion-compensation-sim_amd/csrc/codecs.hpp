@@ -47,6 +47,9 @@ static_assert(kLvxUnitPoints % kCodecBlock == 0, "unit = whole blocks");
 #ifndef MC_LVX_UNITS
 #define MC_LVX_UNITS 1       // batch-source LVX: k_lvx_units (1) or the generic k_lvx_packages (0)
 #endif
+#ifndef MC_PCD_MEASURE_SCALAR
+#define MC_PCD_MEASURE_SCALAR 1   // float32 measure pass: wave-uniform tile arithmetic (scalar), DPP wave sum
+#endif
 #ifndef MC_PCD_NOBAR
 #define MC_PCD_NOBAR 0       // packed PCD write pass: no barrier after a tile's stores (pcd_tile_store)
 #endif
@@ -888,12 +891,17 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
   static_assert(kPcdMeasureTiles % (kPcdBlock / 64) == 0, "whole tiles per wave");
   constexpr int NT = kPcdMeasureWaveTiles;
   const int lane = threadIdx.x & 63;
+  // the wave index as a scalar: the tile, its frame and its offsets are then wave-uniform — scalar
+  // loads and branches instead of vector loads of the frame tables and a divergent frame search
+  // ahead of the point loads (MC_PCD_MEASURE_SCALAR)
+  const int wave = MC_PCD_MEASURE_SCALAR ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))
+                                         : (int)(threadIdx.x >> 6);
   int32_t f = codec_frame_of(a.src, u0);
   int left[NT];   // lines of the tile at and after this lane's first (frame-relative, may be <= 0)
   float4 V[NT][4];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    const int64_t u = u0 + (threadIdx.x >> 6) * NT + j;   // a wave's tiles are consecutive
+    const int64_t u = u0 + wave * NT + j;   // a wave's tiles are consecutive
     left[j] = 0;
     if (u < a.src.n_units) {
       // tile u = block (poff_f + 256 (u - unit_off_f)) / 256: a wave-uniform base (scalar arithmetic)
@@ -902,29 +910,32 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
       const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
       left[j] = (int)min_i64(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock) - 4 * lane;
       const float* q = a.src.cols + blk * a.src.C * kBlkPts + 4 * lane;
-      if (left[j] > 0) {
+      // the whole block is allocated (frames are padded to blocks): every lane loads, results past
+      // the frame's end are ignored below
 #pragma unroll
-        for (int c = 0; c < 4; ++c) V[j][c] = *reinterpret_cast<const float4*>(q + c * kBlkPts);
-      }
+      for (int c = 0; c < 4; ++c) V[j][c] = *reinterpret_cast<const float4*>(q + c * kBlkPts);
     }
   }
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    const int64_t u = u0 + (threadIdx.x >> 6) * NT + j;
+    const int64_t u = u0 + wave * NT + j;
     if (u >= a.src.n_units) break;   // wave-uniform
     int v = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (i < left[j]) {
-        const float c[4] = {f4g(V[j][0], i), f4g(V[j][1], i), f4g(V[j][2], i), f4g(V[j][3], i)};
-        const int l = pcd_fast_len_f32(c);
-        // a line outside the packed path flags the tile; its exact bytes come from
-        // k_pcd_measure_list (the byte formatter would double this kernel's registers)
-        v += l < 0 ? (1 << 20) : l;
-      }
+      const float c[4] = {f4g(V[j][0], i), f4g(V[j][1], i), f4g(V[j][2], i), f4g(V[j][3], i)};
+      const int l = pcd_fast_len_f32(c);
+      // a line outside the packed path flags the tile; its exact bytes come from
+      // k_pcd_measure_list (the byte formatter would double this kernel's registers)
+      v += i < left[j] ? (l < 0 ? (1 << 20) : l) : 0;
     }
+    // wave sum by DPP (the shuffle loop compiled to six ds_bpermute round trips)
+    if (MC_PCD_MEASURE_SCALAR) {
+      v = __builtin_amdgcn_readlane(wave_scan_incl(v), 63);
+    } else {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    }
     if (lane == 0) a.tile_bytes[u] = pcd_tile_word(v);
   }
 }
@@ -1048,10 +1059,10 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
       const int left = (int)min_i64(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock);
       vn = (int)threadIdx.x < left;
+      // the tile's block is allocated whole: every lane loads (no branch around the loads), a lane
+      // past the frame's end formats a value it never emits
       const float* q = a.src.cols + blk * a.src.C * kBlkPts + threadIdx.x;
-      if (vn) {
-        cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
-      }
+      cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
       flag_n = ldu(a.tile_bytes + u);
       gn = ldu(a.tile_pos + u);
     };
@@ -1095,6 +1106,109 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       const int64_t G = ldu(a.tile_pos + u);
       const int total = pcd_tile_text(T, valid, G, s_wave, s_text4);
       pcd_tile_store(a, G, total, s_text4);
+    }
+  }
+}
+
+// Float32 source, producer / consumer (MC_PCD_PC=1): a workgroup of 8 waves in two roles.  Waves
+// 0-3 (producers) load, convert and scan a tile's lines and write its text into one of two LDS
+// buffers; waves 4-7 (consumers) copy the previous tile's buffer to HBM meanwhile.  A producer wave
+// then never issues a global store and a consumer wave never a load, so no wave's wait for its
+// next tile's loads also waits for its own stores (vmcnt counts both on CDNA; in k_pcd_write every
+// tile's load consumption waits for the previous tile's stores to complete).  Two barriers per tile:
+// the producers' scan exchange and the hand-over; the consumers take part in both.
+//   buffer b = tile parity: producers write buffer b of tile u after barrier 1 of tile u; the
+//   consumers' reads of tile u - 2 (same buffer) ended before they reached barrier 1 of tile u - 1.
+#ifndef MC_PCD_PC
+#define MC_PCD_PC 0
+#endif
+#ifndef MC_PCD_PC_TILES
+#define MC_PCD_PC_TILES 8    // tiles per producer / consumer workgroup (pipeline fill and drain per workgroup)
+#endif
+constexpr int kPcdPcTiles = MC_PCD_PC_TILES;
+__global__ __launch_bounds__(2 * kPcdBlock) void k_pcd_write_pc(const PcdArgs a) {
+  __shared__ int s_wave[kPcdBlock / 64];
+  __shared__ uint4 s_text[2][kPcdPackedText / 16 + 1];
+  __shared__ int64_t s_G[2];
+  __shared__ int s_total[2];
+  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdPcTiles;   // grid = units exactly
+  const int64_t u_end = u0 + kPcdPcTiles < a.src.n_units ? u0 + kPcdPcTiles : a.src.n_units;
+  const int tid = (int)threadIdx.x & (kPcdBlock - 1);
+  if (threadIdx.x < kPcdBlock) {
+    // producers: k_pcd_write<true>'s fetch / convert, one tile ahead
+    int32_t f = codec_frame_of(a.src, u0);
+    float cn[4] = {0.f, 0.f, 0.f, 0.f};
+    bool vn = false;
+    int32_t flag_n = 0;
+    int64_t gn = 0;
+    PcdText Tn;
+    auto fetch = [&](int64_t u) {
+      f = codec_advance(a.src.unit_off, f, u);
+      const int64_t k = u - ldu(a.src.unit_off + f);
+      const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
+      const int left = (int)min_i64(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock);
+      vn = tid < left;
+      const float* q = a.src.cols + blk * a.src.C * kBlkPts + tid;
+      cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
+      flag_n = ldu(a.tile_bytes + u);
+      gn = ldu(a.tile_pos + u);
+    };
+    auto convert = [&]() {
+      PcdFast P;
+      pcd_fast_vals_packed(cn, P);
+      pcd_text(P, Tn);
+      if (!vn) Tn.len = 0;
+    };
+    if (u0 < u_end) fetch(u0);
+    convert();
+    for (int64_t u = u0; u < u_end; ++u) {
+      const int b = (int)((u - u0) & 1);
+      const PcdText T = Tn;
+      const bool valid = vn;
+      const bool packed = !(flag_n & kPcdSlowTile);   // workgroup-uniform
+      const int64_t G = gn;
+      if (u + 1 < u_end) fetch(u + 1);
+      int total = 0;
+      if (packed) {
+        const int excl = block_scan(T.len, s_wave, total) - T.len;   // barrier 1
+        if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text[b]), (int)(G & 15) + excl);
+      } else {
+        __syncthreads();                                               // barrier 1
+      }
+      if (tid == 0) { s_G[b] = G; s_total[b] = packed ? total : -1; }
+      convert();
+      __syncthreads();                                                 // barrier 2: hand-over
+    }
+  } else {
+    // consumers: tile u's text to HBM once the producers hand it over
+    for (int64_t u = u0; u < u_end; ++u) {
+      const int b = (int)((u - u0) & 1);
+      __syncthreads();                                                 // barrier 1
+      __syncthreads();                                                 // barrier 2
+      const int total = s_total[b];
+      if (total < 0) continue;                                         // byte-path tile
+      const int64_t G = s_G[b];
+      const int lo = (int)(G & 15), hi = lo + total;
+      char* const g = a.out + (G - lo);
+      const uint4* const t4 = s_text[b];
+      const char* const lds = reinterpret_cast<const char*>(t4);
+      const int f0 = (lo + 15) >> 4, f1 = hi >> 4;
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      for (int c = f0 + tid; c < f1; c += kPcdBlock) {
+        const uint4 v = t4[c];
+        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + 16 * c));
+      }
+      if (tid < 2) {
+        int bb = lo, e = hi;
+        if (f0 <= f1) {
+          if (tid == 0) e = 16 * f0;
+          else bb = 16 * f1;
+        } else if (tid == 1) {
+          e = bb;
+        }
+#pragma clang loop vectorize(disable) unroll(disable)
+        for (; bb < e; ++bb) g[bb] = lds[bb];
+      }
     }
   }
 }
