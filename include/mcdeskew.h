@@ -278,9 +278,12 @@ int mc_transform_affine(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int32_t 
 /* The same on the caller's float64 rows, bit-identical to the reference (numpy's accumulation of
  * (T @ points_h.T).T, CSIM:230): rows (N, ld) with ld 3 (w = 1, CSIM:223-225) or 4 (the 4th column is
  * w, CSIM:227), frames back to back (counts[f] rows); mats = 3x4 [A | b] row-major, 1 or n_frames of
- * them; out (N, 3) float64 (CSIM:233).  Synchronous. */
+ * them; out (N, 3) float64 (CSIM:233).  A frame is one transform_points call: numpy sums a one-row
+ * call (a matrix-vector product) in another order than a larger one, and both are repeated.  per_row
+ * != 0 treats every row as its own call — _transform_coordinates' per-point loop (CSIM:2117-2141).
+ * Synchronous. */
 int mc_affine_rows_f64(mc_ctx* ctx, int32_t n_frames, const int64_t* counts, const double* rows, int64_t ld,
-                       int32_t n_mats, const double* mats, double* out);
+                       int32_t n_mats, const double* mats, int per_row, double* out);
 
 /* HIP-event timing of the hot kernels (main deskew kernel and the pose-prep kernel) */
 int mc_timing_enable(mc_ctx* ctx, int enable);

@@ -98,7 +98,7 @@ _SIGS = {
     "mc_transform_affine": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, _pd, c_int]),
     "mc_transform_pointcloud_f64": (c_int, [c_void_p, _pd, c_int64, c_int64, _pd, _pd, _pd]),
     "mc_rotation_from_euler_xyz": (c_int, [c_int64, _pd, _pd]),
-    "mc_affine_rows_f64": (c_int, [c_void_p, c_int32, _pi64, _pd, c_int64, c_int32, _pd, _pd]),
+    "mc_affine_rows_f64": (c_int, [c_void_p, c_int32, _pi64, _pd, c_int64, c_int32, _pd, c_int, _pd]),
     "mc_deskew_points_f64": (c_int, [c_void_p, c_int, c_int32, _pi64, _pd, c_int64, _pi64, _pd, _pi64, _pd]),
     # frames / outs: arrays of row pointers (passed as the address of a uintp array)
     "mc_align_frames_host_f64": (c_int, [c_void_p, c_int32, c_void_p, _pi64, _pi64, _pd, c_int, c_void_p]),

@@ -108,11 +108,14 @@ class CoordinateTransformer:
         return transform_arrays(frames, T, context=self.context)
 
 
-def transform_arrays(frames: Sequence[np.ndarray], T, context: Context | None = None) -> List[np.ndarray]:
+def transform_arrays(frames: Sequence[np.ndarray], T, context: Context | None = None,
+                     per_point: bool = False) -> List[np.ndarray]:
     """T @ [p, 1] (or T @ p for (N,4) homogeneous rows) for every cloud; one matrix for all, or one
     per cloud ((F,4,4) / (F,3,4)).  Returns (N_i, 3) float64 arrays, computed in float64 on the
     device with numpy's accumulation order: equal to the reference's values bit for bit
-    (mc_affine_rows_f64)."""
+    (mc_affine_rows_f64).  Each cloud is one ``T @ points.T`` product; ``per_point`` makes every
+    point its own (1, 3) product, as _transform_coordinates' loop does (CSIM:2117-2141) — numpy
+    rounds a one-point product differently."""
     arrs = [np.asarray(f) for f in frames]
     if any(a.ndim != 2 for a in arrs):
         raise IndexError("tuple index out of range")     # points.shape[1] on a 1-D array (CSIM:223)
@@ -126,7 +129,7 @@ def transform_arrays(frames: Sequence[np.ndarray], T, context: Context | None = 
         return [np.zeros((len(a), 3)) for a in arrs]
     ctx = context or default_context()
     rows = arrs[0] if len(arrs) == 1 else np.concatenate(arrs)
-    out = ctx.affine_rows(counts, rows, T)
+    out = ctx.affine_rows(counts, rows, T, per_row=per_point)
     return [out[o:o + n] for o, n in zip(np.concatenate([[0], np.cumsum(counts)[:-1]]), counts)]
 
 
@@ -160,10 +163,12 @@ def transform_coordinates(frames_data: List[Dict], target_system: str, gps_data:
         if moved.any():
             sel = np.flatnonzero(moved)
             for f, xyz in zip(sel, transform_arrays([frames_xyz[f] for f in sel], Ts[sel],
-                                                    context=transformer.context)):
+                                                    context=transformer.context, per_point=True)):
                 new_xyz[f] = xyz
     elif (CoordinateSystem.SENSOR, target_system) in transformer.transformations:
-        new_xyz = transformer.transform_frames(frames_xyz, CoordinateSystem.SENSOR, target_system)
+        # CSIM:2137-2139: transform_points on one (1, 3) point at a time
+        new_xyz = transform_arrays(frames_xyz, transformer.transformations[(CoordinateSystem.SENSOR, target_system)],
+                                   context=transformer.context, per_point=True)
     else:
         logger.warning(f"No transformation available from {CoordinateSystem.SENSOR} to {target_system}")
         new_xyz = frames_xyz

@@ -171,13 +171,8 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
     if (F > 0)
       hipLaunchKernelGGL(k_lvx_frames, dim3((F + kCodecBlock - 1) / kCodecBlock), dim3(kCodecBlock), 0, c->stream,
                          a, (int64_t)0);
-    if (n_pkg > 0 && a.src.cols && MC_LVX_UNITS)
-      hipLaunchKernelGGL(k_lvx_units, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
-    else if (n_pkg > 0 && a.src.cols && kLvxUnitsPerWG > 1)
-      hipLaunchKernelGGL(k_lvx_packages_cols, dim3((uint32_t)((n_pkg + kLvxUnitsPerWG - 1) / kLvxUnitsPerWG)),
-                         dim3(kCodecBlock), 0, c->stream, a);
-    else if (n_pkg > 0)
-      hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
+    if (n_pkg > 0)
+      hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kLvxNT), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());
   int err = 0;
@@ -333,10 +328,7 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   const dim3 grid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    if (a.src.cols && MC_PCD_PC)
-      hipLaunchKernelGGL(k_pcd_write_pc, dim3((uint32_t)((n_tiles + kPcdPcTiles - 1) / kPcdPcTiles)),
-                         dim3(2 * kPcdBlock), 0, c->stream, a);
-    else if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
+    if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
     else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kPcdBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());

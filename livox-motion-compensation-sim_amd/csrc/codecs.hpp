@@ -44,9 +44,6 @@ constexpr int kLvxUnitPoints = kLvxPkgPerWG * kLvxPkgPoints;    // 768
 constexpr int kLvxLds = kLvxPkgPerWG * kLvxPkg + 16;            // + alignment shift
 constexpr int kLvxSlots = kLvxUnitPoints / kCodecBlock;         // 3 batch blocks per unit
 static_assert(kLvxUnitPoints % kCodecBlock == 0, "unit = whole blocks");
-#ifndef MC_LVX_UNITS
-#define MC_LVX_UNITS 1       // batch-source LVX: k_lvx_units (1) or the generic k_lvx_packages (0)
-#endif
 #ifndef MC_PCD_MEASURE_SCALAR
 #define MC_PCD_MEASURE_SCALAR 1   // float32 measure pass: wave-uniform tile arithmetic (scalar), DPP wave sum
 #endif
@@ -127,19 +124,71 @@ __device__ __forceinline__ int32_t codec_advance(const int64_t* __restrict__ uni
   return f;
 }
 
+// Codec stores and loads (A/B knobs).  MC_CODEC_ST: a text / record chunk's 16-byte store, 1 = nt
+// (builtin), 2 = sc1 write-through (inline asm + s_nop 1, as st_pol<2> in kernels.hpp: the data VGPRs
+// are read after issue).  MC_CODEC_LD: 1 = the batch-source point loads non-temporal.  MC_CODEC_EDGE:
+// 1 = a piece's partial end chunks stored by 32 lanes at once, one byte each (0: a byte loop in one
+// lane per end).
+#ifndef MC_CODEC_ST
+#define MC_CODEC_ST 1
+#endif
+#ifndef MC_CODEC_LD
+#define MC_CODEC_LD 0
+#endif
+#ifndef MC_CODEC_EDGE
+#define MC_CODEC_EDGE 0
+#endif
+typedef unsigned int codec_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void codec_st16(char* p, const uint4& v) {
+  codec_v4u t = {v.x, v.y, v.z, v.w};
+  if constexpr (MC_CODEC_ST == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
+  } else {
+    __builtin_nontemporal_store(t, reinterpret_cast<codec_v4u*>(p));
+  }
+}
+__device__ __forceinline__ float codec_ld(const float* p) {
+  if constexpr (MC_CODEC_LD == 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+__device__ __forceinline__ float4 codec_ld4(const float* p) {
+  if constexpr (MC_CODEC_LD == 1) {
+    typedef float v4f_ __attribute__((ext_vector_type(4)));
+    const v4f_ t = __builtin_nontemporal_load(reinterpret_cast<const v4f_*>(p));
+    return make_float4(t.x, t.y, t.z, t.w);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+// bytes of LDS [lo, hi) outside the full chunks [f0, f1) (the partial end chunks) -> g, lanes t < 32
+// of the workgroup, one byte each: lanes 0-15 the head chunk lo / 16, lanes 16-31 the tail chunk hi / 16
+__device__ __forceinline__ void codec_store_edges(char* __restrict__ g, const char* lds, int lo, int hi, int f0, int f1,
+                                                  int t) {
+  if (t < 32) {
+    const int ch = t < 16 ? lo >> 4 : hi >> 4;
+    const int b = 16 * ch + (t & 15);
+    const bool in = b >= lo && b < hi && !(ch >= f0 && ch < f1) && !(t >= 16 && (lo >> 4) == (hi >> 4));
+    if (in) g[b] = lds[b];
+  }
+}
+
 // Store LDS bytes [lo, hi) to g + [lo, hi), where lds and g agree modulo 16: whole 16-byte chunks
 // with dwordx4 stores, the partial chunks at either end byte by byte.  All threads participate.
 // (Partial chunks from one 16-byte LDS read + predicated byte stores: 50 instead of 56 VGPRs in the
 // LVX kernel but LVX 310.4 vs 308.2, PCD 808.4 vs 803.3 us, profiles/round4/s12: not taken.)
 template <int NT = kCodecBlock>   // NT: threads of the workgroup
 __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const char* lds, int lo, int hi) {
+  if constexpr (MC_CODEC_EDGE == 1) {
+    const int f0 = (lo + 15) >> 4, f1 = hi >> 4;
+    for (int c = f0 + (int)threadIdx.x; c < f1; c += NT) codec_st16(g + 16 * c, *reinterpret_cast<const uint4*>(lds + 16 * c));
+    codec_store_edges(g, lds, lo, hi, f0, f1, (int)threadIdx.x);
+    return;
+  }
   const int c0 = lo >> 4, c1 = (hi + 15) >> 4;
   for (int c = c0 + threadIdx.x; c < c1; c += NT) {
     const int b0 = c << 4;
     if (b0 >= lo && b0 + 16 <= hi) {
-      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-      const uint4 v = *reinterpret_cast<const uint4*>(lds + b0);
-      __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + b0));
+      codec_st16(g + b0, *reinterpret_cast<const uint4*>(lds + b0));
     } else {
       const int e = b0 + 16 < hi ? b0 + 16 : hi;
       for (int b = b0 > lo ? b0 : lo; b < e; ++b) g[b] = lds[b];
@@ -165,11 +214,28 @@ __device__ __forceinline__ int32_t lvx_fixed(double v, double scale, double lo, 
   return (int32_t)fmin(fmax(s, lo), hi);
 }
 
+// MC_LVX_DIAG (diagnostic builds only, wrong output): 1 = no point loads (records formed from the slot
+// index), 2 = no HBM stores (the assembled LDS piece is read but only a never-true test of it stores),
+// 3 = both.  Naming the packer's limiter: its time with each part removed (tools/ab_codecs.py).
+#ifndef MC_LVX_DIAG
+#define MC_LVX_DIAG 0
+#endif
 // One unit = up to 8 consecutive packages of one frame = one contiguous byte range of the file.
 // Phase 1: a thread per point slot writes its 14-byte record (7 halfwords, zero for the padding
 // slots of the last package, LMC:245-248) and threads 0..k*11 the 22-byte package headers
 // (LMC:204-237) into LDS.  Phase 2: codec_store_piece.
-__global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
+// Rejected (tools/ab_codecs.py --source batch): 2 / 4 / 8 units per workgroup with the next unit's
+// points loaded while one is stored (305.0 vs 333.9-356.4 us, profiles/round3/s69); a batch-only unit
+// kernel with 32-bit scalar unit arithmetic, all 12 loads of a lane up front and branch-free records
+// (336.8 vs 306.8 us, profiles/round5/s01).
+// MC_LVX_NT: threads per workgroup (256: three points per thread, one after the other — each lane's
+// loads wait before the next point's are issued; 768: one point per thread, all loads at once)
+#ifndef MC_LVX_NT
+#define MC_LVX_NT 256
+#endif
+constexpr int kLvxNT = MC_LVX_NT;
+static_assert(kLvxNT % 64 == 0 && kLvxNT >= kLvxPkgPerWG * (kLvxPkgHdr / 2), "whole waves; one header halfword per thread");
+__global__ __launch_bounds__(kLvxNT) void k_lvx_packages(const LvxArgs a) {
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
   const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
@@ -187,11 +253,13 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   const bool hi = a.has_int ? a.has_int[f] != 0 : a.src.ld > 3;
   const int64_t row0 = frow + pkg0 * kLvxPkgPoints;
 
-  for (int i = threadIdx.x; i < k * kLvxPkgPoints; i += kCodecBlock) {
+  for (int i = threadIdx.x; i < k * kLvxPkgPoints; i += kLvxNT) {
     const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
     uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
     uint32_t x = 0, y = 0, z = 0, refl = 0;
-    if (i < n) {
+    if ((MC_LVX_DIAG & 1) && i < n) {
+      x = (uint32_t)i; y = x * 3u; z = x ^ 0x5555u; refl = x & 255u;
+    } else if (i < n) {
       double v[4];
       codec_point(a.src, f, row0 + i, v);
       x = (uint32_t)lvx_fixed(v[0], 1000.0, -2147483648.0, 2147483647.0, a.err);
@@ -206,7 +274,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   }
   // dev 0, version 5 | slot 0, lidar 1 | reserved, status (4 B) | ts type 1 | data type 2 |
   // reserved (3 B) | timestamp (8 B)
-  for (int h = threadIdx.x; h < k * (kLvxPkgHdr / 2); h += kCodecBlock) {
+  for (int h = threadIdx.x; h < k * (kLvxPkgHdr / 2); h += kLvxNT) {
     const int pk = h / (kLvxPkgHdr / 2), w = h - pk * (kLvxPkgHdr / 2);
     uint32_t v;
     switch (w) {
@@ -220,175 +288,12 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
     s16[((shift + pk * kLvxPkg) >> 1) + w] = (uint16_t)v;
   }
   __syncthreads();
-  codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
-}
-
-// Batch source, one unit per workgroup (MC_LVX_UNITS=1): the unit's frame from codec_frame_of and
-// every per-unit quantity in 32-bit scalar arithmetic (frames < 2^31 points, checked by the host); the
-// unit's 3 blocks loaded under workgroup-uniform guards (no divergent load branches), each lane's
-// records formed branch-free (a NaN only sets a flag, stored once per lane: the per-value error
-// branches and their stores were most of the old kernel's 689 scalar instructions); padding slots and
-// slots past the unit's packages are written too — as zero records inside the LDS buffer, outside
-// the stored piece where no package exists.
-__global__ __launch_bounds__(kCodecBlock) void k_lvx_units(const LvxArgs a) {
-  __shared__ uint4 s_buf[kLvxLds / 16 + 1];
-  uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
-  const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
-  const int32_t f = codec_frame_of(a.src, u);
-  const uint32_t fcount = (uint32_t)(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f));
-  const uint32_t ui = (uint32_t)(u - ldu(a.src.unit_off + f));
-  const uint32_t pkg0 = ui * kLvxPkgPerWG;
-  const uint32_t fpkgs = (fcount + kLvxPkgPoints - 1) / kLvxPkgPoints;
-  const int k = (int)min(fpkgs - pkg0, (uint32_t)kLvxPkgPerWG);
-  const int n = (int)min(fcount - pkg0 * kLvxPkgPoints, (uint32_t)(k * kLvxPkgPoints));
-  const int64_t S = ldu(a.frame_pos + f) + kLvxFrameHdr + (int64_t)pkg0 * kLvxPkg;   // even
-  const int shift = (int)(S & 15);
-  const uint64_t ts = ldu(a.ts_ns + f);
-  const bool hi = a.has_int ? a.has_int[f] != 0 : true;
-  const float* q0 = a.src.cols + ((ldu(a.src.poff + f) >> 8) + 3 * (int64_t)ui) * a.src.C * kBlkPts + threadIdx.x;
-  // all 12 loads back to back: block j of a short unit re-reads the unit's last block (results unused)
-  const int jl = (n - 1) / kCodecBlock;
-  float v[kLvxSlots][4];
-#pragma unroll
-  for (int j = 0; j < kLvxSlots; ++j)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[j][c] = q0[((j < jl ? j : jl) * a.src.C + c) * kBlkPts];
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < kLvxSlots; ++j) {
-    const int i = j * kCodecBlock + (int)threadIdx.x;
-    const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
-    uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
-    const bool ok = i < n;
-    // int(np.clip(v * 1000, ...)) (LMC:259-261): the float32 value times 1000 is exact in float64
-    uint32_t w[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double sc = (double)v[j][c] * (c < 3 ? 1000.0 : 255.0);
-      bad |= ok && sc != sc;
-      w[c] = (uint32_t)(int32_t)(c < 3 ? fmin(fmax(sc, -2147483648.0), 2147483647.0) : fmin(fmax(sc, 0.0), 255.0));
-    }
-    const uint32_t refl = hi ? w[3] : 128u;   // tag byte 0 (LMC:268)
-    const uint32_t x = ok ? w[0] : 0u, y = ok ? w[1] : 0u, z = ok ? w[2] : 0u, rt = ok ? refl : 0u;
-    r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
-    r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
-    r[4] = (uint16_t)z; r[5] = (uint16_t)(z >> 16);
-    r[6] = (uint16_t)rt;
+  if constexpr ((MC_LVX_DIAG & 2) != 0) {
+    const uint4 v = s_buf[threadIdx.x];   // every LDS word is live; (almost) nothing reaches HBM
+    if (v.x == 0x7eadbeefu && v.y == 0x7eadbeefu) a.out[S] = 1;
+    return;
   }
-  if ((int)threadIdx.x < k * (kLvxPkgHdr / 2)) {   // k * 11 <= 88 header halfwords
-    const int h = threadIdx.x, pk = h / (kLvxPkgHdr / 2), wd = h - pk * (kLvxPkgHdr / 2);
-    uint32_t hv;
-    switch (wd) {
-      case 0: hv = 0x0500u; break;
-      case 1: hv = 0x0100u; break;
-      case 4: hv = 0x0100u; break;
-      case 5: hv = 0x0002u; break;
-      case 7: case 8: case 9: case 10: hv = (uint32_t)(ts >> (16 * (wd - 7))) & 0xffffu; break;
-      default: hv = 0u;
-    }
-    s16[((shift + pk * kLvxPkg) >> 1) + wd] = (uint16_t)hv;
-  }
-  if (bad) *a.err = 1;
-  __syncthreads();
-  codec_store_piece(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
-}
-
-// Batch source.  The loop takes kLvxUnitsPerWG consecutive units per workgroup, unit j + 1's meta
-// data and point values loaded while unit j is assembled and stored (two LDS buffers, one barrier per
-// unit); one unit per workgroup ships (2 / 4 / 8: 305.0 / 306.6 vs 333.9 / 338.5, 356.3 / 356.4 us in
-// the dealt order, profiles/round3/s69).  A unit's first row is a multiple of 768 = 3 blocks into its
-// frame, so thread t's slot j is row t of the unit's block j.
-constexpr int kLvxUnitsPerWG = 1;
-
-struct LvxUnit {
-  int64_t S;     // file offset of the unit's first package
-  int64_t p0;    // padded batch row of the unit's first point
-  uint64_t ts;
-  int k, n;      // packages, points
-  bool hi;
-};
-
-__device__ __forceinline__ LvxUnit lvx_unit(const LvxArgs& a, int32_t f, int64_t u) {
-  LvxUnit U;
-  const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
-  const int64_t fcount = a.src.doff[f + 1] - a.src.doff[f];
-  const int64_t fpkgs = (fcount + kLvxPkgPoints - 1) / kLvxPkgPoints;
-  U.k = (int)((fpkgs - pkg0) < kLvxPkgPerWG ? (fpkgs - pkg0) : kLvxPkgPerWG);
-  const int64_t rem = fcount - pkg0 * kLvxPkgPoints;
-  U.n = (int)(rem < U.k * kLvxPkgPoints ? rem : U.k * kLvxPkgPoints);
-  U.S = a.frame_pos[f] + kLvxFrameHdr + pkg0 * kLvxPkg;
-  U.p0 = a.src.poff[f] + pkg0 * kLvxPkgPoints;
-  U.ts = a.ts_ns[f];
-  U.hi = a.has_int ? a.has_int[f] != 0 : true;
-  return U;
-}
-
-__global__ __launch_bounds__(kCodecBlock) void k_lvx_packages_cols(const LvxArgs a) {
-  __shared__ uint4 s_buf[2][kLvxLds / 16 + 1];
-  const int64_t u0 = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x) * kLvxUnitsPerWG;
-  const int64_t u_end = u0 + kLvxUnitsPerWG < a.src.n_units ? u0 + kLvxUnitsPerWG : a.src.n_units;
-  int32_t f = codec_frame_of(a.src, u0);
-  LvxUnit nu = lvx_unit(a, f, u0);
-  float nv[kLvxSlots][4];
-  auto fetch = [&]() {
-#pragma unroll
-    for (int j = 0; j < kLvxSlots; ++j) {
-      const float* q = a.src.cols + (((nu.p0 >> 8) + j) * a.src.C) * kBlkPts + threadIdx.x;
-      const bool ok = j * kCodecBlock + (int)threadIdx.x < nu.n;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) nv[j][c] = ok ? q[c * kBlkPts] : 0.f;
-    }
-  };
-  fetch();
-  for (int64_t u = u0; u < u_end; ++u) {
-    const LvxUnit cu = nu;
-    float cv[kLvxSlots][4];
-#pragma unroll
-    for (int j = 0; j < kLvxSlots; ++j)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) cv[j][c] = nv[j][c];
-    if (u + 1 < u_end) {
-      f = codec_advance(a.src.unit_off, f, u + 1);
-      nu = lvx_unit(a, f, u + 1);
-      fetch();
-    }
-    uint4* const buf = s_buf[(u - u0) & 1];
-    uint16_t* const s16 = reinterpret_cast<uint16_t*>(buf);
-    const int shift = (int)(cu.S & 15);
-#pragma unroll
-    for (int j = 0; j < kLvxSlots; ++j) {
-      const int i = j * kCodecBlock + (int)threadIdx.x;
-      if (i >= cu.k * kLvxPkgPoints) break;
-      const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
-      uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
-      uint32_t x = 0, y = 0, z = 0, refl = 0;
-      if (i < cu.n) {
-        x = (uint32_t)lvx_fixed(cv[j][0], 1000.0, -2147483648.0, 2147483647.0, a.err);
-        y = (uint32_t)lvx_fixed(cv[j][1], 1000.0, -2147483648.0, 2147483647.0, a.err);
-        z = (uint32_t)lvx_fixed(cv[j][2], 1000.0, -2147483648.0, 2147483647.0, a.err);
-        refl = cu.hi ? (uint32_t)lvx_fixed(cv[j][3], 255.0, 0.0, 255.0, a.err) : 128u;
-      }
-      r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
-      r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
-      r[4] = (uint16_t)z; r[5] = (uint16_t)(z >> 16);
-      r[6] = (uint16_t)refl;
-    }
-    if ((int)threadIdx.x < cu.k * (kLvxPkgHdr / 2)) {   // k * 11 <= 88 header halfwords
-      const int h = threadIdx.x, pk = h / (kLvxPkgHdr / 2), w = h - pk * (kLvxPkgHdr / 2);
-      uint32_t v;
-      switch (w) {
-        case 0: v = 0x0500u; break;
-        case 1: v = 0x0100u; break;
-        case 4: v = 0x0100u; break;
-        case 5: v = 0x0002u; break;
-        case 7: case 8: case 9: case 10: v = (uint32_t)(cu.ts >> (16 * (w - 7))) & 0xffffu; break;
-        default: v = 0u;
-      }
-      s16[((shift + pk * kLvxPkg) >> 1) + w] = (uint16_t)v;
-    }
-    __syncthreads();   // the other buffer's stores (unit j - 1) were issued before this barrier
-    codec_store_piece(a.out + (cu.S - shift), reinterpret_cast<const char*>(buf), shift, shift + cu.k * kLvxPkg);
-  }
+  codec_store_piece<kLvxNT>(a.out + (S - shift), reinterpret_cast<const char*>(s_buf), shift, shift + k * kLvxPkg);
 }
 
 // LMC:178-193: frame header = own offset, next frame's offset (0 for the last), frame_id
@@ -913,7 +818,7 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
       // the whole block is allocated (frames are padded to blocks): every lane loads, results past
       // the frame's end are ignored below
 #pragma unroll
-      for (int c = 0; c < 4; ++c) V[j][c] = *reinterpret_cast<const float4*>(q + c * kBlkPts);
+      for (int c = 0; c < 4; ++c) V[j][c] = codec_ld4(q + c * kBlkPts);
     }
   }
 #pragma unroll
@@ -1011,12 +916,10 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
   char* const g = a.out + (G - lo);
   const char* const lds = reinterpret_cast<const char*>(s_text4);
   const int f0 = (lo + 15) >> 4, f1 = hi >> 4;   // full chunks [f0, f1)
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) {
-    const uint4 v = s_text4[c];
-    __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + 16 * c));
-  }
-  if (threadIdx.x < 2) {
+  for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) codec_st16(g + 16 * c, s_text4[c]);
+  if (MC_CODEC_EDGE == 1) {
+    codec_store_edges(g, lds, lo, hi, f0, f1, (int)threadIdx.x);
+  } else if (threadIdx.x < 2) {
     int b = lo, e = hi;                                    // a piece inside one chunk: lane 0 alone
     if (f0 <= f1) {
       if (threadIdx.x == 0) e = 16 * f0;                   // head: [lo, 16 f0)
@@ -1062,7 +965,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       // the tile's block is allocated whole: every lane loads (no branch around the loads), a lane
       // past the frame's end formats a value it never emits
       const float* q = a.src.cols + blk * a.src.C * kBlkPts + threadIdx.x;
-      cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
+      cn[0] = codec_ld(q); cn[1] = codec_ld(q + kBlkPts); cn[2] = codec_ld(q + 2 * kBlkPts); cn[3] = codec_ld(q + 3 * kBlkPts);
       flag_n = ldu(a.tile_bytes + u);
       gn = ldu(a.tile_pos + u);
     };
@@ -1106,109 +1009,6 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       const int64_t G = ldu(a.tile_pos + u);
       const int total = pcd_tile_text(T, valid, G, s_wave, s_text4);
       pcd_tile_store(a, G, total, s_text4);
-    }
-  }
-}
-
-// Float32 source, producer / consumer (MC_PCD_PC=1): a workgroup of 8 waves in two roles.  Waves
-// 0-3 (producers) load, convert and scan a tile's lines and write its text into one of two LDS
-// buffers; waves 4-7 (consumers) copy the previous tile's buffer to HBM meanwhile.  A producer wave
-// then never issues a global store and a consumer wave never a load, so no wave's wait for its
-// next tile's loads also waits for its own stores (vmcnt counts both on CDNA; in k_pcd_write every
-// tile's load consumption waits for the previous tile's stores to complete).  Two barriers per tile:
-// the producers' scan exchange and the hand-over; the consumers take part in both.
-//   buffer b = tile parity: producers write buffer b of tile u after barrier 1 of tile u; the
-//   consumers' reads of tile u - 2 (same buffer) ended before they reached barrier 1 of tile u - 1.
-#ifndef MC_PCD_PC
-#define MC_PCD_PC 0
-#endif
-#ifndef MC_PCD_PC_TILES
-#define MC_PCD_PC_TILES 8    // tiles per producer / consumer workgroup (pipeline fill and drain per workgroup)
-#endif
-constexpr int kPcdPcTiles = MC_PCD_PC_TILES;
-__global__ __launch_bounds__(2 * kPcdBlock) void k_pcd_write_pc(const PcdArgs a) {
-  __shared__ int s_wave[kPcdBlock / 64];
-  __shared__ uint4 s_text[2][kPcdPackedText / 16 + 1];
-  __shared__ int64_t s_G[2];
-  __shared__ int s_total[2];
-  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdPcTiles;   // grid = units exactly
-  const int64_t u_end = u0 + kPcdPcTiles < a.src.n_units ? u0 + kPcdPcTiles : a.src.n_units;
-  const int tid = (int)threadIdx.x & (kPcdBlock - 1);
-  if (threadIdx.x < kPcdBlock) {
-    // producers: k_pcd_write<true>'s fetch / convert, one tile ahead
-    int32_t f = codec_frame_of(a.src, u0);
-    float cn[4] = {0.f, 0.f, 0.f, 0.f};
-    bool vn = false;
-    int32_t flag_n = 0;
-    int64_t gn = 0;
-    PcdText Tn;
-    auto fetch = [&](int64_t u) {
-      f = codec_advance(a.src.unit_off, f, u);
-      const int64_t k = u - ldu(a.src.unit_off + f);
-      const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
-      const int left = (int)min_i64(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock);
-      vn = tid < left;
-      const float* q = a.src.cols + blk * a.src.C * kBlkPts + tid;
-      cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
-      flag_n = ldu(a.tile_bytes + u);
-      gn = ldu(a.tile_pos + u);
-    };
-    auto convert = [&]() {
-      PcdFast P;
-      pcd_fast_vals_packed(cn, P);
-      pcd_text(P, Tn);
-      if (!vn) Tn.len = 0;
-    };
-    if (u0 < u_end) fetch(u0);
-    convert();
-    for (int64_t u = u0; u < u_end; ++u) {
-      const int b = (int)((u - u0) & 1);
-      const PcdText T = Tn;
-      const bool valid = vn;
-      const bool packed = !(flag_n & kPcdSlowTile);   // workgroup-uniform
-      const int64_t G = gn;
-      if (u + 1 < u_end) fetch(u + 1);
-      int total = 0;
-      if (packed) {
-        const int excl = block_scan(T.len, s_wave, total) - T.len;   // barrier 1
-        if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text[b]), (int)(G & 15) + excl);
-      } else {
-        __syncthreads();                                               // barrier 1
-      }
-      if (tid == 0) { s_G[b] = G; s_total[b] = packed ? total : -1; }
-      convert();
-      __syncthreads();                                                 // barrier 2: hand-over
-    }
-  } else {
-    // consumers: tile u's text to HBM once the producers hand it over
-    for (int64_t u = u0; u < u_end; ++u) {
-      const int b = (int)((u - u0) & 1);
-      __syncthreads();                                                 // barrier 1
-      __syncthreads();                                                 // barrier 2
-      const int total = s_total[b];
-      if (total < 0) continue;                                         // byte-path tile
-      const int64_t G = s_G[b];
-      const int lo = (int)(G & 15), hi = lo + total;
-      char* const g = a.out + (G - lo);
-      const uint4* const t4 = s_text[b];
-      const char* const lds = reinterpret_cast<const char*>(t4);
-      const int f0 = (lo + 15) >> 4, f1 = hi >> 4;
-      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-      for (int c = f0 + tid; c < f1; c += kPcdBlock) {
-        const uint4 v = t4[c];
-        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(g + 16 * c));
-      }
-      if (tid < 2) {
-        int bb = lo, e = hi;
-        if (f0 <= f1) {
-          if (tid == 0) e = 16 * f0;
-          else bb = 16 * f1;
-        } else if (tid == 1) {
-          e = bb;
-        }
-#pragma clang loop vectorize(disable) unroll(disable)
-        for (; bb < e; ++bb) g[bb] = lds[bb];
-      }
     }
   }
 }

@@ -160,10 +160,6 @@ struct DeskewArgs {
 #ifndef MC_XCD_STAGE
 #define MC_XCD_STAGE 1       // the LDS stager pair's tile order
 #endif
-#ifndef MC_FRAME_GROUPS
-#define MC_FRAME_GROUPS 0    // frame kernel: 0 = quad decomposition, 1 = one float4 group per lane (the
-                             // per-point kernels' sub-tile structure, deskew_frame_groups)
-#endif
 // 16-byte non-temporal store (output is written once and never re-read by this kernel)
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -987,89 +983,34 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
 }
 
 
-// Frame kernel in the per-point kernels' structure (MC_FRAME_GROUPS=1): one workgroup per 1024-point
-// sub-tile of one frame, every lane one float4 group of all four columns (4 loads, 4 stores), the
-// frame's [R | t] rows in SGPRs (scalar loads of a workgroup-uniform record), the sub-tile order and
-// sc1 stores of the SLERP kernel.  The same float64 arithmetic and rounding as the quad kernel, so the
-// output is byte-identical.
-template <bool PCD = false>
-__device__ __forceinline__ void deskew_frame_groups(const DeskewArgs& a, const uint32_t pre) {
-  const int64_t n_sub = (int64_t)a.n_tiles * kSub;
-  const uint32_t nb = gridDim.x - pre;
-  const int tid = threadIdx.x;
-  for (int64_t it = blockIdx.x - pre; it < n_sub; it += nb) {
-    const int64_t st = nb < n_sub ? it : (a.xcd_order ? xcd_unit<1>(it, n_sub) : it);
-    const Tile tl = ldu(a.tiles + st / kSub);
-    const int g0 = (int)(st % kSub) * kBlock;
-    if (g0 >= tl.ngroups) continue;   // uniform: empty sub-tile of a short tile
-    const int g = g0 + tid;
-    const bool act = g < tl.ngroups;
-    const int64_t p = tl.pstart + 4 * (int64_t)(act ? g : g0);
-    const float* q = a.in + bidx((int)a.in_C, 0, p);
-    const float4 X = ld4(q), Y = ld4(q + kBlkPts), Z = ld4(q + 2 * kBlkPts), I = ld4(q + 3 * kBlkPts);
-    const FrameRow r0 = ldu(a.frame_tbl + 3 * tl.frame + 0);
-    const FrameRow r1 = ldu(a.frame_tbl + 3 * tl.frame + 1);
-    const FrameRow r2 = ldu(a.frame_tbl + 3 * tl.frame + 2);
-    float4 ox, oy, oz;
-#define MC_XF(c)                     \
-  ox.c = xf_row(r0, X.c, Y.c, Z.c);  \
-  oy.c = xf_row(r1, X.c, Y.c, Z.c);  \
-  oz.c = xf_row(r2, X.c, Y.c, Z.c);
-    MC_XF(x) MC_XF(y) MC_XF(z) MC_XF(w)
-#undef MC_XF
-    if (act) {
-      float* o = a.out + bidx((int)a.out_C, 0, p);
-      st_out(o, ox);
-      st_out(o + kBlkPts, oy);
-      st_out(o + 2 * kBlkPts, oz);
-      st_out(o + 3 * kBlkPts, I);
-    }
-    if constexpr (PCD) {
-      const int64_t i0 = p - ldu(a.fpoff + tl.frame), n = ldu(a.fcount + tl.frame);
-      PcdCount pc;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const auto v = PcdCount::lanes(act && i0 + c < n);
-        pc.add(v, f4g(ox, c));
-        pc.add(v, f4g(oy, c));
-        pc.add(v, f4g(oz, c));
-        pc.add(v, f4g(I, c));
-      }
-      const int bytes = pc.bytes();
-      const int wg = g0 + (tid & ~63);   // the wave's first group: one 256-point block of the output
-      if ((tid & 63) == 0 && wg < tl.ngroups) a.pcd_len[(tl.pstart + 4 * (int64_t)wg) >> 8] = bytes;
-    }
-  }
-}
-
-// workgroup units per sub-tile of the frame kernel (the launch grid, mcdeskew.hip deskew_plan)
-constexpr int kFrameUnitsPerSub = MC_FRAME_GROUPS ? 1 : kQuadUnitsPerSub;
-template <bool PCD = false>
-__device__ __forceinline__ void deskew_frame_any(const DeskewArgs& a, const uint32_t pre) {
-  if constexpr (MC_FRAME_GROUPS) deskew_frame_groups<PCD>(a, pre);
-  else deskew_frame_quad<PCD>(a, pre);
-}
-
 __global__ __launch_bounds__(kBlock) void k_deskew_frame(const DeskewArgs a) {
   span_start(a.span);
-  deskew_frame_any(a, 0u);
+  deskew_frame_quad(a, 0u);
   span_end(a.span);
 }
 
 // Path A with the ASCII PCD text bytes of every output block (mc_deskew_pcd)
-__global__ __launch_bounds__(kBlock) void k_deskew_frame_pcd(const DeskewArgs a) { deskew_frame_any<true>(a, 0u); }
+__global__ __launch_bounds__(kBlock) void k_deskew_frame_pcd(const DeskewArgs a) { deskew_frame_quad<true>(a, 0u); }
 
 // ---- float64 rows: the reference's own arrays, bit for bit ---------------------------------------
 // R p + t (LMC:775: (R @ p.T).T + t) the way numpy's matmul accumulates it: per output an ascending
 // FMA chain over k, fma(R[i][2], z, fma(R[i][1], y, R[i][0] * x)), then + t[i] rounded on its own
 // (numpy's dgemm, measured on the reference's box: tools/fma_order.py).  P = {R row-major | t}; with
 // the host's scipy-faithful R (rot.cpp) the result equals the reference's float64 value exactly.
+// A one-point frame is a matrix-vector product for numpy (its dgemv), which accumulates
+// fma(R[i][2], z, fma(R[i][0], x, R[i][1] * y)) instead (tools/fma_order.py, single-row cases): `single`.
 __device__ __forceinline__ void frame_apply(const double* __restrict__ P, double x, double y, double z, double& ox,
-                                            double& oy, double& oz) {
+                                            double& oy, double& oz, bool single = false) {
 #pragma clang fp contract(off)
-  ox = __builtin_fma(P[2], z, __builtin_fma(P[1], y, P[0] * x)) + P[9];
-  oy = __builtin_fma(P[5], z, __builtin_fma(P[4], y, P[3] * x)) + P[10];
-  oz = __builtin_fma(P[8], z, __builtin_fma(P[7], y, P[6] * x)) + P[11];
+  if (single) {
+    ox = __builtin_fma(P[2], z, __builtin_fma(P[0], x, P[1] * y)) + P[9];
+    oy = __builtin_fma(P[5], z, __builtin_fma(P[3], x, P[4] * y)) + P[10];
+    oz = __builtin_fma(P[8], z, __builtin_fma(P[6], x, P[7] * y)) + P[11];
+  } else {
+    ox = __builtin_fma(P[2], z, __builtin_fma(P[1], y, P[0] * x)) + P[9];
+    oy = __builtin_fma(P[5], z, __builtin_fma(P[4], y, P[3] * x)) + P[10];
+    oz = __builtin_fma(P[8], z, __builtin_fma(P[7], y, P[6] * x)) + P[11];
+  }
 }
 
 // the frame of row `row`: last f with doff[f] <= row
@@ -1089,7 +1030,8 @@ __global__ __launch_bounds__(kBlock) void k_align_rows_f64(const double* __restr
                                                            int64_t r0, const int64_t* __restrict__ doff, int32_t F,
                                                            const double* __restrict__ pose, double* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const double* P = pose + 12 * (int64_t)row_frame(doff, F, r0 + i);
+    const int32_t f = row_frame(doff, F, r0 + i);
+    const double* P = pose + 12 * (int64_t)f;
     const double* q = in + i * ld;
     double x, y, z, w;
     if (ld == 4) {
@@ -1100,7 +1042,7 @@ __global__ __launch_bounds__(kBlock) void k_align_rows_f64(const double* __restr
       x = q[0]; y = q[1]; z = q[2]; w = q[3];
     }
     double ox, oy, oz;
-    frame_apply(P, x, y, z, ox, oy, oz);
+    frame_apply(P, x, y, z, ox, oy, oz, doff[f + 1] - doff[f] == 1);
     double* o = out + 4 * i;
     *reinterpret_cast<double2*>(o) = double2{ox, oy};
     *reinterpret_cast<double2*>(o + 2) = double2{oz, w};
@@ -1110,19 +1052,28 @@ __global__ __launch_bounds__(kBlock) void k_align_rows_f64(const double* __restr
 // CoordinateTransformer.transform_points (CSIM:214-233): (T @ [p, w].T).T[:, :3] per row with the
 // 4x4 T's top 3x4 [A | b] of the row's frame (mats + 12 * frame, or one matrix for all); w = the 4th
 // column of (n, 4) homogeneous rows, 1 for (n, 3) rows (CSIM:223-225's column of ones).  numpy's
-// accumulation over k = 0..3: fma(b_i, w, fma(A_i2, z, fma(A_i1, y, A_i0 * x))); out (n, 3).
+// accumulation over k = 0..3 for a frame of several rows (dgemm): fma(b_i, w, fma(A_i2, z,
+// fma(A_i1, y, A_i0 * x))); for a one-row frame, or every row with per_row (the reference's
+// per-point loop, CSIM:2117-2141, one 4x1 product per point — numpy's dgemv):
+// (A_i0 x + A_i2 z) + (A_i1 y + b_i w), every product rounded (tools/fma_order.py); out (n, 3).
 __global__ __launch_bounds__(kBlock) void k_affine_rows_f64(const double* __restrict__ in, int64_t ld, int64_t n,
                                                             const int64_t* __restrict__ doff, int32_t F,
                                                             const double* __restrict__ mats, int32_t n_mats,
-                                                            double* __restrict__ out) {
+                                                            int per_row, double* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const double* M = mats + (n_mats == 1 ? 0 : 12 * (int64_t)row_frame(doff, F, i));
+    const int32_t f = row_frame(doff, F, i);
+    const double* M = mats + (n_mats == 1 ? 0 : 12 * (int64_t)f);
+    const bool single = per_row || doff[f + 1] - doff[f] == 1;
     const double* q = in + i * ld;
     const double x = q[0], y = q[1], z = q[2], w = ld == 4 ? q[3] : 1.0;
     double* o = out + 3 * i;
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
-      o[r] = __builtin_fma(M[4 * r + 3], w, __builtin_fma(M[4 * r + 2], z, __builtin_fma(M[4 * r + 1], y, M[4 * r] * x)));
+    for (int r = 0; r < 3; ++r) {
+#pragma clang fp contract(off)
+      const double* m = M + 4 * r;
+      o[r] = single ? (m[0] * x + m[2] * z) + (m[1] * y + m[3] * w)
+                    : __builtin_fma(m[3], w, __builtin_fma(m[2], z, __builtin_fma(m[1], y, m[0] * x)));
+    }
   }
 }
 
@@ -1612,7 +1563,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_deskew_frame_next(const DeskewArg
     prep_body<0>(p, blockIdx.x);
     return;
   }
-  deskew_frame_any(a, pre);
+  deskew_frame_quad(a, pre);
   span_end(a.span);
 }
 

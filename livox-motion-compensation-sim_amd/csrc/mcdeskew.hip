@@ -716,7 +716,7 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   // frame mode: one workgroup per tile (2 float4 groups per thread); per-point modes: one per
   // kBlock-group sub-tile (1 group per thread, kSub sub-tiles per tile)
   int32_t units = in->n_tiles * kSub;
-  if (mode == MC_MODE_FRAME) units = in->n_tiles * kSub * kFrameUnitsPerSub;
+  if (mode == MC_MODE_FRAME) units = in->n_tiles * kSub * kQuadUnitsPerSub;   // the quad decomposition
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
   // sub-tile order: default_order, or mc_tune_order's measured choice
@@ -1305,7 +1305,7 @@ int mc_align_frames_host_f64(mc_ctx* c, int32_t F, const double* const* frames, 
 }
 
 int mc_affine_rows_f64(mc_ctx* c, int32_t F, const int64_t* counts, const double* rows, int64_t ld, int32_t n_mats,
-                       const double* mats, double* out) {
+                       const double* mats, int per_row, double* out) {
   CHECK_ARG(c && (F == 0 || counts) && mats, "NULL argument");
   CHECK_ARG(F >= 0, "n_frames must be >= 0");
   CHECK_ARG(ld == 3 || ld == 4, "rows need 3 or 4 columns (got %lld)", (long long)ld);
@@ -1346,7 +1346,7 @@ int mc_affine_rows_f64(mc_ctx* c, int32_t F, const int64_t* counts, const double
     const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, zero_copy ? 1024 : 65536);
     hipLaunchKernelGGL(k_affine_rows_f64, dim3(grid), dim3(kBlock), 0, s,
                        reinterpret_cast<const double*>(base + 8 * w_rows), ld, n, reinterpret_cast<const int64_t*>(base),
-                       F, reinterpret_cast<const double*>(base + 8 * w_mat), n_mats, d_out);
+                       F, reinterpret_cast<const double*>(base + 8 * w_mat), n_mats, per_row ? 1 : 0, d_out);
   }
   HIPCHK(hipGetLastError());
   if (!zero_copy) HIPCHK(hipMemcpyAsync(out, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, s));

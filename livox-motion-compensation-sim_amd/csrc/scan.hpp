@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
             *reinterpret_cast<double2*>(q + 2) = double2{pz, sc.w[e]};
             if (a.aligned) {
               double ax, ay, az;
-              frame_apply(P, px, py, pz, ax, ay, az);
+              frame_apply(P, px, py, pz, ax, ay, az, a.doff[f + 1] - doff == 1);
               double* w = a.aligned + 4 * (doff + o);
               *reinterpret_cast<double2*>(w) = double2{ax, ay};
               *reinterpret_cast<double2*>(w + 2) = double2{az, sc.w[e]};

@@ -134,6 +134,10 @@ def make_kat(lmc):
         out[f"t{i}"] = np.array(t)
         out[f"r{i}"] = np.array(r)
         out[f"out{i}"] = sim.transform_pointcloud(pts, {"translation": np.array(t), "rotation": np.array(r)})
+        # every point as a one-point frame: numpy's matrix-vector product sums in another order
+        out[f"one{i}"] = np.vstack([sim.transform_pointcloud(pts[j:j + 1], {"translation": np.array(t),
+                                                                              "rotation": np.array(r)})
+                                    for j in range(len(pts))])
     out["empty_out"] = sim.transform_pointcloud(np.zeros((0, 4)), {"translation": np.zeros(3), "rotation": np.zeros(3)})
     # one frame above the zero-copy size (the library's DMA row pipeline path), highway-scale pose
     # (points regenerated by the test from this seed; the output's sha256 and every 1000th row kept)

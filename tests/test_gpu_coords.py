@@ -40,6 +40,11 @@ def test_transform_points_matches_reference(mc, gpu_ctx):
     T = ct.transformations[("sensor", "local")]
     same = check(out4, g["tp4/sensor/local"], g["p4"], T, "homogeneous")
     assert same or not np.array_equal(T, g["T/sensor/local"])
+    # (1, 3) calls: numpy's matrix-vector order, as _transform_coordinates' per-point loop recorded it
+    xyz = g["tc/in/0"]
+    one = np.vstack([ct.transform_points(xyz[j:j + 1], "sensor", "local") for j in range(len(xyz))])
+    if np.array_equal(ct.transformations[("sensor", "local")], g["T/sensor/local"]):
+        assert np.array_equal(one, g["tc/local/0"]), int(np.count_nonzero(one != g["tc/local/0"]))
     # missing pair: a warning and the very same array back
     assert ct.transform_points(p3, "vehicle", "sensor") is p3
     with pytest.raises(ValueError):

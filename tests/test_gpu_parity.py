@@ -64,6 +64,14 @@ def test_transform_pointcloud_known_answers(mc, gpu_ctx):
     assert np.array_equal(bo[::1000], g["big/rows"])
     assert hashlib.sha256(np.ascontiguousarray(bo).tobytes()).digest() == g["big/sha256"].tobytes()
     assert sim.transform_pointcloud(np.zeros((0, 4)), {"translation": np.zeros(3), "rotation": np.zeros(3)}).shape == (0, 4)
+    # one-point frames: numpy's matrix-vector product (another summation order) reproduced as well,
+    # alone and inside a batch of one-point frames
+    for i in range(int(g["n_cases"])):
+        tf = {"translation": g[f"t{i}"], "rotation": g[f"r{i}"]}
+        one = g[f"one{i}"]
+        assert np.array_equal(sim.transform_pointcloud(pts[5:6], tf), one[5:6]), i
+        got = np.vstack(sim.align_frames([pts[j:j + 1] for j in range(len(pts))], [tf] * len(pts)))
+        assert np.array_equal(got, one), (i, int(np.count_nonzero(got != one)))
     with pytest.raises(IndexError):
         sim.transform_pointcloud(np.zeros((5, 3)), {"translation": np.zeros(3), "rotation": np.zeros(3)})
     with pytest.raises(IndexError):

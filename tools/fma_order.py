@@ -13,6 +13,11 @@ fma(a2, x2, fma(a1, x1, a0 * x0)) and the descending one.  Measured in the build
 (OpenBLAS 0.3.29 Haswell-family dgemm, the box the golden fixtures come from): the ascending chain
 matches every value, the others miss 25-45 %.
 
+One-row products (a frame of one point; CSIM:2137's per-point transform_points) go through dgemv
+and sum in other orders, checked here as "single": 3x3 fma(a2, x2, fma(a0, x0, a1 * x1)), 4x4
+(a0 x0 + a2 x2) + (a1 x1 + a3 x3) with every product rounded (frame_apply(single) and
+k_affine_rows_f64's per-row order).  Row counts 2..257 and 1000 all take the ascending chain.
+
     python tools/fma_order.py
 """
 import ctypes
@@ -32,7 +37,9 @@ void chain(const double* A, int K, const double* X, int64_t n, int order, double
       const double* a = A + K * i; const double* x = X + K * r; double s;
       if (order == 0) { s = a[0] * x[0]; for (int k = 1; k < K; ++k) s = s + a[k] * x[k]; }
       else if (order == 1) { s = a[0] * x[0]; for (int k = 1; k < K; ++k) s = fma(a[k], x[k], s); }
-      else { s = a[K - 1] * x[K - 1]; for (int k = K - 2; k >= 0; --k) s = fma(a[k], x[k], s); }
+      else if (order == 2) { s = a[K - 1] * x[K - 1]; for (int k = K - 2; k >= 0; --k) s = fma(a[k], x[k], s); }
+      else if (K == 3) s = fma(a[2], x[2], fma(a[0], x[0], a[1] * x[1]));            /* one-row 3x3 */
+      else s = (a[0] * x[0] + a[2] * x[2]) + (a[1] * x[1] + a[3] * x[3]);           /* one-row 4x4 */
       o[3 * r + i] = s;
     }
 }
@@ -78,6 +85,27 @@ def main():
             miss.append(int(np.count_nonzero(o != ref)))
         print(f"{name:28s} values {ref.size}: mismatches plain {miss[0]}, fma ascending {miss[1]}, "
               f"fma descending {miss[2]}")
+
+    # one-row products, one numpy call per point (dgemv): the "single" order (order 3)
+    m = 20_000
+    single = {"LMC:775 one point (R @ p.T).T + t": [], "CSIM:230 one point T @ [p, w]": []}
+    miss = {k: [0, 0] for k in single}
+    for i in range(m):
+        p = d3[i:i + 1]
+        for name, ref, A, X, add in (
+                ("LMC:775 one point (R @ p.T).T + t", (R @ p.T).T + t, R, p, t),
+                ("CSIM:230 one point T @ [p, w]", (T @ p4[i:i + 1].T).T[:, :3], T[:3], p4[i:i + 1], None)):
+            for j, order in enumerate((1, 3)):
+                o = run(A, X, order)
+                if add is not None:
+                    o = o + add
+                miss[name][j] += int(np.count_nonzero(o != ref))
+    for name, (asc, one) in miss.items():
+        print(f"{name:34s} values {3 * m}: mismatches fma ascending {asc}, single {one}")
+    # several rows: the ascending chain at every small count
+    small = [k for k in list(range(2, 70)) + [255, 256, 257, 1000]
+             if not np.array_equal(run(R, d3[:k], 1) + t, (R @ d3[:k].T).T + t)]
+    print("row counts 2..69, 255-257, 1000 not matching the ascending chain:", small)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@
 #   pmc     tools/pmc_traffic.py (deskew kernels, then --aux), profiles/pmc_traffic.json copied out
 #   latency tools/latency.py ($LAT_ARGS)
 #   prof    rocprofv3 --kernel-trace --stats of the same bench command
+#   probe   tools/issue_probe (issue cost of the codec kernels' vector / LDS instructions)
 # Usage (repo root, on the GPU box):  STEPS="tests ab" bash tools/gpu_session.sh <tag>
 set -u
 TAG=${1:-s}
@@ -82,6 +83,10 @@ for step in $STEPS; do
       python3 tools/roofline_from_trace.py --trace "$OUT/prof" --bench "$OUT/prof_bench.json" \
         --out "$OUT/roofline_trace.json" > /dev/null 2>> "$OUT/prof.err"
       echo "[roofline_from_trace] rc=$?" | tee -a "$OUT/steps.log" ;;
+    probe)
+      timeout -k 10 300 tools/issue_probe > "$OUT/issue_probe.json" 2> "$OUT/issue_probe.err"
+      stop_if_fault $? probe
+      cat "$OUT/issue_probe.json" ;;
     *) echo "unknown step $step" ;;
   esac
 done
