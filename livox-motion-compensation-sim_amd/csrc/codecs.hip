@@ -168,7 +168,10 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
   a.err = c->d_codec_err;
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    if (F > 0)
+    // frame headers: written by each frame's first unit (MC_LVX_FRAME_HDR), so this launch only when
+    // a frame has no points (and therefore no unit)
+    const bool empty_frame = std::any_of(counts, counts + F, [](int64_t n) { return n == 0; });
+    if (F > 0 && (!MC_LVX_FRAME_HDR || empty_frame))
       hipLaunchKernelGGL(k_lvx_frames, dim3((F + kCodecBlock - 1) / kCodecBlock), dim3(kCodecBlock), 0, c->stream,
                          a, (int64_t)0);
     if (n_pkg > 0)

@@ -22,12 +22,14 @@ sys.path.insert(0, ROOT)
 import mcamd as mc  # noqa: E402
 
 
-def setup(lib, counts, source="aos"):
+def setup(lib, counts, source="aos", flush_on=False):
     ctx = mc.Context(0, lib_path=lib)
     b = ctx.batch(counts)
     b.synth(seed=0, frame_id_base=1000)
-    src = ctx.device_buffer(int(counts.sum()) * 32)
-    b.fetch_aos_device(src)
+    src = None
+    if source == "aos":
+        src = ctx.device_buffer(int(counts.sum()) * 32)
+        b.fetch_aos_device(src)
     F = len(counts)
     pos = mc.codecs.lvx_layout(counts)
     lvx_out = ctx.device_buffer(int(pos[-1]))
@@ -54,7 +56,7 @@ def setup(lib, counts, source="aos"):
         mc._lib.check(ctx.lib.mc_pcd_encode(ctx.handle, src.ptr, 4, F, ptr(counts, c_int64), pcd_out.ptr, cap,
                                             ptr(bpos, c_int64)), "pcd_encode")
 
-    flush_buf = ctx.batch(np.full(len(counts), int(counts.max()), np.int64), with_time=True)
+    flush_buf = ctx.batch(np.full(len(counts), int(counts.max()), np.int64), with_time=True) if flush_on else None
 
     def flush():
         flush_buf.checksum()
@@ -76,10 +78,15 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the byte-identity check (diagnostic builds)")
     ap.add_argument("--source", default="aos", choices=["aos", "batch"],
                     help="encode from a device (N,4) float64 AoS array or from the batch's float32 columns")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="independent allocations per library (placement moves a kernel by a few %%); a "
+                         "library's figure is the median over its replicas' medians")
     args = ap.parse_args()
-    libs = [l for l in args.libs.split(",") if l]
+    base_libs = [l for l in args.libs.split(",") if l]
     counts = np.full(args.frames, args.points, np.int64)
-    arms = {lib: setup(lib, counts, args.source) for lib in libs}
+    # replicas alternate across libraries so that no variant gets all the early (or late) allocations
+    libs = [f"{lib}#{r}" if args.replicas > 1 else lib for r in range(args.replicas) for lib in base_libs]
+    arms = {arm: setup(arm.split("#")[0], counts, args.source, args.flush) for arm in libs}
     times = {lib: {"lvx": [], "pcd": []} for lib in libs}
     order = list(libs)
     rng = random.Random(1)
@@ -122,6 +129,15 @@ def main():
         out[name] = {k: {"median_us": statistics.median(v), "min_us": min(v)} for k, v in times[lib].items()}
         print(f"{name:22s} lvx median {out[name]['lvx']['median_us']:8.1f} us   pcd (measure+write) median "
               f"{out[name]['pcd']['median_us']:8.1f} us", flush=True)
+    if args.replicas > 1:
+        for lib in base_libs:
+            name = os.path.basename(lib)
+            per = {k: [out[f"{name}#{r}"][k]["median_us"] for r in range(args.replicas)] for k in ("lvx", "pcd")}
+            out[name] = {k: {"median_us": statistics.median(v), "replica_medians_us": v} for k, v in per.items()}
+            lvx_reps = ", ".join(f"{x:.1f}" for x in per["lvx"])
+            pcd_reps = ", ".join(f"{x:.1f}" for x in per["pcd"])
+            print(f"{name:22s} over {args.replicas} replicas: lvx {out[name]['lvx']['median_us']:8.1f} us ({lvx_reps})"
+                  f"   pcd {out[name]['pcd']['median_us']:8.1f} us ({pcd_reps})", flush=True)
     print(json.dumps(out))
     if bad:
         raise SystemExit(f"outputs differ from {os.path.basename(libs[0])}: {bad}")

@@ -4,11 +4,14 @@
 // cost.  Reported: shader cycles (s_memtime ticks) per wave-instruction per SIMD = one wave's
 // elapsed ticks / (its instructions x the waves sharing its SIMD).  LDS rows: one ds_write per
 // instruction at a lane stride of 16 bytes plus a byte misalignment (the PCD text stores are
-// unaligned 12-byte writes).
+// unaligned 12-byte writes).  LDS atomics need natural alignment: a ds_or_b64 at a 4-byte offset
+// aborts the queue (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION, profiles/round5/s03), so only
+// aligned atomics are probed.
 //   hipcc -O3 --offload-arch=gfx950 tools/issue_probe.hip -o tools/issue_probe && tools/issue_probe
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #define R8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #define P8(X) X(0, 8) X(1, 9) X(2, 10) X(3, 11) X(4, 12) X(5, 13) X(6, 14) X(7, 15)
@@ -95,13 +98,30 @@ template <int BITS, int MIS>
 __global__ __launch_bounds__(256) void k_lds(uint64_t* out, int iters) {
   __shared__ uint4 buf[256 + 2];
   const uint32_t a = (uint32_t)(uintptr_t)(reinterpret_cast<char*>(buf) + 16 * (threadIdx.x & 255) + MIS);
-  const uint32_t v0 = threadIdx.x;
+  uint32_t v0 = threadIdx.x;
   const uint64_t w64 = v0 * 3ull;
   const v3u w96 = {v0, v0 + 1, v0 + 2};
   const v4u w128 = {v0, v0 + 1, v0 + 2, v0 + 3};
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
     if constexpr (BITS == 8) asm volatile(W8("ds_write_b8") ::"v"(a), "v"(v0) : "memory");
+    if constexpr (BITS == 16) asm volatile(W8("ds_write_b16") ::"v"(a), "v"(v0) : "memory");
+    if constexpr (BITS == 33) asm volatile(W8("ds_or_b32") ::"v"(a), "v"(v0) : "memory");
+    if constexpr (BITS == 65) asm volatile(W8("ds_or_b64") ::"v"(a), "v"(w64) : "memory");
+    if constexpr (BITS == 34)
+      asm volatile("ds_write2_b32 %0, %1, %1 offset1:1\n\tds_write2_b32 %0, %1, %1 offset1:1\n\t"
+                   "ds_write2_b32 %0, %1, %1 offset1:1\n\tds_write2_b32 %0, %1, %1 offset1:1\n\t"
+                   "ds_write2_b32 %0, %1, %1 offset1:1\n\tds_write2_b32 %0, %1, %1 offset1:1\n\t"
+                   "ds_write2_b32 %0, %1, %1 offset1:1\n\tds_write2_b32 %0, %1, %1 offset1:1\n\t" ::"v"(a), "v"(v0)
+                   : "memory");
+    if constexpr (BITS == 129) {
+      v4u r0, r1;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2\n\tds_read_b128 %0, %2\n\tds_read_b128 %1, %2\n\t"
+                   "ds_read_b128 %0, %2\n\tds_read_b128 %1, %2\n\tds_read_b128 %0, %2\n\tds_read_b128 %1, %2\n\t"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=v"(r0), "=v"(r1) : "v"(a) : "memory");
+      v0 += r0.x + r1.y;
+    }
     if constexpr (BITS == 32) asm volatile(W8("ds_write_b32") ::"v"(a), "v"(v0) : "memory");
     if constexpr (BITS == 64) asm volatile(W8("ds_write_b64") ::"v"(a), "v"(w64) : "memory");
     if constexpr (BITS == 96) asm volatile(W8("ds_write_b96") ::"v"(a), "v"(w96) : "memory");
@@ -110,6 +130,7 @@ __global__ __launch_bounds__(256) void k_lds(uint64_t* out, int iters) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0) out[2 * (blockIdx.x * 4 + (threadIdx.x >> 6))] = t1 - t0;
+  if (v0 == 0xdeadbeefu) out[1] = v0;
 }
 
 template <int BITS, int MIS>
@@ -117,12 +138,15 @@ static void run_lds(uint64_t* d_out, uint64_t* h_out, int blocks, int wps, int i
   for (int rep = 0; rep < 2; ++rep) {
     const int n = rep ? iters : 4;
     hipLaunchKernelGGL((k_lds<BITS, MIS>), dim3(blocks), dim3(256), 0, 0, d_out, n);
-    hipDeviceSynchronize();
+    if (hipDeviceSynchronize() != hipSuccess) {   // e.g. a misaligned LDS atomic: stop, report nothing more
+      fprintf(stderr, "ds %d misaligned %d: kernel failed\n", BITS, MIS);
+      exit(3);
+    }
     if (!rep) continue;
     hipMemcpy(h_out, d_out, sizeof(uint64_t) * 2 * blocks * 4, hipMemcpyDeviceToHost);
     double sum = 0;
     for (int w = 0; w < blocks * 4; ++w) sum += (double)h_out[2 * w];
-    printf("{\"op\": \"ds_write_b%d misaligned %d\", \"ticks_per_wave_instr_per_cu\": %.2f}\n", BITS, MIS,
+    printf("{\"op\": \"ds %d (8/16/32/64/96/128: write_bN, 33: or_b32, 65: or_b64, 34: write2_b32, 129: read_b128) misaligned %d\", \"ticks_per_wave_instr_per_cu\": %.2f}\n", BITS, MIS,
            sum / (blocks * 4) / ((double)n * 8 * wps * 4));
   }
 }
@@ -130,7 +154,10 @@ static void run_lds(uint64_t* d_out, uint64_t* h_out, int blocks, int wps, int i
 template <int OP>
 static double run_valu(uint64_t* d_out, uint64_t* h_out, int blocks, int wps, int iters) {
   hipLaunchKernelGGL(k_valu<OP>, dim3(blocks), dim3(256), 0, 0, d_out, iters, 12345u);
-  hipDeviceSynchronize();
+  if (hipDeviceSynchronize() != hipSuccess) {
+    fprintf(stderr, "%s: kernel failed\n", kNames[OP]);
+    exit(3);
+  }
   hipMemcpy(h_out, d_out, sizeof(uint64_t) * 2 * blocks * 4, hipMemcpyDeviceToHost);
   double sum = 0;
   for (int w = 0; w < blocks * 4; ++w) sum += (double)h_out[2 * w];
@@ -161,6 +188,17 @@ int main() {
   all_ops<0>(d_out, h_out, blocks, wps, 2000);
   // LDS: wps workgroups of 4 waves per CU (4 KB each) share the CU's LDS pipe (ticks per wave-instruction per CU)
   run_lds<8, 0>(d_out, h_out, blocks, wps, 500);
+  run_lds<8, 1>(d_out, h_out, blocks, wps, 500);
+  run_lds<16, 0>(d_out, h_out, blocks, wps, 500);
+  run_lds<16, 2>(d_out, h_out, blocks, wps, 500);
+  run_lds<33, 0>(d_out, h_out, blocks, wps, 500);
+  run_lds<33, 4>(d_out, h_out, blocks, wps, 500);
+  run_lds<65, 0>(d_out, h_out, blocks, wps, 500);
+  run_lds<34, 0>(d_out, h_out, blocks, wps, 500);
+  run_lds<34, 4>(d_out, h_out, blocks, wps, 500);
+  run_lds<129, 0>(d_out, h_out, blocks, wps, 500);
+  run_lds<129, 4>(d_out, h_out, blocks, wps, 500);
+  run_lds<129, 1>(d_out, h_out, blocks, wps, 500);
   run_lds<32, 0>(d_out, h_out, blocks, wps, 500);
   run_lds<64, 0>(d_out, h_out, blocks, wps, 500);
   run_lds<64, 4>(d_out, h_out, blocks, wps, 500);
