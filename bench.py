@@ -520,7 +520,7 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     alg = 16 * n_rank + int(pos[-1])
     rep["lvx"] = {"file_bytes": int(pos[-1]), "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
                   "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
-                  "bytes_per_point": alg / n_rank, "traffic_over_algorithmic": aux_traffic("k_lvx_units", "k_lvx_packages")}
+                  "bytes_per_point": alg / n_rank, "traffic_over_algorithmic": aux_traffic("k_lvx_packages")}
     bpos = np.zeros(F + 1, np.int64)
     cap = n_rank * 48
     out = ctx.device_buffer(cap)

@@ -168,14 +168,14 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
   a.err = c->d_codec_err;
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
-    // frame headers: written by each frame's first unit (MC_LVX_FRAME_HDR), so this launch only when
-    // a frame has no points (and therefore no unit)
+    // frame headers: each frame's first unit writes its own, so this launch only when a frame has no
+    // points (and therefore no unit)
     const bool empty_frame = std::any_of(counts, counts + F, [](int64_t n) { return n == 0; });
-    if (F > 0 && (!MC_LVX_FRAME_HDR || empty_frame))
+    if (F > 0 && empty_frame)
       hipLaunchKernelGGL(k_lvx_frames, dim3((F + kCodecBlock - 1) / kCodecBlock), dim3(kCodecBlock), 0, c->stream,
                          a, (int64_t)0);
     if (n_pkg > 0)
-      hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kLvxNT), 0, c->stream, a);
+      hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
   }
   HIPCHK(hipGetLastError());
   int err = 0;

@@ -47,9 +47,6 @@ static_assert(kLvxUnitPoints % kCodecBlock == 0, "unit = whole blocks");
 #ifndef MC_PCD_MEASURE_SCALAR
 #define MC_PCD_MEASURE_SCALAR 1   // float32 measure pass: wave-uniform tile arithmetic (scalar), DPP wave sum
 #endif
-#ifndef MC_PCD_NOBAR
-#define MC_PCD_NOBAR 0       // packed PCD write pass: no barrier after a tile's stores (pcd_tile_store)
-#endif
 #ifndef MC_PCD_TILES_PER_WG
 #define MC_PCD_TILES_PER_WG 4   // 4 / 8 / 16 / 32: 1048.0 / 1023.5 / 1029.2 / 1054.9 us (profiles/round2/s26,
                                 // XCD unit order); in the dealt order 4 wins: write pass 788.0 / 741.0 vs
@@ -124,48 +121,12 @@ __device__ __forceinline__ int32_t codec_advance(const int64_t* __restrict__ uni
   return f;
 }
 
-// Single naturally aligned LDS stores the compiler may not merge into wider (misaligned) ones:
-// volatile stores through LDS-address-space pointers (ds_write_b16 / ds_write_b32)
-typedef __attribute__((address_space(3))) volatile uint16_t lds_v16;
-typedef __attribute__((address_space(3))) volatile uint32_t lds_v32;
-__device__ __forceinline__ void lds_st16(void* p, uint16_t v) { *(lds_v16*)p = v; }
-__device__ __forceinline__ void lds_st32(void* p, uint32_t v) { *(lds_v32*)p = v; }
-
-// Codec stores and loads (A/B knobs).  MC_CODEC_ST: a text / record chunk's 16-byte store, 1 = nt
-// (builtin), 2 = sc1 write-through (inline asm + s_nop 1, as st_pol<2> in kernels.hpp: the data VGPRs
-// are read after issue).  MC_CODEC_LD: 1 = the batch-source point loads non-temporal.  MC_CODEC_EDGE:
-// 1 = a piece's partial end chunks stored by 32 lanes at once, one byte each (0: a byte loop in one
-// lane per end).
-#ifndef MC_CODEC_ST
-#define MC_CODEC_ST 1
-#endif
-#ifndef MC_CODEC_LD
-#define MC_CODEC_LD 0
-#endif
-#ifndef MC_CODEC_EDGE
-#define MC_CODEC_EDGE 0
-#endif
+// A text / record chunk's 16-byte store: non-temporal (sc1 write-through, the deskew kernels' policy:
+// LVX 336.6 vs 304.3 us, PCD measure + write 1065.4 vs 798.9 us, profiles/round5/s02; non-temporal
+// point loads: LVX +-0, PCD 776.0 vs 772.5-798.9 us across identical builds — not taken)
 typedef unsigned int codec_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void codec_st16(char* p, const uint4& v) {
-  codec_v4u t = {v.x, v.y, v.z, v.w};
-  if constexpr (MC_CODEC_ST == 2) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(t) : "memory");
-  } else {
-    __builtin_nontemporal_store(t, reinterpret_cast<codec_v4u*>(p));
-  }
-}
-__device__ __forceinline__ float codec_ld(const float* p) {
-  if constexpr (MC_CODEC_LD == 1) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-__device__ __forceinline__ float4 codec_ld4(const float* p) {
-  if constexpr (MC_CODEC_LD == 1) {
-    typedef float v4f_ __attribute__((ext_vector_type(4)));
-    const v4f_ t = __builtin_nontemporal_load(reinterpret_cast<const v4f_*>(p));
-    return make_float4(t.x, t.y, t.z, t.w);
-  } else {
-    return *reinterpret_cast<const float4*>(p);
-  }
+  __builtin_nontemporal_store(codec_v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<codec_v4u*>(p));
 }
 // bytes of LDS [lo, hi) outside the full chunks [f0, f1) (the partial end chunks) -> g, lanes t < 32
 // of the workgroup, one byte each: lanes 0-15 the head chunk lo / 16, lanes 16-31 the tail chunk hi / 16
@@ -181,16 +142,14 @@ __device__ __forceinline__ void codec_store_edges(char* __restrict__ g, const ch
 
 // Store LDS bytes [lo, hi) to g + [lo, hi), where lds and g agree modulo 16: whole 16-byte chunks
 // with dwordx4 stores, the partial chunks at either end byte by byte.  All threads participate.
+// MAXCH > 0: the piece holds at most MAXCH chunks; each lane issues all of its LDS chunk reads before
+// its first store (the loop waits for every read) and 32 lanes store the end bytes at once (LVX 293.0
+// vs 296.0 us, profiles/round5/s04).  MAXCH = 0: a loop (the byte path's pieces vary in size).
 // (Partial chunks from one 16-byte LDS read + predicated byte stores: 50 instead of 56 VGPRs in the
 // LVX kernel but LVX 310.4 vs 308.2, PCD 808.4 vs 803.3 us, profiles/round4/s12: not taken.)
-// MAXCH > 0 (with MC_CODEC_STORE_UNROLL): the piece holds at most MAXCH chunks; each lane issues all
-// of its LDS chunk reads before its first store, and the end bytes go out 32 lanes at once.
-#ifndef MC_CODEC_STORE_UNROLL
-#define MC_CODEC_STORE_UNROLL 0
-#endif
 template <int NT = kCodecBlock, int MAXCH = 0>   // NT: threads of the workgroup
 __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const char* lds, int lo, int hi) {
-  if constexpr (MC_CODEC_STORE_UNROLL && MAXCH > 0) {
+  if constexpr (MAXCH > 0) {
     const int f0 = (lo + 15) >> 4, f1 = hi >> 4;
     constexpr int kIt = (MAXCH + NT - 1) / NT;
     uint4 v[kIt];
@@ -204,12 +163,6 @@ __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const ch
       const int c = f0 + (int)threadIdx.x + u * NT;
       if (c < f1) codec_st16(g + 16 * c, v[u]);
     }
-    codec_store_edges(g, lds, lo, hi, f0, f1, (int)threadIdx.x);
-    return;
-  }
-  if constexpr (MC_CODEC_EDGE == 1) {
-    const int f0 = (lo + 15) >> 4, f1 = hi >> 4;
-    for (int c = f0 + (int)threadIdx.x; c < f1; c += NT) codec_st16(g + 16 * c, *reinterpret_cast<const uint4*>(lds + 16 * c));
     codec_store_edges(g, lds, lo, hi, f0, f1, (int)threadIdx.x);
     return;
   }
@@ -245,35 +198,27 @@ __device__ __forceinline__ int32_t lvx_fixed(double v, double scale, double lo, 
 
 // MC_LVX_DIAG (diagnostic builds only, wrong output): 1 = no point loads (records formed from the slot
 // index), 2 = no HBM stores (the assembled LDS piece is read but only a never-true test of it stores),
-// 3 = both.  Naming the packer's limiter: its time with each part removed (tools/ab_codecs.py).
+// 3 = both.  Naming the packer's limiter: its time with each part removed (tools/ab_codecs.py,
+// profiles/round5/s02: 196.0 / 186.6 / 117.1 vs 304.3 us).
 #ifndef MC_LVX_DIAG
 #define MC_LVX_DIAG 0
 #endif
-#ifndef MC_LVX_FRAME_HDR
-#define MC_LVX_FRAME_HDR 0
-#endif
-#ifndef MC_LVX_PRELOAD
-#define MC_LVX_PRELOAD 0
-#endif
-#ifndef MC_LVX_ALIGNED
-#define MC_LVX_ALIGNED 0     // records as naturally aligned LDS stores (b16 + 3 x b32) instead of b96 + b16
-#endif
 // One unit = up to 8 consecutive packages of one frame = one contiguous byte range of the file.
 // Phase 1: a thread per point slot writes its 14-byte record (7 halfwords, zero for the padding
-// slots of the last package, LMC:245-248) and threads 0..k*11 the 22-byte package headers
-// (LMC:204-237) into LDS.  Phase 2: codec_store_piece.
+// slots of the last package, LMC:245-248), threads 0..k*11 the 22-byte package headers
+// (LMC:204-237) and, in a frame's first unit, threads 96..107 the frame header (LMC:178-193: own
+// offset, next frame's offset, frame id) into LDS.  Phase 2: codec_store_piece.  k_lvx_frames writes
+// the headers of frames without points (they have no unit).  Folding the frame headers in removed a
+// launch: 296.0 vs 302.2 us (profiles/round5/s04).
 // Rejected (tools/ab_codecs.py --source batch): 2 / 4 / 8 units per workgroup with the next unit's
 // points loaded while one is stored (305.0 vs 333.9-356.4 us, profiles/round3/s69); a batch-only unit
 // kernel with 32-bit scalar unit arithmetic, all 12 loads of a lane up front and branch-free records
-// (336.8 vs 306.8 us, profiles/round5/s01).
-// MC_LVX_NT: threads per workgroup (256: three points per thread, one after the other — each lane's
-// loads wait before the next point's are issued; 768: one point per thread, all loads at once)
-#ifndef MC_LVX_NT
-#define MC_LVX_NT 256
-#endif
-constexpr int kLvxNT = MC_LVX_NT;
-static_assert(kLvxNT % 64 == 0 && kLvxNT >= kLvxPkgPerWG * (kLvxPkgHdr / 2), "whole waves; one header halfword per thread");
-__global__ __launch_bounds__(kLvxNT) void k_lvx_packages(const LvxArgs a) {
+// (336.8 vs 306.8 us, profiles/round5/s01); 768 / 512 threads per workgroup (497.8 / 384.6 vs 304.3
+// us, s02); records as naturally aligned LDS stores instead of the compiler's ds_write_b96 at 2-byte
+// alignment (303.5 vs 305.3, s03) and with every point load issued up front (301.2; 315.4 vs 293.0
+// on top of the folded headers and unrolled stores, s04).
+__global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
+  static_assert(kCodecBlock >= 96 + 12 && kLvxPkgPerWG * (kLvxPkgHdr / 2) <= 96, "header threads");
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
   const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
@@ -285,35 +230,16 @@ __global__ __launch_bounds__(kLvxNT) void k_lvx_packages(const LvxArgs a) {
   const int k = (int)((fpkgs - pkg0) < kLvxPkgPerWG ? (fpkgs - pkg0) : kLvxPkgPerWG);
   const int64_t rem = fcount - pkg0 * kLvxPkgPoints;
   const int n = (int)(rem < k * kLvxPkgPoints ? rem : k * kLvxPkgPoints);
-  // a frame's first unit also writes the frame header (LMC:178-193) ahead of its packages
-  // (MC_LVX_FRAME_HDR; k_lvx_frames then runs only for frames without points)
-  const int hdr = (MC_LVX_FRAME_HDR && pkg0 == 0) ? kLvxFrameHdr : 0;
+  const int hdr = pkg0 == 0 ? kLvxFrameHdr : 0;                            // frame header bytes first
   const int64_t S = a.frame_pos[f] + kLvxFrameHdr + pkg0 * kLvxPkg - hdr;   // piece start, even
   const int shift = (int)(S & 15) + hdr;                                    // LDS offset of the first package
   const uint64_t ts = a.ts_ns[f];
   const bool hi = a.has_int ? a.has_int[f] != 0 : a.src.ld > 3;
   const int64_t row0 = frow + pkg0 * kLvxPkgPoints;
-  // MC_LVX_PRELOAD (batch source): every point load of the workgroup's unit issued before the first
-  // record is formed (otherwise each pass of the loop waits for its own loads)
-  constexpr int kIt = (kLvxUnitPoints + kLvxNT - 1) / kLvxNT;
-  float pv[MC_LVX_PRELOAD ? kIt : 1][4];
-  const bool pre = MC_LVX_PRELOAD && a.src.cols != nullptr && !(MC_LVX_DIAG & 1);
-  if (pre) {
-    const int64_t p0 = ldu(a.src.poff + f) + pkg0 * kLvxPkgPoints;   // padded row of the unit's first point
-#pragma unroll
-    for (int j = 0; j < (MC_LVX_PRELOAD ? kIt : 1); ++j) {
-      const int i = j * kLvxNT + (int)threadIdx.x;
-      if (i < n) {
-        const float* q = a.src.cols + bidx(a.src.C, 0, p0 + i);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) pv[j][c] = q[c * kBlkPts];
-      }
-    }
-  }
 
 #pragma unroll
-  for (int j = 0; j < kIt; ++j) {
-    const int i = j * kLvxNT + (int)threadIdx.x;
+  for (int j = 0; j < kLvxSlots; ++j) {   // a unit's 768 slots: three passes of the workgroup
+    const int i = j * kCodecBlock + (int)threadIdx.x;
     if (i >= k * kLvxPkgPoints) break;
     const int pk = i / kLvxPkgPoints, slot = i - pk * kLvxPkgPoints;
     uint16_t* r = s16 + ((shift + pk * kLvxPkg + kLvxPkgHdr + slot * kLvxRec) >> 1);
@@ -322,41 +248,20 @@ __global__ __launch_bounds__(kLvxNT) void k_lvx_packages(const LvxArgs a) {
       x = (uint32_t)i; y = x * 3u; z = x ^ 0x5555u; refl = x & 255u;
     } else if (i < n) {
       double v[4];
-      if (MC_LVX_PRELOAD && pre) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = pv[MC_LVX_PRELOAD ? j : 0][c];
-      } else {
-        codec_point(a.src, f, row0 + i, v);
-      }
+      codec_point(a.src, f, row0 + i, v);
       x = (uint32_t)lvx_fixed(v[0], 1000.0, -2147483648.0, 2147483647.0, a.err);
       y = (uint32_t)lvx_fixed(v[1], 1000.0, -2147483648.0, 2147483647.0, a.err);
       z = (uint32_t)lvx_fixed(v[2], 1000.0, -2147483648.0, 2147483647.0, a.err);
       refl = hi ? (uint32_t)lvx_fixed(v[3], 255.0, 0.0, 255.0, a.err) : 128u;   // tag byte 0
     }
-    if constexpr (MC_LVX_ALIGNED) {
-      // naturally aligned LDS stores only: a record starts at 0 or 2 mod 4 (14-byte records), so it is
-      // one halfword and three dwords either way (a misaligned 8 / 12-byte LDS store costs 6-8x an
-      // aligned one on gfx950, tools/issue_probe.hip, profiles/round5/s02)
-      char* const b = reinterpret_cast<char*>(r);
-      const bool odd = (reinterpret_cast<uintptr_t>(b) & 2) != 0;
-      const uint32_t w0 = odd ? __builtin_amdgcn_perm(y, x, 0x05040302u) : x;      // x_hi | y_lo, or x
-      const uint32_t w1 = odd ? __builtin_amdgcn_perm(z, y, 0x05040302u) : y;
-      const uint32_t w2 = odd ? __builtin_amdgcn_perm(refl, z, 0x05040302u) : z;
-      char* const d = odd ? b + 2 : b;
-      lds_st16(odd ? b : b + 12, (uint16_t)(odd ? x : refl));
-      lds_st32(d, w0);
-      lds_st32(d + 4, w1);
-      lds_st32(d + 8, w2);
-    } else {
-      r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
-      r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
-      r[4] = (uint16_t)z; r[5] = (uint16_t)(z >> 16);
-      r[6] = (uint16_t)refl;
-    }
+    r[0] = (uint16_t)x; r[1] = (uint16_t)(x >> 16);
+    r[2] = (uint16_t)y; r[3] = (uint16_t)(y >> 16);
+    r[4] = (uint16_t)z; r[5] = (uint16_t)(z >> 16);
+    r[6] = (uint16_t)refl;
   }
   // dev 0, version 5 | slot 0, lidar 1 | reserved, status (4 B) | ts type 1 | data type 2 |
   // reserved (3 B) | timestamp (8 B)
-  for (int h = threadIdx.x; h < k * (kLvxPkgHdr / 2); h += kLvxNT) {
+  for (int h = threadIdx.x; h < k * (kLvxPkgHdr / 2); h += kCodecBlock) {
     const int pk = h / (kLvxPkgHdr / 2), w = h - pk * (kLvxPkgHdr / 2);
     uint32_t v;
     switch (w) {
@@ -381,8 +286,8 @@ __global__ __launch_bounds__(kLvxNT) void k_lvx_packages(const LvxArgs a) {
     if (v.x == 0x7eadbeefu && v.y == 0x7eadbeefu) a.out[S] = 1;
     return;
   }
-  codec_store_piece<kLvxNT, kLvxLds / 16 + 1>(a.out + (S - (shift - hdr)), reinterpret_cast<const char*>(s_buf),
-                                              shift - hdr, shift + k * kLvxPkg);
+  codec_store_piece<kCodecBlock, kLvxLds / 16 + 1>(a.out + (S - (shift - hdr)), reinterpret_cast<const char*>(s_buf),
+                                                   shift - hdr, shift + k * kLvxPkg);
 }
 
 // LMC:178-193: frame header = own offset, next frame's offset (0 for the last), frame_id
@@ -735,27 +640,16 @@ __device__ __forceinline__ int pcd_fast_len_f32(const float c[4]) {
 // The products are 24-bit multiply-adds (v_mad_i32_i24 by __mul24 with a negative constant, no
 // range masks).  Against the two 3-digit halves in 32-bit SWAR: 802.8 vs 806.8 us measure + write
 // (profiles/round4/s17).
-// MC_PCD_MULHI=1: the three quotients as one v_mul_hi_u32 each (ceil(2^32 / d) is exact for these
-// ranges: the excess adds < 1e-7 to quotients whose fraction is at most 1 - 1 / d) — gfx950 issues
-// v_mul_hi_u32 at the 24-bit multiplies' rate (tools/issue_probe.hip, profiles/round5/s02), so a
-// multiply + shift (or mask + multiply) becomes one instruction.
-#ifndef MC_PCD_STORE_UNROLL
-#define MC_PCD_STORE_UNROLL 0   // a tile's chunk stores: all LDS reads first, then the stores; parallel end bytes
-#endif
-#ifndef MC_PCD_MULHI
-#define MC_PCD_MULHI 0
-#endif
 __device__ __forceinline__ void digit_groups(uint32_t N, uint32_t ip, uint32_t& g01, uint32_t& g23, uint32_t& g4) {
   const uint32_t fp = N + (uint32_t)__mul24((int)ip, -1000000);                         // < 10^6
-  uint32_t g2 = MC_PCD_MULHI ? __umulhi(fp, 429497u)                                    // fp / 10^4
-                             : (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32);
+  uint32_t g2 = (uint32_t)(((uint64_t)(fp & 0xFFFFFu) * 429497ull) >> 32);             // fp / 10^4
   // opaque to the optimiser: it recognises fp - (fp / 10^4) 10^4 as fp % 10^4 and lowers that
   // through a quarter-rate 64-bit multiply-add
   asm("" : "+v"(g2));
   const uint32_t r4 = fp + (uint32_t)__mul24((int)g2, -10000);                          // < 10^4
-  const uint32_t g3 = MC_PCD_MULHI ? __umulhi(r4, 42949673u) : __umul24(r4, 5243u) >> 19;   // r4 / 100
+  const uint32_t g3 = __umul24(r4, 5243u) >> 19;                                        // r4 / 100
   g4 = r4 - g3 * 100u;
-  const uint32_t g0 = MC_PCD_MULHI ? __umulhi(ip, 42949673u) : __umul24(ip, 5243u) >> 19;   // ip / 100
+  const uint32_t g0 = __umul24(ip, 5243u) >> 19;                                        // ip / 100
   const uint32_t g1 = ip - g0 * 100u;
   g01 = g0 | (g1 << 16);
   g23 = g2 | (g3 << 16);
@@ -814,98 +708,42 @@ __device__ __forceinline__ void pcd_text(const PcdFast& P, PcdText& T) {
   T.len = len;
 }
 
-// One packed line at byte `off` of the tile text; the fields go to LDS as bytes at their final
-// offsets (the compiler merges them into unaligned ds_write_b64 / b96).  Values 3, 2, 1 are written
-// in that order, each storing its 4-digit field and a '-' unconditionally (at most 5 bytes before its
-// '.'): bytes left of its own head fall inside the previous value of the same line, which is written
-// afterwards and overwrites them.  Value 0 stores exactly its own bytes, so no lane ever writes
-// another line's text: no zeroing, no atomics.  (Value 0's integer text as one unaligned 8-byte
-// store at the line start, spilling into its own fraction: 3 fewer VALU instructions per line but
-// +11 % LDS-active cycles, measure + write 817.8 vs 775.2 us, profiles/round4/s24 — not taken.)
-__device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, int off) {
-  int pa[4];   // the '.' of each value
-  pa[0] = off + 4 + T.d[0];
-#pragma unroll
-  for (int k = 1; k < 4; ++k) pa[k] = pa[k - 1] + 12 + T.d[k];
-#pragma unroll
-  for (int k = 3; k >= 1; --k) {
-    uint8_t* const q = base + pa[k];
-    put4(q - 4, T.D[k]);
-    put4(q, T.A[k]);
-    put4(q + 4, T.B[k]);
-    // value k starts at pa[k - 1] + 8: its '-', or (positive) the previous value's separator slot,
-    // which that value rewrites afterwards
-    base[pa[k - 1] + 7 + T.ng[k]] = '-';
-  }
-  uint8_t* const q = base + pa[0];
-  put4(q, T.A[0]);
-  put4(q + 4, T.B[0]);
-  const uint32_t D = T.D[0];
-  q[-1] = (uint8_t)(D >> 24);
-  if (T.q0 <= 2) q[-2] = (uint8_t)(D >> 16);
-  if (T.q0 <= 1) q[-3] = (uint8_t)(D >> 8);
-  if (T.q0 == 0) q[-4] = (uint8_t)D;
-  if (T.ng[0]) base[off] = '-';
-}
-
-#ifndef MC_PCD_OR
-#define MC_PCD_OR 0      // 1: ds_or_b32 text assembly, 2: ds_or_b64 (0: unaligned text stores)
-#endif
-// MC_PCD_OR: the same line as OR-ed, naturally aligned dwords into a zeroed text buffer — unaligned
-// 8 / 12-byte LDS stores cost 6-8x an aligned store on gfx950 (tools/issue_probe.hip,
-// profiles/round5/s02).  Value k's 13 bytes from its sign slot (the '.' at pa - 5 + 5: sign or zero,
-// the integer digits with leading zeros blanked, ". d1 d2 d3", "d4 d5 d6 sep") shifted to the dword
-// grid: 4 ds_or_b32 whose zero bytes leave the neighbours' text (other values of the line, other
-// lanes' lines) untouched.  base is 16 bytes into the buffer (value 0's window may start up to 5
-// bytes before the line).
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-__device__ __forceinline__ void lds_or32(uint8_t* p, uint32_t v) {
-  __hip_atomic_fetch_or((lds_u32*)(void*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
+// One packed line at byte `off` of the tile text, OR-ed into the zeroed text buffer (pcd_tile_text) as
+// naturally aligned 8-byte words: value k's 16 bytes [pa - 8, pa + 8) — H = the 8 bytes ending at its
+// '.' (zeros, its '-' if negative, its integer digits with the leading zeros blanked), then A, B —
+// shifted to the 8-byte grid are three ds_or_b64 whose zero bytes leave the neighbours' text (the
+// line's other values, other lanes' lines) untouched.  Naturally aligned LDS stores issue at 4.6
+// ticks per wave-instruction, the unaligned 8 / 12-byte stores of byte-offset text at 36
+// (tools/issue_probe.hip, profiles/round5/s02); against those stores (values 3..1 as unaligned
+// 12-byte fields overwriting each other's heads, value 0 byte by byte): measure + write 772.1 / 782.5
+// vs 788.7 / 793.5 us, fused write pass 630.9 / 635.2 vs 639.8 / 642.7 us (profiles/round5/s03, s04;
+// ds_or_b32 on 4-byte words ran alike but took more VALU).  base is 16 bytes into the buffer (value
+// 0's window starts up to 7 bytes before its line).
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 __device__ __forceinline__ void lds_or64(uint8_t* p, uint64_t v) {
   __hip_atomic_fetch_or((lds_u64*)(void*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// MC_PCD_OR=2: 8-byte granules.  Value k's 16 bytes [pa - 8, pa + 8): H = 8 bytes ending at its '.'
-// (sign or zero, blanked leading zeros, the digits), then A | B; shifted to the qword grid: 3 ds_or_b64.
-__device__ __forceinline__ void pcd_emit_line_or64(const PcdText& T, uint8_t* base, int off) {
-  int pa = off + 4 + T.d[0];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (k > 0) pa += 12 + T.d[k];
-    const int q = T.ng[k] - T.d[k];
-    const uint32_t Dm = T.D[k] & (0xFFFFFFFFu << (8 * q));
-    const uint64_t H = ((uint64_t)Dm << 32) | ((uint64_t)(T.ng[k] ? 0x2Du : 0u) << (24 + 8 * q));
-    const uint64_t AB = ((uint64_t)T.B[k] << 32) | T.A[k];
-    const int s0 = pa - 8, r = s0 & 7;
-    uint8_t* const w = base + (s0 - r);
-    const int sh = 8 * r;   // 0 .. 56
-    lds_or64(w, H << sh);
-    lds_or64(w + 8, sh ? (AB << sh) | (H >> (64 - sh)) : AB);
-    lds_or64(w + 16, sh ? AB >> (64 - sh) : 0ull);
-  }
+// one value whose '.' is at byte pa: D its 4 integer digit characters, q of them leading zeros, ng 1
+// if negative
+__device__ __forceinline__ void pcd_emit_value(uint8_t* base, int pa, uint32_t D, uint32_t A, uint32_t B, int q,
+                                               int ng) {
+  const uint32_t Dm = D & (0xFFFFFFFFu << (8 * q));
+  const uint64_t H = ((uint64_t)Dm << 32) | ((uint64_t)(ng ? 0x2Du : 0u) << (24 + 8 * q));
+  const uint64_t AB = ((uint64_t)B << 32) | A;
+  const int s0 = pa - 8, r = s0 & 7;
+  uint8_t* const w = base + (s0 - r);   // 8-byte aligned
+  const int sh = 8 * r;                 // 0 .. 56
+  // x >> (64 - sh) as (x >> 8) >> (56 - sh): zero at sh = 0 (one 64-bit shift takes its amount mod 64)
+  lds_or64(w, H << sh);
+  lds_or64(w + 8, (AB << sh) | ((H >> 8) >> (56 - sh)));
+  lds_or64(w + 16, (AB >> 8) >> (56 - sh));
 }
-__device__ __forceinline__ void pcd_emit_line_or(const PcdText& T, uint8_t* base, int off) {
-  if constexpr (MC_PCD_OR == 2) { pcd_emit_line_or64(T, base, off); return; }
+__device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, int off) {
   int pa = off + 4 + T.d[0];   // the '.' of value k
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (k > 0) pa += 12 + T.d[k];
-    const int q = T.ng[k] - T.d[k];                                  // leading zero digits (0..3)
-    uint32_t Dm = T.D[k] & (0xFFFFFFFFu << (8 * q));
-    const uint32_t sgn = T.ng[k] ? 0x2Du : 0u;
-    Dm |= q > 0 ? sgn << (8 * (q - 1)) : 0u;                        // '-' inside the digit dword
-    const uint32_t S = q > 0 ? 0u : sgn;                             // '-' before 4 integer digits
-    // E = the 16 bytes from pa - 5: S, Dm, A, B, then zeros
-    const uint32_t E0 = S | (Dm << 8), E1 = __builtin_amdgcn_alignbyte(T.A[k], Dm, 3),
-                   E2 = __builtin_amdgcn_alignbyte(T.B[k], T.A[k], 3), E3 = T.B[k] >> 24;
-    const int s0 = pa - 5, r = s0 & 3;
-    uint8_t* const w = base + (s0 - r);
-    const uint32_t sh = 32 - 8 * r;   // 32 (r = 0) .. 8
-    lds_or32(w, E0 << (8 * r));
-    lds_or32(w + 4, (uint32_t)((((uint64_t)E1 << 32) | E0) >> sh));
-    lds_or32(w + 8, (uint32_t)((((uint64_t)E2 << 32) | E1) >> sh));
-    lds_or32(w + 12, (uint32_t)((((uint64_t)E3 << 32) | E2) >> sh));
+    pcd_emit_value(base, pa, T.D[k], T.A[k], T.B[k], T.ng[k] - T.d[k], T.ng[k]);
   }
 }
 
@@ -979,7 +817,7 @@ __device__ __forceinline__ void pcd_measure_waves(const PcdArgs& a, int64_t u0) 
       // the whole block is allocated (frames are padded to blocks): every lane loads, results past
       // the frame's end are ignored below
 #pragma unroll
-      for (int c = 0; c < 4; ++c) V[j][c] = codec_ld4(q + c * kBlkPts);
+      for (int c = 0; c < 4; ++c) V[j][c] = *reinterpret_cast<const float4*>(q + c * kBlkPts);
     }
   }
 #pragma unroll
@@ -1063,21 +901,15 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 // modulo 16), then stored with codec_store_piece.  Tiles flagged slow are skipped
 // (k_pcd_write_bytes writes them).  A packed line is at most 52 bytes, so a tile's text always fits.
 // pcd_tile_text: the tile's lines in LDS, -> the tile's text bytes; pcd_tile_store: its stores.
-constexpr int kPcdTextLead = MC_PCD_OR ? 1 : 0;   // uint4 chunks before the text (pcd_emit_line_or)
+constexpr int kPcdTextLead = 1;   // uint4 chunks before the text (pcd_emit_line's windows start early)
 constexpr int kPcdTextChunks = kPcdPackedText / 16 + 1 + kPcdTextLead;
 __device__ __forceinline__ int pcd_tile_text(const PcdText& T, bool valid, int64_t G, int* s_wave, uint4* s_text4) {
-  if constexpr (MC_PCD_OR) {
-    // the buffer is zeroed before the scan's barrier; the previous tile's reads of it ended before the
-    // barrier that closed its stores (pcd_tile_store, MC_PCD_NOBAR=0)
-    for (int c = threadIdx.x; c < kPcdTextChunks; c += kPcdBlock) s_text4[c] = make_uint4(0u, 0u, 0u, 0u);
-  }
+  // the buffer is zeroed before the scan's barrier; the previous tile's reads of it ended before the
+  // barrier that closed its stores (pcd_tile_store)
+  for (int c = threadIdx.x; c < kPcdTextChunks; c += kPcdBlock) s_text4[c] = make_uint4(0u, 0u, 0u, 0u);
   int total;
   const int excl = block_scan(T.len, s_wave, total) - T.len;
-  if constexpr (MC_PCD_OR) {
-    if (valid) pcd_emit_line_or(T, reinterpret_cast<uint8_t*>(s_text4 + kPcdTextLead), (int)(G & 15) + excl);
-  } else {
-    if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text4), (int)(G & 15) + excl);
-  }
+  if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text4 + kPcdTextLead), (int)(G & 15) + excl);
   __syncthreads();
   return total;
 }
@@ -1088,26 +920,10 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
   char* const g = a.out + (G - lo);
   const char* const lds = reinterpret_cast<const char*>(s_text4);
   const int f0 = (lo + 15) >> 4, f1 = hi >> 4;   // full chunks [f0, f1)
-  if constexpr (MC_PCD_STORE_UNROLL) {
-    // every LDS read of the lane's chunks before its first store (the loop waits for each read)
-    constexpr int kIt = (kPcdPackedText / 16 + 1 + kPcdBlock - 1) / kPcdBlock;
-    uint4 v[kIt];
-#pragma unroll
-    for (int u = 0; u < kIt; ++u) {
-      const int c = f0 + (int)threadIdx.x + u * kPcdBlock;
-      if (c < f1) v[u] = s_text4[c];
-    }
-#pragma unroll
-    for (int u = 0; u < kIt; ++u) {
-      const int c = f0 + (int)threadIdx.x + u * kPcdBlock;
-      if (c < f1) codec_st16(g + 16 * c, v[u]);
-    }
-  } else {
-    for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) codec_st16(g + 16 * c, s_text4[c]);
-  }
-  if (MC_CODEC_EDGE == 1 || MC_PCD_STORE_UNROLL) {
-    codec_store_edges(g, lds, lo, hi, f0, f1, (int)threadIdx.x);
-  } else if (threadIdx.x < 2) {
+  // (all of a lane's chunk reads before its stores, with the end bytes by 32 lanes: 816.5 vs 793.5 us,
+  // profiles/round5/s04 — the LVX pieces gain from it, these do not)
+  for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) codec_st16(g + 16 * c, s_text4[c]);
+  if (threadIdx.x < 2) {
     int b = lo, e = hi;                                    // a piece inside one chunk: lane 0 alone
     if (f0 <= f1) {
       if (threadIdx.x == 0) e = 16 * f0;                   // head: [lo, 16 f0)
@@ -1118,15 +934,12 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
 #pragma clang loop vectorize(disable) unroll(disable)
     for (; b < e; ++b) g[b] = lds[b];
   }
-  // s_wave / s_text are reused by the next tile, but only after its scan's barrier, which every lane
-  // reaches after these LDS reads (__syncthreads waits for them); s_wave was read before this tile's
-  // text barrier.  MC_PCD_NOBAR drops this barrier.
-  if (!MC_PCD_NOBAR) __syncthreads();
+  // the next tile zeroes s_text and rewrites s_wave: this barrier closes this tile's reads of both
+  __syncthreads();
 }
 
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
-  static_assert(!MC_PCD_OR || !MC_PCD_NOBAR, "the OR text needs the barrier after a tile's stores");
   __shared__ int s_wave[kPcdBlock / 64];
   __shared__ uint4 s_text4[kPcdTextChunks];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
@@ -1154,7 +967,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       // the tile's block is allocated whole: every lane loads (no branch around the loads), a lane
       // past the frame's end formats a value it never emits
       const float* q = a.src.cols + blk * a.src.C * kBlkPts + threadIdx.x;
-      cn[0] = codec_ld(q); cn[1] = codec_ld(q + kBlkPts); cn[2] = codec_ld(q + 2 * kBlkPts); cn[3] = codec_ld(q + 3 * kBlkPts);
+      cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
       flag_n = ldu(a.tile_bytes + u);
       gn = ldu(a.tile_pos + u);
     };

@@ -1,10 +1,10 @@
 // Host build of the device "%.6f" line writer in livox-motion-compensation-sim_amd/csrc/codecs.hpp
 // (the section from `struct PcdFast` to `kPcdSlowTile`, spliced in by tests/test_pcd_formatter_host.py
 // at FORMATTER_SECTION) with host stand-ins for the gfx950 intrinsics it uses.  Every line of a
-// 256-line tile is written in reverse lane order into a buffer filled with a marker byte, at a tile
-// offset modulo 16, as the kernel's lanes may interleave; the text is compared with the C library's
-// correctly rounded "%.6f" (the same digits as Python's formatting) and no byte outside the text may
-// change.  Exit status = number of bad tiles.
+// 256-line tile is OR-ed in reverse lane order into a zeroed buffer 16 bytes in (as the kernel's
+// pcd_tile_text does), at a tile offset modulo 16, as the kernel's lanes may interleave; the text is
+// compared with the C library's correctly rounded "%.6f" (the same digits as Python's formatting) and
+// no byte outside the text may become non-zero.  Exit status = number of bad tiles.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -19,6 +19,15 @@
 #define __noinline__
 #define __ATOMIC_RELAXED 0
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
+// ds_or_b64 (an LDS atomic OR): the host's plain read-modify-write
+template <class T>
+static inline T __hip_atomic_fetch_or(T* p, T v, int, int) {
+  T o;
+  std::memcpy(&o, p, sizeof o);
+  const T n = o | v;
+  std::memcpy(p, &n, sizeof n);
+  return o;
+}
 static inline uint32_t __umul24(uint32_t a, uint32_t b) { return (a & 0xffffffu) * (b & 0xffffffu); }
 // v_mul_i32_i24: the low 24 bits of each operand as signed integers
 static inline int __mul24(int a, int b) {
@@ -123,7 +132,7 @@ int main(int argc, char** argv) {
     check(INFINITY);
   }
   for (int t = 0; t < N / 256; ++t) {
-    std::memset(buf.data(), 0xA5, buf.size() * 4);   // the writer must not rely on zeros
+    std::memset(buf.data(), 0, buf.size() * 4);   // pcd_tile_text zeroes the text buffer
     const int shift = t % 16;
     int off = shift;
     std::string want;
@@ -174,12 +183,12 @@ int main(int argc, char** argv) {
       want += line;
     }
     for (int l = 255; l >= 0; --l)
-      if (P[l].ok) pcd_emit_line(T[l], reinterpret_cast<uint8_t*>(buf.data()), offs[l]);
-    const std::string got(reinterpret_cast<const char*>(buf.data()) + shift, off - shift);
+      if (P[l].ok) pcd_emit_line(T[l], reinterpret_cast<uint8_t*>(buf.data()) + 16, offs[l]);
+    const std::string got(reinterpret_cast<const char*>(buf.data()) + 16 + shift, off - shift);
     // nothing written outside the tile's text
-    const unsigned char* bb = reinterpret_cast<const unsigned char*>(buf.data());
-    for (size_t i = 0; i < buf.size() * 4; ++i)
-      if ((i < (size_t)shift || i >= (size_t)off) && bb[i] != 0xA5) {
+    const unsigned char* bb = reinterpret_cast<const unsigned char*>(buf.data()) + 16;
+    for (size_t i = 0; i + 16 < buf.size() * 4; ++i)
+      if ((i < (size_t)shift || i >= (size_t)off) && bb[i] != 0) {
         ++bad;
         std::printf("tile %d: byte %zu outside the text [%d, %d) was written\n", t, i, shift, off);
         break;

@@ -145,7 +145,8 @@ def test_batch_source_encoders_match_f64_source(mc, gpu_ctx, with_time):
     assert lvx == mc.codecs.encode_lvx([{"frame_id": i, "timestamp": t, "points": h}
                                         for i, t, h in zip(ids, ts, h2)], gpu_ctx)
     # clipping (LMC:259-261, 268): coordinates past +-2^31 mm, intensities outside [0, 1]; frames of
-    # 1 / 767 / 768 / 769 / 1537 points (k_lvx_units: a unit is 768 points = 3 blocks)
+    # 1 / 767 / 768 / 769 / 1537 points (a k_lvx_packages unit is 768 points = 3 blocks; a frame's
+    # first unit writes its frame header)
     cc = np.array([767, 1, 768, 769, 1537], np.int64)
     m = int(cc.sum())
     clip = np.column_stack([rng.normal(0, 40, (m, 3)), rng.uniform(-0.3, 1.3, m)])

@@ -71,8 +71,8 @@ def main():
     n_out = int(scans.n_points)
     alg = {
         "k_soa_to_aos": 48 * n, "k_aos_to_soa": 48 * n,
-        "k_lvx_packages": 16 * n + int(pos[-1]) - 88 - 24 * args.frames,
-        "k_lvx_units": 16 * n + int(pos[-1]) - 88 - 24 * args.frames,
+        # the points in, the file out but its 88-byte header (the frame headers too: round 5)
+        "k_lvx_packages": 16 * n + int(pos[-1]) - 88,
         "k_pcd_measure": 16 * n, "k_pcd_write": 16 * n + int(bpos[-1]),
         # scene x, y, z once + the poses once + the visibility words + the per-(tile, frame) counts
         "k_scan_count": 24 * E + poses + bits + 4 * tiles * Fp,

@@ -48,7 +48,7 @@ def run_pass(mode, counter, outdir, frames, points):
     return statistics.median(vals), len(vals)
 
 
-AUX = ["k_soa_to_aos", "k_aos_to_soa", "k_lvx_packages", "k_lvx_units", "k_pcd_measure", "k_pcd_write",
+AUX = ["k_soa_to_aos", "k_aos_to_soa", "k_lvx_packages", "k_pcd_measure", "k_pcd_write",
        "k_scan_count", "k_scan_emit"]
 
 
