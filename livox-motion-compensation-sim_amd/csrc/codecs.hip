@@ -145,7 +145,7 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
   std::vector<uint8_t> blob;
   const size_t o_doff = put(blob, doff.data(), doff.size());
   const size_t o_unit = put(blob, units.data(), units.size());
-  const size_t o_pos = put(blob, pos.data(), (size_t)F);
+  const size_t o_pos = put(blob, pos.data(), (size_t)F + 1);
   const size_t o_ids = put(blob, frame_ids, (size_t)F);
   const size_t o_ts = put(blob, ts_ns, (size_t)F);
   const size_t o_hi = has_int ? put(blob, has_int, (size_t)F) : 0;

@@ -181,7 +181,7 @@ __device__ __forceinline__ void codec_store_piece(char* __restrict__ g, const ch
 // ---- LVX v1.1 -------------------------------------------------------------------------------
 struct LvxArgs {
   CodecFrames src;
-  const int64_t* frame_pos;     // [F] byte offset of each frame in the file
+  const int64_t* frame_pos;     // [F + 1] byte offset of each frame in the file, then the file size
   const uint64_t* frame_id;     // [F]
   const uint64_t* ts_ns;        // [F] package timestamp, int(timestamp * 1e9) (LMC:176)
   const uint8_t* has_int;       // [F] frame has an intensity column (else reflectivity 128), or null
@@ -217,23 +217,72 @@ __device__ __forceinline__ int32_t lvx_fixed(double v, double scale, double lo, 
 // us, s02); records as naturally aligned LDS stores instead of the compiler's ds_write_b96 at 2-byte
 // alignment (303.5 vs 305.3, s03) and with every point load issued up front (301.2; 315.4 vs 293.0
 // on top of the folded headers and unrolled stores, s04).
+// MC_LVX_SPEC: the unit's frame metadata loaded for the frame guess in the same scalar round as the
+// guess's check (one round trip instead of two before the point loads); a wrong guess reloads.
+#ifndef MC_LVX_SPEC
+#define MC_LVX_SPEC 0
+#endif
+struct LvxMeta {
+  int64_t u0, u1;     // unit_off[f], unit_off[f + 1]
+  int64_t d0, d1;     // doff[f], doff[f + 1]
+  int64_t p0;         // poff[f] (batch source)
+  int64_t pos, pos1;  // frame_pos[f], frame_pos[f + 1]
+  uint64_t ts, id;
+};
+__device__ __forceinline__ LvxMeta lvx_meta(const LvxArgs& a, int32_t f) {
+  LvxMeta m;
+  m.u0 = ldu(a.src.unit_off + f);
+  m.u1 = ldu(a.src.unit_off + f + 1);
+  m.d0 = ldu(a.src.doff + f);
+  m.d1 = ldu(a.src.doff + f + 1);
+  m.p0 = a.src.cols ? ldu(a.src.poff + f) : 0;
+  m.pos = ldu(a.frame_pos + f);
+  m.pos1 = ldu(a.frame_pos + f + 1);
+  m.ts = ldu(a.ts_ns + f);
+  m.id = ldu(a.frame_id + f);
+  return m;
+}
 __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   static_assert(kCodecBlock >= 96 + 12 && kLvxPkgPerWG * (kLvxPkgHdr / 2) <= 96, "header threads");
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
   const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
-  const int32_t f = codec_frame_of(a.src, u);
-  const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
-  const int64_t frow = a.src.doff[f];
-  const int64_t fcount = a.src.doff[f + 1] - frow;
+  int32_t f;
+  LvxMeta m;
+  if constexpr (MC_LVX_SPEC) {
+    int64_t g = (int64_t)((double)u * a.src.frames_per_unit + 1e-6);
+    f = (int32_t)(g < a.src.F - 1 ? g : a.src.F - 1);
+    m = lvx_meta(a, f);
+    // all of the guess's loads issued before the check waits for any (the compiler would sink the
+    // ones a wrong guess discards below the branch)
+    asm volatile("" ::"s"(m.u0), "s"(m.u1), "s"(m.d0), "s"(m.d1), "s"(m.p0), "s"(m.pos), "s"(m.pos1), "s"(m.ts),
+                 "s"(m.id));
+    if (!(m.u0 <= u && u < m.u1)) {
+      f = codec_frame_of(a.src, u);
+      m = lvx_meta(a, f);
+    }
+  } else {
+    f = codec_frame_of(a.src, u);
+    m.u0 = a.src.unit_off[f];
+    m.d0 = a.src.doff[f];
+    m.d1 = a.src.doff[f + 1];
+    m.pos = a.frame_pos[f];
+    m.pos1 = f + 1 < a.src.F ? a.frame_pos[f + 1] : 0;
+    m.ts = a.ts_ns[f];
+    m.id = a.frame_id[f];
+    m.p0 = 0;
+  }
+  const int64_t pkg0 = (u - m.u0) * kLvxPkgPerWG;
+  const int64_t frow = m.d0;
+  const int64_t fcount = m.d1 - frow;
   const int64_t fpkgs = (fcount + kLvxPkgPoints - 1) / kLvxPkgPoints;
   const int k = (int)((fpkgs - pkg0) < kLvxPkgPerWG ? (fpkgs - pkg0) : kLvxPkgPerWG);
   const int64_t rem = fcount - pkg0 * kLvxPkgPoints;
   const int n = (int)(rem < k * kLvxPkgPoints ? rem : k * kLvxPkgPoints);
   const int hdr = pkg0 == 0 ? kLvxFrameHdr : 0;                            // frame header bytes first
-  const int64_t S = a.frame_pos[f] + kLvxFrameHdr + pkg0 * kLvxPkg - hdr;   // piece start, even
-  const int shift = (int)(S & 15) + hdr;                                    // LDS offset of the first package
-  const uint64_t ts = a.ts_ns[f];
+  const int64_t S = m.pos + kLvxFrameHdr + pkg0 * kLvxPkg - hdr;   // piece start, even
+  const int shift = (int)(S & 15) + hdr;                           // LDS offset of the first package
+  const uint64_t ts = m.ts;
   const bool hi = a.has_int ? a.has_int[f] != 0 : a.src.ld > 3;
   const int64_t row0 = frow + pkg0 * kLvxPkgPoints;
 
@@ -248,7 +297,12 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
       x = (uint32_t)i; y = x * 3u; z = x ^ 0x5555u; refl = x & 255u;
     } else if (i < n) {
       double v[4];
-      codec_point(a.src, f, row0 + i, v);
+      if (MC_LVX_SPEC && a.src.cols) {
+        const float* q = a.src.cols + bidx(a.src.C, 0, m.p0 + pkg0 * kLvxPkgPoints + i);
+        v[0] = q[0]; v[1] = q[kBlkPts]; v[2] = q[2 * kBlkPts]; v[3] = q[3 * kBlkPts];
+      } else {
+        codec_point(a.src, f, row0 + i, v);
+      }
       x = (uint32_t)lvx_fixed(v[0], 1000.0, -2147483648.0, 2147483647.0, a.err);
       y = (uint32_t)lvx_fixed(v[1], 1000.0, -2147483648.0, 2147483647.0, a.err);
       z = (uint32_t)lvx_fixed(v[2], 1000.0, -2147483648.0, 2147483647.0, a.err);
@@ -276,8 +330,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   }
   if (hdr && threadIdx.x >= 96 && threadIdx.x < 96 + 12) {   // own offset, next frame's (0 after the last), id
     const int i = (int)threadIdx.x - 96;
-    const uint64_t q = i < 4 ? (uint64_t)a.frame_pos[f]
-                             : i < 8 ? (f + 1 < a.src.F ? (uint64_t)a.frame_pos[f + 1] : 0ull) : a.frame_id[f];
+    const uint64_t q = i < 4 ? (uint64_t)m.pos : i < 8 ? (f + 1 < a.src.F ? (uint64_t)m.pos1 : 0ull) : m.id;
     s16[((shift - hdr) >> 1) + i] = (uint16_t)(q >> (16 * (i & 3)));
   }
   __syncthreads();

@@ -11,6 +11,7 @@
 #   pmc     tools/pmc_traffic.py (deskew kernels, then --aux), profiles/pmc_traffic.json copied out
 #   latency tools/latency.py ($LAT_ARGS)
 #   prof    rocprofv3 --kernel-trace --stats of the same bench command
+#   smi     rocm-smi clocks / power / temperature appended to smi.log
 #   probe   tools/issue_probe (issue cost of the codec kernels' vector / LDS instructions)
 # Usage (repo root, on the GPU box):  STEPS="tests ab" bash tools/gpu_session.sh <tag>
 set -u
@@ -83,6 +84,9 @@ for step in $STEPS; do
       python3 tools/roofline_from_trace.py --trace "$OUT/prof" --bench "$OUT/prof_bench.json" \
         --out "$OUT/roofline_trace.json" > /dev/null 2>> "$OUT/prof.err"
       echo "[roofline_from_trace] rc=$?" | tee -a "$OUT/steps.log" ;;
+    smi)
+      timeout -k 10 60 rocm-smi --showclocks --showpower --showtemp >> "$OUT/smi.log" 2>&1
+      echo "---- $(date +%T)" >> "$OUT/smi.log" ;;
     probe)
       timeout -k 10 300 tools/issue_probe > "$OUT/issue_probe.json" 2> "$OUT/issue_probe.err"
       stop_if_fault $? probe
