@@ -216,73 +216,25 @@ __device__ __forceinline__ int32_t lvx_fixed(double v, double scale, double lo, 
 // (336.8 vs 306.8 us, profiles/round5/s01); 768 / 512 threads per workgroup (497.8 / 384.6 vs 304.3
 // us, s02); records as naturally aligned LDS stores instead of the compiler's ds_write_b96 at 2-byte
 // alignment (303.5 vs 305.3, s03) and with every point load issued up front (301.2; 315.4 vs 293.0
-// on top of the folded headers and unrolled stores, s04).
-// MC_LVX_SPEC: the unit's frame metadata loaded for the frame guess in the same scalar round as the
-// guess's check (one round trip instead of two before the point loads); a wrong guess reloads.
-#ifndef MC_LVX_SPEC
-#define MC_LVX_SPEC 0
-#endif
-struct LvxMeta {
-  int64_t u0, u1;     // unit_off[f], unit_off[f + 1]
-  int64_t d0, d1;     // doff[f], doff[f + 1]
-  int64_t p0;         // poff[f] (batch source)
-  int64_t pos, pos1;  // frame_pos[f], frame_pos[f + 1]
-  uint64_t ts, id;
-};
-__device__ __forceinline__ LvxMeta lvx_meta(const LvxArgs& a, int32_t f) {
-  LvxMeta m;
-  m.u0 = ldu(a.src.unit_off + f);
-  m.u1 = ldu(a.src.unit_off + f + 1);
-  m.d0 = ldu(a.src.doff + f);
-  m.d1 = ldu(a.src.doff + f + 1);
-  m.p0 = a.src.cols ? ldu(a.src.poff + f) : 0;
-  m.pos = ldu(a.frame_pos + f);
-  m.pos1 = ldu(a.frame_pos + f + 1);
-  m.ts = ldu(a.ts_ns + f);
-  m.id = ldu(a.frame_id + f);
-  return m;
-}
+// on top of the folded headers and unrolled stores, s04); the frame metadata loaded for the frame
+// guess in the guess's own scalar round (297.9 vs 292.4, s06).
 __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   static_assert(kCodecBlock >= 96 + 12 && kLvxPkgPerWG * (kLvxPkgHdr / 2) <= 96, "header threads");
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
   const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
-  int32_t f;
-  LvxMeta m;
-  if constexpr (MC_LVX_SPEC) {
-    int64_t g = (int64_t)((double)u * a.src.frames_per_unit + 1e-6);
-    f = (int32_t)(g < a.src.F - 1 ? g : a.src.F - 1);
-    m = lvx_meta(a, f);
-    // all of the guess's loads issued before the check waits for any (the compiler would sink the
-    // ones a wrong guess discards below the branch)
-    asm volatile("" ::"s"(m.u0), "s"(m.u1), "s"(m.d0), "s"(m.d1), "s"(m.p0), "s"(m.pos), "s"(m.pos1), "s"(m.ts),
-                 "s"(m.id));
-    if (!(m.u0 <= u && u < m.u1)) {
-      f = codec_frame_of(a.src, u);
-      m = lvx_meta(a, f);
-    }
-  } else {
-    f = codec_frame_of(a.src, u);
-    m.u0 = a.src.unit_off[f];
-    m.d0 = a.src.doff[f];
-    m.d1 = a.src.doff[f + 1];
-    m.pos = a.frame_pos[f];
-    m.pos1 = f + 1 < a.src.F ? a.frame_pos[f + 1] : 0;
-    m.ts = a.ts_ns[f];
-    m.id = a.frame_id[f];
-    m.p0 = 0;
-  }
-  const int64_t pkg0 = (u - m.u0) * kLvxPkgPerWG;
-  const int64_t frow = m.d0;
-  const int64_t fcount = m.d1 - frow;
+  const int32_t f = codec_frame_of(a.src, u);
+  const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
+  const int64_t frow = a.src.doff[f];
+  const int64_t fcount = a.src.doff[f + 1] - frow;
   const int64_t fpkgs = (fcount + kLvxPkgPoints - 1) / kLvxPkgPoints;
   const int k = (int)((fpkgs - pkg0) < kLvxPkgPerWG ? (fpkgs - pkg0) : kLvxPkgPerWG);
   const int64_t rem = fcount - pkg0 * kLvxPkgPoints;
   const int n = (int)(rem < k * kLvxPkgPoints ? rem : k * kLvxPkgPoints);
   const int hdr = pkg0 == 0 ? kLvxFrameHdr : 0;                            // frame header bytes first
-  const int64_t S = m.pos + kLvxFrameHdr + pkg0 * kLvxPkg - hdr;   // piece start, even
-  const int shift = (int)(S & 15) + hdr;                           // LDS offset of the first package
-  const uint64_t ts = m.ts;
+  const int64_t S = a.frame_pos[f] + kLvxFrameHdr + pkg0 * kLvxPkg - hdr;   // piece start, even
+  const int shift = (int)(S & 15) + hdr;                                    // LDS offset of the first package
+  const uint64_t ts = a.ts_ns[f];
   const bool hi = a.has_int ? a.has_int[f] != 0 : a.src.ld > 3;
   const int64_t row0 = frow + pkg0 * kLvxPkgPoints;
 
@@ -297,12 +249,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
       x = (uint32_t)i; y = x * 3u; z = x ^ 0x5555u; refl = x & 255u;
     } else if (i < n) {
       double v[4];
-      if (MC_LVX_SPEC && a.src.cols) {
-        const float* q = a.src.cols + bidx(a.src.C, 0, m.p0 + pkg0 * kLvxPkgPoints + i);
-        v[0] = q[0]; v[1] = q[kBlkPts]; v[2] = q[2 * kBlkPts]; v[3] = q[3 * kBlkPts];
-      } else {
-        codec_point(a.src, f, row0 + i, v);
-      }
+      codec_point(a.src, f, row0 + i, v);
       x = (uint32_t)lvx_fixed(v[0], 1000.0, -2147483648.0, 2147483647.0, a.err);
       y = (uint32_t)lvx_fixed(v[1], 1000.0, -2147483648.0, 2147483647.0, a.err);
       z = (uint32_t)lvx_fixed(v[2], 1000.0, -2147483648.0, 2147483647.0, a.err);
@@ -330,7 +277,8 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   }
   if (hdr && threadIdx.x >= 96 && threadIdx.x < 96 + 12) {   // own offset, next frame's (0 after the last), id
     const int i = (int)threadIdx.x - 96;
-    const uint64_t q = i < 4 ? (uint64_t)m.pos : i < 8 ? (f + 1 < a.src.F ? (uint64_t)m.pos1 : 0ull) : m.id;
+    const uint64_t q = i < 4 ? (uint64_t)a.frame_pos[f] : i < 8 ? (f + 1 < a.src.F ? (uint64_t)a.frame_pos[f + 1] : 0ull)
+                                                             : a.frame_id[f];
     s16[((shift - hdr) >> 1) + i] = (uint16_t)(q >> (16 * (i & 3)));
   }
   __syncthreads();
@@ -956,10 +904,22 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 // pcd_tile_text: the tile's lines in LDS, -> the tile's text bytes; pcd_tile_store: its stores.
 constexpr int kPcdTextLead = 1;   // uint4 chunks before the text (pcd_emit_line's windows start early)
 constexpr int kPcdTextChunks = kPcdPackedText / 16 + 1 + kPcdTextLead;
+// MC_PCD_ZERO_ON_READ: the text buffer is zeroed once per workgroup, then each chunk right after its
+// store read it (and the end chunks after their bytes), instead of a zeroing pass per tile
+#ifndef MC_PCD_ZERO_ON_READ
+#define MC_PCD_ZERO_ON_READ 0
+#endif
+__device__ __forceinline__ void pcd_text_zero(uint4* s_text4) {
+#pragma unroll
+  for (int u = 0; u < (kPcdTextChunks + kPcdBlock - 1) / kPcdBlock; ++u) {
+    const int c = (int)threadIdx.x + u * kPcdBlock;
+    if (c < kPcdTextChunks) s_text4[c] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
 __device__ __forceinline__ int pcd_tile_text(const PcdText& T, bool valid, int64_t G, int* s_wave, uint4* s_text4) {
   // the buffer is zeroed before the scan's barrier; the previous tile's reads of it ended before the
   // barrier that closed its stores (pcd_tile_store)
-  for (int c = threadIdx.x; c < kPcdTextChunks; c += kPcdBlock) s_text4[c] = make_uint4(0u, 0u, 0u, 0u);
+  if (!MC_PCD_ZERO_ON_READ) pcd_text_zero(s_text4);
   int total;
   const int excl = block_scan(T.len, s_wave, total) - T.len;
   if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text4 + kPcdTextLead), (int)(G & 15) + excl);
@@ -968,14 +928,17 @@ __device__ __forceinline__ int pcd_tile_text(const PcdText& T, bool valid, int64
 }
 // codec_store_piece for a tile's text: the full 16-byte chunks in a loop without per-chunk tests,
 // the (at most two) partial end chunks by lanes 0 and 1
-__device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int total, const uint4* s_text4) {
+__device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int total, uint4* s_text4) {
   const int lo = (int)(G & 15), hi = lo + total;
   char* const g = a.out + (G - lo);
   const char* const lds = reinterpret_cast<const char*>(s_text4);
   const int f0 = (lo + 15) >> 4, f1 = hi >> 4;   // full chunks [f0, f1)
   // (all of a lane's chunk reads before its stores, with the end bytes by 32 lanes: 816.5 vs 793.5 us,
   // profiles/round5/s04 — the LVX pieces gain from it, these do not)
-  for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) codec_st16(g + 16 * c, s_text4[c]);
+  for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) {
+    codec_st16(g + 16 * c, s_text4[c]);
+    if (MC_PCD_ZERO_ON_READ) s_text4[c] = make_uint4(0u, 0u, 0u, 0u);
+  }
   if (threadIdx.x < 2) {
     int b = lo, e = hi;                                    // a piece inside one chunk: lane 0 alone
     if (f0 <= f1) {
@@ -984,8 +947,11 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
     } else if (threadIdx.x == 1) {
       e = b;
     }
+    const int b0 = b;
 #pragma clang loop vectorize(disable) unroll(disable)
     for (; b < e; ++b) g[b] = lds[b];
+    // a partial end chunk (no lane of the loop above reads it)
+    if (MC_PCD_ZERO_ON_READ && b0 < e) s_text4[b0 >> 4] = make_uint4(0u, 0u, 0u, 0u);
   }
   // the next tile zeroes s_text and rewrites s_wave: this barrier closes this tile's reads of both
   __syncthreads();
@@ -997,6 +963,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ uint4 s_text4[kPcdTextChunks];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
+  if (MC_PCD_ZERO_ON_READ) pcd_text_zero(s_text4);   // ordered before the first ORs by the scan's barrier
   if constexpr (F32) {
     // Tile j + 1's loads are in flight while tile j is formatted, and converted (pcd_text)
     // between tile j's LDS text and its stores.  vmcnt counts stores as well as loads, and a load
