@@ -491,6 +491,16 @@ def measure_scan(ctx, cfg, tr, reps, cpu_budget):
     return rep
 
 
+def steady(ctx, fn, ms=100.0):
+    """Untimed calls of fn for ~ms milliseconds before a measurement: these figures follow idle stretches
+    of the bench (its CPU legs), and from idle the device needs tens of ms of load to reach its steady
+    rate (as the headline's spin-up, spin_up)."""
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        fn()
+        ctx.sync()
+
+
 def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     """SURVEY §8f row 3, reported beside the hot path: the byte-exact writers (LVX v1.1 LMC:24-272,
     ASCII PCD LMC:932-948) encoding the rank's whole deskewed batch straight from its float32
@@ -509,7 +519,7 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     def lvx():
         mc._lib.check(ctx.lib.mc_lvx_encode_batch(ctx.handle, b_out.handle, ptr(ids, c_uint64), ptr(ts, c_uint64),
                                                   out.ptr, int(pos[-1])), "lvx_encode_batch")
-    lvx()
+    steady(ctx, lvx)
     ctx.read_timing()
     ctx.timing(True)
     for _ in range(reps):
@@ -528,7 +538,7 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     def pcd():
         mc._lib.check(ctx.lib.mc_pcd_encode_batch(ctx.handle, b_out.handle, out.ptr, cap, ptr(bpos, c_int64)),
                       "pcd_encode_batch")
-    pcd()
+    steady(ctx, pcd)
     ctx.read_timing()
     ctx.timing(True)
     for _ in range(reps):
@@ -582,9 +592,7 @@ def measure_deskew_pcd(ctx, b_in, b_out, mode, n_rank, reps):
             mc._lib.check(ctx.lib.mc_deskew_pcd(ctx.handle, b_in.handle, b_out.handle, mc._lib.MODES[mode],
                                                 mc._lib.POSE_SELECT["searchsorted"], buf.ptr, cap, ptr(pos, c_int64)),
                           "deskew_pcd")
-        for fn in (separate, fused):
-            fn()
-        ctx.sync()
+        steady(ctx, lambda: (separate(), fused()))
         ctx.read_timing()
         for _ in range(reps):
             for name, fn in (("separate", separate), ("fused", fused)):

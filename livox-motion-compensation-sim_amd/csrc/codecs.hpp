@@ -904,10 +904,10 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 // pcd_tile_text: the tile's lines in LDS, -> the tile's text bytes; pcd_tile_store: its stores.
 constexpr int kPcdTextLead = 1;   // uint4 chunks before the text (pcd_emit_line's windows start early)
 constexpr int kPcdTextChunks = kPcdPackedText / 16 + 1 + kPcdTextLead;
-// MC_PCD_ZERO_ON_READ: the text buffer is zeroed once per workgroup, then each chunk right after its
-// store read it (and the end chunks after their bytes), instead of a zeroing pass per tile
-#ifndef MC_PCD_ZERO_ON_READ
-#define MC_PCD_ZERO_ON_READ 0
+// MC_PCD_DIAG (diagnostic builds only, wrong output), bits: 1 = no text chunk stores to HBM, 2 = no
+// digit conversion (a fixed 40-byte line), 4 = no LDS text emission.  Naming the write pass's limiter.
+#ifndef MC_PCD_DIAG
+#define MC_PCD_DIAG 0
 #endif
 __device__ __forceinline__ void pcd_text_zero(uint4* s_text4) {
 #pragma unroll
@@ -919,16 +919,16 @@ __device__ __forceinline__ void pcd_text_zero(uint4* s_text4) {
 __device__ __forceinline__ int pcd_tile_text(const PcdText& T, bool valid, int64_t G, int* s_wave, uint4* s_text4) {
   // the buffer is zeroed before the scan's barrier; the previous tile's reads of it ended before the
   // barrier that closed its stores (pcd_tile_store)
-  if (!MC_PCD_ZERO_ON_READ) pcd_text_zero(s_text4);
+  pcd_text_zero(s_text4);
   int total;
   const int excl = block_scan(T.len, s_wave, total) - T.len;
-  if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text4 + kPcdTextLead), (int)(G & 15) + excl);
+  if (valid && !(MC_PCD_DIAG & 4)) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text4 + kPcdTextLead), (int)(G & 15) + excl);
   __syncthreads();
   return total;
 }
 // codec_store_piece for a tile's text: the full 16-byte chunks in a loop without per-chunk tests,
 // the (at most two) partial end chunks by lanes 0 and 1
-__device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int total, uint4* s_text4) {
+__device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int total, const uint4* s_text4) {
   const int lo = (int)(G & 15), hi = lo + total;
   char* const g = a.out + (G - lo);
   const char* const lds = reinterpret_cast<const char*>(s_text4);
@@ -936,8 +936,12 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
   // (all of a lane's chunk reads before its stores, with the end bytes by 32 lanes: 816.5 vs 793.5 us,
   // profiles/round5/s04 — the LVX pieces gain from it, these do not)
   for (int c = f0 + (int)threadIdx.x; c < f1; c += kPcdBlock) {
-    codec_st16(g + 16 * c, s_text4[c]);
-    if (MC_PCD_ZERO_ON_READ) s_text4[c] = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr ((MC_PCD_DIAG & 1) != 0) {   // diagnostic: the chunk is read, (almost) never stored
+      const uint4 v = s_text4[c];
+      if (v.x == 0x7eadbeefu && v.y == 0x7eadbeefu) codec_st16(g + 16 * c, v);
+    } else {
+      codec_st16(g + 16 * c, s_text4[c]);
+    }
   }
   if (threadIdx.x < 2) {
     int b = lo, e = hi;                                    // a piece inside one chunk: lane 0 alone
@@ -947,11 +951,8 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
     } else if (threadIdx.x == 1) {
       e = b;
     }
-    const int b0 = b;
 #pragma clang loop vectorize(disable) unroll(disable)
     for (; b < e; ++b) g[b] = lds[b];
-    // a partial end chunk (no lane of the loop above reads it)
-    if (MC_PCD_ZERO_ON_READ && b0 < e) s_text4[b0 >> 4] = make_uint4(0u, 0u, 0u, 0u);
   }
   // the next tile zeroes s_text and rewrites s_wave: this barrier closes this tile's reads of both
   __syncthreads();
@@ -963,13 +964,15 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ uint4 s_text4[kPcdTextChunks];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
-  if (MC_PCD_ZERO_ON_READ) pcd_text_zero(s_text4);   // ordered before the first ORs by the scan's barrier
   if constexpr (F32) {
     // Tile j + 1's loads are in flight while tile j is formatted, and converted (pcd_text)
     // between tile j's LDS text and its stores.  vmcnt counts stores as well as loads, and a load
     // consumed with stores in flight waits for them too: consumed after tile j's stores, it would
     // wait for their completion; consumed before them, it waits only for tile j - 1's, long done.
     // One call site and no branch around it, so no path carries a load into the next iteration.
+    // (Rejected, profiles/round5: two tiles' loads in flight with a fixed store count per lane so the
+    // compiler's vmcnt waits stay exact, 986.1 vs 792.0 us (s09); 8 tiles per workgroup 826.4, the
+    // text zeroed as it is read 802.1 (s07).)
     const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
     float cn[4] = {0.f, 0.f, 0.f, 0.f};
     bool vn = false;
@@ -993,8 +996,19 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
     };
     auto convert = [&]() {
       PcdFast P;
-      pcd_fast_vals_packed(cn, P);   // (invalid lanes convert zeros / stale values: length zeroed)
-      pcd_text(P, Tn);
+      if constexpr ((MC_PCD_DIAG & 2) != 0) {   // diagnostic: a fixed 40-byte line from the loaded values' bits
+        const uint32_t h = __float_as_uint(cn[0]) ^ __float_as_uint(cn[1]) ^ __float_as_uint(cn[2]) ^ __float_as_uint(cn[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          Tn.D[k] = 0x30303030u + (h & 0x01010101u); Tn.A[k] = 0x3030302Eu; Tn.B[k] = 0x20303030u;
+          Tn.ng[k] = 0; Tn.d[k] = -2;
+        }
+        Tn.q0 = 2;
+        Tn.len = 40;
+      } else {
+        pcd_fast_vals_packed(cn, P);   // (invalid lanes convert zeros / stale values: length zeroed)
+        pcd_text(P, Tn);
+      }
       if (!vn) Tn.len = 0;
       // pins the conversion here: the compiler would otherwise sink it below the stores, to its use
       asm volatile("" ::"v"(Tn.D[0]), "v"(Tn.D[1]), "v"(Tn.D[2]), "v"(Tn.D[3]), "v"(Tn.A[0]), "v"(Tn.A[1]),
