@@ -905,7 +905,8 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 constexpr int kPcdTextLead = 1;   // uint4 chunks before the text (pcd_emit_line's windows start early)
 constexpr int kPcdTextChunks = kPcdPackedText / 16 + 1 + kPcdTextLead;
 // MC_PCD_DIAG (diagnostic builds only, wrong output), bits: 1 = no text chunk stores to HBM, 2 = no
-// digit conversion (a fixed 40-byte line), 4 = no LDS text emission.  Naming the write pass's limiter.
+// digit conversion (a fixed 40-byte line), 4 = no LDS text emission, 8 = waves format and store their
+// own 64 lines without the tile's barriers.  Naming the write pass's limiter.
 #ifndef MC_PCD_DIAG
 #define MC_PCD_DIAG 0
 #endif
@@ -961,7 +962,7 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
-  __shared__ uint4 s_text4[kPcdTextChunks];
+  __shared__ uint4 s_text4[(MC_PCD_DIAG & 8) ? 4 * ((64 * 52 + 16) / 16 + 2) : kPcdTextChunks];
   const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {
@@ -1023,6 +1024,28 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
       const bool packed = !(flag_n & kPcdSlowTile);   // workgroup-uniform
       const int64_t G = gn;
       if (u + 1 < u_end) fetch(u + 1);
+      if constexpr ((MC_PCD_DIAG & 8) != 0) {
+        // diagnostic: every wave formats and stores its own 64 lines with no barrier (wave scan, a
+        // private LDS region, its own chunk stores) at made-up positions — the cost of the tile's
+        // workgroup-wide scan and barriers
+        constexpr int kWaveChunks = (64 * 52 + 16) / 16 + 2;
+        const int wid = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+        uint4* const wt = s_text4 + wid * kWaveChunks;
+        if (packed) {
+          for (int c = lane; c < kWaveChunks; c += 64) wt[c] = make_uint4(0u, 0u, 0u, 0u);
+          const int incl = wave_scan_incl(T.len);
+          const int tot = __builtin_amdgcn_readlane(incl, 63);
+          const int64_t Gw = G + wid * 2600;
+          const int lo = (int)(Gw & 15), hi = lo + tot;
+          if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(wt + 1), lo + incl - T.len);
+          convert();
+          char* const g = a.out + (Gw - lo);
+          for (int c = ((lo + 15) >> 4) + lane; c < (hi >> 4); c += 64) codec_st16(g + 16 * c, wt[1 + c]);
+        } else {
+          convert();
+        }
+        continue;
+      }
       int total = 0;
       if (packed) total = pcd_tile_text(T, valid, G, s_wave, s_text4);
       convert();
