@@ -328,7 +328,7 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
     return fail(MC_ERR_SPACE, "PCD text needs %lld bytes, buffer has %lld", (long long)run, (long long)out_bytes);
   CHECK_ARG(d_out, "d_out is NULL");
   HIPCHK(hipMemcpyAsync(d + o_tp, tpos.data(), tpos.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-  const dim3 grid((uint32_t)((n_tiles + kPcdTilesPerWG - 1) / kPcdTilesPerWG));
+  const dim3 grid((uint32_t)((n_tiles + kPcdWriteTiles - 1) / kPcdWriteTiles));
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
     if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);

@@ -906,9 +906,9 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
 // pcd_tile_text: the tile's lines in LDS, -> the tile's text bytes; pcd_tile_store: its stores.
 constexpr int kPcdTextLead = 1;   // uint4 chunks before the text (pcd_emit_line's windows start early)
 constexpr int kPcdTextChunks = kPcdPackedText / 16 + 1 + kPcdTextLead;
-// MC_PCD_DIAG (diagnostic builds only, wrong output), bits: 1 = no text chunk stores to HBM, 2 = no
-// digit conversion (a fixed 40-byte line), 4 = no LDS text emission, 8 = waves format and store their
-// own 64 lines without the tile's barriers.  Naming the write pass's limiter.
+// MC_PCD_DIAG (diagnostic builds only, wrong output), bits: 1 = no text chunk stores to HBM, 4 = no
+// LDS text emission (profiles/round5/s08 also ran 2 = no digit conversion and 8 = waves storing their
+// own 64 lines without the tile's barriers, in the write loop this unrolled pass replaced).
 #ifndef MC_PCD_DIAG
 #define MC_PCD_DIAG 0
 #endif
@@ -961,100 +961,81 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
   __syncthreads();
 }
 
+// Tiles per write workgroup.  The float32 pass unrolls a workgroup's tiles and issues the point
+// loads of two tiles before the first is converted, so that two tiles' loads are in flight and every
+// vmcnt wait the compiler places is exact (no loop carries a load).  Kernel time with the tiles of
+// one workgroup in a loop (one tile's loads ahead) vs unrolled: 640.1 vs 588.0 us at 2 tiles, 626.4
+// at 1 (rocprofv3, profiles/round5/s19); measure + write 787.6 vs 739.0 us, fused write pass 722.6
+// vs 671.8 us (s18).  Rejected (s13-s16): 3 / 4 / 6 / 8 tiles unrolled with loads two or three tiles
+// ahead 738.8-806.2 us; a fixed number of stores per lane (buffer stores, those with nothing to store
+// dropped past the record count) so that the waits would not cover the previous tile's stores, 820.3
+// vs 787.6 us.
+#ifndef MC_PCD_WRITE_TILES
+#define MC_PCD_WRITE_TILES 2
+#endif
+constexpr int kPcdWriteTiles = MC_PCD_WRITE_TILES;
+
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
-  __shared__ uint4 s_text4[(MC_PCD_DIAG & 8) ? 4 * ((64 * 52 + 16) / 16 + 2) : kPcdTextChunks];
-  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
+  __shared__ uint4 s_text4[kPcdTextChunks];
+  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdWriteTiles;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {
-    // Tile j + 1's loads are in flight while tile j is formatted, and converted (pcd_text)
-    // between tile j's LDS text and its stores.  vmcnt counts stores as well as loads, and a load
-    // consumed with stores in flight waits for them too: consumed after tile j's stores, it would
-    // wait for their completion; consumed before them, it waits only for tile j - 1's, long done.
-    // One call site and no branch around it, so no path carries a load into the next iteration.
-    // (Rejected, profiles/round5: two tiles' loads in flight with a fixed store count per lane so the
-    // compiler's vmcnt waits stay exact, 986.1 vs 792.0 us (s09); 8 tiles per workgroup 826.4, the
-    // text zeroed as it is read 802.1 (s07).)
-    const int64_t u_end = u0 + kPcdTilesPerWG < a.src.n_units ? u0 + kPcdTilesPerWG : a.src.n_units;
-    float cn[4] = {0.f, 0.f, 0.f, 0.f};
-    bool vn = false;
-    int32_t flag_n = 0;
-    int64_t gn = 0;
-    PcdText Tn;
+    // Order per tile j: loads of tile j + 2, tile j's LDS text, tile j + 1 converted, tile j's
+    // stores.  vmcnt counts stores as well as loads: tile j + 1's conversion waits for its loads and
+    // for tile j - 1's stores (issued before them), never for tile j's.  Tiles past the grid's end
+    // load the last tile again and store nothing; a tile that is not packed is formatted all the same
+    // (bounded: 36-52 bytes a line) and not stored (k_pcd_write_bytes writes it).
+    constexpr int K = kPcdWriteTiles, D = K < 2 ? K : 2;
+    const int64_t nu = a.src.n_units;
+    float cv[K][4];
+    bool vv[K];
+    int32_t flag[K];
+    int64_t gpos[K];
     // tile u is block (poff_f + 256 (u - unit_off_f)) / 256 of the batch: its columns start at a
     // workgroup-uniform address (scalar arithmetic), a lane's line at + threadIdx.x
-    auto fetch = [&](int64_t u) {
+    auto fetch = [&](int j) {
+      const bool live = u0 + j < nu;
+      const int64_t u = live ? u0 + j : nu - 1;
       f = codec_advance(a.src.unit_off, f, u);
       const int64_t k = u - ldu(a.src.unit_off + f);                       // tile of frame f
       const int64_t blk = (ldu(a.src.poff + f) >> 8) + k;
       const int left = (int)min_i64(ldu(a.src.doff + f + 1) - ldu(a.src.doff + f) - k * kPcdBlock, kPcdBlock);
-      vn = (int)threadIdx.x < left;
+      vv[j] = live && (int)threadIdx.x < left;
       // the tile's block is allocated whole: every lane loads (no branch around the loads), a lane
       // past the frame's end formats a value it never emits
       const float* q = a.src.cols + blk * a.src.C * kBlkPts + threadIdx.x;
-      cn[0] = q[0]; cn[1] = q[kBlkPts]; cn[2] = q[2 * kBlkPts]; cn[3] = q[3 * kBlkPts];
-      flag_n = ldu(a.tile_bytes + u);
-      gn = ldu(a.tile_pos + u);
+      cv[j][0] = q[0]; cv[j][1] = q[kBlkPts]; cv[j][2] = q[2 * kBlkPts]; cv[j][3] = q[3 * kBlkPts];
+      flag[j] = live ? ldu(a.tile_bytes + u) : kPcdSlowTile;
+      gpos[j] = ldu(a.tile_pos + u);
     };
-    auto convert = [&]() {
+    auto conv = [&](int j, PcdText& T) {
       PcdFast P;
-      if constexpr ((MC_PCD_DIAG & 2) != 0) {   // diagnostic: a fixed 40-byte line from the loaded values' bits
-        const uint32_t h = __float_as_uint(cn[0]) ^ __float_as_uint(cn[1]) ^ __float_as_uint(cn[2]) ^ __float_as_uint(cn[3]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          Tn.D[k] = 0x30303030u + (h & 0x01010101u); Tn.A[k] = 0x3030302Eu; Tn.B[k] = 0x20303030u;
-          Tn.ng[k] = 0; Tn.d[k] = -2;
-        }
-        Tn.q0 = 2;
-        Tn.len = 40;
-      } else {
-        pcd_fast_vals_packed(cn, P);   // (invalid lanes convert zeros / stale values: length zeroed)
-        pcd_text(P, Tn);
-      }
-      if (!vn) Tn.len = 0;
+      pcd_fast_vals_packed(cv[j], P);   // (invalid lanes convert stale values: length zeroed)
+      pcd_text(P, T);
+      if (!vv[j]) T.len = 0;
       // pins the conversion here: the compiler would otherwise sink it below the stores, to its use
-      asm volatile("" ::"v"(Tn.D[0]), "v"(Tn.D[1]), "v"(Tn.D[2]), "v"(Tn.D[3]), "v"(Tn.A[0]), "v"(Tn.A[1]),
-                   "v"(Tn.A[2]), "v"(Tn.A[3]), "v"(Tn.B[0]), "v"(Tn.B[1]), "v"(Tn.B[2]), "v"(Tn.B[3]), "v"(Tn.len)
+      asm volatile("" ::"v"(T.D[0]), "v"(T.D[1]), "v"(T.D[2]), "v"(T.D[3]), "v"(T.A[0]), "v"(T.A[1]),
+                   "v"(T.A[2]), "v"(T.A[3]), "v"(T.B[0]), "v"(T.B[1]), "v"(T.B[2]), "v"(T.B[3]), "v"(T.len)
                    : "memory");
     };
-    if (u0 < u_end) fetch(u0);
-    convert();
-    for (int64_t u = u0; u < u_end; ++u) {
-      const PcdText T = Tn;
-      const bool valid = vn;
-      const bool packed = !(flag_n & kPcdSlowTile);   // workgroup-uniform
-      const int64_t G = gn;
-      if (u + 1 < u_end) fetch(u + 1);
-      if constexpr ((MC_PCD_DIAG & 8) != 0) {
-        // diagnostic: every wave formats and stores its own 64 lines with no barrier (wave scan, a
-        // private LDS region, its own chunk stores) at made-up positions — the cost of the tile's
-        // workgroup-wide scan and barriers
-        constexpr int kWaveChunks = (64 * 52 + 16) / 16 + 2;
-        const int wid = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-        uint4* const wt = s_text4 + wid * kWaveChunks;
-        if (packed) {
-          for (int c = lane; c < kWaveChunks; c += 64) wt[c] = make_uint4(0u, 0u, 0u, 0u);
-          const int incl = wave_scan_incl(T.len);
-          const int tot = __builtin_amdgcn_readlane(incl, 63);
-          const int64_t Gw = G + wid * 2600;
-          const int lo = (int)(Gw & 15), hi = lo + tot;
-          if (valid) pcd_emit_line(T, reinterpret_cast<uint8_t*>(wt + 1), lo + incl - T.len);
-          convert();
-          char* const g = a.out + (Gw - lo);
-          for (int c = ((lo + 15) >> 4) + lane; c < (hi >> 4); c += 64) codec_st16(g + 16 * c, wt[1 + c]);
-        } else {
-          convert();
-        }
-        continue;
-      }
-      int total = 0;
-      if (packed) total = pcd_tile_text(T, valid, G, s_wave, s_text4);
-      convert();
-      if (packed) pcd_tile_store(a, G, total, s_text4 + kPcdTextLead);
+    PcdText T0, T1;
+#pragma unroll
+    for (int j = 0; j < D; ++j) fetch(j);
+    conv(0, T0);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      PcdText& T = (j & 1) ? T1 : T0;
+      PcdText& Tn = (j & 1) ? T0 : T1;
+      if (j + D < K) fetch(j + D);
+      const int total = pcd_tile_text(T, vv[j], gpos[j], s_wave, s_text4);
+      if (j + 1 < K) conv(j + 1, Tn);
+      if (!(flag[j] & kPcdSlowTile)) pcd_tile_store(a, gpos[j], total, s_text4 + kPcdTextLead);
+      else __syncthreads();   // (pcd_tile_store's closing barrier)
     }
   } else {
-    for (int j = 0; j < kPcdTilesPerWG; ++j) {
+    for (int j = 0; j < kPcdWriteTiles; ++j) {
       const int64_t u = u0 + j;
       if (u >= a.src.n_units) break;
       if (ldu(a.tile_bytes + u) & kPcdSlowTile) continue;   // workgroup-uniform
