@@ -166,6 +166,7 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
   a.has_int = has_int ? reinterpret_cast<const uint8_t*>(d + o_hi) : nullptr;
   a.out = static_cast<char*>(d_out);
   a.err = c->d_codec_err;
+  a.order = src.batch ? src.batch->hot_order ^ 1 : 0;   // start where the last kernel over the batch ended
   {
     TimedRegion tr(c, &c->codec_ev, c->stream);
     // frame headers: each frame's first unit writes its own, so this launch only when a frame has no
@@ -176,6 +177,7 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
                          a, (int64_t)0);
     if (n_pkg > 0)
       hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
+      if (src.batch) src.batch->hot_order = a.order;
   }
   HIPCHK(hipGetLastError());
   int err = 0;
@@ -267,6 +269,11 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
   a.tile_pos = reinterpret_cast<const int64_t*>(d + o_tp);
   a.out = static_cast<char*>(d_out);
   a.err = c->d_codec_err;
+  // batch source: each pass starts where the previous kernel over the batch ended (stream_unit);
+  // fused (d_measured): the write pass follows the deskew kernel directly
+  const int hot = src.batch ? src.batch->hot_order : 1;
+  a.morder = hot ^ 1;
+  a.worder = hot ^ 1;
   std::vector<int32_t> tb((size_t)n_tiles);
   bool measured = false;
   if (d_measured) {
@@ -276,6 +283,7 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
     if (measured) a.tile_bytes = const_cast<int32_t*>(d_measured);   // the write pass reads it (no slow flags)
   }
   if (!measured) {
+    a.worder = a.morder ^ 1;
     {
       TimedRegion tr(c, &c->codec_ev, c->stream);
       const int per = a.src.cols ? kPcdMeasureTiles : kPcdTilesPerWG;   // tiles per measure workgroup
@@ -334,6 +342,7 @@ int pcd_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, v
     if (a.src.cols) hipLaunchKernelGGL(k_pcd_write<true>, grid, dim3(kPcdBlock), 0, c->stream, a);
     else hipLaunchKernelGGL(k_pcd_write<false>, grid, dim3(kPcdBlock), 0, c->stream, a);
   }
+  if (src.batch) src.batch->hot_order = a.worder;
   HIPCHK(hipGetLastError());
   if (!slow.empty()) {
     // the list rides in the scratch blob's tile-byte slots, which k_pcd_write has finished reading

@@ -187,6 +187,7 @@ struct LvxArgs {
   const uint8_t* has_int;       // [F] frame has an intensity column (else reflectivity 128), or null
   char* out;                    // file base
   int* err;                     // set to 1 on a NaN coordinate / intensity (LMC:259, 268 int(nan))
+  int order;                    // stream_unit order of the package units
 };
 
 // int(np.clip(v * scale, lo, hi)) (LMC:259-261, 268): truncation toward zero after the clip
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(kCodecBlock) void k_lvx_packages(const LvxArgs a) {
   static_assert(kCodecBlock >= 96 + 12 && kLvxPkgPerWG * (kLvxPkgHdr / 2) <= 96, "header threads");
   __shared__ uint4 s_buf[kLvxLds / 16 + 1];
   uint16_t* const s16 = reinterpret_cast<uint16_t*>(s_buf);
-  const int64_t u = xcd_unit<MC_XCD_LVX>(blockIdx.x, gridDim.x);   // grid = units exactly
+  const int64_t u = stream_unit(a.order, blockIdx.x, gridDim.x);   // grid = units exactly
   const int32_t f = codec_frame_of(a.src, u);
   const int64_t pkg0 = (u - a.src.unit_off[f]) * kLvxPkgPerWG;
   const int64_t frow = a.src.doff[f];
@@ -457,6 +458,7 @@ struct PcdArgs {
   const int64_t* tile_pos;      // write: byte offset of each tile's text in `out`
   char* out;
   int* err;                     // 1: a value beyond the formatter's range
+  int morder, worder;           // stream_unit orders of the float32 measure pass / of the write pass
 };
 
 struct PcdLine {
@@ -869,7 +871,7 @@ __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure_list(const PcdArgs a,
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_measure(const PcdArgs a) {
   if constexpr (F32) {
-    pcd_measure_waves(a, xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdMeasureTiles);
+    pcd_measure_waves(a, stream_unit(a.morder, blockIdx.x, gridDim.x) * kPcdMeasureTiles);
   } else {
     __shared__ int s_wave[kPcdBlock / 64];
     const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdTilesPerWG;   // grid = units exactly
@@ -979,7 +981,7 @@ template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
   __shared__ uint4 s_text4[kPcdTextChunks];
-  const int64_t u0 = xcd_unit<MC_XCD_CODEC>(blockIdx.x, gridDim.x) * kPcdWriteTiles;   // grid = units exactly
+  const int64_t u0 = stream_unit(a.worder, blockIdx.x, gridDim.x) * kPcdWriteTiles;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {
     // Order per tile j: loads of tile j + 2, tile j's LDS text, tile j + 1 converted, tile j's

@@ -185,6 +185,10 @@ struct mc_batch {
   std::vector<int64_t> counts, poff, doff;
   std::vector<int32_t> ftile;      // first tile of each frame (F+1), host copy
   int32_t n_tiles = 0;
+  // stream_unit order (layout.hpp) of the last kernel that went over the batch's points: its last
+  // units may still be in the Infinity Cache, so the codec kernels run the opposite direction
+  // (a hint for speed only; kernels that do not record it leave it stale)
+  mutable int hot_order = 0;
   // blocked columns: block k (points 256k .. 256k+255) holds its C columns of 256 values back to
   // back, C * P values in all (mc::bidx); t_ns, when present, is column 4 (int32 bits)
   float* d_cols = nullptr;
@@ -213,4 +217,6 @@ namespace mcimpl {
 // mc_deskew's body; pcd_len != nullptr: the *_pcd deskew kernels also write each output block's
 // ASCII PCD text bytes there (mc_deskew_pcd)
 int deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t* pcd_len);
+// the sub-tile order (0 dealt, 1 XCD-contiguous) mc_deskew's kernel takes for this mode and batch
+int deskew_order(const mc_ctx* c, const mc_batch* in, int mode);
 }  // namespace mcimpl

@@ -25,6 +25,20 @@ __device__ __forceinline__ int64_t xcd_unit(int64_t b, int64_t n) {
   return x * per + (x < rem ? x : rem) + i;
 }
 
+// Stream order of a launch over n units (workgroup b -> unit): bit 1 = the 8 contiguous XCD ranges of
+// xcd_unit<true> (else in order), bit 0 = reversed (within each range).  Codec kernels take the order
+// that starts where the previous kernel over the same batch ended (mc_batch::hot_order), while those
+// points may still sit in the 256 MB Infinity Cache.  A bijection on [0, n) for any n.
+__device__ __forceinline__ int64_t stream_unit(int order, int64_t b, int64_t n) {
+  const bool rev = (order & 1) != 0;
+  if (order & 2) {
+    const int64_t x = b % kXcds, i = b / kXcds, per = n / kXcds, rem = n % kXcds;
+    const int64_t len = per + (x < rem ? 1 : 0), start = x * per + (x < rem ? x : rem);
+    return start + (rev ? len - 1 - i : i);
+  }
+  return rev ? n - 1 - b : b;
+}
+
 // 64-bit integer minimum (HIP's min / max templates resolve int64_t arguments through float64
 // conversions on gfx950: six VALU instructions for a wave-uniform value)
 __device__ __forceinline__ int64_t min_i64(int64_t a, int64_t b) { return a < b ? a : b; }

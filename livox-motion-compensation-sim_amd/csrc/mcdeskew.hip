@@ -719,12 +719,10 @@ void deskew_plan(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pos
   if (mode == MC_MODE_FRAME) units = in->n_tiles * kSub * kQuadUnitsPerSub;   // the quad decomposition
   sp->grid = (uint32_t)launch_grid(c, units);
   sp->kernel = mode;
-  // sub-tile order: default_order, or mc_tune_order's measured choice
-  da.xcd_order = default_order(mode, in->P);
-  // a device-measured choice for this mode and batch size (mc_tune_order) overrides the default
-  const mc_ctx::OrderTune& ot = c->order_tune[mode];
-  if (ot.order >= 0 && ot.P == in->P) da.xcd_order = ot.order;
+  da.xcd_order = mcimpl::deskew_order(c, in, mode);
+  in->hot_order = out->hot_order = da.xcd_order ? 2 : 0;   // (the deskew kernels run forward)
 }
+
 
 // A span slot for a timed deskew launch (null when the pool is spent: that launch has events only).
 // The pool is allocated and zeroed by mc_create: allocating it at the first timed launch idled the
@@ -788,6 +786,13 @@ int mc_deskew(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_s
 }
 
 }  // extern "C"
+
+// sub-tile order: default_order, or a device-measured choice for this mode and batch size
+// (mc_tune_order)
+int mcimpl::deskew_order(const mc_ctx* c, const mc_batch* in, int mode) {
+  const mc_ctx::OrderTune& ot = c->order_tune[mode];
+  return ot.order >= 0 && ot.P == in->P ? ot.order : default_order(mode, in->P);
+}
 
 int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t* pcd_len) {
   if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
