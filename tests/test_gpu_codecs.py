@@ -323,3 +323,22 @@ def test_pcd_batch_many_tiles_space_and_sizes(mc, gpu_ctx):
         buf.close()
     for f, c in enumerate(counts):
         assert mc.codecs.pcd_header(int(c)) + text[pos[f]:pos[f + 1]] == got[f]
+
+
+@pytest.mark.parametrize("mode", ["pose_slerp", "frame"])
+def test_codec_unit_orders_give_the_same_bytes(mc, gpu_ctx, mode):
+    """The codec launches start where the last kernel over the batch ended (mc_batch::hot_order,
+    layout.hpp stream_unit): after a deskew in dealt order (SLERP) or in XCD ranges (frame mode),
+    encodes in a row run the batch forwards and backwards, whole or by XCD range; every file must
+    equal the oracle's (ragged frames, an empty one, partial units and tiles)."""
+    counts = np.array([4096, 3, 2500, 0, 10_000, 7, 256, 257, 20_003, 1], np.int64)
+    b = _deskew_setup(mc, gpu_ctx, counts)
+    out = gpu_ctx.deskew(b, gpu_ctx.batch(counts), mode=mode)
+    host = out.split(out.download_aos())
+    want_pcd = [C.pcd_ascii_bytes(h) for h in host]
+    ids, ts = np.arange(len(counts)) + 90, np.arange(len(counts)) * 0.1
+    want_lvx = C.lvx_bytes([{"frame_id": i, "timestamp": t, "points": h} for i, t, h in zip(ids, ts, host)])
+    for _ in range(2):   # each call flips the direction of the next
+        assert mc.codecs.encode_pcd_batch(out) == want_pcd
+        assert mc.codecs.encode_lvx_batch(out, ids, ts) == want_lvx
+    assert mc.codecs.deskew_pcd_frames(b, out, mode=mode) == want_pcd
