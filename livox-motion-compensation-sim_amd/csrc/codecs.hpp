@@ -25,10 +25,9 @@
                              // XCD-contiguous, fused PCD share 0.514 / 0.519 vs 0.502 / 0.500, measure +
                              // write 1012.1 vs 1024.1 us (profiles/round3/s61)
 #endif
-#ifndef MC_XCD_LVX
-#define MC_XCD_LVX 0         // LVX unit order: dealt — 304.5 / 305.5 / 305.1 vs 310.6 / 314.9 / 319.5 us
-                             // XCD-contiguous, 3 interleaved A/Bs (profiles/round3/s58, s59)
-#endif
+// (The LVX packer and the float32 PCD passes take their unit order at run time from the batch's hot
+// end, layout.hpp stream_unit; standalone, dealt beat XCD-contiguous for LVX as well: 304.5 / 305.5 /
+// 305.1 vs 310.6 / 314.9 / 319.5 us, profiles/round3/s58, s59.)
 
 namespace mc {
 
@@ -53,7 +52,7 @@ static_assert(kLvxUnitPoints % kCodecBlock == 0, "unit = whole blocks");
                                 // 822.6 / 772.1 us (SLERP / frame source), fused PCD share 0.527 / 0.561 vs
                                 // 0.507 / 0.537 (profiles/round3/s66, s67)
 #endif
-constexpr int kPcdTilesPerWG = MC_PCD_TILES_PER_WG;             // PCD tiles of kCodecBlock lines per workgroup
+constexpr int kPcdTilesPerWG = MC_PCD_TILES_PER_WG;             // PCD tiles per measure / byte-path workgroup
 constexpr int kPcdBlock = 256;   // PCD: threads per workgroup = lines per tile (512: 1088 / 1085 vs 1080 us, profiles/round2/s40)
 constexpr int kPcdTileText = kPcdBlock * 64;                     // LDS text buffer per tile (packed lines <= 52 B)
 constexpr int kPcdPackedText = kPcdBlock * 52 + 16;              // a packed tile's text + its HBM offset mod 16
