@@ -530,7 +530,9 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     alg = 16 * n_rank + int(pos[-1])
     rep["lvx"] = {"file_bytes": int(pos[-1]), "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
                   "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
-                  "bytes_per_point": alg / n_rank, "traffic_over_algorithmic": aux_traffic("k_lvx_packages")}
+                  "bytes_per_point": alg / n_rank, "traffic_over_algorithmic": aux_traffic("k_lvx_packages"),
+                  "note": "back-to-back encodes of one batch; each starts where the previous kernel over the batch "
+                          "ended (DESIGN §4 codec unit order)"}
     bpos = np.zeros(F + 1, np.int64)
     cap = n_rank * 48
     out = ctx.device_buffer(cap)
@@ -550,7 +552,7 @@ def measure_codecs(ctx, b_out, n_rank, reps, cpu_budget):
     alg = 16 * n_rank + text
     rep["pcd_ascii"] = {"text_bytes": text, "kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3,
                         "GBs": alg / ms / 1e6, "frac": alg / ms / 1e6 / HBM_PEAK_GBS,
-                        "bytes_per_point": alg / n_rank, "note": "measure + write passes",
+                        "bytes_per_point": alg / n_rank, "note": "measure + write passes, each starting where the previous kernel over the batch ended",
                         "traffic_over_algorithmic": aux_traffic("k_pcd_measure", "k_pcd_write")}
     if cpu_budget > 0:
         from oracle import codecs as C
