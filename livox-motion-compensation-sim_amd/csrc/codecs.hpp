@@ -964,13 +964,13 @@ __device__ __forceinline__ void pcd_tile_store(const PcdArgs& a, int64_t G, int 
 
 // Tiles per write workgroup.  The float32 pass unrolls a workgroup's tiles and issues the point
 // loads of two tiles before the first is converted, so that two tiles' loads are in flight and every
-// vmcnt wait the compiler places is exact (no loop carries a load).  Kernel time with the tiles of
-// one workgroup in a loop (one tile's loads ahead) vs unrolled: 640.1 vs 588.0 us at 2 tiles, 626.4
-// at 1 (rocprofv3, profiles/round5/s19); measure + write 787.6 vs 739.0 us, fused write pass 722.6
-// vs 671.8 us (s18).  Rejected (s13-s16): 3 / 4 / 6 / 8 tiles unrolled with loads two or three tiles
-// ahead 738.8-806.2 us; a fixed number of stores per lane (buffer stores, those with nothing to store
-// dropped past the record count) so that the waits would not cover the previous tile's stores, 820.3
-// vs 787.6 us.
+// vmcnt wait the compiler places is exact (no loop carries a load).  Kernel time of the previous
+// pass (4 tiles in a loop, one tile's loads ahead) vs 2 tiles unrolled: 640.1 vs 588.0 us, 1 tile
+// 626.4 (rocprofv3, profiles/round5/s19); measure + write 787.6 vs 739.0 us, fused write pass 722.6
+// vs 671.8 us (s18).  Rejected (s13-s16, measure + write): 3 / 4 / 6 / 8 tiles unrolled with loads
+// two or three tiles ahead 738.8-806.2 us; a fixed number of stores per lane (buffer stores, those
+// with nothing to store dropped past the record count) so that the waits would not cover the
+// previous tile's stores, 820.3 vs 787.6 us.
 #ifndef MC_PCD_WRITE_TILES
 #define MC_PCD_WRITE_TILES 2
 #endif
