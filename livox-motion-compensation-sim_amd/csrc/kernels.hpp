@@ -904,7 +904,9 @@ __device__ __forceinline__ void deskew_frame_body(const DeskewArgs& a) {
 // every lane of the quad through DPP quad broadcasts (no LDS), lane c < 3 forms output column c of
 // the four points (R row c . p + t_c in float64, xf_row), lane 3 passes the
 // intensities through.  A bare 16 B-in / 16 B-out stream runs at 6.61-6.68 TB/s with one load and
-// one store per lane vs 6.12 with four of each (tools/stage_probe.hip, profiles/round2/s07).
+// one store per lane vs 6.12 with four of each (tools/stage_probe.hip, profiles/round2/s07).  Output
+// stores sc1 (the deskew kernels' policy): 296.7 vs 306.8 us non-temporal, 303.8 plain
+// (profiles/round5/s31).
 constexpr int kQuadGroups = kBlock / 4;   // float4 groups per workgroup in the quad decomposition
 
 // kQuadU quarters (64 float4 groups each) per workgroup: each lane issues U column loads before any
