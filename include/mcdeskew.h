@@ -80,6 +80,12 @@ extern "C" {
 
 /* batch creation flags */
 #define MC_BATCH_WITH_TIME 1u  /* allocate the t_ns column (needed by SLERP / IMU modes) */
+/* Keep the ASCII PCD text length (LMC:948) of every 256-point block beside the columns: the
+ * kernels that write the batch's x|y|z|intensity (mc_deskew / mc_deskew_steps into it, the stager
+ * mc_batch_upload_aos_f64 / mc_batch_stage_aos_f64_device, mc_scan_emit) also write those sums, so
+ * mc_pcd_encode_batch skips its measure pass.  Any other write of the columns (column uploads,
+ * synth, affine, gathers, mc_tune_order) marks the sums stale and the encoder measures again. */
+#define MC_BATCH_WITH_PCD_LEN 2u
 
 typedef struct mc_ctx mc_ctx;
 typedef struct mc_batch mc_batch;
@@ -113,6 +119,9 @@ int mc_batch_info(const mc_batch* b, int64_t* n_points, int64_t* padded_points, 
                   int32_t* n_tiles);
 /* padded frame offsets (n_frames+1 entries) as laid out on the device */
 int mc_batch_padded_offsets(const mc_batch* b, int64_t* poff_out);
+/* 1 when the batch's per-block PCD text sums describe its current columns (MC_BATCH_WITH_PCD_LEN
+ * and the last write of the columns produced them), else 0 */
+int mc_batch_pcd_len_current(const mc_batch* b, int32_t* current);
 /* per-frame reference time in seconds (LMC:792-793 lidar_times) for SEARCHSORTED / SLERP */
 int mc_batch_set_frame_times(mc_batch* b, const double* t_frame);
 /* per-frame start timestamp in ns (CSIM:2049 frame['timestamp']) for MC_MODE_IMU */

@@ -27,6 +27,7 @@ MC_MODE_IMU = 2
 MC_POSE_SEARCHSORTED = 0
 MC_POSE_DIRECT = 1
 MC_BATCH_WITH_TIME = 1
+MC_BATCH_WITH_PCD_LEN = 2
 
 MODES = {"frame": MC_MODE_FRAME, "pose_slerp": MC_MODE_POSE_SLERP, "imu": MC_MODE_IMU}
 POSE_SELECT = {"searchsorted": MC_POSE_SEARCHSORTED, "direct": MC_POSE_DIRECT}
@@ -60,6 +61,7 @@ _SIGS = {
     "mc_batch_destroy": (c_int, [c_void_p]),
     "mc_batch_info": (c_int, [c_void_p, _pi64, _pi64, _pi32, _pi32]),
     "mc_batch_padded_offsets": (c_int, [c_void_p, _pi64]),
+    "mc_batch_pcd_len_current": (c_int, [c_void_p, _pi32]),
     "mc_batch_set_frame_times": (c_int, [c_void_p, _pd]),
     "mc_batch_set_frame_start_ns": (c_int, [c_void_p, _pi64]),
     "mc_batch_upload_aos_f64": (c_int, [c_void_p, _pd, c_int64]),

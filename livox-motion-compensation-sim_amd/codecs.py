@@ -104,6 +104,14 @@ def encode_lvx(frames_data: List[dict], context: Context | None = None) -> bytes
         buf.close()
 
 
+def encode_lvx_device_rows(rows: DeviceBuffer, counts, frames_data: List[dict]) -> bytes:
+    """encode_lvx of ``frames_data`` whose points are already on the device as (N, 4) float64 rows,
+    frames back to back (``counts``): no host staging or upload (save_lvx after simulate_frames)."""
+    ids = [_u64(fd["frame_id"], "frame_id") for fd in frames_data]
+    ts = [_u64(int(fd["timestamp"] * 1e9), "timestamp_ns") for fd in frames_data]   # LMC:176
+    return _lvx_encode_device(rows.ctx, rows.ptr, 4, counts, ids, ts, None).tobytes()
+
+
 def encode_lvx_batch(batch: Batch, frame_ids, timestamps) -> bytes:
     """LVX file of a device batch's frames, encoded from the batch's float32 columns in HBM
     (mc_lvx_encode_batch): the records of the reference writer applied to ``batch.download_aos()``."""
@@ -140,6 +148,9 @@ class LivoxLVXWriter:
         self._context = context
 
     def write_compatible_lvx(self, filename: str, frames_data: List[dict]) -> bool:
+        return self._write(filename, frames_data, lambda: encode_lvx(frames_data, self._context))
+
+    def _write(self, filename: str, frames_data: List[dict], encode) -> bool:
         # LMC:70-77: argument validation raises; any failure after it returns False
         if not filename or not isinstance(filename, str):
             raise ValueError("Invalid filename provided")
@@ -148,7 +159,7 @@ class LivoxLVXWriter:
         try:
             print(f"Writing LVX file: {filename}")
             with open(filename, "wb") as f:
-                data = encode_lvx(frames_data, self._context)
+                data = encode()
                 f.write(data)
             print(f"✅ LVX file created successfully: {len(data):,} bytes")
             return True
@@ -204,6 +215,11 @@ def encode_pcd_bodies(clouds: Sequence[np.ndarray], context: Context | None = No
         return _pcd_bodies_device(ctx, buf.ptr, 4, counts)
     finally:
         buf.close()
+
+
+def encode_pcd_bodies_device_rows(rows: DeviceBuffer, counts) -> List[bytes]:
+    """encode_pcd_bodies of clouds already on the device as (N, 4) float64 rows, back to back."""
+    return _pcd_bodies_device(rows.ctx, rows.ptr, 4, counts)
 
 
 def encode_pcd(points, context: Context | None = None) -> bytes:

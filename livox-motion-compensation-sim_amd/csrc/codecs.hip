@@ -175,9 +175,10 @@ int lvx_encode(mc_ctx* c, const Source& src, int32_t F, const int64_t* counts, c
     if (F > 0 && empty_frame)
       hipLaunchKernelGGL(k_lvx_frames, dim3((F + kCodecBlock - 1) / kCodecBlock), dim3(kCodecBlock), 0, c->stream,
                          a, (int64_t)0);
-    if (n_pkg > 0)
+    if (n_pkg > 0) {
       hipLaunchKernelGGL(k_lvx_packages, dim3((uint32_t)n_pkg), dim3(kCodecBlock), 0, c->stream, a);
       if (src.batch) src.batch->hot_order = a.order;
+    }
   }
   HIPCHK(hipGetLastError());
   int err = 0;
@@ -206,7 +207,9 @@ int mc_pcd_encode_batch(mc_ctx* c, const mc_batch* b, void* d_out, int64_t out_b
   CHECK_ARG(b->ctx == c, "batch belongs to another context");
   Source src;
   src.batch = b;
-  return pcd_encode(c, src, b->F, b->counts.data(), d_out, out_bytes, body_pos);
+  // MC_BATCH_WITH_PCD_LEN: the kernel that last wrote the columns left their text sums (no measure pass)
+  return pcd_encode(c, src, b->F, b->counts.data(), d_out, out_bytes, body_pos,
+                    b->pcd_current() ? b->d_pcd_len : nullptr);
 }
 
 int mc_deskew_pcd(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, void* d_out,
@@ -215,6 +218,10 @@ int mc_deskew_pcd(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int po
   CHECK_ARG(out != in, "mc_deskew_pcd needs an output batch other than the input");
   CHECK_ARG(out->ctx == c, "batch belongs to another context");
   DeviceGuard g(c->device);
+  if (out->d_pcd_len) {   // MC_BATCH_WITH_PCD_LEN: the deskew writes the batch's own sums
+    if (int r = mcimpl::deskew_call(c, in, out, mode, pose_select, nullptr)) return r;
+    return mc_pcd_encode_batch(c, out, d_out, out_bytes, body_pos);
+  }
   // one text-byte slot per 256-point block of the output batch (= one PCD tile)
   const int64_t blocks = out->P / kBlkPts;
   if (blocks > c->pcd_len_cap) {

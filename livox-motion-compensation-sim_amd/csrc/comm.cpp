@@ -10,6 +10,7 @@
 // librccl is dlopen'ed on first use so the core library loads without it.
 #include "../../include/mcdeskew.h"
 #include "internal.hpp"
+#include "gather.hpp"
 #include "plan.hpp"
 
 #include <dlfcn.h>
@@ -69,9 +70,7 @@ int need_rccl() {
 }
 }  // namespace
 
-// per rank in the plan allgather: padded length, columns, merged padded length, merged columns
-// (root), frames, frame-count hash, merged frames, merged frame-count hash (root)
-constexpr int kPlanWords = 8;
+using mcgather::kPlanWords;
 
 struct mc_comm {
   mc_ctx* ctx = nullptr;
@@ -125,6 +124,67 @@ hipError_t finish_on_device(const mcplan::GatherPlan& G, int nranks, int root, c
     if (e_ != hipSuccess) return fail(MC_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+// mcgather::Transport over RCCL on the context stream: the plan words through one ncclAllGather of
+// device scratch, shards as grouped ncclSend / ncclRecv, the finishing copies as HIP copies.
+namespace {
+struct RcclGather {
+  mc_comm* c;
+  hipStream_t s;
+};
+int rg_hip(hipError_t e, const char* what) {
+  return e == hipSuccess ? MC_OK : fail(MC_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+int rg_nccl(ncclResult_t r, const char* what) {
+  return r == ncclSuccess ? MC_OK : fail(MC_ERR_COMM, "%s: %s", what, g_rccl.GetErrorString(r));
+}
+mcgather::Transport rccl_transport(RcclGather* x) {
+  mcgather::Transport T;
+  T.self = x;
+  T.nranks = x->c->nranks;
+  T.rank = x->c->rank;
+  T.allgather_i64 = [](void* p, const int64_t* mine, int n, int64_t* all) {
+    RcclGather* g = static_cast<RcclGather*>(p);
+    int64_t* d = g->c->d_scratch;   // [nranks * kPlanWords | own words]
+    const int nr = g->c->nranks;
+    if (int r = rg_hip(hipMemcpyAsync(d + (size_t)n * nr, mine, sizeof(int64_t) * n, hipMemcpyHostToDevice, g->s),
+                       "plan upload")) return r;
+    if (int r = rg_nccl(g_rccl.AllGather(d + (size_t)n * nr, d, (size_t)n, ncclInt64, g->c->comm, g->s),
+                        "ncclAllGather")) return r;
+    if (int r = rg_hip(hipMemcpyAsync(all, d, sizeof(int64_t) * n * nr, hipMemcpyDeviceToHost, g->s), "plan download"))
+      return r;
+    return rg_hip(hipStreamSynchronize(g->s), "plan sync");
+  };
+  T.group_start = [](void*) { return rg_nccl(g_rccl.GroupStart(), "ncclGroupStart"); };
+  T.group_end = [](void*) { return rg_nccl(g_rccl.GroupEnd(), "ncclGroupEnd"); };
+  T.send = [](void* p, const float* buf, int64_t n, int peer) {
+    RcclGather* g = static_cast<RcclGather*>(p);
+    return rg_nccl(g_rccl.Send(buf, (size_t)n, ncclFloat32, peer, g->c->comm, g->s), "ncclSend");
+  };
+  T.recv = [](void* p, float* buf, int64_t n, int peer) {
+    RcclGather* g = static_cast<RcclGather*>(p);
+    return rg_nccl(g_rccl.Recv(buf, (size_t)n, ncclFloat32, peer, g->c->comm, g->s), "ncclRecv");
+  };
+  T.stage = [](void* p, int64_t values, float** out) {
+    RcclGather* g = static_cast<RcclGather*>(p);
+    if (int r = ensure_stage(&g->c->d_stage, &g->c->stage_cap, values)) return r;
+    *out = g->c->d_stage;
+    return MC_OK;
+  };
+  T.copy = [](void* p, float* d, const float* src, int64_t n) {
+    RcclGather* g = static_cast<RcclGather*>(p);
+    return rg_hip(hipMemcpyAsync(d, src, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, g->s), "gather copy");
+  };
+  T.copy2d = [](void* p, float* d, int64_t dp, const float* src, int64_t sp, int64_t w, int64_t rows) {
+    RcclGather* g = static_cast<RcclGather*>(p);
+    return rg_hip(hipMemcpy2DAsync(d, (size_t)dp * sizeof(float), src, (size_t)sp * sizeof(float),
+                                   (size_t)w * sizeof(float), (size_t)rows, hipMemcpyDeviceToDevice, g->s),
+                  "gather re-pitch");
+  };
+  T.sync = [](void* p) { return rg_hip(hipStreamSynchronize(static_cast<RcclGather*>(p)->s), "gather sync"); };
+  return T;
+}
+}  // namespace
+
 extern "C" {
 
 int mc_comm_unique_id(char id_out[128]) {
@@ -173,58 +233,24 @@ int mc_comm_destroy(mc_comm* c) {
 
 int mc_comm_gather_batch(mc_comm* c, const mc_batch* local, int root, mc_batch* merged) {
   if (!c || !local) return fail(MC_ERR_INVALID, "NULL argument");
-  if (root < 0 || root >= c->nranks) return fail(MC_ERR_INVALID, "bad root %d", root);
   if (local->ctx != c->ctx) return fail(MC_ERR_INVALID, "batch belongs to another context");
   const bool is_root = c->rank == root;
-  if (is_root && !merged) return fail(MC_ERR_INVALID, "root needs a merged batch");
-  if (is_root && merged->ctx != c->ctx) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
+  if (is_root && merged && merged->ctx != c->ctx) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
   HIPCHK(hipSetDevice(c->ctx->device));
-  hipStream_t s = c->ctx->stream;
-  // every rank's (padded length, column count, frame count, hash of its frame counts) and the
-  // root's merged ones: all ranks then hold the whole plan and reject a bad one together, before
-  // any send (equal padded totals do not make the same frame order)
-  const int64_t nan = -1;
-  const int64_t mine[kPlanWords] = {
-      local->P, local->C, is_root ? merged->P : nan, is_root ? merged->C : nan, (int64_t)local->F,
-      (int64_t)mcplan::counts_hash(local->counts.data(), local->F), is_root ? (int64_t)merged->F : nan,
-      is_root ? (int64_t)mcplan::counts_hash(merged->counts.data(), merged->F) : nan};
-  const int nr = c->nranks;
-  HIPCHK(hipMemcpyAsync(c->d_scratch + kPlanWords * nr, mine, sizeof(mine), hipMemcpyHostToDevice, s));
-  NCCLCHK(g_rccl.AllGather(c->d_scratch + kPlanWords * nr, c->d_scratch, kPlanWords, ncclInt64, c->comm, s));
-  std::vector<int64_t> all(kPlanWords * (size_t)nr);
-  HIPCHK(hipMemcpyAsync(all.data(), c->d_scratch, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  std::vector<int64_t> P(nr), C(nr), F(nr);
-  std::vector<uint64_t> H(nr);
-  for (int q = 0; q < nr; ++q) {
-    const int64_t* w = all.data() + kPlanWords * (size_t)q;
-    P[q] = w[0]; C[q] = w[1]; F[q] = w[4]; H[q] = (uint64_t)w[5];
+  RcclGather X{c, c->ctx->stream};
+  const mcgather::Transport T = rccl_transport(&X);
+  mcgather::Shard sh;
+  sh.P = local->P; sh.C = local->C; sh.F = local->F; sh.counts = local->counts.data(); sh.cols = local->d_cols;
+  mcgather::Merged mg;
+  if (is_root && merged) {
+    mg.P = merged->P; mg.C = merged->C; mg.F = merged->F; mg.counts = merged->counts.data(); mg.cols = merged->d_cols;
+    merged->wrote(false);
   }
-  const int64_t* wr = all.data() + kPlanWords * (size_t)root;
-  mcplan::GatherPlan G;
-  std::string perr = mcplan::plan_gather(nr, root, P.data(), C.data(), wr[2], wr[3], &G);
-  if (perr.empty()) perr = mcplan::check_frame_hashes(nr, F.data(), H.data(), wr[6], (uint64_t)wr[7]);
-  if (!perr.empty()) return fail(MC_ERR_INVALID, "%s", perr.c_str());
-  if (!is_root) {
-    if (local->P > 0) {
-      NCCLCHK(g_rccl.GroupStart());
-      NCCLCHK(g_rccl.Send(local->d_cols, (size_t)(local->C * local->P), ncclFloat32, root, c->comm, s));
-      NCCLCHK(g_rccl.GroupEnd());
-    }
-    HIPCHK(hipStreamSynchronize(s));
-    return MC_OK;
-  }
-  if (int r = ensure_stage(&c->d_stage, &c->stage_cap, G.stage_values)) return r;
-  NCCLCHK(g_rccl.GroupStart());
-  for (int q = 0; q < nr; ++q) {
-    if (q == root || P[q] == 0) continue;
-    float* dst = mcplan::gather_dst(G, q, merged->d_cols, merged->C, c->d_stage);
-    NCCLCHK(g_rccl.Recv(dst, (size_t)(C[q] * P[q]), ncclFloat32, q, c->comm, s));
-  }
-  NCCLCHK(g_rccl.GroupEnd());
-  HIPCHK(finish_on_device(G, nr, root, P.data(), C.data(), merged, local->d_cols, c->d_stage, s));
-  HIPCHK(hipStreamSynchronize(s));
-  merged->trange_valid = false;   // column 4 (t_ns) was written: its cached spans are stale
+  std::string msg;
+  const int r = mcgather::run(T, root, sh, is_root && merged ? &mg : nullptr, &msg);
+  if (r == mcgather::kBadPlan) return fail(MC_ERR_INVALID, "%s", msg.c_str());
+  if (r) return r;   // the primitive recorded its message (mc_last_error)
+  if (is_root) merged->trange_valid = false;   // column 4 (t_ns) was written: its cached spans are stale
   return MC_OK;
 }
 
@@ -286,6 +312,7 @@ int mc_gather_batches(mc_ctx* ctx, int32_t n, const mc_batch* const* shards, int
   hipStream_t s = ctx->stream;
   float* stage = nullptr;
   if (G.stage_values > 0) HIPCHK(hipMalloc(&stage, (size_t)G.stage_values * sizeof(float)));
+  merged->wrote(false);
   hipError_t e = hipSuccess;
   for (int32_t q = 0; q < n && e == hipSuccess; ++q) {
     if (q == root || P[q] == 0) continue;

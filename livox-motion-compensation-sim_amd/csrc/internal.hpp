@@ -137,6 +137,10 @@ struct mc_ctx {
   std::vector<int64_t> scan_counts;   // final per-frame counts of the last mc_scan_count
   double scan_par[4] = {0, 0, 0, 0};  // range_min, range_max^2, fov_h/2, fov_v/2
   int64_t scan_cap = 0;
+  // the visibility words / tile offsets above describe the scene of version scan_env_ver; a pass 2
+  // on any other scene is refused (the poses were copied to d_scan_pose by the count itself)
+  uint64_t env_ver = 0, scan_env_ver = 0;
+  bool scan_valid = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> scan_ev;
   // output codecs: per-call frame / unit tables carved from one scratch buffer, error flag
   void* d_codec = nullptr;
@@ -211,6 +215,16 @@ struct mc_batch {
   mc::FrameWin* d_swin = nullptr;  // per sub-tile window, double-buffered (2 * n_sub)
   double* d_partial = nullptr;
   bool has_times = false, has_starts = false, trange_valid = false;
+  // MC_BATCH_WITH_PCD_LEN: ASCII PCD text bytes per 256-point block (layout.hpp PcdCount sums).
+  // data_ver counts the writes of the x|y|z|intensity columns; pcd_ver is the data_ver the sums
+  // were written with (current iff equal).
+  int32_t* d_pcd_len = nullptr;
+  uint64_t data_ver = 1, pcd_ver = 0;
+  void wrote(bool with_sums) {                               // after queueing a write of the columns
+    ++data_ver;
+    if (with_sums && d_pcd_len) pcd_ver = data_ver;
+  }
+  bool pcd_current() const { return d_pcd_len && pcd_ver == data_ver; }
 };
 
 namespace mcimpl {

@@ -1630,6 +1630,7 @@ struct LayoutArgs {
   const int64_t* poff; const int64_t* doff; const int64_t* counts;
   float* cols; int32_t C;   // blocked columns x|y|z|i[|t_ns]; C == 5 carries the t_ns column
   int64_t dbase;            // AoS row of the first frame covered (a frame range's fetch: doff[f0]; else 0)
+  int32_t* pcd_len;         // stager, MC_BATCH_WITH_PCD_LEN: ASCII PCD bytes per 256-point block, or nullptr
   __device__ __forceinline__ float& col(int c, int64_t p) const { return cols[bidx(C, c, p)]; }
   __device__ __forceinline__ int32_t& tns(int64_t p) const {
     return reinterpret_cast<int32_t*>(cols)[bidx(C, 4, p)];
@@ -1692,8 +1693,11 @@ __device__ __forceinline__ void soa_to_aos_unit(const LayoutArgs& a, double* __r
   }
 }
 
+// pcd_len: wave c also sums column c's text bytes over the unit's valid points (PcdCount, one
+// wave reduction); the four waves' sums meet in LDS and lane 0 of wave 0 writes the block's total.
 __device__ __forceinline__ void aos_to_soa_unit(const LayoutArgs& a, const double* __restrict__ aos) {
   __shared__ float s[4 * kUnitRow];
+  __shared__ int s_part[4];
   const int64_t n_units = (int64_t)a.n_tiles * kStageQuarters;
   const int t = threadIdx.x;
   for (int64_t it = blockIdx.x; it < n_units; it += gridDim.x) {
@@ -1719,9 +1723,17 @@ __device__ __forceinline__ void aos_to_soa_unit(const LayoutArgs& a, const doubl
     }
     __syncthreads();
     const int c = t >> 6, gi = t & 63;
-    if (g0 + gi < tl.ngroups)
-      st_pol<kStageSt>(a.cols + bidx(a.C, c, p0 + 4 * gi), *reinterpret_cast<const float4*>(&s[c * kUnitRow + 4 * gi]));
+    const float4 v = *reinterpret_cast<const float4*>(&s[c * kUnitRow + 4 * gi]);
+    if (g0 + gi < tl.ngroups) st_pol<kStageSt>(a.cols + bidx(a.C, c, p0 + 4 * gi), v);
+    if (a.pcd_len) {   // uniform
+      PcdCount pc;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pc.add(loc0 + 4 * gi + k < cnt, f4g(v, k));
+      const int bytes = pc.bytes();
+      if (gi == 0) s_part[c] = bytes;
+    }
     __syncthreads();
+    if (a.pcd_len && t == 0) a.pcd_len[p0 >> 8] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
   }
 }
 
@@ -1731,7 +1743,9 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
     aos_to_soa_unit(a, aos);
     return;
   }
-  // wider rows (ld > 4: extra columns the reference carries along): one point per lane
+  // wider rows (ld > 4: extra columns the reference carries along): one point per lane, one
+  // 256-point block (kBlock lanes) per pass, so a block's PCD text bytes are one workgroup sum
+  __shared__ int s_part[kBlock / 64];
   for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const Tile tl = ldu(a.tiles + tile);
     const int64_t poff = ldu(a.poff + tl.frame), doff = ldu(a.doff + tl.frame), cnt = ldu(a.counts + tl.frame);
@@ -1740,11 +1754,22 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
     const int64_t rest = min_i64(np, cnt - loc0);
     const int nv = rest > 0 ? (int)rest : 0;                          // valid ones
     const double* src = aos + (doff + loc0) * ld;
-    for (int j = threadIdx.x; j < np; j += kBlock) {
+    for (int j0 = 0; j0 < np; j0 += kBlock) {
+      const int j = j0 + (int)threadIdx.x;
       float r[4] = {0.f, 0.f, 0.f, 0.f};
       if (j < nv)
         for (int c = 0; c < 4; ++c) r[c] = (float)src[(int64_t)j * ld + c];
-      for (int c = 0; c < 4; ++c) a.col(c, tl.pstart + j) = r[c];
+      if (j < np)
+        for (int c = 0; c < 4; ++c) a.col(c, tl.pstart + j) = r[c];
+      if (a.pcd_len) {   // uniform; j0 is a block boundary (tiles hold whole blocks)
+        PcdCount pc;
+        for (int c = 0; c < 4; ++c) pc.add(j < nv, r[c]);
+        const int bytes = pc.bytes();
+        if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = bytes;
+        __syncthreads();
+        if (threadIdx.x == 0) a.pcd_len[(tl.pstart + j0) >> 8] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+        __syncthreads();
+      }
     }
   }
 }

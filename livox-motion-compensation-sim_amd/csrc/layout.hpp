@@ -76,6 +76,7 @@ __device__ __forceinline__ int i4c(const int4& v, int c) {
 // a ballot per term added up on the scalar unit was slower (+15 / +36 / +47 us: the 64-bit masks
 // spilled SGPRs into VGPR lanes, profiles/round3/s12).
 constexpr int kPcdSlowValue = 1 << 20;
+constexpr uint32_t kPcdSlowBits = 0x45863000u;   // |v| >= 4294.0f as a float32 bit pattern
 struct PcdCount {
   int n = 0;          // this lane's sum
   uint32_t amax = 0;  // largest |v| bit pattern of the lane's valid values (NaN / inf above any finite)
@@ -91,7 +92,7 @@ struct PcdCount {
     int t = n;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    const bool slow = __builtin_amdgcn_ballot_w64(amax >= 0x45863000u) != 0;   // |v| >= 4294.0f
+    const bool slow = __builtin_amdgcn_ballot_w64(amax >= kPcdSlowBits) != 0;
     return t + (slow ? kPcdSlowValue : 0);
   }
 };

@@ -62,6 +62,7 @@ static LayoutArgs layout_of(const mc_batch* b) {
   a.poff = b->d_poff; a.doff = b->d_doff; a.counts = b->d_counts;
   a.cols = b->d_cols; a.C = b->C;
   a.dbase = 0;
+  a.pcd_len = nullptr;
   return a;
 }
 
@@ -71,6 +72,7 @@ static int upload_column(mc_batch* b, const T* src, int col) {
   void* st = nullptr;
   if (int r = ctx_stage(c, (size_t)b->N * sizeof(T), &st)) return r;
   HIPCHK(hipMemcpyAsync(st, src, (size_t)b->N * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  if (col < 4) b->wrote(false);
   hipLaunchKernelGGL((k_column<T, 0>), dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream,
                      layout_of(b), col, static_cast<const T*>(st), static_cast<T*>(nullptr));
   HIPCHK(hipGetLastError());
@@ -310,6 +312,8 @@ int mc_batch_create(mc_ctx* c, int32_t F, const int64_t* counts, uint32_t flags,
     if ((r = dev_alloc(&b->d_swin, 2 * n_sub))) return bail(r);
   }
   if ((r = dev_alloc(&b->d_partial, 5 * (size_t)b->n_tiles))) return bail(r);
+  if ((flags & MC_BATCH_WITH_PCD_LEN) && (r = dev_alloc(&b->d_pcd_len, std::max<int64_t>(b->P / kBlkPts, 1))))
+    return bail(r);
   hipStream_t s = c->stream;
   auto cpy = [&](void* d, const void* h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s); };
   if (F > 0) {
@@ -340,6 +344,7 @@ int mc_batch_destroy(mc_batch* b) {
   if (b->d_frec) (void)hipFree(b->d_frec);
   b->d_frec = nullptr;
   dev_free(b->d_ftile); dev_free(b->d_strange); dev_free(b->d_swin);
+  dev_free(b->d_pcd_len);
   delete b;
   return MC_OK;
 }
@@ -356,6 +361,12 @@ int mc_batch_info(const mc_batch* b, int64_t* n, int64_t* padded, int32_t* F, in
 int mc_batch_padded_offsets(const mc_batch* b, int64_t* poff) {
   CHECK_ARG(b && poff, "NULL argument");
   std::memcpy(poff, b->poff.data(), (b->F + 1) * sizeof(int64_t));
+  return MC_OK;
+}
+
+int mc_batch_pcd_len_current(const mc_batch* b, int32_t* current) {
+  CHECK_ARG(b && current, "NULL argument");
+  *current = b->pcd_current() ? 1 : 0;
   return MC_OK;
 }
 
@@ -395,12 +406,16 @@ static int launch_stage(mc_batch* b, const double* d_aos, int64_t ld) {
   mc_ctx* c = b->ctx;
   if (b->n_tiles == 0) return MC_OK;
   queued_async(c);
+  LayoutArgs a = layout_of(b);
+  a.pcd_len = b->d_pcd_len;   // MC_BATCH_WITH_PCD_LEN: the stager sums each block's text bytes
   {
     TimedRegion tr(c, &c->layout_ev, c->stream);
     hipLaunchKernelGGL(k_aos_to_soa, dim3(launch_grid(c, stage_units(b->n_tiles, ld))), dim3(kBlock), 0, c->stream,
-                       layout_of(b), d_aos, ld);
+                       a, d_aos, ld);
   }
+  b->wrote(false);
   HIPCHK(hipGetLastError());
+  b->wrote(true);
   return MC_OK;
 }
 // batch columns -> device AoS (N,4) f64 (async, timed as a layout kernel)
@@ -579,6 +594,7 @@ int mc_batch_synth(mc_batch* b, uint64_t seed, int64_t frame_id_base) {
   if (b->n_tiles == 0) return MC_OK;
   mc_ctx* c = b->ctx;
   DeviceGuard g(c->device);
+  b->wrote(false);
   hipLaunchKernelGGL(k_synth, dim3(launch_grid(c, b->n_tiles)), dim3(kBlock), 0, c->stream, layout_of(b), seed,
                      frame_id_base);
   HIPCHK(hipGetLastError());
@@ -797,6 +813,8 @@ int mcimpl::deskew_order(const mc_ctx* c, const mc_batch* in, int mode) {
 int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select, int32_t* pcd_len) {
   if (int r = deskew_check(c, in, out, mode, pose_select)) return r;
   if (in->F == 0) return MC_OK;
+  if (!pcd_len) pcd_len = out->d_pcd_len;   // MC_BATCH_WITH_PCD_LEN: the *_pcd kernels keep its sums
+  out->wrote(false);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
   if (mode != MC_MODE_FRAME && !in->trange_valid) {
@@ -856,6 +874,7 @@ int mcimpl::deskew_call(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, 
     }
     ev.keep(&c->main_ev);
     HIPCHK(hipGetLastError());
+    out->wrote(pcd_len != nullptr && pcd_len == out->d_pcd_len);
     // after a speculative launch the next prep (on a miss) writes the half its prep workgroups write
     c->prep_fence = speculate;
   } else {
@@ -873,7 +892,9 @@ namespace {
 // The launches of n steps over the two table halves of `plan` (step i reads half i & 1 of plan):
 // step 0's k_prep, then n deskew launches of which the first n - 1 carry the next step's prep.
 // Every `every`-th step's kernel (and prep) is timed.
-void issue_steps(mc_ctx* c, const StepPlan* plan, int mode, int32_t n_steps, int32_t every) {
+// last_pcd: the last step's launch also writes the output blocks' PCD text bytes there (its output is
+// what the batch keeps; the launches before it have no PCD variant of the fused next-prep kernel).
+void issue_steps(mc_ctx* c, const StepPlan* plan, int mode, int32_t n_steps, int32_t every, int32_t* last_pcd) {
   hipStream_t s = c->stream;
   (void)mode;
   auto sampled = [&](int32_t i) { return every > 0 && i % every == every / 2; };
@@ -888,8 +909,12 @@ void issue_steps(mc_ctx* c, const StepPlan* plan, int mode, int32_t n_steps, int
     LaunchEvents ev(c, sampled(i));
     StepPlan sp = plan[i & 1];
     if (ev.e0) sp.da.span = span_take(c);
-    if (i + 1 < n_steps) launch_fused(sp, plan[(i + 1) & 1], s, ev.e0, ev.e1);
-    else launch_main(sp, s, ev.e0, ev.e1);
+    if (i + 1 < n_steps) {
+      launch_fused(sp, plan[(i + 1) & 1], s, ev.e0, ev.e1);
+    } else {
+      sp.da.pcd_len = last_pcd;
+      launch_main(sp, s, ev.e0, ev.e1);
+    }
     ev.keep(&c->main_ev);
   }
 }
@@ -909,8 +934,10 @@ int deskew_steps_pipelined(mc_ctx* c, const mc_batch* in, mc_batch* out, int mod
   deskew_plan(c, in, out, mode, pose_select, h0, &plan[0]);
   deskew_plan(c, in, out, mode, pose_select, h0 ^ 1, &plan[1]);
   if (plan[0].da.copy_t) out->trange_valid = false;
-  issue_steps(c, plan, mode, n_steps, every);
+  out->wrote(false);
+  issue_steps(c, plan, mode, n_steps, every, plan[0].kernel >= 0 ? out->d_pcd_len : nullptr);
   HIPCHK(hipGetLastError());
+  if (plan[0].kernel >= 0 && n_steps > 0) out->wrote(true);
   c->buf = h0 ^ (n_steps & 1);   // the half the last launch did not read
   c->prep_fence = false;
   return MC_OK;
@@ -944,6 +971,7 @@ int mc_tune_order(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int po
   deskew_plan(c, in, out, mode, pose_select, h0, &plan[0]);
   deskew_plan(c, in, out, mode, pose_select, h0 ^ 1, &plan[1]);
   if (plan[0].da.copy_t) out->trange_valid = false;
+  out->wrote(false);      // plain kernels only: any PCD text sums of out go stale
   c->prep_fence = true;   // the first prep is an ordinary packet: waits for everything queued before it
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIPCHK(hipEventCreate(&e0));
@@ -959,10 +987,10 @@ int mc_tune_order(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int po
       // the previous round's last launch may read either half (odd `launches`): the warm-up's first
       // prep is an ordinary packet, so it waits for that launch
       c->prep_fence = true;
-      issue_steps(c, plan, mode, 2, 0);   // untimed: this order's own steady state
+      issue_steps(c, plan, mode, 2, 0, nullptr);   // untimed: this order's own steady state
       c->prep_fence = false;
       e = hipEventRecord(e0, s);
-      issue_steps(c, plan, mode, launches, 0);
+      issue_steps(c, plan, mode, launches, 0, nullptr);
       if (e == hipSuccess) e = hipEventRecord(e1, s);
       if (e == hipSuccess) e = hipEventSynchronize(e1);
       float ms = 0.f;
@@ -1012,225 +1040,36 @@ constexpr size_t kPipeBytes = (size_t)kPipeRows * 4 * sizeof(double);
 constexpr int64_t kZeroCopyRows = 1 << 15;                             // below: zero-copy kernels
 constexpr int kPoolThreads = 16;                                       // the box's CPU share per GPU
 constexpr int64_t kJobRows = 8192;                                     // rows per host copy job (256 KB)
-static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
-                        const int64_t* d_doff, const double* d_pose, double* const* outs);
-
-// pinned, device-mapped host scratch of at least `bytes` (the zero-copy path of the single calls)
-static int ctx_pin(mc_ctx* c, size_t bytes, char** out) {
-  if (bytes > c->pin_bytes) {
-    if (c->h_pin) { (void)hipStreamSynchronize(c->stream); (void)hipHostFree(c->h_pin); c->h_pin = nullptr; }
-    c->pin_bytes = 0;
-    HIPCHK(hipHostMalloc(&c->h_pin, bytes, hipHostMallocMapped | hipHostMallocCoherent));
-    c->pin_bytes = bytes;
-  }
-  *out = static_cast<char*>(c->h_pin);
-  return MC_OK;
-}
-
-// Frames of host float64 rows through k_align_rows_f64 with the per-frame poses pose12 (F x 12,
-// host): below kZeroCopyRows rows the kernel reads and writes pinned, device-mapped host memory
-// (no DMA round trips for the reference's per-frame calls); above, the DMA row pipeline.
-static int align_host_rows(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
-                           const std::vector<double>& pose12, double* const* outs) {
-  const int32_t F = (int32_t)doff.size() - 1;
-  const int64_t n = doff[F];
-  if (n >= kZeroCopyRows) {
-    void* st = nullptr;
-    const size_t tab_b = doff.size() * sizeof(int64_t) + pose12.size() * sizeof(double);
-    if (int r = ctx_stage(c, tab_b, &st)) return r;
-    int64_t* d_doff = static_cast<int64_t*>(st);
-    double* d_pose = reinterpret_cast<double*>(d_doff + doff.size());
-    HIPCHK(hipMemcpyAsync(d_doff, doff.data(), doff.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(d_pose, pose12.data(), pose12.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    return row_pipeline(c, frames, lds, doff, d_doff, d_pose, outs);
-  }
-  // pinned [doff (F+1) | poses (12 F) | rows (n, 4) | out (n, 4)], 8-byte words
-  const size_t w_pose = doff.size(), w_rows = w_pose + pose12.size(), w_out = w_rows + 4 * (size_t)n;
-  char* base = nullptr;
-  if (int r = ctx_pin(c, (w_out + 4 * (size_t)n) * 8, &base)) return r;
-  double* pin = reinterpret_cast<double*>(base);
-  std::memcpy(pin, doff.data(), doff.size() * 8);
-  std::memcpy(pin + w_pose, pose12.data(), pose12.size() * 8);
-  for (int32_t f = 0; f < F; ++f) {
-    const int64_t m = doff[f + 1] - doff[f], ld = lds[f];
-    double* dst = pin + w_rows + 4 * doff[f];
-    if (ld == 4) std::memcpy(dst, frames[f], (size_t)m * 4 * sizeof(double));
-    else for (int64_t i = 0; i < m; ++i) std::memcpy(dst + 4 * i, frames[f] + i * ld, 4 * sizeof(double));
-  }
-  {
-    TimedRegion tr(c, &c->main_ev, c->stream);
-    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
-    hipLaunchKernelGGL(k_align_rows_f64, dim3(grid), dim3(kBlock), 0, c->stream, pin + w_rows, (int64_t)4, n,
-                       (int64_t)0, reinterpret_cast<const int64_t*>(pin), F, pin + w_pose, pin + w_out);
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
-  for (int32_t f = 0; f < F; ++f)
-    if (doff[f + 1] > doff[f])
-      std::memcpy(outs[f], pin + w_out + 4 * doff[f], (size_t)(doff[f + 1] - doff[f]) * 4 * sizeof(double));
-  return MC_OK;
-}
-
-int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
-                                const double* translation, double* out) {
-  CHECK_ARG(c && rpy && translation, "NULL argument");
-  CHECK_ARG(n >= 0, "negative point count");
-  if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 1 with size %lld", (long long)ld);
-  if (n == 0) return MC_OK;
-  CHECK_ARG(points && out, "NULL points / out");
-  DeviceGuard g(c->device);
-  if (int r = sync_all(c)) return r;
-  // LMC:774: R = Rotation.from_euler('xyz', rotation).as_matrix(), scipy's arithmetic (rot.cpp)
-  std::vector<double> pose(12);
-  mcrot::euler_xyz_scipy(rpy, pose.data());
-  for (int k = 0; k < 3; ++k) pose[9 + k] = translation[k];
-  const std::vector<int64_t> doff{0, n};
-  const double* fr[1] = {points};
-  const int64_t lds[1] = {ld};
-  double* const outs[1] = {out};
-  return align_host_rows(c, fr, lds, doff, pose, outs);
-}
-
-// ---- per-point modes on host float64 rows (k_points_f64) --------------------------------------
-
-int mc_deskew_points_f64(mc_ctx* c, int mode, int32_t F, const int64_t* counts, const double* points, int64_t ld,
-                         const int64_t* t_ns, const double* frame_times, const int64_t* frame_start_ns, double* out) {
-  CHECK_ARG(c, "ctx is NULL");
-  CHECK_ARG(mode == MC_MODE_POSE_SLERP || mode == MC_MODE_IMU, "mode %d: MC_MODE_POSE_SLERP or MC_MODE_IMU expected",
-            mode);
-  CHECK_ARG(F >= 0, "n_frames must be >= 0");
-  CHECK_ARG(F == 0 || counts, "counts is NULL");
-  if (ld < 3) return fail(MC_ERR_INDEX, "points need at least 3 columns (x, y, z); got %lld", (long long)ld);
-  std::vector<int64_t> doff((size_t)F + 1, 0);
-  for (int32_t f = 0; f < F; ++f) {
-    CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
-    doff[f + 1] = doff[f] + counts[f];
-  }
-  if (mode == MC_MODE_POSE_SLERP) {
-    if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
-    CHECK_ARG(F == 0 || frame_times, "frame times are NULL");
-  } else {
-    if (c->M < 1) return fail(MC_ERR_STATE, "no IMU samples uploaded (mc_set_imu)");
-    CHECK_ARG(F == 0 || frame_start_ns, "frame start times are NULL");
-  }
-  const int64_t n = doff[F];
-  if (n == 0) return MC_OK;
-  CHECK_ARG(points && t_ns && out, "NULL points / t_ns / out");
-  DeviceGuard g(c->device);
-  if (int r = sync_all(c)) return r;
-  hipStream_t s = c->stream;
-  // the segment table of the uploaded trajectory / IMU samples (k_prep's table lanes, no frames)
-  const uint64_t ver = mode == MC_MODE_POSE_SLERP ? c->traj_ver : c->imu_ver;
-  const int64_t nseg = mode == MC_MODE_POSE_SLERP ? std::max<int64_t>(c->T - 1, 1) : c->M;
-  const size_t seg_b = (size_t)nseg * (mode == MC_MODE_POSE_SLERP ? sizeof(PoseSeg) : sizeof(ImuSeg));
-  if (!(c->d_seg64 && c->seg64_mode == mode && c->seg64_ver == ver)) {
-    c->seg64_mode = -1;
-    if (seg_b > c->seg64_bytes) {
-      if (c->d_seg64) (void)hipFree(c->d_seg64);
-      c->d_seg64 = nullptr;
-      c->seg64_bytes = 0;
-      HIPCHK(hipMalloc(&c->d_seg64, seg_b));
-      c->seg64_bytes = seg_b;
-    }
-    PrepArgs pa;
-    std::memset(&pa, 0, sizeof(pa));
-    pa.mode = mode;
-    pa.n_frames = 0;
-    pa.time = c->d_time; pa.pos = c->d_pos; pa.rpy = c->d_rpy; pa.T = c->T;
-    pa.imu_ts = c->d_imu_ts; pa.gyro = c->d_gyro; pa.M = c->M;
-    pa.pose_seg = static_cast<PoseSeg*>(c->d_seg64);
-    pa.imu_seg = static_cast<ImuSeg*>(c->d_seg64);
-    pa.nseg = nseg;
-    const uint32_t blocks = (uint32_t)(((nseg + 63) / 64 + 3) / 4);
-    hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(kBlock), 0, s, pa);
-    HIPCHK(hipGetLastError());
-    c->seg64_mode = mode;
-    c->seg64_ver = ver;
-  }
-  // scratch: [doff (F+1) | per-frame value (F) | t_ns (n) | points (n, ld) | out (n, 4)], 8-byte words;
-  // pinned and device-mapped below kZeroCopyRows rows (the kernel reads and writes host memory: no
-  // DMA round trips for the reference's per-frame calls), a device staging buffer above
-  const size_t w_doff = 0, w_fv = (size_t)F + 1, w_t = w_fv + (size_t)F, w_pts = w_t + (size_t)n,
-               w_out = w_pts + (size_t)n * (size_t)ld, words = w_out + 4 * (size_t)n;
-  const bool zero_copy = n < kZeroCopyRows;
-  char* base = nullptr;
-  if (zero_copy) {
-    if (int r = ctx_pin(c, words * 8, &base)) return r;
-    std::memcpy(base + 8 * w_doff, doff.data(), doff.size() * 8);
-    std::memcpy(base + 8 * w_fv, mode == MC_MODE_POSE_SLERP ? static_cast<const void*>(frame_times)
-                                                            : static_cast<const void*>(frame_start_ns), (size_t)F * 8);
-    std::memcpy(base + 8 * w_t, t_ns, (size_t)n * 8);
-    std::memcpy(base + 8 * w_pts, points, (size_t)n * (size_t)ld * 8);
-  } else {
-    void* st = nullptr;
-    if (int r = ctx_stage(c, words * 8, &st)) return r;
-    base = static_cast<char*>(st);
-    HIPCHK(hipMemcpyAsync(base + 8 * w_doff, doff.data(), doff.size() * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(base + 8 * w_fv, mode == MC_MODE_POSE_SLERP ? static_cast<const void*>(frame_times)
-                                                                      : static_cast<const void*>(frame_start_ns),
-                          (size_t)F * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(base + 8 * w_t, t_ns, (size_t)n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(base + 8 * w_pts, points, (size_t)n * (size_t)ld * 8, hipMemcpyHostToDevice, s));
-  }
-  PointsF64Args a;
-  std::memset(&a, 0, sizeof(a));
-  a.pts = reinterpret_cast<const double*>(base + 8 * w_pts); a.ld = ld; a.n = n;
-  a.t_ns = reinterpret_cast<const int64_t*>(base + 8 * w_t);
-  a.doff = reinterpret_cast<const int64_t*>(base + 8 * w_doff); a.F = F;
-  a.ftime = reinterpret_cast<const double*>(base + 8 * w_fv);
-  a.fstart = reinterpret_cast<const int64_t*>(base + 8 * w_fv);
-  a.pose_time = c->d_time; a.pose_seg = static_cast<const PoseSeg*>(c->d_seg64); a.nseg = nseg;
-  a.imu_ts = c->d_imu_ts; a.imu_seg = static_cast<const ImuSeg*>(c->d_seg64);
-  a.ntab = mode == MC_MODE_POSE_SLERP ? c->T : c->M;
-  a.out = reinterpret_cast<double*>(base + 8 * w_out);
-  const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, zero_copy ? 1024 : 65536);
-  {
-    TimedRegion tr(c, &c->main_ev, s);
-    if (mode == MC_MODE_POSE_SLERP) hipLaunchKernelGGL(k_points_f64<1>, dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL(k_points_f64<2>, dim3(grid), dim3(kBlock), 0, s, a);
-  }
-  HIPCHK(hipGetLastError());
-  if (!zero_copy) HIPCHK(hipMemcpyAsync(out, a.out, (size_t)n * 32, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  if (zero_copy) std::memcpy(out, a.out, (size_t)n * 32);
-  return MC_OK;
-}
-
-// ---- host arrays <-> device: the row pipeline ------------------------------------------------
-// Rows of the concatenated frames travel in chunks: the host pool copies a chunk into pinned
-// memory (compacting rows to 4 columns), DMA to HBM, k_align_rows_f64, DMA back, the pool copies
-// the rows out to the caller's arrays — chunk k's host copies overlap chunk k±1's DMA and kernel.
-
-static void host_rows(mc_ctx* c, const std::vector<int64_t>& doff, int64_t r0, int64_t r1,
-                      const std::function<void(int32_t, int64_t, int64_t)>& seg) {
-  // segments (frame, row_a, row_b) of [r0, r1), at most kJobRows rows each, run on the pool
-  std::vector<std::array<int64_t, 3>> jobs;
-  int32_t f = (int32_t)(std::upper_bound(doff.begin(), doff.end(), r0) - doff.begin()) - 1;
-  for (; f < (int32_t)doff.size() - 1 && doff[f] < r1; ++f)
-    for (int64_t a = std::max(doff[f], r0), e = std::min(doff[f + 1], r1); a < e; a += kJobRows)
-      jobs.push_back({f, a, std::min(a + kJobRows, e)});
-  if (!c->pool) c->pool.reset(new mcimpl::HostPool(kPoolThreads));
-  c->pool->run((int64_t)jobs.size(), [&](int64_t j) { seg((int32_t)jobs[j][0], jobs[j][1], jobs[j][2]); });
-}
-
+// Variants (MCDESKEW_ROWPIPE, A/B of round 6): 0 = staged, one stream (H2D, kernel, D2H in order);
+// 1 = staged, the D2H on the side stream (chunk k's D2H beside chunk k+1's H2D: PCIe both ways);
+// 2 = direct: no host staging copies, DMA straight from the caller's 4-column frames and into its
+// contiguous output (HIP's pageable copies), D2H on the side stream.
 static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
                         const int64_t* d_doff, const double* d_pose, double* const* outs) {
   const int32_t F = (int32_t)doff.size() - 1;
   const int64_t n = doff[F];
-  if (!c->h_pipe) HIPCHK(hipHostMalloc(&c->h_pipe, 4 * kPipeBytes, hipHostMallocDefault));
+  int variant = 1;
+  if (const char* v = std::getenv("MCDESKEW_ROWPIPE")) variant = std::atoi(v);
+  bool dense = true;   // every frame 4 columns wide and the outputs one contiguous (n, 4) array
+  for (int32_t f = 0; f < F && dense; ++f)
+    dense = (lds[f] == 4 || doff[f + 1] == doff[f]) && outs[f] == outs[0] + 4 * doff[f];
+  if (variant == 2 && !dense) variant = 1;
+  if (!c->h_pipe && variant != 2) HIPCHK(hipHostMalloc(&c->h_pipe, 4 * kPipeBytes, hipHostMallocDefault));
   if (!c->d_pipe) HIPCHK(hipMalloc(&c->d_pipe, 4 * kPipeBytes));
-  double* pin[4];
+  double* pin[4] = {nullptr, nullptr, nullptr, nullptr};
   double* dev[4];
   for (int k = 0; k < 4; ++k) {
-    pin[k] = reinterpret_cast<double*>(static_cast<char*>(c->h_pipe) + k * kPipeBytes);
+    if (c->h_pipe) pin[k] = reinterpret_cast<double*>(static_cast<char*>(c->h_pipe) + k * kPipeBytes);
     dev[k] = reinterpret_cast<double*>(static_cast<char*>(c->d_pipe) + k * kPipeBytes);
   }
-  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
+  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
   for (int b = 0; b < 2; ++b) {
     HIPCHK(hipEventCreateWithFlags(&ev_in[b], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_out[b], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_k[b], hipEventDisableTiming));
   }
   hipStream_t s = c->stream;
+  hipStream_t so = variant == 0 ? c->stream : c->side;   // the D2H stream
   auto copy_out = [&](int64_t k) {
     const int64_t r0 = k * kPipeRows, r1 = std::min(n, r0 + kPipeRows);
     const double* src = pin[2 + (k & 1)];
@@ -1243,41 +1082,64 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
   for (int64_t k = 0; k < K && rc == MC_OK; ++k) {
     const int b = (int)(k & 1);
     const int64_t r0 = k * kPipeRows, r1 = std::min(n, r0 + kPipeRows), m = r1 - r0;
-    if (k >= 2) (void)hipEventSynchronize(ev_in[b]);                 // pinned input b is free again
-    double* dst = pin[b];
-    host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t e) {
-      const int64_t ld = lds[f];
-      const double* sp = frames[f] + (a - doff[f]) * ld;
-      double* dp = dst + 4 * (a - r0);
-      if (ld == 4) {
-        std::memcpy(dp, sp, (size_t)(e - a) * 4 * sizeof(double));
-      } else {
-        for (int64_t i = 0; i < e - a; ++i) std::memcpy(dp + 4 * i, sp + i * ld, 4 * sizeof(double));
+    hipError_t e = hipSuccess;
+    if (variant == 2) {
+      // the caller's rows of [r0, r1) straight into dev[b] (a run of whole or partial frames)
+      int32_t f = (int32_t)(std::upper_bound(doff.begin(), doff.end(), r0) - doff.begin()) - 1;
+      for (; e == hipSuccess && f < F && doff[f] < r1; ++f) {
+        const int64_t a = std::max(doff[f], r0), z = std::min(doff[f + 1], r1);
+        if (z > a)
+          e = hipMemcpyAsync(dev[b] + 4 * (a - r0), frames[f] + 4 * (a - doff[f]), (size_t)(z - a) * 32,
+                             hipMemcpyHostToDevice, s);
       }
-    });
-    hipError_t e = hipMemcpyAsync(dev[b], pin[b], (size_t)m * 32, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipEventRecord(ev_in[b], s);
+    } else {
+      if (k >= 2) (void)hipEventSynchronize(ev_in[b]);                 // pinned input b is free again
+      double* dst = pin[b];
+      host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t z) {
+        const int64_t ld = lds[f];
+        const double* sp = frames[f] + (a - doff[f]) * ld;
+        double* dp = dst + 4 * (a - r0);
+        if (ld == 4) {
+          std::memcpy(dp, sp, (size_t)(z - a) * 4 * sizeof(double));
+        } else {
+          for (int64_t i = 0; i < z - a; ++i) std::memcpy(dp + 4 * i, sp + i * ld, 4 * sizeof(double));
+        }
+      });
+      e = hipMemcpyAsync(dev[b], pin[b], (size_t)m * 32, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipEventRecord(ev_in[b], s);
+    }
+    // dev[2 + b] is free once chunk k-2's D2H (stream so) has finished
+    if (e == hipSuccess && k >= 2 && so != s) e = hipStreamWaitEvent(s, ev_out[b], 0);
     if (e == hipSuccess) {
       TimedRegion tr(c, &c->main_ev, s);
       hipLaunchKernelGGL(k_align_rows_f64, dim3((unsigned)std::min<int64_t>((m + kBlock - 1) / kBlock, 4096)),
                          dim3(kBlock), 0, s, dev[b], (int64_t)4, m, r0, d_doff, F, d_pose, dev[2 + b]);
     }
     if (e == hipSuccess) e = hipGetLastError();
-    if (e == hipSuccess && k >= 1) {                                // chunk k-1's rows are back: copy out
+    if (e == hipSuccess && so != s) {
+      e = hipEventRecord(ev_k[b], s);
+      if (e == hipSuccess) e = hipStreamWaitEvent(so, ev_k[b], 0);
+    }
+    if (variant != 2 && e == hipSuccess && k >= 1) {                // chunk k-1's rows are back: copy out
       e = hipEventSynchronize(ev_out[b ^ 1]);
       if (e == hipSuccess) copy_out(k - 1);
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(pin[2 + b], dev[2 + b], (size_t)m * 32, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipEventRecord(ev_out[b], s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(variant == 2 ? outs[0] + 4 * r0 : pin[2 + b], dev[2 + b], (size_t)m * 32,
+                         hipMemcpyDeviceToHost, so);
+    if (e == hipSuccess) e = hipEventRecord(ev_out[b], so);
     if (e != hipSuccess) rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
   }
   if (rc == MC_OK && K > 0) {
     const hipError_t e = hipEventSynchronize(ev_out[(K - 1) & 1]);
-    if (e == hipSuccess) copy_out(K - 1);
-    else rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
+    if (e != hipSuccess) rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
+    else if (variant != 2) copy_out(K - 1);
   }
+  (void)hipStreamSynchronize(so);
   (void)hipStreamSynchronize(s);
-  for (int b = 0; b < 2; ++b) { (void)hipEventDestroy(ev_in[b]); (void)hipEventDestroy(ev_out[b]); }
+  for (int b = 0; b < 2; ++b) {
+    (void)hipEventDestroy(ev_in[b]); (void)hipEventDestroy(ev_out[b]); (void)hipEventDestroy(ev_k[b]);
+  }
   return rc;
 }
 
@@ -1383,6 +1245,7 @@ int mc_transform_affine(mc_ctx* c, const mc_batch* in, mc_batch* out, int32_t n_
   queued_async(c);
   HIPCHK(hipMemcpyAsync(frame_tbl, tbl.data(), tbl.size() * sizeof(FrameRow), hipMemcpyHostToDevice, s));
   if (in->n_tiles > 0) {
+    out->wrote(false);
     DeskewArgs da;
     std::memset(&da, 0, sizeof(da));
     da.in = in->d_cols; da.in_C = in->C;
@@ -1466,6 +1329,8 @@ int mc_set_environment(mc_ctx* c, int64_t n, const double* env, int64_t ld) {
   CHECK_ARG(n == 0 || env, "scene pointer is NULL");
   DeviceGuard g(c->device);
   if (int r = sync_all(c)) return r;
+  ++c->env_ver;              // any earlier mc_scan_count's state is now stale
+  c->scan_valid = false;
   dev_free(c->d_env);
   c->E = 0;
   // scan.hpp's column layout: x, y, z, intensity float64, transposed here once per scene
@@ -1500,6 +1365,7 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   dev_free(c->d_scan_pose); dev_free(c->d_scan_tcount); dev_free(c->d_scan_toff);
   dev_free(c->d_scan_nvis);
   c->scan_F = 0;
+  c->scan_valid = false;
   if (int r = dev_alloc(&c->d_scan_pose, 12 * (size_t)std::max(F, 1))) return r;
   const int32_t Fp = scan_fpad(F);   // per-tile rows of counts / offsets, frames padded to kScanFrames
   if (int r = dev_alloc(&c->d_scan_tcount, (size_t)std::max(Fp, 1) * std::max(tiles, 1))) return r;
@@ -1513,7 +1379,11 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
   c->scan_counts.assign(F, 0);
   c->scan_F = F;
   c->scan_tiles = tiles;
-  if (F == 0) return MC_OK;
+  c->scan_env_ver = c->env_ver;
+  if (F == 0) {
+    c->scan_valid = true;
+    return MC_OK;
+  }
   // per-frame sensor pose {R | t} (LMC:804-812; R as scipy computes it, LMC:726), host-side
   std::vector<double> pose(12 * (size_t)F);
   mcrot::frame_poses(c->h_time.data(), c->h_pos.data(), c->h_rpy.data(), c->T, frame_times, F, pose_select,
@@ -1559,12 +1429,15 @@ int mc_scan_count(mc_ctx* c, int32_t F, const double* frame_times, int pose_sele
     c->scan_counts[f] = k;
     counts_out[f] = k;
   }
+  c->scan_valid = true;
   return MC_OK;
 }
 
 // pass 2 of the last mc_scan_count: the batch's float32 columns (out != nullptr) or the reference's
 // float64 rows (local, aligned: device (N, 4) arrays, aligned may be nullptr)
 static int scan_emit(mc_ctx* c, mc_batch* out, const double* noise, double* d_local, double* d_aligned) {
+  if (!c->scan_valid || c->scan_env_ver != c->env_ver)
+    return fail(MC_ERR_STATE, "no mc_scan_count for the current scene (mc_set_environment since the count?)");
   int64_t N = 0;
   for (int64_t k : c->scan_counts) N += k;
   if (c->scan_F == 0 || N == 0 || c->scan_tiles == 0) return MC_OK;
@@ -1587,6 +1460,9 @@ static int scan_emit(mc_ctx* c, mc_batch* out, const double* noise, double* d_lo
   ea.tile_off = c->d_scan_toff; ea.nvis = c->d_scan_nvis; ea.vis_bits = c->d_scan_bits; ea.noise = d_noise;
   if (out) {
     ea.poff = out->d_poff; ea.doff = out->d_doff; ea.cols = out->d_cols; ea.C = out->C;
+    out->wrote(false);
+    ea.pcd_len = out->d_pcd_len;   // MC_BATCH_WITH_PCD_LEN: per-point atomic adds into zeroed slots
+    if (ea.pcd_len) HIPCHK(hipMemsetAsync(ea.pcd_len, 0, (size_t)(out->P / kBlkPts) * sizeof(int32_t), c->stream));
   } else {
     ea.doff = d_doff; ea.local = d_local; ea.aligned = d_aligned;
   }
@@ -1598,6 +1474,7 @@ static int scan_emit(mc_ctx* c, mc_batch* out, const double* noise, double* d_lo
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (out) out->wrote(true);
   return MC_OK;
 }
 

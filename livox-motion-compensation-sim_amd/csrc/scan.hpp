@@ -200,6 +200,7 @@ struct ScanEmitArgs {
   float* cols; int32_t C;   // the output batch's blocked columns (kernels.hpp bidx)
   double* local;            // ROWS: (N_out, 4) float64 sensor-frame rows (LMC:770), dense order
   double* aligned;          // ROWS: (N_out, 4) float64 R p + t of those rows (LMC:831), or nullptr
+  int32_t* pcd_len;         // columns, MC_BATCH_WITH_PCD_LEN: per-block ASCII PCD bytes (zeroed), or nullptr
 };
 
 // ROWS = false: float32 columns of a batch; ROWS = true: the reference's float64 rows (local and,
@@ -272,10 +273,17 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
             }
           } else {
             float* q = a.cols + bidx(a.C, 0, poff + o);
-            q[0] = (float)px;
-            q[kBlkPts] = (float)py;
-            q[2 * kBlkPts] = (float)pz;
-            q[3 * kBlkPts] = (float)sc.w[e];
+            const float v[4] = {(float)px, (float)py, (float)pz, (float)sc.w[e]};
+            q[0] = v[0];
+            q[kBlkPts] = v[1];
+            q[2 * kBlkPts] = v[2];
+            q[3 * kBlkPts] = v[3];
+            if (a.pcd_len) {   // this line's text bytes (layout.hpp PcdCount), one atomic per point
+              PcdCount pc;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) pc.add(true, v[k]);
+              atomicAdd(a.pcd_len + ((poff + o) >> 8), pc.n + (pc.amax >= kPcdSlowBits ? kPcdSlowValue : 0));
+            }
           }
         }
       }

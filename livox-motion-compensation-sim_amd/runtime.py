@@ -82,8 +82,8 @@ class Context:
         self._imu_last = (ts.copy(), g.copy())
 
     # ---- batches -------------------------------------------------------------------------
-    def batch(self, counts, with_time: bool = False) -> "Batch":
-        return Batch(self, counts, with_time)
+    def batch(self, counts, with_time: bool = False, with_pcd_len: bool = False) -> "Batch":
+        return Batch(self, counts, with_time, with_pcd_len)
 
     def deskew(self, inp: "Batch", out: "Batch | None" = None, mode: str = "frame",
                pose_select: str = "searchsorted") -> "Batch":
@@ -138,9 +138,18 @@ class Context:
         env = np.asarray(environment)
         if env.ndim != 2:
             raise IndexError(f"too many indices for array: array is {env.ndim}-dimensional, but 2 were indexed")
-        env = np.ascontiguousarray(env, dtype=np.float64)
-        check(self.lib.mc_set_environment(self.handle, env.shape[0], ptr(env, c_double), env.shape[1]),
-              "set_environment")
+        if env.shape[1] < 4:
+            raise IndexError(f"index 3 is out of bounds for axis 1 with size {env.shape[1]}")
+        # the device holds x, y, z, intensity only: skip the upload when those are the same bytes as
+        # the scene already there (whoever uploaded it; compared by value, like set_imu)
+        env4 = np.ascontiguousarray(env[:, :4], dtype=np.float64)
+        last = getattr(self, "_env_last", None)
+        if last is not None and last.shape == env4.shape and np.array_equal(
+                last.view(np.uint64), env4.view(np.uint64)):
+            return
+        self._env_last = None
+        check(self.lib.mc_set_environment(self.handle, env4.shape[0], ptr(env4, c_double), 4), "set_environment")
+        self._env_last = env4.copy()   # env4 may be a view of the caller's array
 
     def _scan_count(self, frame_times, config: dict, pose_select: str, rng):
         t = np.ascontiguousarray(np.atleast_1d(frame_times), dtype=np.float64)
@@ -174,25 +183,32 @@ class Context:
         return out
 
     def scan_rows(self, frame_times, config: dict, pose_select: str = "searchsorted", rng=np.random,
-                  aligned: bool = True):
+                  aligned: bool = True, keep_device: bool = False):
         """:meth:`scan` into the reference's own float64 arrays (mc_scan_emit_f64): returns
         (counts, local, aligned) with local / aligned (N, 4) float64 host arrays, frames back to back
         — scan_environment's output and transform_pointcloud of it with the frame's pose (LMC:815,
-        831), equal to the reference's values bit for bit; ``aligned=False``: local only (None)."""
+        831), equal to the reference's values bit for bit; ``aligned=False``: local only (None).
+        ``keep_device``: also return the two device (N, 4) float64 buffers (DeviceBuffer, the
+        caller closes them), e.g. for the writers that follow (save_results)."""
         counts, noise = self._scan_count(frame_times, config, pose_select, rng)
         n = int(counts.sum())
         if n == 0:
-            return counts, np.zeros((0, 4)), (np.zeros((0, 4)) if aligned else None)
+            empty = (counts, np.zeros((0, 4)), (np.zeros((0, 4)) if aligned else None))
+            return empty + ((None, None),) if keep_device else empty
         loc = DeviceBuffer(self, n * 32)
         al = DeviceBuffer(self, n * 32) if aligned else None
+        keep = False
         try:
             check(self.lib.mc_scan_emit_f64(self.handle, ptr(noise, c_double), loc.ptr, al.ptr if al else None),
                   "scan_emit_f64")
-            return counts, loc.to_host(np.float64, (n, 4)), (al.to_host(np.float64, (n, 4)) if al else None)
+            host = (counts, loc.to_host(np.float64, (n, 4)), (al.to_host(np.float64, (n, 4)) if al else None))
+            keep = keep_device
+            return host + ((loc, al),) if keep_device else host
         finally:
-            loc.close()
-            if al:
-                al.close()
+            if not keep:
+                loc.close()
+                if al:
+                    al.close()
 
     def affine_rows(self, counts, rows, mats, per_row: bool = False) -> np.ndarray:
         """(T @ [p, w].T).T[:, :3] on float64 rows (mc_affine_rows_f64): rows (N, 3) (w = 1) or
@@ -281,15 +297,18 @@ class DeviceBuffer:
 class Batch:
     """Device-resident ragged frame batch (blocked CSR: 256-point blocks of float32 columns in HBM)."""
 
-    def __init__(self, ctx: Context, counts, with_time: bool = False):
+    def __init__(self, ctx: Context, counts, with_time: bool = False, with_pcd_len: bool = False):
         self.ctx = ctx
         self.lib = ctx.lib
         self.counts = np.ascontiguousarray(np.atleast_1d(counts), dtype=np.int64)
         if self.counts.ndim != 1 or (self.counts < 0).any():
             raise ValueError("counts must be a 1-D array of non-negative frame sizes")
         self.with_time = bool(with_time)
+        self.with_pcd_len = bool(with_pcd_len)
         h = c_void_p()
-        flags = _lib.MC_BATCH_WITH_TIME if with_time else 0
+        # with_pcd_len: the kernels that write the columns also keep each block's ASCII PCD text
+        # length, so encode_pcd_batch needs no measure pass (include/mcdeskew.h MC_BATCH_WITH_PCD_LEN)
+        flags = (_lib.MC_BATCH_WITH_TIME if with_time else 0) | (_lib.MC_BATCH_WITH_PCD_LEN if with_pcd_len else 0)
         check(self.lib.mc_batch_create(ctx.handle, len(self.counts), ptr(self.counts, c_int64), flags,
                                        ctypes.byref(h)), "batch_create")
         self.handle = h
@@ -302,6 +321,12 @@ class Batch:
 
     def close(self):
         self._fin()
+
+    def pcd_len_current(self) -> bool:
+        """True when the per-block PCD text sums describe the current columns."""
+        v = c_int32()
+        check(self.lib.mc_batch_pcd_len_current(self.handle, ctypes.byref(v)), "pcd_len_current")
+        return bool(v.value)
 
     def padded_offsets(self) -> np.ndarray:
         o = np.zeros(self.n_frames + 1, np.int64)

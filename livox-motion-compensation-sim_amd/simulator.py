@@ -177,14 +177,11 @@ class LiDARMotionSimulator:
 
     # ---- scanning (LMC:701-770) and the frame loop (LMC:778-858) ----------------------------
     def _load_environment(self, environment) -> np.ndarray:
-        """Upload the scene once per distinct array (identity, buffer, shape and sum)."""
+        """Make ``environment`` the context's scene.  The context compares the scene's bytes with
+        the one it holds and uploads only on a difference, so simulators sharing a context, and
+        in-place edits of one array, always scan the scene they pass."""
         env = np.asarray(environment)
-        if env.ndim != 2:
-            raise IndexError(f"too many indices for array: array is {env.ndim}-dimensional, but 2 were indexed")
-        key = (id(environment), env.__array_interface__["data"][0], env.shape, float(np.sum(env[:, :4])))
-        if getattr(self, "_env_key", None) != key:
-            self.context.set_environment(env)
-            self._env_key = key
+        self.context.set_environment(env)
         return env
 
     def scan_environment(self, environment, sensor_pose):
@@ -220,7 +217,9 @@ class LiDARMotionSimulator:
         self._load_environment(environment)
         ctx = self.context
         ctx.set_trajectory(trajectory["time"], trajectory["position_gps"], trajectory["orientation_imu"])
-        counts, local, aligned = ctx.scan_rows(times, self.config, pose_select="searchsorted")
+        self._drop_rows()
+        counts, local, aligned, (d_local, d_aligned) = ctx.scan_rows(times, self.config, pose_select="searchsorted",
+                                                                       keep_device=True)
         offs = np.concatenate([[0], np.cumsum(counts)])
         idx = np.clip(np.searchsorted(trajectory["time"], times), 0, len(trajectory["time"]) - 1)
         raw, al, motion = [], [], []
@@ -235,8 +234,19 @@ class LiDARMotionSimulator:
                            "gps_lon": p[0] / (111320.0 * np.cos(np.radians(40.0))) - 74.0,
                            "gps_alt": p[2], "imu_roll": o[0], "imu_pitch": o[1], "imu_yaw": o[2],
                            "vel_x": v[0], "vel_y": v[1], "vel_z": v[2]})
+        if d_local is not None:
+            self._rows = _DeviceRows(counts, local, aligned, d_local, d_aligned, raw, al)
         return {"raw_scans": raw, "aligned_pointclouds": al, "motion_data": motion,
                 "trajectory": trajectory, "environment": environment}
+
+    def _drop_rows(self):
+        rows, self._rows = getattr(self, "_rows", None), None
+        if rows is not None:
+            rows.close()
+
+    def _rows_of(self, results) -> Optional["_DeviceRows"]:
+        rows = getattr(self, "_rows", None)
+        return rows if rows is not None and rows.matches(results) else None
 
     def run_simulation(self, environment):
         """LMC:778-858 given the scene: trajectory + sensor noise (LMC:784-785, global RNG), then
@@ -269,8 +279,13 @@ class LiDARMotionSimulator:
         pd.DataFrame(results["motion_data"]).to_csv(os.path.join(output_dir, "motion_data.csv"), index=False)
         raw = [s["points_local"] for s in results["raw_scans"]]
         aligned = list(results["aligned_pointclouds"])
-        bodies = _codecs.encode_pcd_bodies(raw + aligned, self.context) if raw or aligned else []
-        raw_b, al_b = bodies[:len(raw)], bodies[len(raw):]
+        rows = self._rows_of(results)
+        if rows is not None:     # simulate_frames' own result: its rows are still on the device
+            raw_b = _codecs.encode_pcd_bodies_device_rows(rows.d_local, rows.counts)
+            al_b = _codecs.encode_pcd_bodies_device_rows(rows.d_aligned, rows.counts)
+        else:
+            bodies = _codecs.encode_pcd_bodies(raw + aligned, self.context) if raw or aligned else []
+            raw_b, al_b = bodies[:len(raw)], bodies[len(raw):]
         pcd_dir = os.path.join(output_dir, "raw_scans_pcd")
         os.makedirs(pcd_dir, exist_ok=True)
         for s, pts, body in zip(results["raw_scans"], raw, raw_b):
@@ -318,8 +333,14 @@ class LiDARMotionSimulator:
         frames_data = [{"frame_id": s["frame_id"], "timestamp": s["timestamp"], "points": s["points_local"]}
                        for s in results["raw_scans"]]
         print("Generating corrected LVX format...")
+        rows = self._rows_of(results)
         try:
-            _codecs.LivoxLVXWriter(self.context).write_compatible_lvx(f"{base_filename}.lvx", frames_data)
+            w = _codecs.LivoxLVXWriter(self.context)
+            if rows is not None:   # simulate_frames' own result: encode from its device rows
+                w._write(f"{base_filename}.lvx", frames_data,
+                         lambda: _codecs.encode_lvx_device_rows(rows.d_local, rows.counts, frames_data))
+            else:
+                w.write_compatible_lvx(f"{base_filename}.lvx", frames_data)
             print(f"✅ Corrected LVX format: {base_filename}.lvx")
         except Exception as e:
             print(f"❌ LVX generation failed: {e}")
@@ -331,6 +352,49 @@ class LiDARMotionSimulator:
         if not aligned:
             return np.zeros((0, 4))
         return np.vstack(aligned)
+
+
+def _digest(a: np.ndarray) -> int:
+    import xxhash
+    return xxhash.xxh3_64_intdigest(memoryview(np.ascontiguousarray(a)).cast("B"))
+
+
+class _DeviceRows:
+    """The device copies of one simulate_frames result's local and aligned rows (mc_scan_emit_f64's
+    (N, 4) float64 output), so save_results / save_lvx encode them without staging and uploading the
+    host arrays again.  Used only while the result still holds the very lists and arrays
+    simulate_frames returned and their bytes are unchanged (identity + a 64-bit xxh3 digest of each
+    row array): any replaced frame or in-place edit sends the writers back to the host arrays."""
+
+    def __init__(self, counts, local, aligned, d_local, d_aligned, raw_list, al_list):
+        self.counts = np.ascontiguousarray(counts, np.int64)
+        self.local, self.aligned = local, aligned
+        self.d_local, self.d_aligned = d_local, d_aligned
+        self.raw_list, self.al_list = raw_list, al_list
+        self.local_views = [s["points_local"] for s in raw_list]
+        self.al_views = list(al_list)
+        try:
+            self.h = (_digest(local), _digest(aligned))
+        except ImportError:
+            self.h = None
+
+    def matches(self, results) -> bool:
+        if self.h is None or self.d_aligned is None:
+            return False
+        raw, al = results.get("raw_scans"), results.get("aligned_pointclouds")
+        if raw is not self.raw_list or al is not self.al_list or len(raw) != len(self.local_views) \
+                or len(al) != len(self.al_views):
+            return False
+        if any(s.get("points_local") is not v for s, v in zip(raw, self.local_views)):
+            return False
+        if any(a is not v for a, v in zip(al, self.al_views)):
+            return False
+        return (_digest(self.local), _digest(self.aligned)) == self.h
+
+    def close(self):
+        for b in (self.d_local, self.d_aligned):
+            if b is not None:
+                b.close()
 
 
 def _stack_aos(frames: List[np.ndarray]) -> np.ndarray:

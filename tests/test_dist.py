@@ -4,7 +4,9 @@ blocked-CSR batch layout; the root assembles the merged batch at the offsets of 
 gather plan (mc_gather_plan, the host half of mc_comm_gather_batch) from point-to-point
 sends / receives — the transfers mc_comm_gather_batch issues as ncclSend / ncclRecv — including
 shards whose column count differs (t_ns carried) and is re-pitched.  On GPUs the same plan drives
-RCCL (tests/test_gpu_gather_issue.py covers the device copies / re-pitch in one process)."""
+RCCL (tests/test_gpu_gather_issue.py covers the device copies / re-pitch in one process), and the
+library's own C++ gather sequence (csrc/gather.cpp) runs between forked processes over a socket
+transport (worlds 2, 3, 8)."""
 import multiprocessing as mp
 import os
 import socket
@@ -230,6 +232,93 @@ def test_gather_plan_rejects_narrow_shards_and_bad_totals():
     with pytest.raises(ValueError, match="root"):
         d.gather_plan([256], [4], 256, 4, root=1)
     assert d.gather_plan([0, 256], [4, 4], 256, 4)["offset"].tolist() == [0, 0]
+
+
+# ---------------------------------------------------------------------------------------------
+# the product's gather sequence (csrc/gather.cpp, behind mc_comm_gather_batch) between processes
+# ---------------------------------------------------------------------------------------------
+CSRC = os.path.join(ROOT, "livox-motion-compensation-sim_amd", "csrc")
+SAN = ["-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+       "-fno-omit-frame-pointer"]
+
+
+@pytest.fixture(scope="module")
+def gather_exe(tmp_path_factory):
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    exe = tmp_path_factory.mktemp("gs") / "gather_sockets"
+    subprocess.run(["g++", *SAN, f"-I{CSRC}", os.path.join(ROOT, "tests", "host", "gather_sockets.cpp"),
+                    os.path.join(CSRC, "gather.cpp"), os.path.join(CSRC, "plan.cpp"), "-o", str(exe)],
+                   check=True, capture_output=True, text=True)
+    return str(exe)
+
+
+def _run_sockets(exe, d, world, root, shard_counts, Cs, merged_counts, merged_C, shards):
+    import subprocess
+    P = [int(((np.asarray(sc, np.int64) + 255) // 256 * 256).sum()) for sc in shard_counts]
+    mP = int(((np.asarray(merged_counts, np.int64) + 255) // 256 * 256).sum())
+    lines = [f"{world} {root}", " ".join(map(str, [mP, merged_C, len(merged_counts), *merged_counts]))]
+    for q in range(world):
+        lines.append(" ".join(map(str, [P[q], Cs[q], len(shard_counts[q]), *shard_counts[q]])))
+        shards[q].astype(np.float32).tofile(os.path.join(d, f"shard_{q}.bin"))
+    with open(os.path.join(d, "meta.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe, d], capture_output=True, text=True, timeout=120, env=env)
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+    merged = None
+    if r.returncode == 0:
+        merged = np.fromfile(os.path.join(d, "merged.bin"), np.float32)
+        assert merged.size == mP * merged_C
+    return r, merged
+
+
+@pytest.mark.parametrize("world,root", [(2, 0), (3, 1), (8, 5)])
+def test_socket_transport_runs_the_product_gather_sequence(gather_exe, tmp_path, world, root):
+    """mc_comm_gather_batch's own C++ sequence (plan all-gather, frame-hash check, grouped
+    send / receive, the finishing copies and re-pitch: mcgather::run) between ``world`` forked
+    processes over Unix sockets, under ASan + UBSan; the root's merged batch, read back in frame
+    order, is np.vstack of the shards (LMC:887-889).  Shards come from plan_shards; one of them has
+    5 columns (t_ns carried, re-pitched), one is empty, frames are ragged."""
+    d = pkg().dist
+    rng = np.random.default_rng(100 + world)
+    counts = rng.choice([1, 7, 255, 256, 257, 3000, 10_001], 3 * world).astype(np.int64)
+    b = d.plan_shards(counts, world)
+    shard_counts = [counts[b[r]:b[r + 1]].tolist() for r in range(world)]
+    empty = (root + 1) % world                      # an empty shard: its frames move to a neighbour
+    nb = (empty + 1) % world
+    if empty < nb:
+        shard_counts[nb] = shard_counts[empty] + shard_counts[nb]
+    else:
+        shard_counts[nb] = shard_counts[nb] + shard_counts[empty]
+    shard_counts[empty] = []
+    order = sorted(range(world))
+    merged_counts = [c for q in order for c in shard_counts[q]]
+    Cs = [4] * world
+    Cs[(root + 2) % world if world > 2 else nb] = 5       # a re-pitched 5-column shard
+    rows = [rng.standard_normal((int(sum(sc)), 5)).astype(np.float32) for sc in shard_counts]
+    shards = [_blocked(rows[q], shard_counts[q], Cs[q])[0] for q in range(world)]
+    r, merged = _run_sockets(gather_exe, str(tmp_path), world, root, shard_counts, Cs, merged_counts, 4, shards)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert r.stdout.count("status 0") == world
+    got = _unblocked(merged, merged_counts, 4)
+    want = np.vstack([rw[:, :4] for rw in rows])
+    assert np.array_equal(got, want)
+
+
+def test_socket_transport_rejects_a_reordered_merge_on_every_rank(gather_exe, tmp_path):
+    """Equal padded totals but the merged batch's frames in another order: every rank sees the same
+    all-gathered plan words, rejects it (frame-hash check) and moves no data."""
+    world, root = 3, 0
+    shard_counts = [[300, 100], [512], [1]]
+    merged_counts = [100, 300, 512, 1]
+    Cs = [4, 4, 4]
+    shards = [_blocked(np.ones((sum(sc), 4), np.float32), sc, 4)[0] for sc in shard_counts]
+    r, merged = _run_sockets(gather_exe, str(tmp_path), world, root, shard_counts, Cs, merged_counts, 4, shards)
+    assert r.returncode == 3, r.stdout
+    assert r.stdout.count("status -1") == world and merged is None
 
 
 # ---------------------------------------------------------------------------------------------

@@ -342,3 +342,102 @@ def test_codec_unit_orders_give_the_same_bytes(mc, gpu_ctx, mode):
         assert mc.codecs.encode_pcd_batch(out) == want_pcd
         assert mc.codecs.encode_lvx_batch(out, ids, ts) == want_lvx
     assert mc.codecs.deskew_pcd_frames(b, out, mode=mode) == want_pcd
+
+
+def _encode_timed(mc, ctx, b):
+    ctx.sync()
+    ctx.read_timing()
+    ctx.timing(True)
+    got = mc.codecs.encode_pcd_batch(b)
+    ctx.timing(False)
+    return got, ctx.read_timing()["codec_launches"]
+
+
+@pytest.mark.parametrize("mode", ["frame", "pose_slerp", "imu"])
+@pytest.mark.parametrize("big", [False, True])
+def test_pcd_len_batch_deskew_then_encode(mc, gpu_ctx, mode, big):
+    """MC_BATCH_WITH_PCD_LEN: a deskew into the batch (mc_deskew and the last launch of
+    mc_deskew_steps) leaves its blocks' text sums, so mc_pcd_encode_batch runs the write pass only
+    and writes the bytes a plain batch gets through measure + write; a block with a value beyond the
+    packed formatter falls back to the measure pass."""
+    counts = np.array([4096, 3, 2500, 0, 10_000, 7, 256, 257, 100_003, 1], np.int64)
+    b = _deskew_setup(mc, gpu_ctx, counts, with_big=big)
+    plain = gpu_ctx.deskew(b, gpu_ctx.batch(counts), mode=mode)
+    want = mc.codecs.encode_pcd_batch(plain)
+    out = gpu_ctx.batch(counts, with_pcd_len=True)
+    assert not out.pcd_len_current()
+    for issue in ("deskew", "steps"):
+        if issue == "deskew":
+            gpu_ctx.deskew(b, out, mode=mode)
+        else:
+            gpu_ctx.deskew_steps(b, out, 3, mode=mode)
+        assert out.pcd_len_current()
+        got, launches = _encode_timed(mc, gpu_ctx, out)
+        assert got == want, (mode, issue)
+        assert launches >= 2 if big else launches == 1, (mode, issue, launches)
+    assert np.array_equal(out.download_aos(), plain.download_aos())
+    # any other write of the columns makes the sums stale: the encoder measures again
+    gpu_ctx.tune_order(b, out, mode=mode, launches=2, rounds=2)
+    assert not out.pcd_len_current()
+    got, launches = _encode_timed(mc, gpu_ctx, out)
+    assert got == want and launches >= 2
+
+
+@pytest.mark.parametrize("ld", [4, 6])
+def test_pcd_len_batch_stager_and_stale_writes(mc, gpu_ctx, ld):
+    """The stager (AoS float64 -> columns, ld 4 and wider rows) writes the sums too; column uploads,
+    synth and affine writes leave them stale.  Bytes always equal the oracle's."""
+    rng = np.random.default_rng(12)
+    counts = np.array([255, 256, 257, 0, 1, 5000, 2049], np.int64)
+    n = int(counts.sum())
+    pts = np.column_stack([rng.normal(0, 80, (n, 3)), rng.uniform(0, 1, n), rng.normal(0, 1, (n, ld - 4))])
+    pts[7, 0] = -0.0
+    pts[300, 1] = 999.9999996      # rounds up to 1000.000000 at six decimals (f32: 1000.0)
+    b = gpu_ctx.batch(counts, with_pcd_len=True)
+    b.upload_aos(pts)
+    assert b.pcd_len_current()
+    host = b.split(b.download_aos())
+    got, launches = _encode_timed(mc, gpu_ctx, b)
+    assert launches == 1
+    assert got == [C.pcd_ascii_bytes(h) for h in host]
+    x, y, z, i = b.download_columns()
+    b.upload_columns(x=x * 2)
+    assert not b.pcd_len_current()
+    host2 = b.split(b.download_aos())
+    got, launches = _encode_timed(mc, gpu_ctx, b)
+    assert launches >= 2 and got == [C.pcd_ascii_bytes(h) for h in host2]
+    b.upload_aos(pts)
+    assert b.pcd_len_current()
+    b.synth(seed=1)
+    assert not b.pcd_len_current()
+    b.upload_aos(pts)
+    gpu_ctx.transform_affine(b, b, np.eye(4)[:3])
+    assert not b.pcd_len_current()
+    # a slow value through the stager: sums current, but the encoder must still measure that block
+    pts[5100, 2] = 1e7
+    b.upload_aos(pts)
+    host3 = b.split(b.download_aos())
+    got, launches = _encode_timed(mc, gpu_ctx, b)
+    assert launches >= 2 and got == [C.pcd_ascii_bytes(h) for h in host3]
+
+
+def test_pcd_len_batch_scan_emit(mc, gpu_ctx):
+    """mc_scan_emit into a MC_BATCH_WITH_PCD_LEN batch adds each point's text bytes to its block
+    (atomics into zeroed slots): write pass only, bytes as the oracle's."""
+    sim = mc.LiDARMotionSimulator({"points_per_frame": 3000, "lidar_range_noise": 0.01}, context=gpu_ctx)
+    rng = np.random.default_rng(3)
+    env = np.column_stack([rng.uniform(-80, 80, (60_000, 3)), rng.uniform(0, 1, 60_000)])
+    env[:, 2] *= 0.1
+    sim._load_environment(env)
+    times = np.linspace(0, 10, 9)
+    tr = {"time": times, "position_gps": rng.normal(0, 3, (9, 3)), "orientation_imu": rng.normal(0, 0.3, (9, 3))}
+    gpu_ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+    np.random.seed(5)
+    counts, noise = gpu_ctx._scan_count(times, sim.config, "searchsorted", np.random)
+    out = gpu_ctx.batch(counts, with_pcd_len=True)
+    mc._lib.check(gpu_ctx.lib.mc_scan_emit(gpu_ctx.handle, out.handle, mc._lib.ptr(noise, mc._lib.c_double)), "emit")
+    assert out.pcd_len_current()
+    host = out.split(out.download_aos())
+    got, launches = _encode_timed(mc, gpu_ctx, out)
+    assert launches == 1
+    assert got == [C.pcd_ascii_bytes(h) for h in host]

@@ -64,3 +64,37 @@ def test_run_simulation_save_results_byte_identical(mc, gpu_ctx, name, tmp_path)
     assert log_lines(log.getvalue().replace(str(out), "<out>")) == log_lines(ref["log"])
     n = sum(ref["frame_counts"])
     print(f"{name}: {len(got)} files, {sum(v[0] for v in got.values())} bytes, {n} points: byte-identical")
+
+
+def test_save_results_reuses_device_rows_only_while_unchanged(mc, gpu_ctx, tmp_path):
+    """save_results / save_lvx encode simulate_frames' own result from the rows mc_scan_emit_f64 left
+    on the device (no re-upload), but only while the result holds the very arrays with the very
+    bytes simulate_frames returned: an in-place edit or a replaced frame is written from the host
+    arrays, as the reference writes them (LMC:860-931)."""
+    from oracle import codecs as C
+    name = "highway_simple"
+    e = golden(f"lmc_env_{name}.npz")
+    tr = traj_of(name)
+    sim = mc.LiDARMotionSimulator(dict(CFGS[name]), context=gpu_ctx)
+    restore_rng(e)
+    res = sim.simulate_frames(e["environment"], tr, sim.lidar_times())
+    assert sim._rows_of(res) is not None
+    f = next(i for i, s in enumerate(res["raw_scans"]) if len(s["points_local"]) > 3)
+    res["raw_scans"][f]["points_local"][1, 0] += 0.125            # in place, through the view
+    assert sim._rows_of(res) is None
+    res2 = dict(res)
+    out = tmp_path / "edited"
+    with contextlib.redirect_stdout(io.StringIO()):
+        sim.save_results(res2, str(out))
+    with open(out / "raw_scans_pcd" / f"frame_{f:04d}.pcd", "rb") as fh:
+        assert fh.read() == C.pcd_ascii_bytes(res["raw_scans"][f]["points_local"])
+    frames = [{"frame_id": s["frame_id"], "timestamp": s["timestamp"], "points": s["points_local"]}
+              for s in res["raw_scans"]]
+    with open(out / "lidar_data.lvx", "rb") as fh:
+        assert fh.read() == C.lvx_bytes(frames)
+    # a fresh run, one aligned frame replaced by an equal copy: identity fails, bytes still right
+    restore_rng(e)
+    res = sim.simulate_frames(e["environment"], tr, sim.lidar_times())
+    assert sim._rows_of(res) is not None
+    res["aligned_pointclouds"][f] = res["aligned_pointclouds"][f].copy()
+    assert sim._rows_of(res) is None

@@ -206,3 +206,55 @@ def test_scan_noise_consumes_global_rng_like_reference(mc, gpu_ctx):
     assert np.random.random() == after_ref
     for o, r in zip(out, ref):
         assert_scaled_close(o, r, scale_of(r[:, :3]), what="noisy")
+
+
+def test_scene_cache_two_simulators_one_context_and_in_place_edits(mc, gpu_ctx):
+    """The scene lives on the context: two simulators sharing it, alternating two scenes, and
+    in-place edits of one scene array (a row permutation, a sum-preserving +d / -d move) must each
+    scan the scene passed in (LMC:701-770), never a stale upload."""
+    cfg = dict(points_per_frame=4000, lidar_range_noise=0.0)
+    a = mc.LiDARMotionSimulator(cfg, context=gpu_ctx)
+    b = mc.LiDARMotionSimulator(cfg, context=gpu_ctx)
+    env1 = synth_scene(31, 50_000)
+    env2 = synth_scene(32, 50_000)
+    pose = {"position": np.array([1.0, -2.0, 0.5]), "orientation": np.array([0.01, -0.02, 0.7])}
+
+    def check(sim, env, what):
+        ref = R.scan_environment(env, pose, sim.config)
+        out = sim.scan_environment(env, pose)
+        assert out.shape == ref.shape, what
+        assert_scaled_close(out, ref, scale_of(ref[:, :3]) + 1e-3, what=what)
+        assert np.array_equal(out[:, 3], ref[:, 3]), what
+
+    for rep in range(2):
+        check(a, env1, f"A scene 1 rep {rep}")
+        check(b, env2, f"B scene 2 rep {rep}")
+    # same array object, rows permuted in place: changes the subsample and the output order
+    perm = np.random.default_rng(4).permutation(len(env1))
+    env1[:] = env1[perm]
+    check(a, env1, "A scene 1 permuted in place")
+    # sum-preserving edit of two visible points
+    vis = R.scan_environment(env1, pose, dict(a.config, points_per_frame=10 ** 9))
+    assert len(vis) > 2
+    j = np.flatnonzero(np.isin(env1[:, 3], vis[:2, 3]))[:2]
+    env1[j[0], 0] += 0.25
+    env1[j[1], 0] -= 0.25
+    check(a, env1, "A scene 1 +d/-d")
+    check(b, env2, "B scene 2 after A's edits")
+
+
+def test_scan_emit_refuses_stale_scene(mc, gpu_ctx):
+    """mc_scan_emit_f64 after mc_set_environment without a new mc_scan_count: MC_ERR_STATE."""
+    sim = mc.LiDARMotionSimulator(dict(points_per_frame=100, lidar_range_noise=0.0), context=gpu_ctx)
+    env = synth_scene(7, 5000)
+    gpu_ctx.set_environment(env)
+    gpu_ctx.set_trajectory([0.0], np.zeros((1, 3)), np.zeros((1, 3)))
+    counts, _ = gpu_ctx._scan_count([0.0], sim.config, "direct", np.random)
+    assert counts.sum() > 0
+    gpu_ctx.set_environment(env[::-1])
+    buf = gpu_ctx.device_buffer(int(counts.sum()) * 32)
+    try:
+        rc = gpu_ctx.lib.mc_scan_emit_f64(gpu_ctx.handle, None, buf.ptr, None)
+        assert rc == mc._lib.MC_ERR_STATE
+    finally:
+        buf.close()
