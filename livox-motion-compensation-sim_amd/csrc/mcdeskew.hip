@@ -1040,6 +1040,207 @@ constexpr size_t kPipeBytes = (size_t)kPipeRows * 4 * sizeof(double);
 constexpr int64_t kZeroCopyRows = 1 << 15;                             // below: zero-copy kernels
 constexpr int kPoolThreads = 16;                                       // the box's CPU share per GPU
 constexpr int64_t kJobRows = 8192;                                     // rows per host copy job (256 KB)
+static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
+                        const int64_t* d_doff, const double* d_pose, double* const* outs);
+
+// pinned, device-mapped host scratch of at least `bytes` (the zero-copy path of the single calls)
+static int ctx_pin(mc_ctx* c, size_t bytes, char** out) {
+  if (bytes > c->pin_bytes) {
+    if (c->h_pin) { (void)hipStreamSynchronize(c->stream); (void)hipHostFree(c->h_pin); c->h_pin = nullptr; }
+    c->pin_bytes = 0;
+    HIPCHK(hipHostMalloc(&c->h_pin, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    c->pin_bytes = bytes;
+  }
+  *out = static_cast<char*>(c->h_pin);
+  return MC_OK;
+}
+
+// Frames of host float64 rows through k_align_rows_f64 with the per-frame poses pose12 (F x 12,
+// host): below kZeroCopyRows rows the kernel reads and writes pinned, device-mapped host memory
+// (no DMA round trips for the reference's per-frame calls); above, the DMA row pipeline.
+static int align_host_rows(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
+                           const std::vector<double>& pose12, double* const* outs) {
+  const int32_t F = (int32_t)doff.size() - 1;
+  const int64_t n = doff[F];
+  if (n >= kZeroCopyRows) {
+    void* st = nullptr;
+    const size_t tab_b = doff.size() * sizeof(int64_t) + pose12.size() * sizeof(double);
+    if (int r = ctx_stage(c, tab_b, &st)) return r;
+    int64_t* d_doff = static_cast<int64_t*>(st);
+    double* d_pose = reinterpret_cast<double*>(d_doff + doff.size());
+    HIPCHK(hipMemcpyAsync(d_doff, doff.data(), doff.size() * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_pose, pose12.data(), pose12.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return row_pipeline(c, frames, lds, doff, d_doff, d_pose, outs);
+  }
+  // pinned [doff (F+1) | poses (12 F) | rows (n, 4) | out (n, 4)], 8-byte words
+  const size_t w_pose = doff.size(), w_rows = w_pose + pose12.size(), w_out = w_rows + 4 * (size_t)n;
+  char* base = nullptr;
+  if (int r = ctx_pin(c, (w_out + 4 * (size_t)n) * 8, &base)) return r;
+  double* pin = reinterpret_cast<double*>(base);
+  std::memcpy(pin, doff.data(), doff.size() * 8);
+  std::memcpy(pin + w_pose, pose12.data(), pose12.size() * 8);
+  for (int32_t f = 0; f < F; ++f) {
+    const int64_t m = doff[f + 1] - doff[f], ld = lds[f];
+    double* dst = pin + w_rows + 4 * doff[f];
+    if (ld == 4) std::memcpy(dst, frames[f], (size_t)m * 4 * sizeof(double));
+    else for (int64_t i = 0; i < m; ++i) std::memcpy(dst + 4 * i, frames[f] + i * ld, 4 * sizeof(double));
+  }
+  {
+    TimedRegion tr(c, &c->main_ev, c->stream);
+    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
+    hipLaunchKernelGGL(k_align_rows_f64, dim3(grid), dim3(kBlock), 0, c->stream, pin + w_rows, (int64_t)4, n,
+                       (int64_t)0, reinterpret_cast<const int64_t*>(pin), F, pin + w_pose, pin + w_out);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int32_t f = 0; f < F; ++f)
+    if (doff[f + 1] > doff[f])
+      std::memcpy(outs[f], pin + w_out + 4 * doff[f], (size_t)(doff[f + 1] - doff[f]) * 4 * sizeof(double));
+  return MC_OK;
+}
+
+int mc_transform_pointcloud_f64(mc_ctx* c, const double* points, int64_t n, int64_t ld, const double* rpy,
+                                const double* translation, double* out) {
+  CHECK_ARG(c && rpy && translation, "NULL argument");
+  CHECK_ARG(n >= 0, "negative point count");
+  if (ld < 4) return fail(MC_ERR_INDEX, "index 3 is out of bounds for axis 1 with size %lld", (long long)ld);
+  if (n == 0) return MC_OK;
+  CHECK_ARG(points && out, "NULL points / out");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  // LMC:774: R = Rotation.from_euler('xyz', rotation).as_matrix(), scipy's arithmetic (rot.cpp)
+  std::vector<double> pose(12);
+  mcrot::euler_xyz_scipy(rpy, pose.data());
+  for (int k = 0; k < 3; ++k) pose[9 + k] = translation[k];
+  const std::vector<int64_t> doff{0, n};
+  const double* fr[1] = {points};
+  const int64_t lds[1] = {ld};
+  double* const outs[1] = {out};
+  return align_host_rows(c, fr, lds, doff, pose, outs);
+}
+
+// ---- per-point modes on host float64 rows (k_points_f64) --------------------------------------
+
+int mc_deskew_points_f64(mc_ctx* c, int mode, int32_t F, const int64_t* counts, const double* points, int64_t ld,
+                         const int64_t* t_ns, const double* frame_times, const int64_t* frame_start_ns, double* out) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(mode == MC_MODE_POSE_SLERP || mode == MC_MODE_IMU, "mode %d: MC_MODE_POSE_SLERP or MC_MODE_IMU expected",
+            mode);
+  CHECK_ARG(F >= 0, "n_frames must be >= 0");
+  CHECK_ARG(F == 0 || counts, "counts is NULL");
+  if (ld < 3) return fail(MC_ERR_INDEX, "points need at least 3 columns (x, y, z); got %lld", (long long)ld);
+  std::vector<int64_t> doff((size_t)F + 1, 0);
+  for (int32_t f = 0; f < F; ++f) {
+    CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
+    doff[f + 1] = doff[f] + counts[f];
+  }
+  if (mode == MC_MODE_POSE_SLERP) {
+    if (c->T < 1) return fail(MC_ERR_STATE, "no trajectory uploaded (mc_set_trajectory)");
+    CHECK_ARG(F == 0 || frame_times, "frame times are NULL");
+  } else {
+    if (c->M < 1) return fail(MC_ERR_STATE, "no IMU samples uploaded (mc_set_imu)");
+    CHECK_ARG(F == 0 || frame_start_ns, "frame start times are NULL");
+  }
+  const int64_t n = doff[F];
+  if (n == 0) return MC_OK;
+  CHECK_ARG(points && t_ns && out, "NULL points / t_ns / out");
+  DeviceGuard g(c->device);
+  if (int r = sync_all(c)) return r;
+  hipStream_t s = c->stream;
+  // the segment table of the uploaded trajectory / IMU samples (k_prep's table lanes, no frames)
+  const uint64_t ver = mode == MC_MODE_POSE_SLERP ? c->traj_ver : c->imu_ver;
+  const int64_t nseg = mode == MC_MODE_POSE_SLERP ? std::max<int64_t>(c->T - 1, 1) : c->M;
+  const size_t seg_b = (size_t)nseg * (mode == MC_MODE_POSE_SLERP ? sizeof(PoseSeg) : sizeof(ImuSeg));
+  if (!(c->d_seg64 && c->seg64_mode == mode && c->seg64_ver == ver)) {
+    c->seg64_mode = -1;
+    if (seg_b > c->seg64_bytes) {
+      if (c->d_seg64) (void)hipFree(c->d_seg64);
+      c->d_seg64 = nullptr;
+      c->seg64_bytes = 0;
+      HIPCHK(hipMalloc(&c->d_seg64, seg_b));
+      c->seg64_bytes = seg_b;
+    }
+    PrepArgs pa;
+    std::memset(&pa, 0, sizeof(pa));
+    pa.mode = mode;
+    pa.n_frames = 0;
+    pa.time = c->d_time; pa.pos = c->d_pos; pa.rpy = c->d_rpy; pa.T = c->T;
+    pa.imu_ts = c->d_imu_ts; pa.gyro = c->d_gyro; pa.M = c->M;
+    pa.pose_seg = static_cast<PoseSeg*>(c->d_seg64);
+    pa.imu_seg = static_cast<ImuSeg*>(c->d_seg64);
+    pa.nseg = nseg;
+    const uint32_t blocks = (uint32_t)(((nseg + 63) / 64 + 3) / 4);
+    hipLaunchKernelGGL(k_prep, dim3(blocks), dim3(kBlock), 0, s, pa);
+    HIPCHK(hipGetLastError());
+    c->seg64_mode = mode;
+    c->seg64_ver = ver;
+  }
+  // scratch: [doff (F+1) | per-frame value (F) | t_ns (n) | points (n, ld) | out (n, 4)], 8-byte words;
+  // pinned and device-mapped below kZeroCopyRows rows (the kernel reads and writes host memory: no
+  // DMA round trips for the reference's per-frame calls), a device staging buffer above
+  const size_t w_doff = 0, w_fv = (size_t)F + 1, w_t = w_fv + (size_t)F, w_pts = w_t + (size_t)n,
+               w_out = w_pts + (size_t)n * (size_t)ld, words = w_out + 4 * (size_t)n;
+  const bool zero_copy = n < kZeroCopyRows;
+  char* base = nullptr;
+  if (zero_copy) {
+    if (int r = ctx_pin(c, words * 8, &base)) return r;
+    std::memcpy(base + 8 * w_doff, doff.data(), doff.size() * 8);
+    std::memcpy(base + 8 * w_fv, mode == MC_MODE_POSE_SLERP ? static_cast<const void*>(frame_times)
+                                                            : static_cast<const void*>(frame_start_ns), (size_t)F * 8);
+    std::memcpy(base + 8 * w_t, t_ns, (size_t)n * 8);
+    std::memcpy(base + 8 * w_pts, points, (size_t)n * (size_t)ld * 8);
+  } else {
+    void* st = nullptr;
+    if (int r = ctx_stage(c, words * 8, &st)) return r;
+    base = static_cast<char*>(st);
+    HIPCHK(hipMemcpyAsync(base + 8 * w_doff, doff.data(), doff.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_fv, mode == MC_MODE_POSE_SLERP ? static_cast<const void*>(frame_times)
+                                                                      : static_cast<const void*>(frame_start_ns),
+                          (size_t)F * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_t, t_ns, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(base + 8 * w_pts, points, (size_t)n * (size_t)ld * 8, hipMemcpyHostToDevice, s));
+  }
+  PointsF64Args a;
+  std::memset(&a, 0, sizeof(a));
+  a.pts = reinterpret_cast<const double*>(base + 8 * w_pts); a.ld = ld; a.n = n;
+  a.t_ns = reinterpret_cast<const int64_t*>(base + 8 * w_t);
+  a.doff = reinterpret_cast<const int64_t*>(base + 8 * w_doff); a.F = F;
+  a.ftime = reinterpret_cast<const double*>(base + 8 * w_fv);
+  a.fstart = reinterpret_cast<const int64_t*>(base + 8 * w_fv);
+  a.pose_time = c->d_time; a.pose_seg = static_cast<const PoseSeg*>(c->d_seg64); a.nseg = nseg;
+  a.imu_ts = c->d_imu_ts; a.imu_seg = static_cast<const ImuSeg*>(c->d_seg64);
+  a.ntab = mode == MC_MODE_POSE_SLERP ? c->T : c->M;
+  a.out = reinterpret_cast<double*>(base + 8 * w_out);
+  const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, zero_copy ? 1024 : 65536);
+  {
+    TimedRegion tr(c, &c->main_ev, s);
+    if (mode == MC_MODE_POSE_SLERP) hipLaunchKernelGGL(k_points_f64<1>, dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_points_f64<2>, dim3(grid), dim3(kBlock), 0, s, a);
+  }
+  HIPCHK(hipGetLastError());
+  if (!zero_copy) HIPCHK(hipMemcpyAsync(out, a.out, (size_t)n * 32, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (zero_copy) std::memcpy(out, a.out, (size_t)n * 32);
+  return MC_OK;
+}
+
+// ---- host arrays <-> device: the row pipeline ------------------------------------------------
+// Rows of the concatenated frames travel in chunks: the host pool copies a chunk into pinned
+// memory (compacting rows to 4 columns), DMA to HBM, k_align_rows_f64, DMA back, the pool copies
+// the rows out to the caller's arrays — chunk k's host copies overlap chunk k±1's DMA and kernel.
+
+static void host_rows(mc_ctx* c, const std::vector<int64_t>& doff, int64_t r0, int64_t r1,
+                      const std::function<void(int32_t, int64_t, int64_t)>& seg) {
+  // segments (frame, row_a, row_b) of [r0, r1), at most kJobRows rows each, run on the pool
+  std::vector<std::array<int64_t, 3>> jobs;
+  int32_t f = (int32_t)(std::upper_bound(doff.begin(), doff.end(), r0) - doff.begin()) - 1;
+  for (; f < (int32_t)doff.size() - 1 && doff[f] < r1; ++f)
+    for (int64_t a = std::max(doff[f], r0), e = std::min(doff[f + 1], r1); a < e; a += kJobRows)
+      jobs.push_back({f, a, std::min(a + kJobRows, e)});
+  if (!c->pool) c->pool.reset(new mcimpl::HostPool(kPoolThreads));
+  c->pool->run((int64_t)jobs.size(), [&](int64_t j) { seg((int32_t)jobs[j][0], jobs[j][1], jobs[j][2]); });
+}
+
 // Variants (MCDESKEW_ROWPIPE, A/B of round 6): 0 = staged, one stream (H2D, kernel, D2H in order);
 // 1 = staged, the D2H on the side stream (chunk k's D2H beside chunk k+1's H2D: PCIe both ways);
 // 2 = direct: no host staging copies, DMA straight from the caller's 4-column frames and into its
