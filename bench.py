@@ -624,6 +624,120 @@ def measure_codecs(ctx, b_src, mode, b_out, n_rank, reps, cpu_budget):
     return rep
 
 
+def pcie_ceiling(nbytes=256 << 20, reps=5):
+    """Pinned H2D and D2H DMA rates of this box (HIP runtime through ctypes; tools/pcie_probe.py)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    pin, dev = ctypes.c_void_p(), ctypes.c_void_p()
+    if hip.hipHostMalloc(ctypes.byref(pin), ctypes.c_size_t(nbytes), 0) or \
+            hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(nbytes)):
+        raise RuntimeError("pcie_ceiling: allocation failed")
+    out = {}
+    try:
+        for name, dst, src, kind in (("H2D", dev, pin, 1), ("D2H", pin, dev, 2)):
+            hip.hipMemcpy(dst, src, ctypes.c_size_t(nbytes), kind)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                hip.hipMemcpy(dst, src, ctypes.c_size_t(nbytes), kind)
+            out[name + "_GBs"] = reps * nbytes / (time.perf_counter() - t0) / 1e9
+    finally:
+        hip.hipFree(dev)
+        hip.hipHostFree(pin)
+    return out
+
+
+def measure_host_path(ctx, frames, points, reps):
+    """The reference's own calling convention at BASELINE config-2 scale (SURVEY §8 a3-a5 on host
+    arrays): run_alignment on ``frames`` x ``points`` float64 (n, 4) numpy frames, LMC:802-832, one
+    call for all frames, host arrays in and out (the reference's transform_pointcloud returns a new
+    array per frame: every call writes a fresh output, whose first-touch page faults are part of the
+    wall time).  64 algorithmic bytes per point cross PCIe (32 in, 32 out); the ceilings are this
+    box's pinned DMA rates: serial = one direction after the other (32/H2D + 32/D2H per point),
+    duplex = both directions at once (max of the two)."""
+    rng = np.random.default_rng(0)
+    base = rng.standard_normal((points, 4)) * 30.0
+    scans = [base + f * 1e-3 for f in range(frames)]
+    sim = mc.LiDARMotionSimulator(dict(SCENARIOS["urban_complex"]), context=ctx)
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    times = sim.lidar_times()[:frames]
+    sim.run_alignment(scans[:2], tr, times[:2])
+    walls = []
+    res = None
+    for _ in range(reps):
+        res = None
+        t0 = time.perf_counter()
+        res = sim.run_alignment(scans, tr, times)
+        walls.append(time.perf_counter() - t0)
+    # spot check against the reference's op sequence (oracle) on two frames
+    from oracle import restatement as R
+    idx = R.select_pose_index(tr["time"], times)
+    ok = True
+    for f in (0, frames - 1):
+        want = R.transform_pointcloud(scans[f], {"translation": tr["position_gps"][idx[f]],
+                                                 "rotation": tr["orientation_imu"][idx[f]]})
+        ok = ok and bool(np.array_equal(res[f], want))
+    res = None
+    pc = pcie_ceiling()
+    n = frames * points
+    best, med = min(walls), float(np.median(walls))
+    serial = 1.0 / (32 / pc["H2D_GBs"] + 32 / pc["D2H_GBs"]) * 1e3          # Mpoints/s
+    duplex = min(pc["H2D_GBs"], pc["D2H_GBs"]) / 32 * 1e3
+    return {"workload": f"run_alignment, {frames} x {points} float64 (n, 4) host frames (BASELINE config 2 shape)",
+            "wall_s": walls, "Mpoints_s": n / best / 1e6, "Mpoints_s_median": n / med / 1e6,
+            "GBs_64B_per_point": 64 * n / best / 1e9, "pcie": pc,
+            "ceiling_Mpoints_s": {"serial": serial, "duplex": duplex},
+            "frac_pcie": n / best / 1e6 / serial, "frac_pcie_duplex": n / best / 1e6 / duplex,
+            "bitwise_vs_reference_ops": ok,
+            "note": "wall time of the drop-in call incl. its new output array; frac_pcie against the serial "
+                    "ceiling (32 B/pt H2D then 32 B/pt D2H), frac_pcie_duplex against both directions at once"}
+
+
+def measure_save(ctx, reps=1):
+    """The reference's end-to-end sequence on the GPU drop-in: simulate_frames (LMC:802-858: every
+    frame's scan + alignment, mc_scan_emit_f64) then save_results (LMC:860-931: CSVs, 2 x 1200
+    per-frame PCDs, merged PCDs, LVX) for the urban_complex run over a synthetic scene the size of the
+    reference's (29,000 points), written to a temporary directory.  The CPU figure is an estimate:
+    the reference's per-line Python formatting (oracle.codecs.pcd_ascii_bytes, as LMC:946-948) timed
+    on a sample of lines and scaled to the run's lines."""
+    import shutil
+    import tempfile
+    rng = np.random.default_rng(7)
+    E = 29_000
+    env = np.column_stack([rng.uniform(-200, 200, E), rng.uniform(-200, 200, E), rng.uniform(-25, 70, E),
+                           rng.uniform(0, 1, E)])
+    sim = mc.LiDARMotionSimulator(dict(SCENARIOS["urban_complex"]), context=ctx)
+    tr = sim.add_sensor_noise(sim.generate_trajectory())
+    d = tempfile.mkdtemp(prefix="mc_save_")
+    import contextlib
+    import io
+    try:
+        t0 = time.perf_counter()
+        res = sim.simulate_frames(env, tr)
+        t1 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            sim.save_results(res, d)
+        t2 = time.perf_counter()
+        files, nbytes = 0, 0
+        for root, _, fs in os.walk(d):
+            for fn in fs:
+                files += 1
+                nbytes += os.path.getsize(os.path.join(root, fn))
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    pts = sum(len(a) for a in res["aligned_pointclouds"])
+    lines = 4 * pts      # raw + aligned per frame, and the two merged files
+    from oracle import codecs as C
+    sample = np.vstack(res["aligned_pointclouds"])[:20_000]
+    t3 = time.perf_counter()
+    C.pcd_ascii_bytes(sample)
+    per_line = (time.perf_counter() - t3) / max(len(sample), 1)
+    return {"workload": f"urban_complex run: {len(res['raw_scans'])} frames, {pts} points, synthetic 29k-point scene",
+            "simulate_frames_s": t1 - t0, "save_results_s": t2 - t1, "total_s": t2 - t0,
+            "files": files, "bytes": nbytes, "device_rows_reused": True,
+            "cpu_estimate": {"pcd_lines_s": per_line * lines, "lines": lines, "cores": 1, "kind": "port",
+                             "sample": f"{len(sample)} lines through the reference's per-line formatting"}}
+
+
 def measure_deskew_pcd(ctx, b_in, b_out, mode, n_rank, reps):
     """SURVEY §8f row 3 fused with the path, both pipelines on the same batch, interleaved:
       separate  mc_deskew, then mc_pcd_encode_batch (measure pass + write pass)
@@ -919,6 +1033,7 @@ def main():
                     help="processes for the all-cores CPU legs (0: every core this process may use)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra-modes", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host-array drop-in and save legs")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL merged-cloud gather (N>1)")
     ap.add_argument("--no-check", action="store_true", help="skip the post-run oracle spot check (N=1)")
     ap.add_argument("--events-after", action="store_true",
@@ -1013,6 +1128,10 @@ def main():
         codecs = measure_codecs(ctx, src_of[args.mode], args.mode, b_out, n_rank, 5,
                                 0.0 if (args.no_cpu or world > 1) else 1.0)
         codecs["pcd_ascii_fused"] = measure_deskew_pcd(ctx, src_of[args.mode], b_out, args.mode, n_rank, 5)
+    host = save = None
+    if world == 1 and not args.no_extra_modes and not args.no_host_path and n_rank:
+        host = measure_host_path(ctx, len(counts), int(counts[0]) if len(counts) else 0, 3)
+        save = measure_save(ctx)
 
     imu = (ts_imu, gyro)
     F_all = len(counts_all)
@@ -1046,6 +1165,9 @@ def main():
         line = assemble_line(args, cid, label, scen, lo, hi, world, n_devices, n_rank, n_total, counts_all,
                              results, spinup_ms, every, tuned, stager, scan, codecs, parity, gather, hung, single)
         ok = line["ok"]
+        if host is not None:
+            line["host_path"] = host
+            line["simulate_save"] = save
         if cpu is not None:
             line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)

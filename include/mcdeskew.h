@@ -289,8 +289,13 @@ int mc_transform_affine(mc_ctx* ctx, const mc_batch* in, mc_batch* out, int32_t 
  * w, CSIM:227), frames back to back (counts[f] rows); mats = 3x4 [A | b] row-major, 1 or n_frames of
  * them; out (N, 3) float64 (CSIM:233).  A frame is one transform_points call: numpy sums a one-row
  * call (a matrix-vector product) in another order than a larger one, and both are repeated.  per_row
- * != 0 treats every row as its own call — _transform_coordinates' per-point loop (CSIM:2117-2141).
- * Synchronous. */
+ * = MC_AFFINE_PER_ROW treats every row as its own call — _transform_coordinates' per-point loop
+ * (CSIM:2117-2141); MC_AFFINE_TRANSLATE adds b to each row's x, y, z and ignores A — that loop's UTM
+ * branch, point + [utm_x, utm_y, 0] (CSIM:2132), one rounding per coordinate (no products, so a
+ * non-finite coordinate does not spread to the others).  Synchronous. */
+#define MC_AFFINE_PER_FRAME 0
+#define MC_AFFINE_PER_ROW 1
+#define MC_AFFINE_TRANSLATE 2
 int mc_affine_rows_f64(mc_ctx* ctx, int32_t n_frames, const int64_t* counts, const double* rows, int64_t ld,
                        int32_t n_mats, const double* mats, int per_row, double* out);
 

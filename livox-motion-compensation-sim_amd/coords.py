@@ -161,10 +161,16 @@ def transform_coordinates(frames_data: List[Dict], target_system: str, gps_data:
         moved = Ts[:, :2, 3].any(axis=1)
         new_xyz = list(frames_xyz)
         if moved.any():
+            # CSIM:2132 point + [utm_x, utm_y, 0]: a plain add per coordinate on the device (no
+            # products: a non-finite coordinate stays in its own column, as in the reference)
             sel = np.flatnonzero(moved)
-            for f, xyz in zip(sel, transform_arrays([frames_xyz[f] for f in sel], Ts[sel],
-                                                    context=transformer.context, per_point=True)):
-                new_xyz[f] = xyz
+            xs = [frames_xyz[f] for f in sel]
+            counts = np.array([len(x) for x in xs], np.int64)
+            if counts.sum() > 0:
+                ctx = transformer.context or default_context()
+                out = ctx.affine_rows(counts, np.concatenate(xs), Ts[sel][:, :3, :4], translate=True)
+                for f, o, k in zip(sel, np.concatenate([[0], np.cumsum(counts)[:-1]]), counts):
+                    new_xyz[f] = out[o:o + k]
     elif (CoordinateSystem.SENSOR, target_system) in transformer.transformations:
         # CSIM:2137-2139: transform_points on one (1, 3) point at a time
         new_xyz = transform_arrays(frames_xyz, transformer.transformations[(CoordinateSystem.SENSOR, target_system)],

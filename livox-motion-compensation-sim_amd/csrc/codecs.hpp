@@ -742,7 +742,11 @@ __device__ __forceinline__ void pcd_emit_value(uint8_t* base, int pa, uint32_t D
   lds_or64(w + 8, (AB << sh) | ((H >> 8) >> (56 - sh)));
   lds_or64(w + 16, (AB >> 8) >> (56 - sh));
 }
-__device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint8_t* base, int off) {
+// text: the tile's text buffer as 16-byte chunks — typed uint4 so the 8-byte grid pcd_emit_value
+// ORs into is the buffer's own alignment (a ds_or_b64 at a 4-byte LDS offset faults, profiles/round5/s03)
+__device__ __forceinline__ void pcd_emit_line(const PcdText& T, uint4* text, int off) {
+  static_assert(alignof(uint4) % 8 == 0, "the text chunks must keep the 8-byte grid of ds_or_b64");
+  uint8_t* const base = reinterpret_cast<uint8_t*>(text);
   int pa = off + 4 + T.d[0];   // the '.' of value k
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -926,7 +930,7 @@ __device__ __forceinline__ int pcd_tile_text(const PcdText& T, bool valid, int64
   pcd_text_zero(s_text4);
   int total;
   const int excl = block_scan(T.len, s_wave, total) - T.len;
-  if (valid && !(MC_PCD_DIAG & 4)) pcd_emit_line(T, reinterpret_cast<uint8_t*>(s_text4 + kPcdTextLead), (int)(G & 15) + excl);
+  if (valid && !(MC_PCD_DIAG & 4)) pcd_emit_line(T, s_text4 + kPcdTextLead, (int)(G & 15) + excl);
   __syncthreads();
   return total;
 }
@@ -979,7 +983,7 @@ constexpr int kPcdWriteTiles = MC_PCD_WRITE_TILES;
 template <bool F32>
 __global__ __launch_bounds__(kPcdBlock) void k_pcd_write(const PcdArgs a) {
   __shared__ int s_wave[kPcdBlock / 64];
-  __shared__ uint4 s_text4[kPcdTextChunks];
+  __shared__ alignas(16) uint4 s_text4[kPcdTextChunks];
   const int64_t u0 = stream_unit(a.worder, blockIdx.x, gridDim.x) * kPcdWriteTiles;   // grid = units exactly
   int32_t f = codec_frame_of(a.src, u0);
   if constexpr (F32) {

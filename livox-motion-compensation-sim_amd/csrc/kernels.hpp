@@ -1058,6 +1058,7 @@ __global__ __launch_bounds__(kBlock) void k_align_rows_f64(const double* __restr
 // fma(A_i1, y, A_i0 * x))); for a one-row frame, or every row with per_row (the reference's
 // per-point loop, CSIM:2117-2141, one 4x1 product per point — numpy's dgemv):
 // (A_i0 x + A_i2 z) + (A_i1 y + b_i w), every product rounded (tools/fma_order.py); out (n, 3).
+// per_row == 2 (MC_AFFINE_TRANSLATE): p + b, the UTM branch's plain add (CSIM:2132).
 __global__ __launch_bounds__(kBlock) void k_affine_rows_f64(const double* __restrict__ in, int64_t ld, int64_t n,
                                                             const int64_t* __restrict__ doff, int32_t F,
                                                             const double* __restrict__ mats, int32_t n_mats,
@@ -1069,6 +1070,12 @@ __global__ __launch_bounds__(kBlock) void k_affine_rows_f64(const double* __rest
     const double* q = in + i * ld;
     const double x = q[0], y = q[1], z = q[2], w = ld == 4 ? q[3] : 1.0;
     double* o = out + 3 * i;
+    if (per_row == 2) {
+      o[0] = __dadd_rn(x, M[3]);
+      o[1] = __dadd_rn(y, M[7]);
+      o[2] = __dadd_rn(z, M[11]);
+      continue;
+    }
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
 #pragma clang fp contract(off)
@@ -1551,7 +1558,7 @@ __global__ __launch_bounds__(kBlock, kPointsWaves) void k_deskew_points(const De
   span_end(a.span);
 }
 
-// ---- the next step's prep inside this step's launch (mc_deskew_steps, MC_STEPS_PIPELINE) ---------
+// ---- the next step's prep inside this step's launch (mc_deskew_steps) --------------------------
 // Workgroups [0, pre) run k_prep's body for the NEXT step (its table half), the rest this step's
 // deskew over the half the previous launch's prep wrote.  The two halves never alias, and the
 // kernel boundary orders the prep's stores before the next launch's reads, so no flag or fence

@@ -919,7 +919,7 @@ void issue_steps(mc_ctx* c, const StepPlan* plan, int mode, int32_t n_steps, int
   }
 }
 
-// n steps as n launches, step i's launch carrying step i+1's prep (MC_STEPS_PIPELINE): one
+// n steps as n launches, step i's launch carrying step i+1's prep: one
 // standalone k_prep for step 0, then n deskew launches; the kernel boundaries order each prep
 // before the step that reads it, as in mc_deskew.  Step i reads half h0 ^ (i & 1).
 int deskew_steps_pipelined(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int pose_select,
@@ -1035,7 +1035,7 @@ int mc_deskew_steps(mc_ctx* c, const mc_batch* in, mc_batch* out, int mode, int 
   return deskew_steps_pipelined(c, in, out, mode, pose_select, n_steps, sample_every);
 }
 
-constexpr int64_t kPipeRows = 1 << 20;                                 // 32 MB of (n,4) float64
+constexpr int64_t kPipeRows = 1 << 21;                                 // 64 MB of (n,4) float64 (max chunk)
 constexpr size_t kPipeBytes = (size_t)kPipeRows * 4 * sizeof(double);
 constexpr int64_t kZeroCopyRows = 1 << 15;                             // below: zero-copy kernels
 constexpr int kPoolThreads = 16;                                       // the box's CPU share per GPU
@@ -1251,6 +1251,12 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
   const int64_t n = doff[F];
   int variant = 1;
   if (const char* v = std::getenv("MCDESKEW_ROWPIPE")) variant = std::atoi(v);
+  int64_t rows_per = 1 << 20;
+  if (const char* v = std::getenv("MCDESKEW_PIPEROWS")) rows_per = std::max<int64_t>(1 << 12, std::min<int64_t>(kPipeRows, std::atoll(v)));
+  const bool trace = std::getenv("MCDESKEW_ROWPIPE_TRACE") != nullptr;
+  double t_in = 0, t_out = 0, t_wait_in = 0, t_wait_out = 0;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t_start = now();
   bool dense = true;   // every frame 4 columns wide and the outputs one contiguous (n, 4) array
   for (int32_t f = 0; f < F && dense; ++f)
     dense = (lds[f] == 4 || doff[f + 1] == doff[f]) && outs[f] == outs[0] + 4 * doff[f];
@@ -1272,17 +1278,19 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
   hipStream_t s = c->stream;
   hipStream_t so = variant == 0 ? c->stream : c->side;   // the D2H stream
   auto copy_out = [&](int64_t k) {
-    const int64_t r0 = k * kPipeRows, r1 = std::min(n, r0 + kPipeRows);
+    const double t0 = now();
+    const int64_t r0 = k * rows_per, r1 = std::min(n, r0 + rows_per);
     const double* src = pin[2 + (k & 1)];
     host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t e) {
       std::memcpy(outs[f] + 4 * (a - doff[f]), src + 4 * (a - r0), (size_t)(e - a) * 4 * sizeof(double));
     });
+    t_out += now() - t0;
   };
-  const int64_t K = (n + kPipeRows - 1) / kPipeRows;
+  const int64_t K = (n + rows_per - 1) / rows_per;
   int rc = MC_OK;
   for (int64_t k = 0; k < K && rc == MC_OK; ++k) {
     const int b = (int)(k & 1);
-    const int64_t r0 = k * kPipeRows, r1 = std::min(n, r0 + kPipeRows), m = r1 - r0;
+    const int64_t r0 = k * rows_per, r1 = std::min(n, r0 + rows_per), m = r1 - r0;
     hipError_t e = hipSuccess;
     if (variant == 2) {
       // the caller's rows of [r0, r1) straight into dev[b] (a run of whole or partial frames)
@@ -1294,7 +1302,10 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
                              hipMemcpyHostToDevice, s);
       }
     } else {
+      double tw = now();
       if (k >= 2) (void)hipEventSynchronize(ev_in[b]);                 // pinned input b is free again
+      const double t0 = now();
+      t_wait_in += t0 - tw;
       double* dst = pin[b];
       host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t z) {
         const int64_t ld = lds[f];
@@ -1306,6 +1317,7 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
           for (int64_t i = 0; i < z - a; ++i) std::memcpy(dp + 4 * i, sp + i * ld, 4 * sizeof(double));
         }
       });
+      t_in += now() - t0;
       e = hipMemcpyAsync(dev[b], pin[b], (size_t)m * 32, hipMemcpyHostToDevice, s);
       if (e == hipSuccess) e = hipEventRecord(ev_in[b], s);
     }
@@ -1322,7 +1334,9 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
       if (e == hipSuccess) e = hipStreamWaitEvent(so, ev_k[b], 0);
     }
     if (variant != 2 && e == hipSuccess && k >= 1) {                // chunk k-1's rows are back: copy out
+      const double tw = now();
       e = hipEventSynchronize(ev_out[b ^ 1]);
+      t_wait_out += now() - tw;
       if (e == hipSuccess) copy_out(k - 1);
     }
     if (e == hipSuccess)
@@ -1341,6 +1355,10 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
   for (int b = 0; b < 2; ++b) {
     (void)hipEventDestroy(ev_in[b]); (void)hipEventDestroy(ev_out[b]); (void)hipEventDestroy(ev_k[b]);
   }
+  if (trace)
+    std::fprintf(stderr, "rowpipe v%d rows %lld chunks %lld: total %.2f ms, copy-in %.2f, copy-out %.2f, wait-in %.2f, "
+                 "wait-out %.2f ms\n", variant, (long long)rows_per, (long long)K, 1e3 * (now() - t_start), 1e3 * t_in,
+                 1e3 * t_out, 1e3 * t_wait_in, 1e3 * t_wait_out);
   return rc;
 }
 
@@ -1378,6 +1396,7 @@ int mc_affine_rows_f64(mc_ctx* c, int32_t F, const int64_t* counts, const double
   CHECK_ARG(F >= 0, "n_frames must be >= 0");
   CHECK_ARG(ld == 3 || ld == 4, "rows need 3 or 4 columns (got %lld)", (long long)ld);
   CHECK_ARG(n_mats == 1 || n_mats == F, "need 1 or n_frames matrices (got %d for %d frames)", n_mats, F);
+  CHECK_ARG(per_row >= MC_AFFINE_PER_FRAME && per_row <= MC_AFFINE_TRANSLATE, "unknown per_row mode %d", per_row);
   std::vector<int64_t> doff((size_t)F + 1, 0);
   for (int32_t f = 0; f < F; ++f) {
     CHECK_ARG(counts[f] >= 0, "negative frame size at frame %d", f);
@@ -1414,7 +1433,7 @@ int mc_affine_rows_f64(mc_ctx* c, int32_t F, const int64_t* counts, const double
     const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, zero_copy ? 1024 : 65536);
     hipLaunchKernelGGL(k_affine_rows_f64, dim3(grid), dim3(kBlock), 0, s,
                        reinterpret_cast<const double*>(base + 8 * w_rows), ld, n, reinterpret_cast<const int64_t*>(base),
-                       F, reinterpret_cast<const double*>(base + 8 * w_mat), n_mats, per_row ? 1 : 0, d_out);
+                       F, reinterpret_cast<const double*>(base + 8 * w_mat), n_mats, per_row, d_out);
   }
   HIPCHK(hipGetLastError());
   if (!zero_copy) HIPCHK(hipMemcpyAsync(out, d_out, (size_t)n * 24, hipMemcpyDeviceToHost, s));

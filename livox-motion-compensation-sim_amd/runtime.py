@@ -210,11 +210,12 @@ class Context:
                 if al:
                     al.close()
 
-    def affine_rows(self, counts, rows, mats, per_row: bool = False) -> np.ndarray:
+    def affine_rows(self, counts, rows, mats, per_row: bool = False, translate: bool = False) -> np.ndarray:
         """(T @ [p, w].T).T[:, :3] on float64 rows (mc_affine_rows_f64): rows (N, 3) (w = 1) or
         (N, 4) homogeneous, frames of ``counts`` rows back to back, each frame one numpy product (or,
         with ``per_row``, every row its own one-point product); one (3|4, 4) matrix or one per
-        frame.  Returns (N, 3) float64, bit-identical to numpy's (CSIM:230)."""
+        frame.  Returns (N, 3) float64, bit-identical to numpy's (CSIM:230).  ``translate``: the
+        rows' x, y, z plus the matrices' translation column only (CSIM:2132's UTM offset add)."""
         c = np.ascontiguousarray(np.atleast_1d(counts), dtype=np.int64)
         r = np.ascontiguousarray(rows, dtype=np.float64)
         m = np.ascontiguousarray(mats, dtype=np.float64)
@@ -225,7 +226,7 @@ class Context:
         m = np.ascontiguousarray(m[:, :3, :4])
         out = np.empty((r.shape[0], 3), np.float64)
         check(self.lib.mc_affine_rows_f64(self.handle, len(c), ptr(c, c_int64), ptr(r, c_double), r.shape[1],
-                                          len(m), ptr(m, c_double), int(bool(per_row)), ptr(out, c_double)),
+                                          len(m), ptr(m, c_double), 2 if translate else int(bool(per_row)), ptr(out, c_double)),
               "affine_rows")
         return out
 

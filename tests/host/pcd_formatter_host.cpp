@@ -55,6 +55,7 @@ static inline void pk_tens_units(uint32_t v, uint32_t& t, uint32_t& u) {
     u |= ((x - q * 10u) & 0xffffu) << (16 * l);
   }
 }
+struct alignas(16) uint4 { uint32_t x, y, z, w; };   // the kernel's 16-byte text chunks
 using std::fma;
 using std::signbit;
 using std::rint;
@@ -183,7 +184,7 @@ int main(int argc, char** argv) {
       want += line;
     }
     for (int l = 255; l >= 0; --l)
-      if (P[l].ok) pcd_emit_line(T[l], reinterpret_cast<uint8_t*>(buf.data()) + 16, offs[l]);
+      if (P[l].ok) pcd_emit_line(T[l], reinterpret_cast<uint4*>(buf.data()) + 1, offs[l]);
     const std::string got(reinterpret_cast<const char*>(buf.data()) + 16 + shift, off - shift);
     // nothing written outside the tile's text
     const unsigned char* bb = reinterpret_cast<const unsigned char*>(buf.data()) + 16;

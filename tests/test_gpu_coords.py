@@ -124,3 +124,43 @@ def test_transform_arrays_per_frame_matrices_large(mc, gpu_ctx):
     out = mc.coords.transform_arrays(h, Ts, context=gpu_ctx)
     for f, T, o in zip(h, Ts, out):
         assert_scaled_close(o, R.transform_points_h(f, T), scale_of(f[:, :3], T[:3, 3]) * 2)
+
+
+def test_utm_offset_is_a_plain_add(mc, gpu_ctx, monkeypatch):
+    """CSIM:2132 `point_array[0] + np.array([utm_x, utm_y, 0])`: each coordinate one add, so a NaN or
+    inf in one coordinate stays there and -0.0 + 0 gives 0.0 — bit for bit with numpy on the device
+    (MC_AFFINE_TRANSLATE), directly and through transform_coordinates' UTM branch (a stand-in `utm`
+    module: the package is not installed here, and without it the reference leaves points unchanged)."""
+    rng = np.random.default_rng(6)
+    p = rng.normal(0, 40, (1000, 3))
+    p[3] = [np.nan, 1.0, 2.0]
+    p[4] = [1.0, np.inf, -3.0]
+    p[5] = [-0.0, -0.0, -0.0]
+    off = np.array([583_960.123456789, 4_507_523.98765, 0.0])
+    got = gpu_ctx.affine_rows([len(p)], p, np.column_stack([np.eye(3), off]), translate=True)
+    want = p + np.array([off[0], off[1], 0])
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+    class FakeUtm:
+        @staticmethod
+        def from_latlon(lat, lon):
+            return 583_960.0 + lat, 4_507_523.0 + lon, 18, "T"
+    monkeypatch.setattr(mc.coords, "UTM_AVAILABLE", True)
+    monkeypatch.setattr(mc.coords, "utm", FakeUtm, raising=False)
+    ct = mc.CoordinateTransformer(gpu_ctx)
+    frames = []
+    for i in range(3):
+        xyz = p[i * 300:(i + 1) * 300 + (5 if i == 0 else 0)]
+        pts = [mc.LiDARPoint(x=float(x), y=float(y), z=float(z), intensity=1, timestamp=k, ring=0, tag=0)
+               for k, (x, y, z) in enumerate(xyz)]
+        frames.append({"frame_id": i, "timestamp": i * 100_000_000, "points": pts})
+    gps = [mc.GPSData(0, 40.5, -74.25, 10.0, 0.0, 0.0, 0.0, 0.0),
+           mc.GPSData(150_000_000, 40.75, -74.5, 10.0, 0.0, 0.0, 0.0, 0.0)]
+    res = mc.coords.transform_coordinates(frames, "utm", gps, ct)
+    for fr, src in zip(res, frames):
+        s = mc.coords.find_closest_gps_sample(gps, src["timestamp"])
+        ux, uy, _, _ = FakeUtm.from_latlon(s.latitude, s.longitude)
+        xyz = np.array([[q.x, q.y, q.z] for q in src["points"]])
+        want = xyz + np.array([ux, uy, 0])
+        got = np.array([[q.x, q.y, q.z] for q in fr["points"]])
+        assert np.array_equal(got.view(np.uint64), want.view(np.uint64))

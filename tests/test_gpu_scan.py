@@ -258,3 +258,27 @@ def test_scan_emit_refuses_stale_scene(mc, gpu_ctx):
         assert rc == mc._lib.MC_ERR_STATE
     finally:
         buf.close()
+
+
+def test_scan_one_point_in_range_bitwise(mc, gpu_ctx):
+    """LMC:728 with exactly one scene point inside range_max: numpy's (R.T @ d.T).T is a (3,3) @ (3,1)
+    product (R.T F-contiguous), which keeps the multi-row ascending FMA chain (tools/fma_order.py), so
+    the device's sensor-frame point equals the reference expression bit for bit."""
+    from scipy.spatial.transform import Rotation
+    sim = mc.LiDARMotionSimulator({"lidar_range_noise": 0.0}, context=gpu_ctx)
+    rng = np.random.default_rng(17)
+    hits = 0
+    for _ in range(200):
+        pos = rng.uniform(-50, 50, 3)
+        rpy = rng.uniform(-np.pi, np.pi, 3)
+        Rm = Rotation.from_euler("xyz", rpy).as_matrix()
+        r = rng.uniform(2, 80)        # a sensor-frame point well inside the FOV, carried to the world
+        loc = np.array([r, r * rng.uniform(-0.3, 0.3), r * rng.uniform(-0.3, 0.3)])
+        env = np.array([[*(pos + Rm @ loc), 0.37], [*(pos + 500.0), 0.5], [*(pos - 700.0), 0.6]])
+        out = sim.scan_environment(env, {"position": pos, "orientation": rpy})
+        envf = env[:1]
+        want = (Rm.T @ (envf[:, :3] - pos).T).T          # the reference's expression, one row
+        assert out.shape == (1, 4)
+        assert np.array_equal(out[:, :3], want), (out[:, :3] - want)
+        hits += 1
+    assert hits == 200

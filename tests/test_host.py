@@ -178,3 +178,38 @@ def test_rotation_basis_bitwise_equals_scipy():
         lib.mc_rotation_from_euler_xyz(len(rpy), rpy.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                        R.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
         assert np.array_equal(R, Rotation.from_euler("xyz", rpy).as_matrix()), name
+
+
+def test_device_rows_reuse_only_for_the_unchanged_result():
+    """simulator._DeviceRows (save_results / save_lvx encoding simulate_frames' device rows): used only
+    while the result holds the very lists / arrays it returned, with the same bytes — a replaced
+    frame, a replaced list, an in-place edit (even a sum-preserving swap of two rows) all refuse it."""
+    sim_mod = __import__(pkg().__name__ + ".simulator", fromlist=["_DeviceRows"])
+
+    class FakeBuf:
+        closed = False
+
+        def close(self):
+            self.closed = True
+    rng = np.random.default_rng(1)
+    counts = np.array([3, 0, 5])
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    local, aligned = rng.normal(size=(8, 4)), rng.normal(size=(8, 4))
+
+    def result():
+        raw = [{"frame_id": i, "points_local": local[offs[i]:offs[i + 1]]} for i in range(3)]
+        al = [aligned[offs[i]:offs[i + 1]] for i in range(3)]
+        return {"raw_scans": raw, "aligned_pointclouds": al}
+    res = result()
+    rows = sim_mod._DeviceRows(counts, local, aligned, FakeBuf(), FakeBuf(), res["raw_scans"], res["aligned_pointclouds"])
+    assert rows.matches(res)
+    assert rows.matches(dict(res))                                   # a shallow copy of the dict is fine
+    assert not rows.matches(result())                                # other lists
+    local[[0, 1]] = local[[1, 0]]                                    # a row swap keeps every sum
+    assert not rows.matches(res)
+    local[[0, 1]] = local[[1, 0]]
+    assert rows.matches(res)
+    res["aligned_pointclouds"][2] = res["aligned_pointclouds"][2].copy()
+    assert not rows.matches(res)
+    rows.close()
+    assert rows.d_local.closed and rows.d_aligned.closed

@@ -17,6 +17,9 @@ One-row products (a frame of one point; CSIM:2137's per-point transform_points) 
 and sum in other orders, checked here as "single": 3x3 fma(a2, x2, fma(a0, x0, a1 * x1)), 4x4
 (a0 x0 + a2 x2) + (a1 x1 + a3 x3) with every product rounded (frame_apply(single) and
 k_affine_rows_f64's per-row order).  Row counts 2..257 and 1000 all take the ascending chain.
+The exception is LMC:728 with one scene point in range: R.T is F-contiguous there, and its
+(3,3) @ (3,1) product keeps the ascending chain (0 of 60 000 values differ; "single" misses 23 %),
+so scan.hpp's scan_rotate needs no one-point order (round 6).
 
     python tools/fma_order.py
 """
@@ -88,13 +91,16 @@ def main():
 
     # one-row products, one numpy call per point (dgemv): the "single" order (order 3)
     m = 20_000
-    single = {"LMC:775 one point (R @ p.T).T + t": [], "CSIM:230 one point T @ [p, w]": []}
+    single = {"LMC:775 one point (R @ p.T).T + t": [], "CSIM:230 one point T @ [p, w]": [],
+              "LMC:728 one point (R.T @ d.T).T": []}
     miss = {k: [0, 0] for k in single}
     for i in range(m):
         p = d3[i:i + 1]
         for name, ref, A, X, add in (
                 ("LMC:775 one point (R @ p.T).T + t", (R @ p.T).T + t, R, p, t),
-                ("CSIM:230 one point T @ [p, w]", (T @ p4[i:i + 1].T).T[:, :3], T[:3], p4[i:i + 1], None)):
+                ("CSIM:230 one point T @ [p, w]", (T @ p4[i:i + 1].T).T[:, :3], T[:3], p4[i:i + 1], None),
+                # scan_environment with one scene point in range: R.T is F-contiguous here
+                ("LMC:728 one point (R.T @ d.T).T", (R.T @ p.T).T, R.T, p, None)):
             for j, order in enumerate((1, 3)):
                 o = run(A, X, order)
                 if add is not None:

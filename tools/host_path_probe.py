@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--points", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--variants", default="", help="comma list of MCDESKEW_ROWPIPE values to A/B")
+    ap.add_argument("--rows", default="", help="comma list of MCDESKEW_PIPEROWS chunk sizes to A/B")
     args = ap.parse_args()
     F, n = args.frames, args.points
     rng = np.random.default_rng(0)
@@ -41,16 +43,50 @@ def main():
     out["first_touch_out_s"] = time.perf_counter() - t0
     del a
     sim.run_alignment(scans[:2], tr, times[:2])
-    walls = []
-    for _ in range(args.reps):
-        t0 = time.perf_counter()
-        res = sim.run_alignment(scans, tr, times)
-        walls.append(time.perf_counter() - t0)
-        del res
-    out["run_alignment_s"] = walls
-    best = min(walls)
-    out["Mpoints_s"] = F * n / best / 1e6
-    out["GBs_in_plus_out"] = 64 * F * n / best / 1e9
+    ctx = sim.context
+    from ctypes import c_double, c_int64
+    ptr = mc._lib.ptr
+    counts = np.full(F, n, np.int64)
+    lds = np.full(F, 4, np.int64)
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    fp = np.fromiter((f.__array_interface__["data"][0] for f in scans), np.uintp, F)
+    pref = np.zeros((F * n, 4))                                       # pre-faulted, reused output
+    op = (pref.__array_interface__["data"][0] + 32 * offs[:-1]).astype(np.uintp)
+    t = np.ascontiguousarray(times, np.float64)
+    ctx.set_trajectory(tr["time"], tr["position_gps"], tr["orientation_imu"])
+
+    def direct():
+        mc._lib.check(ctx.lib.mc_align_frames_host_f64(ctx.handle, F, fp.ctypes.data, ptr(counts, c_int64),
+                                                       ptr(lds, c_int64), ptr(t, c_double), mc._lib.MC_POSE_SEARCHSORTED,
+                                                       op.ctypes.data), "align")
+    ref = None
+    for v in (args.variants.split(",") if args.variants else [""]):
+        for rows in (args.rows.split(",") if args.rows else [""]):
+            if v:
+                os.environ["MCDESKEW_ROWPIPE"] = v
+            if rows:
+                os.environ["MCDESKEW_PIPEROWS"] = rows
+            walls, pre = [], []
+            res = None
+            for _ in range(args.reps):
+                res = None                                    # the previous result is freed first
+                t0 = time.perf_counter()
+                res = sim.run_alignment(scans, tr, times)
+                walls.append(time.perf_counter() - t0)
+                t0 = time.perf_counter()
+                direct()
+                pre.append(time.perf_counter() - t0)
+            same = None
+            if ref is None:
+                ref = [r.copy() for r in res[:5]]
+            else:
+                same = all(np.array_equal(a, b) for a, b in zip(ref, res[:5]))
+            res = None
+            key = f"variant_{v or 'default'}_rows_{rows or 'default'}"
+            out[key] = {"run_alignment_s": walls, "Mpoints_s": F * n / min(walls) / 1e6,
+                        "Mpoints_s_median": F * n / float(np.median(walls)) / 1e6,
+                        "prefaulted_out_s": pre, "prefaulted_Mpoints_s": F * n / min(pre) / 1e6,
+                        "equal_to_first": same}
     print(json.dumps(out), flush=True)
 
 
