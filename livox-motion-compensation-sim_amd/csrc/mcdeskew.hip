@@ -1241,32 +1241,44 @@ static void host_rows(mc_ctx* c, const std::vector<int64_t>& doff, int64_t r0, i
   c->pool->run((int64_t)jobs.size(), [&](int64_t j) { seg((int32_t)jobs[j][0], jobs[j][1], jobs[j][2]); });
 }
 
-// Variants (MCDESKEW_ROWPIPE, A/B of round 6): 0 = staged, one stream (H2D, kernel, D2H in order);
-// 1 = staged, the D2H on the side stream (chunk k's D2H beside chunk k+1's H2D: PCIe both ways);
-// 2 = direct: no host staging copies, DMA straight from the caller's 4-column frames and into its
-// contiguous output (HIP's pageable copies), D2H on the side stream.
+// Chunk k's H2D (main stream) runs beside chunk k-1's D2H (side stream), and the host pool copies
+// chunk k into pinned memory while the DMA engines move the chunks around it.  Outputs that are one
+// contiguous page-locked array are written by the D2H directly; others (the usual numpy arrays) go
+// through pinned staging and a host copy-out.  For 600 x 100k rows (profiles/round6/s04, s06): one
+// stream for both directions 79-84 ms, two streams 58-64 ms into an already-faulted output (3.84 GB
+// over PCIe: the box's aggregate of both directions, ~64 GB/s, not twice one direction), DMA
+// straight from the caller's pageable frames 157-248 ms, direct D2H into page-locked outputs 61-71 ms
+// (no gain: the link, not the copy-out, bounds it).  MCDESKEW_ROWPIPE_TRACE=1 prints the phase times.
+static bool pinned_range(const void* p, size_t bytes) {
+  for (const char* q : {static_cast<const char*>(p), static_cast<const char*>(p) + bytes - 1}) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
 static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
                         const int64_t* d_doff, const double* d_pose, double* const* outs) {
   const int32_t F = (int32_t)doff.size() - 1;
   const int64_t n = doff[F];
-  int variant = 1;
-  if (const char* v = std::getenv("MCDESKEW_ROWPIPE")) variant = std::atoi(v);
-  int64_t rows_per = 1 << 20;
-  if (const char* v = std::getenv("MCDESKEW_PIPEROWS")) rows_per = std::max<int64_t>(1 << 12, std::min<int64_t>(kPipeRows, std::atoll(v)));
+  const int64_t rows_per = kPipeRows;   // 2 M rows (64 MB) per chunk: 58-61 vs 64 ms at 1 M (round 6, s04 / s06)
+  bool dense = true;   // the outputs are one contiguous (n, 4) array
+  for (int32_t f = 0; f < F && dense; ++f) dense = outs[f] == outs[0] + 4 * doff[f] || doff[f + 1] == doff[f];
+  const bool direct_out = dense && pinned_range(outs[0], (size_t)n * 32);
   const bool trace = std::getenv("MCDESKEW_ROWPIPE_TRACE") != nullptr;
   double t_in = 0, t_out = 0, t_wait_in = 0, t_wait_out = 0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = now();
-  bool dense = true;   // every frame 4 columns wide and the outputs one contiguous (n, 4) array
-  for (int32_t f = 0; f < F && dense; ++f)
-    dense = (lds[f] == 4 || doff[f + 1] == doff[f]) && outs[f] == outs[0] + 4 * doff[f];
-  if (variant == 2 && !dense) variant = 1;
-  if (!c->h_pipe && variant != 2) HIPCHK(hipHostMalloc(&c->h_pipe, 4 * kPipeBytes, hipHostMallocDefault));
+  if (!c->h_pipe) HIPCHK(hipHostMalloc(&c->h_pipe, 4 * kPipeBytes, hipHostMallocDefault));
   if (!c->d_pipe) HIPCHK(hipMalloc(&c->d_pipe, 4 * kPipeBytes));
-  double* pin[4] = {nullptr, nullptr, nullptr, nullptr};
+  double* pin[4];
   double* dev[4];
   for (int k = 0; k < 4; ++k) {
-    if (c->h_pipe) pin[k] = reinterpret_cast<double*>(static_cast<char*>(c->h_pipe) + k * kPipeBytes);
+    pin[k] = reinterpret_cast<double*>(static_cast<char*>(c->h_pipe) + k * kPipeBytes);
     dev[k] = reinterpret_cast<double*>(static_cast<char*>(c->d_pipe) + k * kPipeBytes);
   }
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
@@ -1275,8 +1287,7 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
     HIPCHK(hipEventCreateWithFlags(&ev_out[b], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_k[b], hipEventDisableTiming));
   }
-  hipStream_t s = c->stream;
-  hipStream_t so = variant == 0 ? c->stream : c->side;   // the D2H stream
+  hipStream_t s = c->stream, so = c->side;   // H2D + kernel | D2H
   auto copy_out = [&](int64_t k) {
     const double t0 = now();
     const int64_t r0 = k * rows_per, r1 = std::min(n, r0 + rows_per);
@@ -1291,64 +1302,52 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
   for (int64_t k = 0; k < K && rc == MC_OK; ++k) {
     const int b = (int)(k & 1);
     const int64_t r0 = k * rows_per, r1 = std::min(n, r0 + rows_per), m = r1 - r0;
-    hipError_t e = hipSuccess;
-    if (variant == 2) {
-      // the caller's rows of [r0, r1) straight into dev[b] (a run of whole or partial frames)
-      int32_t f = (int32_t)(std::upper_bound(doff.begin(), doff.end(), r0) - doff.begin()) - 1;
-      for (; e == hipSuccess && f < F && doff[f] < r1; ++f) {
-        const int64_t a = std::max(doff[f], r0), z = std::min(doff[f + 1], r1);
-        if (z > a)
-          e = hipMemcpyAsync(dev[b] + 4 * (a - r0), frames[f] + 4 * (a - doff[f]), (size_t)(z - a) * 32,
-                             hipMemcpyHostToDevice, s);
+    const double tw = now();
+    if (k >= 2) (void)hipEventSynchronize(ev_in[b]);                 // pinned input b is free again
+    const double t0 = now();
+    t_wait_in += t0 - tw;
+    double* dst = pin[b];
+    host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t z) {
+      const int64_t ld = lds[f];
+      const double* sp = frames[f] + (a - doff[f]) * ld;
+      double* dp = dst + 4 * (a - r0);
+      if (ld == 4) {
+        std::memcpy(dp, sp, (size_t)(z - a) * 4 * sizeof(double));
+      } else {
+        for (int64_t i = 0; i < z - a; ++i) std::memcpy(dp + 4 * i, sp + i * ld, 4 * sizeof(double));
       }
-    } else {
-      double tw = now();
-      if (k >= 2) (void)hipEventSynchronize(ev_in[b]);                 // pinned input b is free again
-      const double t0 = now();
-      t_wait_in += t0 - tw;
-      double* dst = pin[b];
-      host_rows(c, doff, r0, r1, [&](int32_t f, int64_t a, int64_t z) {
-        const int64_t ld = lds[f];
-        const double* sp = frames[f] + (a - doff[f]) * ld;
-        double* dp = dst + 4 * (a - r0);
-        if (ld == 4) {
-          std::memcpy(dp, sp, (size_t)(z - a) * 4 * sizeof(double));
-        } else {
-          for (int64_t i = 0; i < z - a; ++i) std::memcpy(dp + 4 * i, sp + i * ld, 4 * sizeof(double));
-        }
-      });
-      t_in += now() - t0;
-      e = hipMemcpyAsync(dev[b], pin[b], (size_t)m * 32, hipMemcpyHostToDevice, s);
-      if (e == hipSuccess) e = hipEventRecord(ev_in[b], s);
-    }
-    // dev[2 + b] is free once chunk k-2's D2H (stream so) has finished
-    if (e == hipSuccess && k >= 2 && so != s) e = hipStreamWaitEvent(s, ev_out[b], 0);
+    });
+    t_in += now() - t0;
+    hipError_t e = hipMemcpyAsync(dev[b], pin[b], (size_t)m * 32, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(ev_in[b], s);
+    // dev[2 + b] is free once chunk k-2's D2H (side stream) has finished
+    if (e == hipSuccess && k >= 2) e = hipStreamWaitEvent(s, ev_out[b], 0);
     if (e == hipSuccess) {
       TimedRegion tr(c, &c->main_ev, s);
       hipLaunchKernelGGL(k_align_rows_f64, dim3((unsigned)std::min<int64_t>((m + kBlock - 1) / kBlock, 4096)),
                          dim3(kBlock), 0, s, dev[b], (int64_t)4, m, r0, d_doff, F, d_pose, dev[2 + b]);
     }
     if (e == hipSuccess) e = hipGetLastError();
-    if (e == hipSuccess && so != s) {
-      e = hipEventRecord(ev_k[b], s);
-      if (e == hipSuccess) e = hipStreamWaitEvent(so, ev_k[b], 0);
-    }
-    if (variant != 2 && e == hipSuccess && k >= 1) {                // chunk k-1's rows are back: copy out
-      const double tw = now();
+    if (e == hipSuccess) e = hipEventRecord(ev_k[b], s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(so, ev_k[b], 0);
+    if (!direct_out && e == hipSuccess && k >= 1) {                 // chunk k-1's rows are back: copy out
+      const double tw2 = now();
       e = hipEventSynchronize(ev_out[b ^ 1]);
-      t_wait_out += now() - tw;
+      t_wait_out += now() - tw2;
       if (e == hipSuccess) copy_out(k - 1);
     }
     if (e == hipSuccess)
-      e = hipMemcpyAsync(variant == 2 ? outs[0] + 4 * r0 : pin[2 + b], dev[2 + b], (size_t)m * 32,
+      e = hipMemcpyAsync(direct_out ? outs[0] + 4 * r0 : pin[2 + b], dev[2 + b], (size_t)m * 32,
                          hipMemcpyDeviceToHost, so);
     if (e == hipSuccess) e = hipEventRecord(ev_out[b], so);
     if (e != hipSuccess) rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
   }
   if (rc == MC_OK && K > 0) {
+    const double tw = now();
     const hipError_t e = hipEventSynchronize(ev_out[(K - 1) & 1]);
+    t_wait_out += now() - tw;
     if (e != hipSuccess) rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
-    else if (variant != 2) copy_out(K - 1);
+    else if (!direct_out) copy_out(K - 1);
   }
   (void)hipStreamSynchronize(so);
   (void)hipStreamSynchronize(s);
@@ -1356,9 +1355,9 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
     (void)hipEventDestroy(ev_in[b]); (void)hipEventDestroy(ev_out[b]); (void)hipEventDestroy(ev_k[b]);
   }
   if (trace)
-    std::fprintf(stderr, "rowpipe v%d rows %lld chunks %lld: total %.2f ms, copy-in %.2f, copy-out %.2f, wait-in %.2f, "
-                 "wait-out %.2f ms\n", variant, (long long)rows_per, (long long)K, 1e3 * (now() - t_start), 1e3 * t_in,
-                 1e3 * t_out, 1e3 * t_wait_in, 1e3 * t_wait_out);
+    std::fprintf(stderr, "rowpipe %s rows %lld chunks %lld: total %.2f ms, copy-in %.2f, copy-out %.2f, wait-in %.2f, "
+                 "wait-out %.2f ms\n", direct_out ? "direct-out" : "staged-out", (long long)rows_per, (long long)K,
+                 1e3 * (now() - t_start), 1e3 * t_in, 1e3 * t_out, 1e3 * t_wait_in, 1e3 * t_wait_out);
   return rc;
 }
 

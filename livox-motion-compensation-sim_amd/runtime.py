@@ -269,6 +269,59 @@ class Context:
         return DeviceBuffer(self, nbytes)
 
 
+class HostPool:
+    """Recycled host blocks for large host-array results (run_alignment / align_frames): a fresh
+    (n, 4) float64 result costs its first-touch page faults (~90 ms for 1.9 GB, as much as moving it
+    over PCIe); a block whose previous array has died is handed out again already faulted.  The
+    returned array is an ordinary writeable numpy array; its block returns here when the last view of
+    it dies and serves the next result it fits (at most twice its size).  At most ``cap`` bytes wait."""
+
+    def __init__(self, cap: int = 8 << 30):
+        import threading
+        self.cap = int(cap)
+        self._free: list = []        # idle blocks (uint8 ndarrays)
+        self._busy: dict = {}        # id(proxy) -> block, while an array uses it
+        self._lock = threading.Lock()
+
+    def empty(self, shape, dtype=np.float64) -> np.ndarray:
+        dt = np.dtype(dtype)
+        count = int(np.prod(shape))
+        n = max(count * dt.itemsize, 1)
+        block = None
+        with self._lock:
+            fits = [i for i, b in enumerate(self._free) if n <= b.nbytes <= 2 * n]
+            if fits:
+                block = self._free.pop(min(fits, key=lambda i: self._free[i].nbytes))
+        if block is None:
+            block = np.empty(n, np.uint8)
+        proxy = (ctypes.c_char * block.nbytes).from_address(block.ctypes.data)
+        key = id(proxy)
+        with self._lock:
+            self._busy[key] = block
+        weakref.finalize(proxy, self._release, key)
+        return np.frombuffer(proxy, dt, count).reshape(shape)
+
+    def _release(self, key):
+        with self._lock:
+            block = self._busy.pop(key, None)
+            if block is not None and sum(b.nbytes for b in self._free) + block.nbytes <= self.cap:
+                self._free.append(block)
+
+    def idle_bytes(self) -> int:
+        with self._lock:
+            return sum(b.nbytes for b in self._free)
+
+
+_host_pool: "HostPool | None" = None
+
+
+def host_pool() -> HostPool:
+    global _host_pool
+    if _host_pool is None:
+        _host_pool = HostPool()
+    return _host_pool
+
+
 class DeviceBuffer:
     """Raw HBM allocation owned by a context (e.g. a device-resident (N,4) float64 AoS cloud)."""
 

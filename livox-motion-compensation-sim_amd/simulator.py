@@ -30,7 +30,9 @@ from . import codecs as _codecs
 from . import config as _config
 from . import trajectory as _traj
 from ._lib import check, fptr, ptr
-from .runtime import Context, default_context, deskew_points_f64
+from .runtime import Context, default_context, deskew_points_f64, host_pool
+
+POOLED_ROWS = 1 << 20   # results of at least this many rows (32 MB) come from the recycled host blocks
 
 
 class LiDARMotionSimulator:
@@ -124,7 +126,10 @@ class LiDARMotionSimulator:
         counts = np.fromiter((f.shape[0] for f in src), np.int64, F)
         lds = np.fromiter((f.shape[1] for f in src), np.int64, F)
         offs = np.concatenate([[0], np.cumsum(counts)])
-        out = np.empty((int(offs[-1]), 4))                     # one allocation; frames are views
+        n = int(offs[-1])
+        # one allocation, frames are views; a large result takes a recycled block when one is idle
+        # (no first-touch page faults), runtime.HostPool
+        out = host_pool().empty((n, 4)) if n >= POOLED_ROWS else np.empty((n, 4))
         fp = np.fromiter((f.__array_interface__["data"][0] for f in src), np.uintp, F)
         op = (out.__array_interface__["data"][0] + 32 * offs[:-1]).astype(np.uintp)
         t = None if times is None else np.ascontiguousarray(times, dtype=np.float64)

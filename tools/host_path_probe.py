@@ -25,8 +25,7 @@ def main():
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--points", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="", help="comma list of MCDESKEW_ROWPIPE values to A/B")
-    ap.add_argument("--rows", default="", help="comma list of MCDESKEW_PIPEROWS chunk sizes to A/B")
+
     args = ap.parse_args()
     F, n = args.frames, args.points
     rng = np.random.default_rng(0)
@@ -60,33 +59,31 @@ def main():
                                                        ptr(lds, c_int64), ptr(t, c_double), mc._lib.MC_POSE_SEARCHSORTED,
                                                        op.ctypes.data), "align")
     ref = None
-    for v in (args.variants.split(",") if args.variants else [""]):
-        for rows in (args.rows.split(",") if args.rows else [""]):
-            if v:
-                os.environ["MCDESKEW_ROWPIPE"] = v
-            if rows:
-                os.environ["MCDESKEW_PIPEROWS"] = rows
-            walls, pre = [], []
-            res = None
-            for _ in range(args.reps):
-                res = None                                    # the previous result is freed first
-                t0 = time.perf_counter()
-                res = sim.run_alignment(scans, tr, times)
-                walls.append(time.perf_counter() - t0)
-                t0 = time.perf_counter()
-                direct()
-                pre.append(time.perf_counter() - t0)
-            same = None
-            if ref is None:
-                ref = [r.copy() for r in res[:5]]
-            else:
-                same = all(np.array_equal(a, b) for a, b in zip(ref, res[:5]))
-            res = None
-            key = f"variant_{v or 'default'}_rows_{rows or 'default'}"
-            out[key] = {"run_alignment_s": walls, "Mpoints_s": F * n / min(walls) / 1e6,
-                        "Mpoints_s_median": F * n / float(np.median(walls)) / 1e6,
-                        "prefaulted_out_s": pre, "prefaulted_Mpoints_s": F * n / min(pre) / 1e6,
-                        "equal_to_first": same}
+    first = True
+    for rows in ("",):
+        walls, pre = [], []
+        res = None
+        for _ in range(args.reps):
+            res = None                                    # the previous result is freed first
+            t0 = time.perf_counter()
+            res = sim.run_alignment(scans, tr, times)
+            walls.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            direct()                                      # into a pre-faulted pageable array
+            pre.append(time.perf_counter() - t0)
+        same = None
+        if ref is None:
+            ref = [r.copy() for r in res[:5]]
+        else:
+            same = all(np.array_equal(a, b) for a, b in zip(ref, res[:5]))
+        res = None
+        out[f"rows_{rows or 'default'}"] = {
+            "run_alignment_s": walls, "Mpoints_s": F * n / min(walls) / 1e6,
+            "Mpoints_s_steady_median": F * n / float(np.median(walls[1:] if len(walls) > 1 else walls)) / 1e6,
+            "first_call_s" if first else "first_call_s_pool_warm": walls[0],
+            "pageable_prefaulted_out_s": pre, "pageable_prefaulted_Mpoints_s": F * n / min(pre) / 1e6,
+            "equal_to_first": same}
+        first = False
     print(json.dumps(out), flush=True)
 
 
