@@ -668,13 +668,13 @@ def measure_host_path(ctx, frames, points, reps):
         t0 = time.perf_counter()
         res = sim.run_alignment(scans, tr, times)
         walls.append(time.perf_counter() - t0)
-    # spot check against the reference's op sequence (oracle) on two frames
+    # spot check, bit for bit, against the reference's op sequence (scipy R, numpy matmul) on two frames
     from oracle import restatement as R
     idx = R.select_pose_index(tr["time"], times)
     ok = True
     for f in (0, frames - 1):
-        want = R.transform_pointcloud(scans[f], {"translation": tr["position_gps"][idx[f]],
-                                                 "rotation": tr["orientation_imu"][idx[f]]})
+        want = R.transform_pointcloud_ref_ops(scans[f], {"translation": tr["position_gps"][idx[f]],
+                                                         "rotation": tr["orientation_imu"][idx[f]]})
         ok = ok and bool(np.array_equal(res[f], want))
     res = None
     pc = pcie_ceiling()
