@@ -376,6 +376,9 @@ def test_pcd_len_batch_deskew_then_encode(mc, gpu_ctx, mode, big):
         assert got == want, (mode, issue)
         assert launches >= 2 if big else launches == 1, (mode, issue, launches)
     assert np.array_equal(out.download_aos(), plain.download_aos())
+    # mc_deskew_pcd into the same kind of batch: the batch's own sums, then the write pass
+    assert mc.codecs.deskew_pcd_frames(b, out, mode=mode) == want
+    assert out.pcd_len_current()
     # any other write of the columns makes the sums stale: the encoder measures again
     gpu_ctx.tune_order(b, out, mode=mode, launches=2, rounds=2)
     assert not out.pcd_len_current()
