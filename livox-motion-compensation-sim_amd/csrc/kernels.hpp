@@ -964,8 +964,8 @@ __device__ __forceinline__ void deskew_frame_quad(const DeskewArgs& a, const uin
         const float4 val = c == 3 ? w : o;
         const int64_t i0 = p[u] - ldu(a.fpoff + tl.frame), n = ldu(a.fcount + tl.frame);
         PcdCount pc;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) pc.add(PcdCount::lanes(act[u] && i0 + k < n), f4g(val, k));
+        pc.add2(act[u] && i0 < n, val.x, act[u] && i0 + 1 < n, val.y);
+        pc.add2(act[u] && i0 + 2 < n, val.z, act[u] && i0 + 3 < n, val.w);
         const int bytes = pc.bytes();   // (every lane: the per-lane variant reduces across the wave)
         if ((threadIdx.x & 63) == 0) s_part[PCD ? u : 0][threadIdx.x >> 6] = bytes;
       }
@@ -1527,11 +1527,9 @@ __global__ __launch_bounds__(kBlock, kPointsWaves) void k_deskew_points(const De
       PcdCount pc;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const auto v = PcdCount::lanes(act && i0 + c < n);
-        pc.add(v, f4g(X, c));
-        pc.add(v, f4g(Y, c));
-        pc.add(v, f4g(Z, c));
-        pc.add(v, f4g(I, c));
+        const bool v = act && i0 + c < n;
+        pc.add2(v, f4g(X, c), f4g(Y, c));
+        pc.add2(v, f4g(Z, c), f4g(I, c));
       }
       const int bytes = pc.bytes();      // (every lane: the per-lane variant reduces across the wave)
       const int wg = g0 + (tid & ~63);   // the wave's first group
@@ -1734,8 +1732,9 @@ __device__ __forceinline__ void aos_to_soa_unit(const LayoutArgs& a, const doubl
     if (g0 + gi < tl.ngroups) st_pol<kStageSt>(a.cols + bidx(a.C, c, p0 + 4 * gi), v);
     if (a.pcd_len) {   // uniform
       PcdCount pc;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) pc.add(loc0 + 4 * gi + k < cnt, f4g(v, k));
+      const int64_t r0 = loc0 + 4 * gi;
+      pc.add2(r0 < cnt, v.x, r0 + 1 < cnt, v.y);
+      pc.add2(r0 + 2 < cnt, v.z, r0 + 3 < cnt, v.w);
       const int bytes = pc.bytes();
       if (gi == 0) s_part[c] = bytes;
     }
@@ -1770,7 +1769,8 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
         for (int c = 0; c < 4; ++c) a.col(c, tl.pstart + j) = r[c];
       if (a.pcd_len) {   // uniform; j0 is a block boundary (tiles hold whole blocks)
         PcdCount pc;
-        for (int c = 0; c < 4; ++c) pc.add(j < nv, r[c]);
+        pc.add2(j < nv, r[0], r[1]);
+        pc.add2(j < nv, r[2], r[3]);
         const int bytes = pc.bytes();
         if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = bytes;
         __syncthreads();

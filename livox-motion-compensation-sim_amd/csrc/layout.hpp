@@ -72,28 +72,77 @@ __device__ __forceinline__ int i4c(const int4& v, int c) {
 // [|v| >= 10] + [|v| >= 100] + [|v| >= 1000] bytes (a float32 never rounds across a power of ten at
 // six decimals: the float32 below 10 is 9.99999905).  Any value outside the packed path (NaN, inf,
 // |v| >= 4294) adds kPcdSlowValue: a block whose count reaches it holds a line for the exact
-// formatter (the measure pass).  Per-lane sums (compares + adds) with one wave reduction at the end:
-// a ballot per term added up on the scalar unit was slower (+15 / +36 / +47 us: the 64-bit masks
-// spilled SGPRs into VGPR lanes, profiles/round3/s12).
+// formatter (the measure pass).
+//
+// Two values at a time in 16-bit halves (round 6): the thresholds 10, 100 and 1000 are float32s
+// whose low 16 bits are zero, so |v| >= T is a compare of the upper halves, and the upper halves of
+// two values pack into one register (v_perm_b32) for the packed 16-bit ALU — each [h >= T] is a
+// saturating subtract and a min (v_pk_sub_u16 clamp, v_pk_min_u16), added with v_pk_add_u16.  The
+// slow test on upper halves flags |v| >= 4288 (0x4586 << 16): a value in [4288, 4294) sends its block
+// to the measure pass, which formats it exactly.  Per-lane sums with one DPP wave reduction at the
+// end (a ballot per term added up on the scalar unit was slower, profiles/round3/s12).
 constexpr int kPcdSlowValue = 1 << 20;
-constexpr uint32_t kPcdSlowBits = 0x45863000u;   // |v| >= 4294.0f as a float32 bit pattern
+constexpr uint32_t kPcdSlowBits = 0x45860000u;   // |v| >= 4288.0f: conservatively outside the packed path
+// per 16-bit half of m: [m > c] (v_pk_sub_u16 clamp saturates at 0, v_pk_min_u16 caps at 1), as
+// inline asm: written with clang's elementwise builtins the two became a compare + select per half
+__device__ __forceinline__ uint32_t pk_gt_u16(uint32_t m, uint32_t c2) {
+  uint32_t d, r;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "v"(m), "s"(c2));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(d), "s"(0x00010001u));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// the wave's sum, in every lane: DPP within each 16-lane row (pairs, quads, half-row and row
+// mirrors), then the four rows' sums read from lanes 0, 16, 32, 48 (no LDS permutes)
+__device__ __forceinline__ int wave_sum_dpp(int t) {
+  t += __builtin_amdgcn_update_dpp(0, t, 0xB1, 0xF, 0xF, true);    // quad_perm [1, 0, 3, 2]
+  t += __builtin_amdgcn_update_dpp(0, t, 0x4E, 0xF, 0xF, true);    // quad_perm [2, 3, 0, 1]
+  t += __builtin_amdgcn_update_dpp(0, t, 0x141, 0xF, 0xF, true);   // row_half_mirror
+  t += __builtin_amdgcn_update_dpp(0, t, 0x140, 0xF, 0xF, true);   // row_mirror
+  return __builtin_amdgcn_readlane(t, 0) + __builtin_amdgcn_readlane(t, 16) + __builtin_amdgcn_readlane(t, 32) +
+         __builtin_amdgcn_readlane(t, 48);
+}
 struct PcdCount {
-  int n = 0;          // this lane's sum
-  uint32_t amax = 0;  // largest |v| bit pattern of the lane's valid values (NaN / inf above any finite)
-  __device__ __forceinline__ void add(bool valid, float v) {
-    const uint32_t u = (uint32_t)__float_as_int(v), ua = u & 0x7fffffffu;
-    const float a = __int_as_float((int)ua);
-    const int len = 9 + (int)(u >> 31) + (a >= 10.0f ? 1 : 0) + (a >= 100.0f ? 1 : 0) + (a >= 1000.0f ? 1 : 0);
-    n += valid ? len : 0;
-    amax = valid && ua > amax ? ua : amax;
+  uint32_t acc = 0;    // two 16-bit halves: signs + integer digits beyond the first, of the lane's values
+  uint32_t amax = 0;   // two 16-bit halves: the largest |v| upper 16 bits
+  int n = 0;           // the lane's valid values (9 bytes each before the counts)
+  // two values (the upper halves packed by v_perm_b32, b's low); an invalid one counts as +0.0 and
+  // adds no bytes
+  __device__ __forceinline__ void add2(bool va, float a, bool vb, float b) {
+    pack(__builtin_amdgcn_perm(va ? __float_as_uint(a) : 0u, vb ? __float_as_uint(b) : 0u, 0x07060302u));
+    n += (va ? 1 : 0) + (vb ? 1 : 0);
   }
-  __device__ __forceinline__ static bool lanes(bool valid) { return valid; }
+  // two values of one point (one validity)
+  __device__ __forceinline__ void add2(bool v, float a, float b) {
+    const uint32_t h = __builtin_amdgcn_perm(__float_as_uint(a), __float_as_uint(b), 0x07060302u);
+    pack(v ? h : 0u);
+    n += v ? 2 : 0;
+  }
+  __device__ __forceinline__ void pack(uint32_t h) {
+    const uint32_t m = h & 0x7FFF7FFFu;
+    acc = pk_add_u16(acc, (h >> 15) & 0x00010001u);
+    acc = pk_add_u16(acc, pk_gt_u16(m, 0x411F411Fu));   // |v| >= 10
+    acc = pk_add_u16(acc, pk_gt_u16(m, 0x42C742C7u));   // |v| >= 100
+    acc = pk_add_u16(acc, pk_gt_u16(m, 0x44794479u));   // |v| >= 1000
+    amax = pk_max_u16(amax, m);
+  }
+  __device__ __forceinline__ int lane_bytes() const { return 9 * n + (int)(acc & 0xFFFFu) + (int)(acc >> 16); }
+  __device__ __forceinline__ bool lane_slow() const {
+    const uint32_t lo = amax & 0xFFFFu, hi = amax >> 16;
+    return (lo > hi ? lo : hi) >= (kPcdSlowBits >> 16);
+  }
   __device__ __forceinline__ int bytes() const {   // the wave total (every lane takes part)
-    int t = n;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    const bool slow = __builtin_amdgcn_ballot_w64(amax >= kPcdSlowBits) != 0;
-    return t + (slow ? kPcdSlowValue : 0);
+    const bool slow = __builtin_amdgcn_ballot_w64(lane_slow()) != 0;
+    return wave_sum_dpp(lane_bytes()) + (slow ? kPcdSlowValue : 0);
   }
 };
 

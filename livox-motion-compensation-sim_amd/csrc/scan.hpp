@@ -280,9 +280,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_emit(const ScanEmitArgs a) {
             q[3 * kBlkPts] = v[3];
             if (a.pcd_len) {   // this line's text bytes (layout.hpp PcdCount), one atomic per point
               PcdCount pc;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) pc.add(true, v[k]);
-              atomicAdd(a.pcd_len + ((poff + o) >> 8), pc.n + (pc.amax >= kPcdSlowBits ? kPcdSlowValue : 0));
+              pc.add2(true, v[0], v[1]);
+              pc.add2(true, v[2], v[3]);
+              atomicAdd(a.pcd_len + ((poff + o) >> 8), pc.lane_bytes() + (pc.lane_slow() ? kPcdSlowValue : 0));
             }
           }
         }
