@@ -235,7 +235,10 @@ int mc_comm_gather_batch(mc_comm* c, const mc_batch* local, int root, mc_batch* 
   if (!c || !local) return fail(MC_ERR_INVALID, "NULL argument");
   if (local->ctx != c->ctx) return fail(MC_ERR_INVALID, "batch belongs to another context");
   const bool is_root = c->rank == root;
-  if (is_root && merged && merged->ctx != c->ctx) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
+  // a root whose merged batch is unusable still joins the plan all-gather as "no merged batch", so
+  // every rank fails together instead of waiting on it
+  const bool foreign = is_root && merged && merged->ctx != c->ctx;
+  if (foreign) merged = nullptr;
   HIPCHK(hipSetDevice(c->ctx->device));
   RcclGather X{c, c->ctx->stream};
   const mcgather::Transport T = rccl_transport(&X);
@@ -248,6 +251,7 @@ int mc_comm_gather_batch(mc_comm* c, const mc_batch* local, int root, mc_batch* 
   }
   std::string msg;
   const int r = mcgather::run(T, root, sh, is_root && merged ? &mg : nullptr, &msg);
+  if (foreign) return fail(MC_ERR_INVALID, "merged batch belongs to another context");
   if (r == mcgather::kBadPlan) return fail(MC_ERR_INVALID, "%s", msg.c_str());
   if (r) return r;   // the primitive recorded its message (mc_last_error)
   if (is_root) merged->trange_valid = false;   // column 4 (t_ns) was written: its cached spans are stale

@@ -14,18 +14,16 @@ int run(const Transport& T, int root, const Shard& local, const Merged* merged, 
     *msg = "bad root " + std::to_string(root);
     return kBadPlan;
   }
-  if (is_root && !merged) {
-    *msg = "root needs a merged batch";
-    return kBadPlan;
-  }
   // 1. every rank's (padded length, column count, frame count, hash of its frame counts) and the
   // root's merged ones: all ranks then hold the whole plan and reject a bad one together, before
-  // any send (equal padded totals do not make the same frame order)
-  const int64_t none = -1;
+  // any send (equal padded totals do not make the same frame order).  A root without a merged
+  // batch still takes part (its words say so), so no rank is left waiting in a collective.
+  const int64_t none = -1, missing = -2;
+  const bool have = is_root && merged;
   const int64_t mine[kPlanWords] = {
-      local.P, local.C, is_root ? merged->P : none, is_root ? merged->C : none, local.F,
-      (int64_t)mcplan::counts_hash(local.counts, local.F), is_root ? merged->F : none,
-      is_root ? (int64_t)mcplan::counts_hash(merged->counts, merged->F) : none};
+      local.P, local.C, have ? merged->P : (is_root ? missing : none), have ? merged->C : none, local.F,
+      (int64_t)mcplan::counts_hash(local.counts, local.F), have ? merged->F : none,
+      have ? (int64_t)mcplan::counts_hash(merged->counts, merged->F) : none};
   std::vector<int64_t> all((size_t)kPlanWords * nr);
   if (int r = T.allgather_i64(T.self, mine, kPlanWords, all.data())) return r;
   std::vector<int64_t> P(nr), C(nr), F(nr);
@@ -35,6 +33,10 @@ int run(const Transport& T, int root, const Shard& local, const Merged* merged, 
     P[q] = w[0]; C[q] = w[1]; F[q] = w[4]; H[q] = (uint64_t)w[5];
   }
   const int64_t* wr = all.data() + (size_t)kPlanWords * root;
+  if (wr[2] == missing) {
+    *msg = "root needs a merged batch";
+    return kBadPlan;
+  }
   // 2. the plan (where each shard lands, which are staged for a re-pitch) and the frame-order check
   mcplan::GatherPlan G;
   std::string perr = mcplan::plan_gather(nr, root, P.data(), C.data(), wr[2], wr[3], &G);

@@ -133,12 +133,12 @@ int rank_main(const std::string& dir, int rank, int world, int root, const Desc&
   sh.P = mine.P; sh.C = mine.C; sh.F = mine.F; sh.counts = mine.counts.data(); sh.cols = cols.data();
   std::vector<float> out;
   mcgather::Merged mg;
-  if (rank == root) {
+  if (rank == root && merged.P >= 0) {
     out.assign((size_t)(merged.C * merged.P), -9.0f);   // every value must be overwritten
     mg.P = merged.P; mg.C = merged.C; mg.F = merged.F; mg.counts = merged.counts.data(); mg.cols = out.data();
   }
-  std::string msg;
-  const int r = mcgather::run(T, root, sh, rank == root ? &mg : nullptr, &msg);
+  std::string msg;   // (a merged line with P < 0: the root passes no merged batch)
+  const int r = mcgather::run(T, root, sh, rank == root && merged.P >= 0 ? &mg : nullptr, &msg);
   std::printf("rank %d status %d %s\n", rank, r, msg.c_str());
   std::fflush(stdout);
   if (r == 0 && rank == root) {

@@ -321,6 +321,25 @@ def test_socket_transport_rejects_a_reordered_merge_on_every_rank(gather_exe, tm
     assert r.stdout.count("status -1") == world and merged is None
 
 
+def test_socket_transport_root_without_merged_batch_fails_everywhere(gather_exe, tmp_path):
+    """A root that passes no merged batch still takes part in the plan all-gather, so every rank
+    returns the error instead of waiting on the root forever."""
+    import subprocess
+    d = str(tmp_path)
+    shard_counts = [[300], [256], [10]]
+    shards = [_blocked(np.ones((sum(sc), 4), np.float32), sc, 4)[0] for sc in shard_counts]
+    for q, sh in enumerate(shards):
+        sh.tofile(os.path.join(d, f"shard_{q}.bin"))
+    P = [512, 256, 256]
+    lines = ["3 1", "-1 4 0"] + [" ".join(map(str, [P[q], 4, 1, shard_counts[q][0]])) for q in range(3)]
+    with open(os.path.join(d, "meta.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    r = subprocess.run([gather_exe, d], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
+    assert r.returncode == 3, r.stdout + r.stderr[-2000:]
+    assert r.stdout.count("status -1 root needs a merged batch") == 3
+
+
 # ---------------------------------------------------------------------------------------------
 # bench.py --gpus N without torchrun: the bench launches its own rank processes
 # ---------------------------------------------------------------------------------------------
