@@ -515,7 +515,8 @@ def measure_codecs(ctx, b_src, mode, b_out, n_rank, reps, cpu_budget):
     read + the encoded bytes written.  PCD: into a MC_BATCH_WITH_PCD_LEN batch the deskew kernel
     also writes each block's text length, so the encoder runs its write pass only; that pass + what
     the sums add to the deskew kernel (its median with sums minus without) is the PCD cost.  The
-    two-pass encoder (measure + write) on a plain batch is reported beside it.  ``frac`` is the cold
+    two-pass encoder (measure + write) on a plain batch is reported beside it, the two interleaved
+    rep by rep (so both deskews run unspeculated, in the same device state).  ``frac`` is the cold
     figure."""
     from ctypes import c_int64, c_uint64, c_void_p
     counts = np.ascontiguousarray(b_out.counts, np.int64)
@@ -544,13 +545,17 @@ def measure_codecs(ctx, b_src, mode, b_out, n_rank, reps, cpu_budget):
         t = ctx.read_timing()
         return t["codec_ms"], t["main_ms"]
 
-    def series(dst, encode):
-        steady(ctx, lambda: one(dst, encode, False))
-        res = {"after_deskew": [], "cold": []}
+    def series(arms):
+        """arms: name -> (deskew target, encode); the arms interleaved rep by rep, so every arm sees
+        the same device state (and consecutive deskews into different batches: none is speculated)"""
+        steady(ctx, lambda: [one(dst, enc, False) for dst, enc in arms.values()])
+        res = {a: {"after_deskew": [], "cold": []} for a in arms}
         for _ in range(reps):
             for kind in ("after_deskew", "cold"):
-                res[kind].append(one(dst, encode, kind == "cold"))
-        return {k: (float(np.median([a for a, _ in v])), float(np.median([b for _, b in v]))) for k, v in res.items()}
+                for a, (dst, enc) in arms.items():
+                    res[a][kind].append(one(dst, enc, kind == "cold"))
+        return {a: {k: (float(np.median([x for x, _ in v])), float(np.median([y for _, y in v])))
+                    for k, v in r.items()} for a, r in res.items()}
 
     def figures(ms, alg):
         return {"kernels_ms": ms, "Mpoints_s": n_rank / ms / 1e3, "GBs": alg / ms / 1e6,
@@ -565,7 +570,7 @@ def measure_codecs(ctx, b_src, mode, b_out, n_rank, reps, cpu_budget):
         def lvx():
             check(ctx.lib.mc_lvx_encode_batch(ctx.handle, b_out.handle, ptr(ids, c_uint64), ptr(ts, c_uint64),
                                               out.ptr, int(pos[-1])), "lvx_encode_batch")
-        m = series(b_out, lvx)
+        m = series({"lvx": (b_out, lvx)})["lvx"]
     finally:
         out.close()
     alg = 16 * n_rank + int(pos[-1])
@@ -584,10 +589,10 @@ def measure_codecs(ctx, b_src, mode, b_out, n_rank, reps, cpu_budget):
                 check(ctx.lib.mc_pcd_encode_batch(ctx.handle, b.handle, text.ptr, cap, ptr(bpos, c_int64)),
                       "pcd_encode_batch")
             return enc
-        m_sum = series(b_pcd, pcd_into(b_pcd))
+        m = series({"sum": (b_pcd, pcd_into(b_pcd)), "two": (b_out, pcd_into(b_out))})
         if not b_pcd.pcd_len_current():
             raise RuntimeError("the deskew into a MC_BATCH_WITH_PCD_LEN batch left no current text sums")
-        m_two = series(b_out, pcd_into(b_out))
+        m_sum, m_two = m["sum"], m["two"]
     finally:
         text.close()
         flush.close()
