@@ -213,3 +213,29 @@ def test_device_rows_reuse_only_for_the_unchanged_result():
     assert not rows.matches(res)
     rows.close()
     assert rows.d_local.closed and rows.d_aligned.closed
+
+
+def test_host_pool_recycles_blocks_only_after_every_view_dies():
+    """runtime.HostPool (large host-array results): an ordinary writeable array whose block returns
+    to the pool only when the array and all its views are gone, is reused for a result it fits
+    (at most twice its size), and is dropped beyond the pool's cap."""
+    rt = pkg().runtime
+    pool = rt.HostPool(cap=1 << 20)
+    a = pool.empty((1000, 4))
+    assert a.flags.writeable and a.shape == (1000, 4) and a.dtype == np.float64
+    a[:] = 3.0
+    addr = a.ctypes.data
+    view = a[10:20]
+    del a
+    assert pool.idle_bytes() == 0                 # the view keeps the block in use
+    assert float(view.sum()) == 3.0 * 40
+    del view
+    assert pool.idle_bytes() == 32_000
+    b = pool.empty((300, 4))                      # 9600 B: the 32 000 B block is more than twice that
+    assert b.ctypes.data != addr and pool.idle_bytes() == 32_000
+    c = pool.empty((900, 4))                      # fits: the same block again
+    assert c.ctypes.data == addr and pool.idle_bytes() == 0
+    del b, c
+    big = pool.empty((40_000, 4))                 # 1.28 MB: beyond the cap when released
+    del big
+    assert pool.idle_bytes() == 32_000 + 9_600
