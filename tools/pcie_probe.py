@@ -1,5 +1,6 @@
 """Host-side transfer ceilings on the GPU box (diagnostic): single-thread host memcpy, pinned
-H2D / D2H DMA and pageable H2D / D2H through the HIP runtime.  These bound the host-array entry
+H2D / D2H DMA, pageable H2D / D2H through the HIP runtime, and pinned H2D + D2H at once on two
+streams (the aggregate both directions carry together).  These bound the host-array entry
 points (transform_pointcloud / run_alignment on numpy arrays), not the device-resident hot path.
 
     python tools/pcie_probe.py [--mb 256]
@@ -43,6 +44,26 @@ def main():
             hip.hipMemcpy(dst, src, ctypes.c_size_t(nb), kind)
         hip.hipDeviceSynchronize()
         out[name + "_GBs"] = 5 * nb / (time.perf_counter() - t0) / 1e9
+    # both directions at once: H2D and D2H of nb bytes each on two streams (distinct buffers)
+    pin2, dev2 = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(pin2), ctypes.c_size_t(nb), 0) == 0
+    assert hip.hipMalloc(ctypes.byref(dev2), ctypes.c_size_t(nb)) == 0
+    s1, s2 = ctypes.c_void_p(), ctypes.c_void_p()
+    hip.hipStreamCreate(ctypes.byref(s1))
+    hip.hipStreamCreate(ctypes.byref(s2))
+    for rep in range(6):
+        t0 = time.perf_counter()
+        hip.hipMemcpyAsync(dev, pin, ctypes.c_size_t(nb), H2D, s1)
+        hip.hipMemcpyAsync(pin2, dev2, ctypes.c_size_t(nb), D2H, s2)
+        hip.hipStreamSynchronize(s1)
+        hip.hipStreamSynchronize(s2)
+        dt = time.perf_counter() - t0
+        if rep:   # (the first pair warms up)
+            out.setdefault("duplex_aggregate_GBs", []).append(2 * nb / dt / 1e9)
+    hip.hipStreamDestroy(s1)
+    hip.hipStreamDestroy(s2)
+    hip.hipFree(dev2)
+    hip.hipHostFree(pin2)
     hip.hipFree(dev)
     hip.hipHostFree(pin)
     print(json.dumps(out))
