@@ -1246,7 +1246,7 @@ static void host_rows(mc_ctx* c, const std::vector<int64_t>& doff, int64_t r0, i
 // contiguous page-locked array are written by the D2H directly; others (the usual numpy arrays) go
 // through pinned staging and a host copy-out.  For 600 x 100k rows (profiles/round6/s04, s06): one
 // stream for both directions 79-84 ms, two streams 58-64 ms into an already-faulted output (3.84 GB
-// over PCIe: the box's aggregate of both directions, ~64 GB/s, not twice one direction), DMA
+// over PCIe; both directions at once carry 55-57 GB/s together on this part, s16), DMA
 // straight from the caller's pageable frames 157-248 ms, direct D2H into page-locked outputs 61-71 ms
 // (no gain: the link, not the copy-out, bounds it).  MCDESKEW_ROWPIPE_TRACE=1 prints the phase times.
 static bool pinned_range(const void* p, size_t bytes) {
