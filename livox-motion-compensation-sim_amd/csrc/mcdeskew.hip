@@ -1242,33 +1242,18 @@ static void host_rows(mc_ctx* c, const std::vector<int64_t>& doff, int64_t r0, i
 }
 
 // Chunk k's H2D (main stream) runs beside chunk k-1's D2H (side stream), and the host pool copies
-// chunk k into pinned memory while the DMA engines move the chunks around it.  Outputs that are one
-// contiguous page-locked array are written by the D2H directly; others (the usual numpy arrays) go
-// through pinned staging and a host copy-out.  For 600 x 100k rows (profiles/round6/s04, s06): one
-// stream for both directions 79-84 ms, two streams 58-64 ms into an already-faulted output (3.84 GB
-// over PCIe; both directions at once carry 55-57 GB/s together on this part, s16), DMA
-// straight from the caller's pageable frames 157-248 ms, direct D2H into page-locked outputs 61-71 ms
-// (no gain: the link, not the copy-out, bounds it).  MCDESKEW_ROWPIPE_TRACE=1 prints the phase times.
-static bool pinned_range(const void* p, size_t bytes) {
-  for (const char* q : {static_cast<const char*>(p), static_cast<const char*>(p) + bytes - 1}) {
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, q) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    if (at.type != hipMemoryTypeHost) return false;
-  }
-  return true;
-}
+// chunk k into pinned memory, and chunk k-1's rows out of it, while the DMA engines move the chunks
+// around them.  For 600 x 100k rows (profiles/round6/s04, s06, s18): one stream for both directions
+// 79-84 ms, two streams 58-66 ms into an already-faulted output (3.84 GB over PCIe; both directions
+// at once carry 55-97 GB/s together depending on the box, s16 / s18), DMA straight from the caller's
+// pageable frames 157-248 ms, D2H straight into page-locked outputs 59-74 ms (no gain over the
+// staged copy-out).  MCDESKEW_ROWPIPE_TRACE=1 prints the phase times.
 
 static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* lds, const std::vector<int64_t>& doff,
                         const int64_t* d_doff, const double* d_pose, double* const* outs) {
   const int32_t F = (int32_t)doff.size() - 1;
   const int64_t n = doff[F];
   const int64_t rows_per = kPipeRows;   // 2 M rows (64 MB) per chunk: 58-61 vs 64 ms at 1 M (round 6, s04 / s06)
-  bool dense = true;   // the outputs are one contiguous (n, 4) array
-  for (int32_t f = 0; f < F && dense; ++f) dense = outs[f] == outs[0] + 4 * doff[f] || doff[f + 1] == doff[f];
-  const bool direct_out = dense && pinned_range(outs[0], (size_t)n * 32);
   const bool trace = std::getenv("MCDESKEW_ROWPIPE_TRACE") != nullptr;
   double t_in = 0, t_out = 0, t_wait_in = 0, t_wait_out = 0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -1330,15 +1315,13 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipEventRecord(ev_k[b], s);
     if (e == hipSuccess) e = hipStreamWaitEvent(so, ev_k[b], 0);
-    if (!direct_out && e == hipSuccess && k >= 1) {                 // chunk k-1's rows are back: copy out
+    if (e == hipSuccess && k >= 1) {                                // chunk k-1's rows are back: copy out
       const double tw2 = now();
       e = hipEventSynchronize(ev_out[b ^ 1]);
       t_wait_out += now() - tw2;
       if (e == hipSuccess) copy_out(k - 1);
     }
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(direct_out ? outs[0] + 4 * r0 : pin[2 + b], dev[2 + b], (size_t)m * 32,
-                         hipMemcpyDeviceToHost, so);
+    if (e == hipSuccess) e = hipMemcpyAsync(pin[2 + b], dev[2 + b], (size_t)m * 32, hipMemcpyDeviceToHost, so);
     if (e == hipSuccess) e = hipEventRecord(ev_out[b], so);
     if (e != hipSuccess) rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
   }
@@ -1347,7 +1330,7 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
     const hipError_t e = hipEventSynchronize(ev_out[(K - 1) & 1]);
     t_wait_out += now() - tw;
     if (e != hipSuccess) rc = fail(MC_ERR_HIP, "row pipeline: %s", hipGetErrorString(e));
-    else if (!direct_out) copy_out(K - 1);
+    else copy_out(K - 1);
   }
   (void)hipStreamSynchronize(so);
   (void)hipStreamSynchronize(s);
@@ -1355,8 +1338,8 @@ static int row_pipeline(mc_ctx* c, const double* const* frames, const int64_t* l
     (void)hipEventDestroy(ev_in[b]); (void)hipEventDestroy(ev_out[b]); (void)hipEventDestroy(ev_k[b]);
   }
   if (trace)
-    std::fprintf(stderr, "rowpipe %s rows %lld chunks %lld: total %.2f ms, copy-in %.2f, copy-out %.2f, wait-in %.2f, "
-                 "wait-out %.2f ms\n", direct_out ? "direct-out" : "staged-out", (long long)rows_per, (long long)K,
+    std::fprintf(stderr, "rowpipe rows %lld chunks %lld: total %.2f ms, copy-in %.2f, copy-out %.2f, wait-in %.2f, "
+                 "wait-out %.2f ms\n", (long long)rows_per, (long long)K,
                  1e3 * (now() - t_start), 1e3 * t_in, 1e3 * t_out, 1e3 * t_wait_in, 1e3 * t_wait_out);
   return rc;
 }

@@ -97,6 +97,31 @@ def test_run_alignment_matches_reference_frames(mc, gpu_ctx, name):
     assert merged.shape == (sum(len(s) for s in scans), 4)
 
 
+def test_run_alignment_large_results_through_recycled_blocks(mc, gpu_ctx):
+    """run_alignment over > 1 M rows (the two-stream row pipeline) into runtime.HostPool blocks: the
+    first result in a fresh block, the next ones in the recycled block once the previous result is
+    dropped.  Every call bitwise equal to the reference's op sequence (scipy R, numpy matmul),
+    ragged frames and a wider (5-column) frame included."""
+    from oracle import restatement as R
+    rng = np.random.default_rng(12)
+    counts = [300_000, 1, 0, 777_777, 250_001]
+    scans = [np.column_stack([rng.normal(0, 40, (n, 3)), rng.uniform(0, 1, n)]) for n in counts]
+    scans[3] = np.column_stack([scans[3], np.full(len(scans[3]), 7.0)])      # a 5-column frame
+    sim = mc.LiDARMotionSimulator(dict(CFGS["urban_complex"]), context=gpu_ctx)
+    tr = traj_of("urban_complex")
+    times = sim.lidar_times()[[3, 4, 5, 6, 7]]
+    idx = R.select_pose_index(tr["time"], times)
+    want = [R.transform_pointcloud_ref_ops(s, {"translation": tr["position_gps"][k],
+                                               "rotation": tr["orientation_imu"][k]}) for s, k in zip(scans, idx)]
+    pool = mc.runtime.host_pool()
+    for call in range(3):
+        out = sim.run_alignment(scans, tr, times)
+        for f, (o, w) in enumerate(zip(out, want)):
+            assert np.array_equal(o, w), (call, f, int(np.count_nonzero(o != w)))
+        del out, o
+        assert pool.idle_bytes() >= sum(counts) * 32          # the block is back for the next call
+
+
 def test_align_frames_ragged_batch(mc, gpu_ctx):
     rng = np.random.default_rng(1)
     counts = [0, 1, 2, 3, 4, 5, 7, 4096, 0, 2049, 2047, 1023, 100_003]
