@@ -311,6 +311,11 @@ class HostPool:
         with self._lock:
             return sum(b.nbytes for b in self._free)
 
+    def clear(self):
+        """Release every idle block (blocks still behind live arrays return to the pool later)."""
+        with self._lock:
+            self._free = []
+
 
 _host_pool: "HostPool | None" = None
 

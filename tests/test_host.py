@@ -239,3 +239,5 @@ def test_host_pool_recycles_blocks_only_after_every_view_dies():
     big = pool.empty((40_000, 4))                 # 1.28 MB: beyond the cap when released
     del big
     assert pool.idle_bytes() == 32_000 + 9_600
+    pool.clear()
+    assert pool.idle_bytes() == 0
