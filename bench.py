@@ -20,6 +20,12 @@ oracle (N = 1), or, at N > 1, the merged cloud is gathered to rank 0 over RCCL (
 and sampled frames of every rank's shard are checked against the oracle (``gather.parity``).  A
 failed or hung gather or a parity miss exits non-zero after the JSON line.
 
+Beside the headline (same line, never part of ``value``): the other two modes, the stager pair,
+scan_environment, the LVX / PCD writers after a fresh deskew and cold (``codecs``), and at N = 1 the
+reference's host-array calling convention at config-2 scale (``host_path``: run_alignment on numpy
+frames, against the box's PCIe DMA rates) and the simulate_frames -> save_results sequence
+(``simulate_save``); the reference's op sequence on the box's cores (``cpu_baseline``).
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mode pose_slerp|frame|imu] [--config C]
     torchrun --nproc-per-node N ... bench.py --gpus N   (one process per GPU, RCCL over xGMI)
 
