@@ -1767,7 +1767,7 @@ __global__ __launch_bounds__(kBlock) void k_aos_to_soa(const LayoutArgs a, const
         for (int c = 0; c < 4; ++c) r[c] = (float)src[(int64_t)j * ld + c];
       if (j < np)
         for (int c = 0; c < 4; ++c) a.col(c, tl.pstart + j) = r[c];
-      if (a.pcd_len) {   // uniform; j0 is a block boundary (tiles hold whole blocks)
+      if (a.pcd_len) {   // uniform; j0 is a block boundary (tiles start on one)
         PcdCount pc;
         pc.add2(j < nv, r[0], r[1]);
         pc.add2(j < nv, r[2], r[3]);
