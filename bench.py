@@ -537,7 +537,10 @@ def measure_codecs(ctx, b_src, mode, b_out, n_rank, reps, cpu_budget):
         check(ctx.lib.mc_memcpy_d2d(ctx.handle, hi, flush.ptr, half), "flush")
 
     def one(dst, encode, flushed):
-        """deskew -> [flush] -> encode; the encode's kernel ms and the deskew's (main) kernel ms"""
+        """flush -> deskew -> [flush] -> encode; the encode's kernel ms and the deskew's (main) kernel
+        ms.  The first flush puts every deskew on the same footing (whatever encode ran before it),
+        so the two PCD arms' deskews compare fairly."""
+        cold()
         ctx.read_timing()
         ctx.timing(True)
         ctx.deskew(b_src, dst, mode=mode)
