@@ -680,9 +680,10 @@ def pcie_ceiling(nbytes=256 << 20, reps=5):
     return out
 
 
-def measure_host_path(ctx, frames, points, reps):
-    """The reference's own calling convention at BASELINE config-2 scale (SURVEY §8 a3-a5 on host
-    arrays): run_alignment on ``frames`` x ``points`` float64 (n, 4) numpy frames, LMC:802-832, one
+def measure_host_path(ctx, cfg, frames, points, reps):
+    """The reference's own calling convention at the workload's scale (BASELINE config 2: 600 x 100k;
+    SURVEY §8 a3-a5 on host arrays): run_alignment on ``frames`` x ``points`` float64 (n, 4) numpy
+    frames with the workload's scenario (``cfg``) poses, LMC:802-832, one
     call for all frames, host arrays in and out (the reference's transform_pointcloud returns a new
     array per frame: every call writes a fresh output, whose first-touch page faults are part of the
     wall time).  64 algorithmic bytes per point cross PCIe (32 in, 32 out); the ceilings are this
@@ -691,7 +692,7 @@ def measure_host_path(ctx, frames, points, reps):
     rng = np.random.default_rng(0)
     base = rng.standard_normal((points, 4)) * 30.0
     scans = [base + f * 1e-3 for f in range(frames)]
-    sim = mc.LiDARMotionSimulator(dict(SCENARIOS["urban_complex"]), context=ctx)
+    sim = mc.LiDARMotionSimulator(dict(cfg), context=ctx)
     tr = sim.add_sensor_noise(sim.generate_trajectory())
     times = sim.lidar_times()[:frames]
     sim.run_alignment(scans[:2], tr, times[:2])
@@ -716,7 +717,7 @@ def measure_host_path(ctx, frames, points, reps):
     best, med = min(walls), float(np.median(walls))
     serial = 1.0 / (32 / pc["H2D_GBs"] + 32 / pc["D2H_GBs"]) * 1e3          # Mpoints/s
     concurrent = pc["both_directions_GBs"] / 64 * 1e3
-    return {"workload": f"run_alignment, {frames} x {points} float64 (n, 4) host frames (BASELINE config 2 shape)",
+    return {"workload": f"run_alignment, {frames} x {points} float64 (n, 4) host frames (the bench workload's shape)",
             "wall_s": walls, "Mpoints_s": n / best / 1e6, "Mpoints_s_median": n / med / 1e6,
             "GBs_64B_per_point": 64 * n / best / 1e9, "pcie": pc,
             "ceiling_Mpoints_s": {"serial": serial, "concurrent": concurrent},
@@ -1163,11 +1164,6 @@ def main():
         codecs = measure_codecs(ctx, src_of[args.mode], args.mode, b_out, n_rank, 5,
                                 0.0 if (args.no_cpu or world > 1) else 1.0)
         codecs["pcd_ascii_fused"] = measure_deskew_pcd(ctx, src_of[args.mode], b_out, args.mode, n_rank, 5)
-    host = save = None
-    if world == 1 and not args.no_extra_modes and not args.no_host_path and n_rank:
-        host = measure_host_path(ctx, len(counts), int(counts[0]) if len(counts) else 0, 3)
-        save = measure_save(ctx)
-
     imu = (ts_imu, gyro)
     F_all = len(counts_all)
     gather = parity = None
@@ -1186,6 +1182,13 @@ def main():
         ctx.sync()
         loc = sorted({0, F_all // 2, F_all - 1})
         parity = check_frames(b_out, args.mode, tr, times_all, imu, counts_all, loc, loc)
+
+    # the legs on the reference's own host-array calling convention load their own (urban_complex)
+    # trajectories into the context: after the parity check, which deskews with the workload's
+    host = save = None
+    if world == 1 and not args.no_extra_modes and not args.no_host_path and n_rank:
+        host = measure_host_path(ctx, cfg, len(counts), int(counts[0]) if len(counts) else 0, 3)
+        save = measure_save(ctx)
 
     single = None
     if world > 1 and rank == 0 and not args.no_single_gpu and n_total:
