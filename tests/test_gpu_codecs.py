@@ -444,3 +444,32 @@ def test_pcd_len_batch_scan_emit(mc, gpu_ctx):
     got, launches = _encode_timed(mc, gpu_ctx, out)
     assert launches == 1
     assert got == [C.pcd_ascii_bytes(h) for h in host]
+
+
+@pytest.mark.parametrize("ld", [4, 6])
+def test_pcd_len_sums_at_the_length_boundaries(mc, gpu_ctx, ld):
+    """The summing stager's text lengths (layout.hpp PcdCount) on the float32 neighbours of every
+    value where "%.6f" changes length (tests/test_pcd_len_rule.py checks the rule itself on the CPU),
+    ±0, denormals and both signs: write pass only, bytes equal to the oracle's; the same values past
+    the slow mark (4288) send their blocks to the measure pass and still match."""
+    def around(b, k=48):
+        c = np.float32(b).view(np.int32)
+        v = np.arange(c - k, c + k + 1, dtype=np.int32).view(np.float32)
+        return np.concatenate([v, -v])
+    vals = np.concatenate([around(b) for b in (5e-7, 1e-6, 1.0, 10.0, 100.0, 1000.0, 4287.0)]
+                          + [np.array([0.0, -0.0, 1e-45, -1e-45, 1.1754942e-38, -1.1754942e-38], np.float32)])
+    rng = np.random.default_rng(21)
+    for extra, launches_ok in ((np.zeros(0, np.float32), lambda k: k == 1),
+                               (np.array([4288.0, -4293.9, 1e6, np.inf], np.float32), lambda k: k >= 2)):
+        v = np.concatenate([vals, extra]).astype(np.float64)
+        n = -(-v.size // 4)
+        cols = np.resize(rng.permutation(v), 4 * n).reshape(n, 4)     # every value in some column
+        pts = np.column_stack([cols, rng.normal(0, 1, (n, ld - 4))]) if ld > 4 else cols
+        counts = np.array([n // 3, 0, n - n // 3 - 5, 5], np.int64)
+        b = gpu_ctx.batch(counts, with_pcd_len=True)
+        b.upload_aos(pts)
+        assert b.pcd_len_current()
+        host = b.split(b.download_aos())
+        got, launches = _encode_timed(mc, gpu_ctx, b)
+        assert launches_ok(launches), launches
+        assert got == [C.pcd_ascii_bytes(h) for h in host]
