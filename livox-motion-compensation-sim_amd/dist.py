@@ -7,7 +7,7 @@ ranks' shards in rank order reproduces it, done as one ragged RCCL gather over x
 (``mc_comm_gather_batch``).
 
 Control plane (rank/world from torchrun's env; barrier, max-over-ranks, RCCL unique-id
-broadcast) is a small TCP star on MASTER_ADDR:MASTER_PORT+1 (stdlib sockets — the GPU
+broadcast) is a small TCP star on MASTER_ADDR:MASTER_PORT+1 or the next free port (stdlib sockets — the GPU
 processes load no torch).  ``Rendezvous`` works on CPU, which the world-size-2 tests use.
 """
 from __future__ import annotations
@@ -80,8 +80,30 @@ def _recv(sock) -> bytes:
     return bytes(buf)
 
 
+def _recv_exact(sock, n: int) -> bytes:
+    buf = b""
+    while len(buf) < n:
+        chunk = sock.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError("peer closed")
+        buf += chunk
+    return buf
+
+
+_MAGIC = b"MCRDV\x00\x00\x01"   # rank 0's greeting, sent first on every accepted connection
+_PORT_TRIES = 32                    # rank 0 takes the first free port of base .. base + 31
+_GREETING_WAIT = 5.0                # seconds a rank waits for the greeting before trying the next port
+
+
 class Rendezvous:
-    """Star-topology control channel: rank 0 accepts world_size-1 connections."""
+    """Star-topology control channel: rank 0 accepts world_size-1 connections.
+
+    Rank 0 listens on MASTER_PORT + 1 (or ``port``), or on the next free port of the 32 above it
+    when that one is taken (say by a service of the launcher); it greets each connection with a
+    magic word before anything else, and a rank sends its (world size, rank) only after that
+    greeting, so a rank that reached a foreign listener (no greeting within ``_GREETING_WAIT``)
+    closes it and tries the next port, and a connection the rank gave up on before rank 0 accepted
+    it never registers (its rank word never arrives)."""
 
     def __init__(self, rank: int, world_size: int, addr: str | None = None, port: int | None = None,
                  timeout: float = 300.0):
@@ -91,33 +113,70 @@ class Rendezvous:
         if world_size == 1:
             return
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
-        port = port if port is not None else int(os.environ.get("MASTER_PORT", "29500")) + 1
+        base = port if port is not None else int(os.environ.get("MASTER_PORT", "29500")) + 1
+        ports = [base + k for k in range(_PORT_TRIES) if base + k < 65536]
         deadline = time.time() + timeout
         if rank == 0:
-            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            srv.bind((addr, port))
-            srv.listen(world_size)
-            srv.settimeout(timeout)
-            while len(self.peers) < world_size - 1:
-                conn, _ = srv.accept()
-                conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                r = struct.unpack("!I", _recv(conn))[0]
-                self.peers[r] = conn
-            srv.close()
-        else:
-            while True:
+            srv, err = None, None
+            for p in ports:
+                srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+                srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
                 try:
-                    s = socket.create_connection((addr, port), timeout=5.0)
+                    srv.bind((addr, p))
                     break
+                except OSError as e:
+                    srv.close()
+                    srv, err = None, e
+            if srv is None:
+                raise OSError(f"rendezvous: no free port in {ports[0]}..{ports[-1]}: {err}")
+            self.port = srv.getsockname()[1]
+            srv.listen(max(world_size, 16))
+            try:
+                while len(self.peers) < world_size - 1:
+                    left = deadline - time.time()
+                    if left <= 0:
+                        raise TimeoutError(f"rendezvous: {len(self.peers) + 1} of {world_size} ranks arrived")
+                    srv.settimeout(left)
+                    conn, _ = srv.accept()
+                    try:
+                        conn.settimeout(10.0)
+                        conn.sendall(_MAGIC)
+                        ws, r = struct.unpack("!II", _recv_exact(conn, 8))
+                        ok = ws == world_size and 0 < r < world_size and r not in self.peers
+                    except (OSError, struct.error):
+                        ok = False
+                    if not ok:
+                        conn.close()
+                        continue
+                    conn.settimeout(timeout)
+                    conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    self.peers[r] = conn
+            finally:
+                srv.close()
+        else:
+            k = 0
+            while True:
+                p = ports[k % len(ports)]
+                k += 1
+                s = None
+                try:
+                    s = socket.create_connection((addr, p), timeout=1.0)
+                    s.settimeout(_GREETING_WAIT)
+                    if _recv_exact(s, len(_MAGIC)) == _MAGIC:
+                        s.sendall(struct.pack("!II", world_size, rank))
+                        break
                 except OSError:
-                    if time.time() > deadline:
-                        raise
+                    pass
+                if s is not None:
+                    s.close()
+                if time.time() > deadline:
+                    raise TimeoutError(f"rendezvous: rank {rank} found no rank 0 on {ports[0]}..{ports[-1]}")
+                if k % len(ports) == 0:
                     time.sleep(0.05)
             s.settimeout(timeout)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            _send(s, struct.pack("!I", rank))
             self.sock = s
+            self.port = p
 
     def allgather(self, obj):
         """Every rank gets the rank-ordered list of every rank's JSON-serialisable obj."""

@@ -76,6 +76,51 @@ def test_rendezvous_processes(world):
         assert blob == b"uid-" + bytes(range(124))
 
 
+@pytest.mark.parametrize("foreign", ["silent", "talks"])
+def test_rendezvous_when_its_port_is_taken(foreign):
+    """MASTER_PORT + 1 held by another service (a listener that never speaks, or one that answers
+    with other bytes): rank 0 takes the next free port, the other ranks find it by its greeting."""
+    import threading
+    port = _free_port()
+    other = socket.socket()
+    other.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    other.bind(("127.0.0.1", port))
+    other.listen(16)
+    stop = threading.Event()
+
+    def talker():
+        other.settimeout(0.2)
+        while not stop.is_set():
+            try:
+                c, _ = other.accept()
+            except OSError:
+                continue
+            c.sendall(b"HTTP/1.1 400 Bad Request\r\n\r\n")
+            c.close()
+    t = threading.Thread(target=talker, daemon=True) if foreign == "talks" else None
+    if t:
+        t.start()
+    try:
+        world = 3
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_rdv_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in ps:
+            p.start()
+        res = sorted(q.get(timeout=120) for _ in ps)
+        for p in ps:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        for rank, got, mx, blob in res:
+            assert got == [{"rank": r, "n": r * 10} for r in range(world)]
+            assert blob == b"uid-" + bytes(range(124))
+    finally:
+        stop.set()
+        if t:
+            t.join()
+        other.close()
+
+
 def _gloo_worker(rank, world, root, port, q):
     import sys
     sys.path.insert(0, ROOT)
