@@ -26,13 +26,20 @@ def _f64(a, shape_tail=None):
 
 
 class Context:
-    """One device + stream.  ``device`` defaults to $MCDESKEW_DEVICE, else $LOCAL_RANK, else 0.
-    ``lib_path`` loads an alternative build of the library (A/B variant runs in one process)."""
+    """One device + stream.  ``device`` defaults to $MCDESKEW_DEVICE, else $LOCAL_RANK modulo the
+    visible devices (a launcher that gives each rank its own HIP_VISIBLE_DEVICES leaves every rank
+    one device, 0), else 0.  ``lib_path`` loads an alternative build of the library (A/B variant runs
+    in one process)."""
 
     def __init__(self, device: int | None = None, lib_path: str | None = None):
         self.lib = _lib.load(lib_path) if lib_path else _lib.load()
+        if device is None and "MCDESKEW_DEVICE" in os.environ:
+            device = int(os.environ["MCDESKEW_DEVICE"])
         if device is None:
-            device = int(os.environ.get("MCDESKEW_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+            n = c_int(0)
+            if device > 0 and self.lib.mc_device_count(ctypes.byref(n)) == 0 and n.value > 0:
+                device %= n.value
         h = c_void_p()
         check(self.lib.mc_create(int(device), ctypes.byref(h)), "mc_create")
         self.handle = h

@@ -840,3 +840,21 @@ def test_launch_spans_match_events(mc, gpu_ctx, mode):
     gpu_ctx.sync()
     assert gpu_ctx.read_timing_spans() == []
     gpu_ctx.read_timing()
+
+
+@pytest.mark.gpu
+def test_local_rank_wraps_to_the_visible_devices(mc, monkeypatch):
+    """Context() under a launcher's LOCAL_RANK picks LOCAL_RANK modulo the visible devices (a rank
+    given its own HIP_VISIBLE_DEVICES sees one device); an explicit device is taken as given."""
+    n = mc.Context.device_count()
+    monkeypatch.delenv("MCDESKEW_DEVICE", raising=False)
+    monkeypatch.setenv("LOCAL_RANK", str(n + 1))
+    ctx = mc.Context()
+    assert ctx.device == (n + 1) % n
+    b = ctx.batch([300])
+    b.synth(seed=1)
+    assert b.download_aos().shape == (300, 4)
+    b.close()
+    monkeypatch.setenv("MCDESKEW_DEVICE", str(n + 1))
+    with pytest.raises(ValueError, match="out of range"):
+        mc.Context()
