@@ -82,8 +82,9 @@ class Context:
         if len(ts) != len(g):
             raise ValueError("timestamp / gyro lengths differ")
         last = getattr(self, "_imu_last", None)
-        if last is not None and np.array_equal(last[0], ts) and np.array_equal(last[1], g):
-            return  # the device already holds these exact samples: skip only the upload
+        if (last is not None and last[1].shape == g.shape and np.array_equal(last[0], ts)
+                and np.array_equal(last[1].view(np.uint64), g.view(np.uint64))):
+            return  # the device already holds these exact bytes (-0.0 and NaN payloads included)
         self._imu_last = None
         check(self.lib.mc_set_imu(self.handle, len(ts), ptr(ts, c_int64), ptr(g, c_double)), "set_imu")
         self._imu_last = (ts.copy(), g.copy())
@@ -288,7 +289,9 @@ class HostPool:
         self.cap = int(cap)
         self._free: list = []        # idle blocks (uint8 ndarrays)
         self._busy: dict = {}        # id(proxy) -> block, while an array uses it
-        self._lock = threading.Lock()
+        # re-entrant: a block's finaliser (_release) may run inside empty() on the same thread, when
+        # an allocation there triggers the cyclic collector and it frees an array of this pool
+        self._lock = threading.RLock()
 
     def empty(self, shape, dtype=np.float64) -> np.ndarray:
         dt = np.dtype(dtype)

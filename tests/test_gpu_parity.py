@@ -858,3 +858,20 @@ def test_local_rank_wraps_to_the_visible_devices(mc, monkeypatch):
     monkeypatch.setenv("MCDESKEW_DEVICE", str(n + 1))
     with pytest.raises(ValueError, match="out of range"):
         mc.Context()
+
+
+@pytest.mark.gpu
+def test_set_imu_uploads_on_any_byte_change(mc, gpu_ctx):
+    """Context.set_imu skips the upload only for the very bytes the device holds: a gyro sample
+    turned from 0.0 into -0.0 (equal as numbers) is uploaded again, as Context.set_environment does
+    for scenes."""
+    ts = np.arange(10, dtype=np.int64) * 5_000_000
+    g = np.zeros((10, 3))
+    gpu_ctx.set_imu(ts, g)
+    first = gpu_ctx._imu_last
+    gpu_ctx.set_imu(ts.copy(), g.copy())
+    assert gpu_ctx._imu_last is first
+    g2 = g.copy()
+    g2[3, 1] = -0.0
+    gpu_ctx.set_imu(ts, g2)
+    assert gpu_ctx._imu_last is not first and np.signbit(gpu_ctx._imu_last[1][3, 1])
