@@ -121,6 +121,40 @@ def test_rendezvous_when_its_port_is_taken(foreign):
         other.close()
 
 
+def test_rendezvous_rank0_ignores_a_stray_connection():
+    """A connection that answers rank 0's greeting with a wrong world size (or closes) is dropped;
+    the real rank still registers."""
+    import struct
+    import threading
+    d = pkg().dist
+    port = _free_port()
+    out = {}
+
+    def root():
+        r = d.Rendezvous(0, 2, "127.0.0.1", port, timeout=60)
+        out["all"] = r.allgather("root")
+        r.close()
+    t = threading.Thread(target=root)
+    t.start()
+    for _ in range(200):   # the stray client: waits for the greeting, then lies about the world
+        try:
+            s = socket.create_connection(("127.0.0.1", port), timeout=1.0)
+            break
+        except OSError:
+            import time
+            time.sleep(0.02)
+    assert s.recv(8) == d._MAGIC
+    s.sendall(struct.pack("!II", 5, 1))
+    s.close()
+    s2 = socket.create_connection(("127.0.0.1", port), timeout=5.0)
+    s2.close()                               # connects and leaves before sending its rank
+    r1 = d.Rendezvous(1, 2, "127.0.0.1", port, timeout=60)
+    got = r1.allgather("one")
+    r1.close()
+    t.join(timeout=60)
+    assert got == ["root", "one"] and out["all"] == ["root", "one"]
+
+
 def _gloo_worker(rank, world, root, port, q):
     import sys
     sys.path.insert(0, ROOT)
